@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""bench.py — disparity frames/s of the MI355X engine (BASELINE.json metric).
+
+Workload (BASELINE.json metric): 1920x1080 rectified synthetic pairs, D=128, 9x9 SAD
+window, the whole device path of depth_map.create_depth_map per frame:
+    disparity (k_match) -> medianBlur 5 + depth post (k_median_i16, fused)
+Inputs are gray u8 pairs already resident in HBM (8 distinct frames per rank, cycled);
+outputs are depth f32, disparity f32 and depth u8 per frame.  One step = one frame pair.
+
+Multi-GPU: one process per GPU (torch.distributed.run), frames sharded across ranks with
+no collective in the data path (weak scaling); value = frames of all ranks / max time.
+
+Extra JSON fields: `roofline` for the dominant kernel (k_match; HIP-event durations
+measured inside the timed region) with the VALU-tap figure beside the HBM one, and
+`cpu_baseline` = the C oracle (oracle/sv_oracle.c, OpenMP) on this host's cores.
+
+torch is imported BEFORE the engine library so libsvhip binds to torch's HIP runtime
+(both ship libamdhip64.so.7; see DESIGN.md "One HIP runtime per process").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch  # noqa: E402  (must precede the engine library load)
+import torch.distributed as dist
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from stereovision_amd.engine import get_engine  # noqa: E402
+from stereovision_amd.synthetic import stereo_batch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_TAP_PEAK = 157.3e12       # v_sad_u8 taps/s (4 taps x 256 CU x 64 x 2.4 GHz)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(H, W, D, win, cost, seconds):
+    """C oracle (the port) timed on this host: whole app-1 path per frame."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sv_oracle_c as C  # test infrastructure, used here only as the CPU baseline
+    lib = C.lib()
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    threads = max(1, min(cores, 16))
+    L, R = stereo_batch(2, H, W, D, seed=4242)
+    depth = np.empty((H, W), np.float32)
+    disp = np.empty((H, W), np.float32)
+    norm = np.empty((H, W), np.uint8)
+    costi = {"sad": 0, "ssd": 1, "hog": 2}[cost]
+
+    def one(i):
+        lib.svo_depth_map(np.ascontiguousarray(L[i % 2]), np.ascontiguousarray(R[i % 2]), H, W,
+                          0, D, win, costi, np.float32(0.3), np.float32(2.0),
+                          np.float32(2.0 - 0.3), depth, disp, norm, threads)
+
+    import ctypes
+    f32 = ctypes.c_float
+    lib.svo_depth_map.argtypes = [C._u8p, C._u8p, C._i, C._i, C._i, C._i, C._i, C._i, f32, f32,
+                                  f32, C._f32p, C._f32p, C._u8p, C._i]
+    lib.svo_depth_map.restype = C._i
+    one(0)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        one(n)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds or n >= 200:
+            break
+    return {
+        "value": round(n / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+        "sample": f"{n} full {W}x{H} frames (D={D}, win={win}, {cost}: disparity + median5 + "
+                  f"depth post) of the C oracle, OpenMP {threads} threads, {dt:.1f} s",
+    }
+
+
+def pmc_traffic(workload_key):
+    """HBM bytes per k_match launch from the committed rocprofv3 PMC summary, if any."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--num-disp", type=int, default=128)
+    ap.add_argument("--win", type=int, default=9)
+    ap.add_argument("--cost", default="sad", choices=["sad", "ssd", "hog"])
+    ap.add_argument("--frames", type=int, default=8, help="distinct resident frames per rank")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed loop")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = local if world > 1 else 0
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+
+    H, W, D, win = args.height, args.width, args.num_disp, args.win
+    F = max(1, args.frames)
+    L, R = stereo_batch(F, H, W, D, seed=1000 * rank)
+    dL = torch.from_numpy(L).to(f"cuda:{dev}")
+    dR = torch.from_numpy(R).to(f"cuda:{dev}")
+    depth = torch.empty((H, W), dtype=torch.float32, device=f"cuda:{dev}")
+    disp = torch.empty((H, W), dtype=torch.float32, device=f"cuda:{dev}")
+    norm = torch.empty((H, W), dtype=torch.uint8, device=f"cuda:{dev}")
+    torch.cuda.synchronize()
+
+    eng = get_engine(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    pL = [dL[i].data_ptr() for i in range(F)]
+    pR = [dR[i].data_ptr() for i in range(F)]
+
+    def step(i):
+        f = i % F
+        eng.depth_map_dev(pL[f], pR[f], H, W, W, 0, D, win, 0.3, 2.0, depth.data_ptr(),
+                          disp.data_ptr(), norm.data_ptr(), cost=args.cost, stream=stream)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    eng.profile(not args.no_profile)
+    eng.profile_reset()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    eng.profile(False)
+    match_ms, match_n = eng.profile_read("match")
+    med_ms, med_n = eng.profile_read("median")
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames = world * args.steps
+    value = frames / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+    npx = H * W
+    k_avg_s = (match_ms / match_n) * 1e-3 if match_n else None
+    k_bytes = 4 * npx                          # 2 u8 images read + int16 map written
+    frame_bytes = 11 * npx                     # 2 u8 in; depth f32 + disparity f32 + u8 out
+    taps = npx * D * win * win
+    roofline = None
+    if k_avg_s:
+        achieved = k_bytes / k_avg_s / 1e9
+        roofline = {
+            "kernel": "k_match", "bound": "hbm", "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": pmc_traffic(f"{W}x{H}_D{D}_w{win}_{args.cost}"),
+            "bytes_per_launch": k_bytes, "avg_launch_us": round(k_avg_s * 1e6, 2),
+            "launches": match_n,
+            "valu": {"achieved_taps_per_s": taps / k_avg_s, "peak_taps_per_s": VALU_TAP_PEAK,
+                     "frac": round(taps / k_avg_s / VALU_TAP_PEAK, 4),
+                     "cells_per_s": npx * D / k_avg_s},
+            "median_post_avg_us": round(med_ms / med_n * 1e3, 2) if med_n else None,
+        }
+
+    result = {
+        "metric": "disparity frames/sec + HBM GB/s, 1920x1080 D=128 win=9, 1/2/4/8 GPU",
+        "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic rectified pairs (stereovision_amd.synthetic, seeds per rank)",
+        "config": {"workload": f"{W}x{H} D={D} win={win} {args.cost.upper()} depth_map path "
+                               "(disparity + median5 + depth post), gray inputs resident in HBM",
+                   "height": H, "width": W, "num_disp": D, "win": win, "cost": args.cost,
+                   "frames_resident_per_rank": F, "parallelism": f"frame-sharded x{world}"},
+        "hbm_gbs_frame_path": round(frame_bytes * value / 1e9, 2),
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(H, W, D, win, args.cost, args.cpu_seconds)
+        except Exception as e:  # the baseline is reported, never required
+            log(f"cpu baseline failed: {e}")
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+/*
+ * stereovision_amd.h — C ABI of the MI355X (gfx950) stereo-disparity engine.
+ *
+ * Drop-in boundary for the reference's disparity hot path.  Every entry point names the
+ * reference call it replaces (file:line under AlexGr5/StereoVision):
+ *
+ *   sv_gray / sv_gray_dev            cv2.cvtColor(img, cv2.COLOR_BGR2GRAY)
+ *                                    depth_map.py:871-880, fused_depth_map.py:979-980
+ *   sv_disparity / sv_disparity_dev  cv2.StereoSGBM_create(...).compute(gl, gr)
+ *                                    depth_map.py:894-909, fused_depth_map.py:988-1004
+ *                                    (replaced by the north_star SAD/SSD/HOG WTA engine;
+ *                                    same int16 x16 output convention)
+ *   sv_median5_f32                   cv2.medianBlur(disparity, 5)
+ *                                    depth_map.py:912, fused_depth_map.py:1007
+ *   sv_depth_post                    depth/clip/mask/normalise NumPy block, depth_map.py:915-937
+ *   sv_scaled_post                   clip/normalise/confidence NumPy block,
+ *                                    fused_depth_map.py:1010-1029
+ *   sv_depth_map                     the whole numeric body of create_depth_map
+ *                                    (depth_map.py:868-937) minus the colormap
+ *   sv_stereo_scaled                 the whole numeric body of create_depth_map_stereo_scaled
+ *                                    (fused_depth_map.py:976-1029) minus colormap/putText
+ *   sv_harris, sv_hog_hist           north_star stages with no reference counterpart
+ *
+ * Conventions
+ *   - plain pointers and sizes only; images are row-major uint8, `stride` in bytes;
+ *   - host (`sv_x`) entry points take caller-owned host buffers and block until the result
+ *     is in them; device (`sv_x_dev`) entry points take device pointers and a hipStream_t
+ *     passed as void* (NULL = the context's own stream) and return after enqueueing;
+ *   - return 0 on success, a negative errno-style code otherwise; no C++ exception crosses
+ *     the ABI; sv_last_error() gives the calling thread's last message;
+ *   - a context is bound to one device; calls on one context are serialised by an internal
+ *     mutex and each call selects the context's device first (device selection is
+ *     per-thread in HIP), so contexts may be used from any thread (the reference calls the
+ *     disparity path from a ThreadPoolExecutor worker, fused_depth_map.py:2591-2598);
+ *   - the context owns its device buffers and pinned staging, grown on demand and reused.
+ */
+#ifndef STEREOVISION_AMD_H
+#define STEREOVISION_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SV_API_VERSION 1
+
+typedef struct sv_ctx sv_ctx;
+
+enum sv_cost { SV_COST_SAD = 0, SV_COST_SSD = 1, SV_COST_HOG = 2 };
+
+enum sv_status {
+    SV_OK = 0,
+    SV_EHIP = -5,     /* HIP runtime error (message in sv_last_error) */
+    SV_ENOMEM = -12,
+    SV_ENODEV = -19,
+    SV_EINVAL = -22,
+    SV_ERANGE = -34   /* parameters whose argmin key would overflow 32 bits */
+};
+
+/* post-processing modes of sv_median_post_dev */
+enum sv_post { SV_POST_NONE = 0, SV_POST_DEPTH = 1, SV_POST_SCALED = 2 };
+
+/* kernel ids for the profiling counters */
+enum sv_kernel {
+    SV_K_GRAY = 0, SV_K_HARRIS = 1, SV_K_HOG = 2, SV_K_MATCH = 3, SV_K_MEDIAN = 4, SV_K_POST = 5,
+    SV_NKERNELS = 6
+};
+
+int sv_version(void);
+const char* sv_last_error(void);
+int sv_device_count(int* n);
+int sv_create(int device, sv_ctx** out);
+void sv_destroy(sv_ctx* ctx);
+int sv_synchronize(sv_ctx* ctx);
+void* sv_stream(sv_ctx* ctx);
+
+/* Engine plan for a configuration: disparities per lane, lanes per group, LDS bytes per
+ * 256-thread block of the matching kernel. */
+int sv_plan(int num_disp, int win, int cost, int* dpl, int* lpg, int* lds_bytes);
+
+/* ---- host-memory entry points (drop-in path) ------------------------------------- */
+int sv_gray(sv_ctx* ctx, const uint8_t* bgr, int H, int W, int stride, uint8_t* gray);
+
+/* left/right: HxW (channels = 1) or HxWx3 BGR (channels = 3).  disp16: HxW int16 = d*16,
+ * invalid = (min_disp-1)*16.  harris (nullable): HxW f32 Harris response of the left
+ * gray image. */
+int sv_disparity(sv_ctx* ctx, const uint8_t* left, const uint8_t* right, int H, int W,
+                 int channels, int stride, int min_disp, int num_disp, int win, int cost,
+                 int16_t* disp16, float* harris);
+
+int sv_median5_f32(sv_ctx* ctx, const float* in, int H, int W, float* out);
+
+/* min_depth/max_depth: float32 of the caller's bounds; depth_range: float32 of
+ * (max_depth - min_depth) computed in double (NumPy-2 semantics of depth_map.py:936);
+ * min_disp_global: the module global MIN_DISP (depth_map.py:932). */
+int sv_depth_post(sv_ctx* ctx, const float* disparity, int n, float min_depth, float max_depth,
+                  float depth_range, float min_disp_global, float* depth_final,
+                  uint8_t* depth_normalized);
+
+int sv_scaled_post(sv_ctx* ctx, const float* disparity, int n, int min_disp, int num_disp,
+                   float* disparity_normalized, uint8_t* normalized_u8, float* confidence);
+
+int sv_depth_map(sv_ctx* ctx, const uint8_t* left, const uint8_t* right, int H, int W,
+                 int channels, int stride, int min_disp, int num_disp, int win, int cost,
+                 float min_depth, float max_depth, float depth_range, float min_disp_global,
+                 float* depth_final, float* disparity, uint8_t* depth_normalized);
+
+int sv_stereo_scaled(sv_ctx* ctx, const uint8_t* left, const uint8_t* right, int H, int W,
+                     int channels, int stride, int min_disp, int num_disp, int win, int cost,
+                     float* disparity_normalized, float* disparity, uint8_t* normalized_u8,
+                     float* confidence);
+
+int sv_harris(sv_ctx* ctx, const uint8_t* gray, int H, int W, int stride, float* out);
+
+/* out: [H][W][10] uint16 (9 bins + 1 zero pad) window histograms */
+int sv_hog_hist(sv_ctx* ctx, const uint8_t* gray, int H, int W, int stride, int win,
+                uint16_t* out);
+
+/* ---- device-memory entry points (zero-copy, row bands for multi-GPU sharding) ---- */
+int sv_gray_dev(sv_ctx* ctx, const uint8_t* d_bgr, int H, int W, int pitch, uint8_t* d_gray,
+                void* stream);
+
+/* Computes output rows [row0, row1) of the disparity map of full-frame gray device images
+ * (halo rows are read from the full frame, so bands tile the frame bit-exactly). */
+int sv_disparity_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int H, int W,
+                     int pitch, int min_disp, int num_disp, int win, int cost, int row0,
+                     int row1, int16_t* d_disp16, int out_pitch, void* stream);
+
+/* medianBlur(.,5)/16 of rows [row0,row1) of an int16 x16 map (halo from the full map),
+ * fused with the post-processing `mode` (sv_post).  DEPTH: out_a = depth_final,
+ * out_u8 = depth_normalized.  SCALED: out_a = disparity_normalized, out_u8 = its u8
+ * image, out_b = confidence. */
+int sv_median_post_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W, int row0, int row1,
+                       int mode, float min_depth, float max_depth, float depth_range,
+                       float min_disp_global, int min_disp, int num_disp, float* d_disparity,
+                       float* d_out_a, uint8_t* d_out_u8, float* d_out_b, void* stream);
+
+/* Whole app-1 device path on gray device images: disparity -> median -> depth post. */
+int sv_depth_map_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int H, int W,
+                     int pitch, int min_disp, int num_disp, int win, int cost, float min_depth,
+                     float max_depth, float depth_range, float min_disp_global, float* d_depth,
+                     float* d_disparity, uint8_t* d_norm, void* stream);
+
+int sv_harris_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, float* d_out,
+                  void* stream);
+int sv_hog_hist_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, int win,
+                    int row0, int row1, uint16_t* d_out, void* stream);
+
+/* ---- profiling: HIP events around every kernel this context launches -------------- */
+int sv_profile_enable(sv_ctx* ctx, int on);
+/* Waits for the recorded events and returns the accumulated device time and launch count
+ * of kernel `kernel` (sv_kernel) since the last reset. */
+int sv_profile_read(sv_ctx* ctx, int kernel, double* total_ms, long long* count);
+int sv_profile_reset(sv_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STEREOVISION_AMD_H */

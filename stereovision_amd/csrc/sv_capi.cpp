@@ -1,0 +1,659 @@
+// sv_capi.cpp — the C ABI (include/stereovision_amd.h) over the gfx950 kernels.
+//
+// A context = one device + one HIP stream + grow-only device buffers + pinned staging.
+// Host entry points stage into pinned memory, run the whole chain on the context stream
+// and copy results back; device entry points only enqueue.  No exception crosses the ABI.
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "sv_internal.h"
+#include "../../include/stereovision_amd.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hipfail(int e, const char* what) {
+    return fail(SV_EHIP, std::string(what) + ": " + hipGetErrorString((hipError_t)e));
+}
+
+#define SV_HIP(call)                                               \
+    do {                                                           \
+        hipError_t e_ = (call);                                    \
+        if (e_ != hipSuccess) return hipfail((int)e_, #call);      \
+    } while (0)
+
+#define SV_LAUNCH(ctx, kid, stream, call)                          \
+    do {                                                           \
+        (ctx)->prof_begin((kid), (stream));                        \
+        int e_ = (call);                                           \
+        if (e_ != 0) return hipfail(e_, #call);                    \
+        (ctx)->prof_end((stream));                                 \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct EvPair {
+    hipEvent_t a, b;
+    int kid;
+};
+
+}  // namespace
+
+struct sv_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin;
+    HostBuf hin, hout;
+    bool prof = false;
+    std::vector<EvPair> pending;
+    std::vector<hipEvent_t> pool;
+    double acc_ms[SV_NKERNELS] = {};
+    long long cnt[SV_NKERNELS] = {};
+    EvPair cur{};
+
+    hipEvent_t get_event() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    void prof_begin(int kid, hipStream_t s) {
+        if (!prof) return;
+        cur.a = get_event();
+        cur.b = get_event();
+        cur.kid = kid;
+        (void)hipEventRecord(cur.a, s);
+    }
+    void prof_end(hipStream_t s) {
+        if (!prof) return;
+        (void)hipEventRecord(cur.b, s);
+        pending.push_back(cur);
+    }
+    void prof_drain() {
+        for (auto& p : pending) {
+            (void)hipEventSynchronize(p.b);
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+                acc_ms[p.kid] += ms;
+                cnt[p.kid] += 1;
+            }
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+};
+
+namespace {
+
+inline hipStream_t pick(sv_ctx* c, void* s) { return s ? static_cast<hipStream_t>(s) : c->stream; }
+
+int check_image(const void* a, int H, int W) {
+    if (!a || H <= 0 || W <= 0) return fail(SV_EINVAL, "null image or non-positive size");
+    return 0;
+}
+
+int check_match(int H, int W, int min_disp, int num_disp, int win, int cost, sv::MatchPlan* plan) {
+    if (H <= 0 || W <= 0) return fail(SV_EINVAL, "non-positive image size");
+    if (num_disp <= 0 || num_disp > 512) return fail(SV_EINVAL, "num_disp must be in [1, 512]");
+    if (win < 1 || win > 15 || (win & 1) == 0) return fail(SV_EINVAL, "win must be odd in [1, 15]");
+    if (min_disp < -4096 || min_disp > 4096) return fail(SV_EINVAL, "min_disp out of range");
+    int rc = sv::plan_match(num_disp, win, cost, plan);
+    if (rc == -34) return fail(SV_ERANGE, "cost range too large for the argmin key");
+    if (rc != 0) return fail(SV_EINVAL, "unsupported (num_disp, win, cost)");
+    return 0;
+}
+
+// Enqueue disparity for rows [row0,row1) of gray device images.
+int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, int pitch,
+                      int min_disp, int num_disp, int win, int cost, int row0, int row1,
+                      int16_t* out, int opitch, hipStream_t s) {
+    sv::MatchPlan plan;
+    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    if (row0 < 0) row0 = 0;
+    if (row1 > H) row1 = H;
+    if (row1 <= row0) return 0;
+    sv::MatchParams a{};
+    a.L = L;
+    a.R = R;
+    a.H = H;
+    a.W = W;
+    a.pitch = pitch;
+    a.minD = min_disp;
+    a.D = num_disp;
+    a.win = win;
+    a.r = cost == SV_COST_HOG ? 0 : win / 2;
+    int maxd = min_disp + num_disp;
+    a.X0 = maxd > 0 ? maxd : 0;
+    a.X1 = W + (min_disp < 0 ? min_disp : 0);
+    if (a.X1 > W) a.X1 = W;
+    if (a.X1 < a.X0) a.X1 = a.X0;
+    a.row0 = row0;
+    a.row1 = row1;
+    a.lpg = plan.lpg;
+    a.lpg_log2 = plan.lpg == 16 ? 4 : plan.lpg == 32 ? 5 : 6;
+    a.dbits = plan.dbits;
+    a.out = out;
+    a.opitch = opitch;
+    if (cost == SV_COST_HOG && a.X1 > a.X0) {
+        const size_t hb = (size_t)H * W * 10 * sizeof(uint16_t);
+        SV_HIP(c->hog[0].ensure(hb));
+        SV_HIP(c->hog[1].ensure(hb));
+        SV_LAUNCH(c, SV_K_HOG, s, sv::launch_hog_hist(L, H, W, pitch, win, row0, row1, c->hog[0].as<uint16_t>(), s));
+        SV_LAUNCH(c, SV_K_HOG, s, sv::launch_hog_hist(R, H, W, pitch, win, row0, row1, c->hog[1].as<uint16_t>(), s));
+        a.HL = c->hog[0].as<uint16_t>();
+        a.HR = c->hog[1].as<uint16_t>();
+    }
+    SV_LAUNCH(c, SV_K_MATCH, s, sv::launch_match(a, plan, cost, s));
+    return 0;
+}
+
+sv::PostParams make_post(int mode, float minf, float maxf, float rangef, float mdg, int min_disp,
+                         int num_disp, float* a, uint8_t* u8, float* b) {
+    sv::PostParams pp{};
+    pp.mode = mode;
+    pp.minf = minf;
+    pp.maxf = maxf;
+    pp.rangef = rangef;
+    pp.min_disp_global = mdg;
+    pp.min_disp = min_disp;
+    pp.num_disp = num_disp;
+    pp.out_a = a;
+    pp.out_u8 = u8;
+    pp.out_b = b;
+    return pp;
+}
+
+// Stage two host images (HxW or HxWx3, any stride) into the context's device gray buffers.
+int stage_pair(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels,
+               int stride) {
+    if (check_image(left, H, W) || check_image(right, H, W)) return SV_EINVAL;
+    if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
+    const size_t row = (size_t)W * channels;
+    if (stride < (int)row) return fail(SV_EINVAL, "stride smaller than a row");
+    const size_t n = row * H;
+    SV_HIP(c->hin.ensure(2 * n));
+    SV_HIP(c->gray[0].ensure((size_t)H * W));
+    SV_HIP(c->gray[1].ensure((size_t)H * W));
+    const uint8_t* src[2] = {left, right};
+    for (int k = 0; k < 2; ++k) {
+        uint8_t* dst = c->hin.as<uint8_t>() + k * n;
+        if ((size_t)stride == row) {
+            std::memcpy(dst, src[k], n);
+        } else {
+            for (int y = 0; y < H; ++y) std::memcpy(dst + y * row, src[k] + (size_t)y * stride, row);
+        }
+    }
+    if (channels == 1) {
+        SV_HIP(hipMemcpyAsync(c->gray[0].p, c->hin.p, n, hipMemcpyHostToDevice, c->stream));
+        SV_HIP(hipMemcpyAsync(c->gray[1].p, c->hin.as<uint8_t>() + n, n, hipMemcpyHostToDevice, c->stream));
+    } else {
+        SV_HIP(c->img[0].ensure(n));
+        SV_HIP(c->img[1].ensure(n));
+        for (int k = 0; k < 2; ++k) {
+            SV_HIP(hipMemcpyAsync(c->img[k].p, c->hin.as<uint8_t>() + k * n, n, hipMemcpyHostToDevice, c->stream));
+            SV_LAUNCH(c, SV_K_GRAY, c->stream,
+                      sv::launch_gray(c->img[k].as<uint8_t>(), H, W, (int)row, c->gray[k].as<uint8_t>(), c->stream));
+        }
+    }
+    return 0;
+}
+
+struct Out {
+    void* host;
+    const void* dev;
+    size_t bytes;
+};
+
+// Copy device results to caller buffers through the pinned output staging, then wait.
+int collect(sv_ctx* c, const Out* outs, int n) {
+    size_t total = 0;
+    for (int i = 0; i < n; ++i)
+        if (outs[i].host) total += (outs[i].bytes + 255) & ~(size_t)255;
+    SV_HIP(c->hout.ensure(total ? total : 256));
+    size_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!outs[i].host) continue;
+        SV_HIP(hipMemcpyAsync(c->hout.as<uint8_t>() + off, outs[i].dev, outs[i].bytes, hipMemcpyDeviceToHost, c->stream));
+        off += (outs[i].bytes + 255) & ~(size_t)255;
+    }
+    SV_HIP(hipStreamSynchronize(c->stream));
+    off = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!outs[i].host) continue;
+        std::memcpy(outs[i].host, c->hout.as<uint8_t>() + off, outs[i].bytes);
+        off += (outs[i].bytes + 255) & ~(size_t)255;
+    }
+    return 0;
+}
+
+struct Guard {
+    sv_ctx* c;
+    std::unique_lock<std::mutex> lk;
+    int rc = 0;
+    explicit Guard(sv_ctx* ctx) : c(ctx), lk(ctx->mu) {
+        hipError_t e = hipSetDevice(ctx->device);
+        if (e != hipSuccess) rc = hipfail((int)e, "hipSetDevice");
+    }
+};
+
+#define SV_ENTER(ctx)                                                       \
+    if (!(ctx)) return fail(SV_EINVAL, "null context");                     \
+    Guard guard_(ctx);                                                      \
+    if (guard_.rc) return guard_.rc
+
+}  // namespace
+
+extern "C" {
+
+int sv_version(void) { return SV_API_VERSION; }
+
+const char* sv_last_error(void) { return g_err.c_str(); }
+
+int sv_device_count(int* n) {
+    if (!n) return fail(SV_EINVAL, "null output");
+    int k = 0;
+    hipError_t e = hipGetDeviceCount(&k);
+    if (e != hipSuccess) {
+        *n = 0;
+        return hipfail((int)e, "hipGetDeviceCount");
+    }
+    *n = k;
+    return 0;
+}
+
+int sv_create(int device, sv_ctx** out) {
+    if (!out) return fail(SV_EINVAL, "null output");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(SV_ENODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(SV_ENODEV, "device index out of range");
+    sv_ctx* c = new (std::nothrow) sv_ctx();
+    if (!c) return fail(SV_ENOMEM, "context allocation failed");
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return hipfail((int)e, "sv_create");
+    }
+    *out = c;
+    return 0;
+}
+
+void sv_destroy(sv_ctx* c) {
+    if (!c) return;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        c->prof_drain();
+        for (auto e : c->pool) (void)hipEventDestroy(e);
+        DevBuf* bufs[] = {&c->img[0], &c->img[1], &c->gray[0], &c->gray[1], &c->d16, &c->fa, &c->fb,
+                          &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin};
+        for (auto* b : bufs) b->release();
+        c->hin.release();
+        c->hout.release();
+        (void)hipStreamDestroy(c->stream);
+    }
+    delete c;
+}
+
+int sv_synchronize(sv_ctx* c) {
+    SV_ENTER(c);
+    SV_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+void* sv_stream(sv_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+int sv_plan(int num_disp, int win, int cost, int* dpl, int* lpg, int* lds_bytes) {
+    sv::MatchPlan p;
+    int rc = sv::plan_match(num_disp, win, cost, &p);
+    if (rc == -34) return fail(SV_ERANGE, "cost range too large for the argmin key");
+    if (rc) return fail(SV_EINVAL, "unsupported (num_disp, win, cost)");
+    if (dpl) *dpl = p.dpl;
+    if (lpg) *lpg = p.lpg;
+    if (lds_bytes) *lds_bytes = (int)sv::match_lds_bytes(p, cost == SV_COST_HOG ? 0 : win / 2, cost);
+    return 0;
+}
+
+// ---------------------------------------------------------------- device entry points
+int sv_gray_dev(sv_ctx* c, const uint8_t* d_bgr, int H, int W, int pitch, uint8_t* d_gray, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_bgr, H, W) || !d_gray) return fail(SV_EINVAL, "bad gray arguments");
+    hipStream_t s = pick(c, stream);
+    SV_LAUNCH(c, SV_K_GRAY, s, sv::launch_gray(d_bgr, H, W, pitch, d_gray, s));
+    return 0;
+}
+
+int sv_disparity_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, int H, int W, int pitch,
+                     int min_disp, int num_disp, int win, int cost, int row0, int row1, int16_t* d_disp16,
+                     int out_pitch, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_left, H, W) || check_image(d_right, H, W) || !d_disp16)
+        return fail(SV_EINVAL, "bad disparity arguments");
+    if (pitch < W || out_pitch < W) return fail(SV_EINVAL, "pitch smaller than width");
+    return enqueue_disparity(c, d_left, d_right, H, W, pitch, min_disp, num_disp, win, cost, row0, row1,
+                             d_disp16, out_pitch, pick(c, stream));
+}
+
+int sv_median_post_dev(sv_ctx* c, const int16_t* d_disp16, int H, int W, int row0, int row1, int mode,
+                       float min_depth, float max_depth, float depth_range, float min_disp_global,
+                       int min_disp, int num_disp, float* d_disparity, float* d_out_a, uint8_t* d_out_u8,
+                       float* d_out_b, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_disp16, H, W) || !d_disparity) return fail(SV_EINVAL, "bad median arguments");
+    if (mode == SV_POST_DEPTH && (!d_out_a || !d_out_u8)) return fail(SV_EINVAL, "depth post outputs missing");
+    if (mode == SV_POST_SCALED && (!d_out_a || !d_out_u8 || !d_out_b || num_disp <= 0))
+        return fail(SV_EINVAL, "scaled post outputs missing");
+    if (row0 < 0) row0 = 0;
+    if (row1 > H) row1 = H;
+    hipStream_t s = pick(c, stream);
+    sv::PostParams pp = make_post(mode, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
+                                  d_out_a, d_out_u8, d_out_b);
+    SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(d_disp16, H, W, row0, row1, d_disparity, pp, s));
+    return 0;
+}
+
+int sv_depth_map_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, int H, int W, int pitch,
+                     int min_disp, int num_disp, int win, int cost, float min_depth, float max_depth,
+                     float depth_range, float min_disp_global, float* d_depth, float* d_disparity,
+                     uint8_t* d_norm, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_left, H, W) || check_image(d_right, H, W) || !d_depth || !d_disparity || !d_norm)
+        return fail(SV_EINVAL, "bad depth-map arguments");
+    hipStream_t s = pick(c, stream);
+    SV_HIP(c->d16.ensure((size_t)H * W * sizeof(int16_t)));
+    int rc = enqueue_disparity(c, d_left, d_right, H, W, pitch, min_disp, num_disp, win, cost, 0, H,
+                               c->d16.as<int16_t>(), W, s);
+    if (rc) return rc;
+    sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                                  num_disp, d_depth, d_norm, nullptr);
+    SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, d_disparity, pp, s));
+    return 0;
+}
+
+int sv_harris_dev(sv_ctx* c, const uint8_t* d_gray, int H, int W, int pitch, float* d_out, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_gray, H, W) || !d_out) return fail(SV_EINVAL, "bad harris arguments");
+    hipStream_t s = pick(c, stream);
+    SV_LAUNCH(c, SV_K_HARRIS, s, sv::launch_harris(d_gray, H, W, pitch, d_out, s));
+    return 0;
+}
+
+int sv_hog_hist_dev(sv_ctx* c, const uint8_t* d_gray, int H, int W, int pitch, int win, int row0, int row1,
+                    uint16_t* d_out, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_gray, H, W) || !d_out) return fail(SV_EINVAL, "bad hog arguments");
+    if (win < 1 || win > 15 || (win & 1) == 0) return fail(SV_EINVAL, "win must be odd in [1, 15]");
+    hipStream_t s = pick(c, stream);
+    SV_LAUNCH(c, SV_K_HOG, s, sv::launch_hog_hist(d_gray, H, W, pitch, win, row0, row1, d_out, s));
+    return 0;
+}
+
+// ---------------------------------------------------------------- host entry points
+int sv_gray(sv_ctx* c, const uint8_t* bgr, int H, int W, int stride, uint8_t* gray) {
+    SV_ENTER(c);
+    if (check_image(bgr, H, W) || !gray) return fail(SV_EINVAL, "bad gray arguments");
+    const size_t row = (size_t)W * 3, n = row * H;
+    if (stride < (int)row) return fail(SV_EINVAL, "stride smaller than a row");
+    SV_HIP(c->hin.ensure(n));
+    for (int y = 0; y < H; ++y) std::memcpy(c->hin.as<uint8_t>() + y * row, bgr + (size_t)y * stride, row);
+    SV_HIP(c->img[0].ensure(n));
+    SV_HIP(c->gray[0].ensure((size_t)H * W));
+    SV_HIP(hipMemcpyAsync(c->img[0].p, c->hin.p, n, hipMemcpyHostToDevice, c->stream));
+    SV_LAUNCH(c, SV_K_GRAY, c->stream,
+              sv::launch_gray(c->img[0].as<uint8_t>(), H, W, (int)row, c->gray[0].as<uint8_t>(), c->stream));
+    Out o[] = {{gray, c->gray[0].p, (size_t)H * W}};
+    return collect(c, o, 1);
+}
+
+int sv_disparity(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels, int stride,
+                 int min_disp, int num_disp, int win, int cost, int16_t* disp16, float* harris) {
+    SV_ENTER(c);
+    if (!disp16) return fail(SV_EINVAL, "null disparity output");
+    sv::MatchPlan plan;
+    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    rc = stage_pair(c, left, right, H, W, channels, stride);
+    if (rc) return rc;
+    SV_HIP(c->d16.ensure((size_t)H * W * sizeof(int16_t)));
+    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
+                           win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
+    if (rc) return rc;
+    if (harris) {
+        SV_HIP(c->harris.ensure((size_t)H * W * sizeof(float)));
+        SV_LAUNCH(c, SV_K_HARRIS, c->stream,
+                  sv::launch_harris(c->gray[0].as<uint8_t>(), H, W, W, c->harris.as<float>(), c->stream));
+    }
+    Out o[] = {{disp16, c->d16.p, (size_t)H * W * sizeof(int16_t)},
+               {harris, c->harris.p, (size_t)H * W * sizeof(float)}};
+    return collect(c, o, 2);
+}
+
+int sv_median5_f32(sv_ctx* c, const float* in, int H, int W, float* out) {
+    SV_ENTER(c);
+    if (check_image(in, H, W) || !out) return fail(SV_EINVAL, "bad median arguments");
+    const size_t n = (size_t)H * W * sizeof(float);
+    SV_HIP(c->hin.ensure(n));
+    SV_HIP(c->fin.ensure(n));
+    SV_HIP(c->fa.ensure(n));
+    std::memcpy(c->hin.p, in, n);
+    SV_HIP(hipMemcpyAsync(c->fin.p, c->hin.p, n, hipMemcpyHostToDevice, c->stream));
+    SV_LAUNCH(c, SV_K_MEDIAN, c->stream, sv::launch_median_f32(c->fin.as<float>(), H, W, c->fa.as<float>(), c->stream));
+    Out o[] = {{out, c->fa.p, n}};
+    return collect(c, o, 1);
+}
+
+static int post_common(sv_ctx* c, const float* disparity, int n, const sv::PostParams& tmpl, float* a,
+                       uint8_t* u8, float* b) {
+    if (!disparity || n <= 0) return fail(SV_EINVAL, "bad post arguments");
+    const size_t nb = (size_t)n * sizeof(float);
+    SV_HIP(c->hin.ensure(nb));
+    SV_HIP(c->fin.ensure(nb));
+    SV_HIP(c->fa.ensure(nb));
+    SV_HIP(c->fb.ensure(nb));
+    SV_HIP(c->u8.ensure((size_t)n));
+    std::memcpy(c->hin.p, disparity, nb);
+    SV_HIP(hipMemcpyAsync(c->fin.p, c->hin.p, nb, hipMemcpyHostToDevice, c->stream));
+    sv::PostParams pp = tmpl;
+    pp.out_a = c->fa.as<float>();
+    pp.out_u8 = c->u8.as<uint8_t>();
+    pp.out_b = c->fb.as<float>();
+    SV_LAUNCH(c, SV_K_POST, c->stream, sv::launch_post(c->fin.as<float>(), n, pp, c->stream));
+    Out o[] = {{a, c->fa.p, nb}, {u8, c->u8.p, (size_t)n}, {b, c->fb.p, nb}};
+    return collect(c, o, 3);
+}
+
+int sv_depth_post(sv_ctx* c, const float* disparity, int n, float min_depth, float max_depth, float depth_range,
+                  float min_disp_global, float* depth_final, uint8_t* depth_normalized) {
+    SV_ENTER(c);
+    if (!depth_final || !depth_normalized) return fail(SV_EINVAL, "null outputs");
+    sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, 0, 0,
+                                  nullptr, nullptr, nullptr);
+    return post_common(c, disparity, n, pp, depth_final, depth_normalized, nullptr);
+}
+
+int sv_scaled_post(sv_ctx* c, const float* disparity, int n, int min_disp, int num_disp,
+                   float* disparity_normalized, uint8_t* normalized_u8, float* confidence) {
+    SV_ENTER(c);
+    if (!disparity_normalized || !normalized_u8 || !confidence || num_disp <= 0)
+        return fail(SV_EINVAL, "bad scaled post arguments");
+    sv::PostParams pp = make_post(SV_POST_SCALED, 0.f, 0.f, 0.f, 0.f, min_disp, num_disp, nullptr, nullptr,
+                                  nullptr);
+    return post_common(c, disparity, n, pp, disparity_normalized, normalized_u8, confidence);
+}
+
+int sv_depth_map(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels, int stride,
+                 int min_disp, int num_disp, int win, int cost, float min_depth, float max_depth,
+                 float depth_range, float min_disp_global, float* depth_final, float* disparity,
+                 uint8_t* depth_normalized) {
+    SV_ENTER(c);
+    if (!depth_final || !disparity || !depth_normalized) return fail(SV_EINVAL, "null outputs");
+    sv::MatchPlan plan;
+    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    rc = stage_pair(c, left, right, H, W, channels, stride);
+    if (rc) return rc;
+    const size_t n = (size_t)H * W;
+    SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
+    SV_HIP(c->fa.ensure(n * sizeof(float)));
+    SV_HIP(c->fb.ensure(n * sizeof(float)));
+    SV_HIP(c->u8.ensure(n));
+    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
+                           win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
+    if (rc) return rc;
+    sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                                  num_disp, c->fb.as<float>(), c->u8.as<uint8_t>(), nullptr);
+    SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
+              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fa.as<float>(), pp, c->stream));
+    Out o[] = {{depth_final, c->fb.p, n * sizeof(float)},
+               {disparity, c->fa.p, n * sizeof(float)},
+               {depth_normalized, c->u8.p, n}};
+    return collect(c, o, 3);
+}
+
+int sv_stereo_scaled(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels,
+                     int stride, int min_disp, int num_disp, int win, int cost, float* disparity_normalized,
+                     float* disparity, uint8_t* normalized_u8, float* confidence) {
+    SV_ENTER(c);
+    if (!disparity_normalized || !disparity || !normalized_u8 || !confidence)
+        return fail(SV_EINVAL, "null outputs");
+    sv::MatchPlan plan;
+    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    rc = stage_pair(c, left, right, H, W, channels, stride);
+    if (rc) return rc;
+    const size_t n = (size_t)H * W;
+    SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
+    SV_HIP(c->fa.ensure(n * sizeof(float)));
+    SV_HIP(c->fb.ensure(n * sizeof(float)));
+    SV_HIP(c->fc.ensure(n * sizeof(float)));
+    SV_HIP(c->u8.ensure(n));
+    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
+                           win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
+    if (rc) return rc;
+    sv::PostParams pp = make_post(SV_POST_SCALED, 0.f, 0.f, 0.f, 0.f, min_disp, num_disp, c->fb.as<float>(),
+                                  c->u8.as<uint8_t>(), c->fc.as<float>());
+    SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
+              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fa.as<float>(), pp, c->stream));
+    Out o[] = {{disparity_normalized, c->fb.p, n * sizeof(float)},
+               {disparity, c->fa.p, n * sizeof(float)},
+               {normalized_u8, c->u8.p, n},
+               {confidence, c->fc.p, n * sizeof(float)}};
+    return collect(c, o, 4);
+}
+
+int sv_harris(sv_ctx* c, const uint8_t* gray, int H, int W, int stride, float* out) {
+    SV_ENTER(c);
+    if (check_image(gray, H, W) || !out || stride < W) return fail(SV_EINVAL, "bad harris arguments");
+    const size_t n = (size_t)H * W;
+    SV_HIP(c->hin.ensure(n));
+    for (int y = 0; y < H; ++y) std::memcpy(c->hin.as<uint8_t>() + (size_t)y * W, gray + (size_t)y * stride, W);
+    SV_HIP(c->gray[0].ensure(n));
+    SV_HIP(c->harris.ensure(n * sizeof(float)));
+    SV_HIP(hipMemcpyAsync(c->gray[0].p, c->hin.p, n, hipMemcpyHostToDevice, c->stream));
+    SV_LAUNCH(c, SV_K_HARRIS, c->stream,
+              sv::launch_harris(c->gray[0].as<uint8_t>(), H, W, W, c->harris.as<float>(), c->stream));
+    Out o[] = {{out, c->harris.p, n * sizeof(float)}};
+    return collect(c, o, 1);
+}
+
+int sv_hog_hist(sv_ctx* c, const uint8_t* gray, int H, int W, int stride, int win, uint16_t* out) {
+    SV_ENTER(c);
+    if (check_image(gray, H, W) || !out || stride < W) return fail(SV_EINVAL, "bad hog arguments");
+    if (win < 1 || win > 15 || (win & 1) == 0) return fail(SV_EINVAL, "win must be odd in [1, 15]");
+    const size_t n = (size_t)H * W;
+    SV_HIP(c->hin.ensure(n));
+    for (int y = 0; y < H; ++y) std::memcpy(c->hin.as<uint8_t>() + (size_t)y * W, gray + (size_t)y * stride, W);
+    SV_HIP(c->gray[0].ensure(n));
+    SV_HIP(c->hog[0].ensure(n * 10 * sizeof(uint16_t)));
+    SV_HIP(hipMemcpyAsync(c->gray[0].p, c->hin.p, n, hipMemcpyHostToDevice, c->stream));
+    SV_LAUNCH(c, SV_K_HOG, c->stream,
+              sv::launch_hog_hist(c->gray[0].as<uint8_t>(), H, W, W, win, 0, H, c->hog[0].as<uint16_t>(), c->stream));
+    Out o[] = {{out, c->hog[0].p, n * 10 * sizeof(uint16_t)}};
+    return collect(c, o, 1);
+}
+
+// ---------------------------------------------------------------- profiling
+int sv_profile_enable(sv_ctx* c, int on) {
+    SV_ENTER(c);
+    c->prof = on != 0;
+    return 0;
+}
+
+int sv_profile_read(sv_ctx* c, int kernel, double* total_ms, long long* count) {
+    SV_ENTER(c);
+    if (kernel < 0 || kernel >= SV_NKERNELS) return fail(SV_EINVAL, "kernel id out of range");
+    c->prof_drain();
+    if (total_ms) *total_ms = c->acc_ms[kernel];
+    if (count) *count = c->cnt[kernel];
+    return 0;
+}
+
+int sv_profile_reset(sv_ctx* c) {
+    SV_ENTER(c);
+    c->prof_drain();
+    for (int k = 0; k < SV_NKERNELS; ++k) {
+        c->acc_ms[k] = 0.0;
+        c->cnt[k] = 0;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,317 @@
+// sv_image.hip — the stencil kernels around the disparity engine (gfx950).
+//
+//  * k_gray        cv2.cvtColor(BGR2GRAY), 14-bit fixed point   (depth_map.py:871-880)
+//  * k_harris      Harris response, cornerHarris(3, 3, 0.04) convention (north_star)
+//  * k_hog_hist    per-pixel 9-bin gradient orientation + window histograms (north_star)
+//  * k_median_i16  medianBlur(disparity, 5) on the int16 x16 map, fused with the
+//                  reference's post-processing (depth_map.py:909-937 or
+//                  fused_depth_map.py:1004-1029) so the filtered map never round-trips HBM
+//  * k_median_f32  medianBlur(f32, 5) for arbitrary float input (the public sv_median5_f32)
+//  * k_post        the post-processing alone on an f32 disparity
+// All are HBM-bound stencils: LDS tiles with halos, one read and one write per pixel.
+// Built with -ffp-contract=off so every f32 operation rounds exactly like NumPy's.
+#include "sv_internal.h"
+#include "sv_median_net.h"
+
+namespace sv {
+namespace {
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
+__device__ __forceinline__ int refl101(int i, int n) {
+    if (n == 1) return 0;
+    i = i < 0 ? -i : i;
+    return i >= n ? 2 * (n - 1) - i : i;
+}
+
+// ---------------------------------------------------------------------------------------
+__global__ void k_gray(const uint8_t* __restrict__ bgr, int H, int W, int pitch,
+                       uint8_t* __restrict__ gray) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    const uint8_t* p = bgr + (size_t)y * pitch + 3 * x;
+    const int v = p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13);
+    gray[(size_t)y * W + x] = (uint8_t)(v >> 14);
+}
+
+__device__ __forceinline__ void sobel(const uint8_t* g, int H, int W, int pitch, int x, int y,
+                                      int& gx, int& gy) {
+    const int xm = refl101(x - 1, W), xp = refl101(x + 1, W);
+    const uint8_t* rm = g + (size_t)refl101(y - 1, H) * pitch;
+    const uint8_t* r0 = g + (size_t)y * pitch;
+    const uint8_t* rp = g + (size_t)refl101(y + 1, H) * pitch;
+    gx = (rm[xp] + 2 * r0[xp] + rp[xp]) - (rm[xm] + 2 * r0[xm] + rp[xm]);
+    gy = (rp[xm] + 2 * rp[x] + rp[xp]) - (rm[xm] + 2 * rm[x] + rm[xp]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Harris: 16x16 output tile; gradient products for the 18x18 reflected neighbourhood.
+constexpr int HT = 16;
+__global__ __launch_bounds__(256) void k_harris(const uint8_t* __restrict__ g, int H, int W,
+                                                int pitch, float* __restrict__ out) {
+    __shared__ int pxx[HT + 2][HT + 2], pxy[HT + 2][HT + 2], pyy[HT + 2][HT + 2];
+    const int x0 = blockIdx.x * HT, y0 = blockIdx.y * HT;
+    for (int i = threadIdx.x; i < (HT + 2) * (HT + 2); i += 256) {
+        const int ty = i / (HT + 2), tx = i % (HT + 2);
+        const int yy = refl101(clampi(y0 - 1 + ty, -1, H), H);
+        const int xx = refl101(clampi(x0 - 1 + tx, -1, W), W);
+        int gx, gy;
+        sobel(g, H, W, pitch, xx, yy, gx, gy);
+        pxx[ty][tx] = gx * gx;
+        pxy[ty][tx] = gx * gy;
+        pyy[ty][tx] = gy * gy;
+    }
+    __syncthreads();
+    const int tx = threadIdx.x % HT, ty = threadIdx.x / HT;
+    const int x = x0 + tx, y = y0 + ty;
+    if (x >= W || y >= H) return;
+    // box over the reflected neighbours: position (x+i) maps to tile column of refl(x+i)
+    int sxx = 0, sxy = 0, syy = 0;
+    for (int j = -1; j <= 1; ++j)
+        for (int i = -1; i <= 1; ++i) {
+            const int ry = refl101(y + j, H) - (y0 - 1);
+            const int rx = refl101(x + i, W) - (x0 - 1);
+            sxx += pxx[ry][rx];
+            sxy += pxy[ry][rx];
+            syy += pyy[ry][rx];
+        }
+    const float s2 = (float)((1.0 / (4.0 * 3.0 * 255.0)) * (1.0 / (4.0 * 3.0 * 255.0)));
+    const float a = (float)sxx * s2, b = (float)sxy * s2, c = (float)syy * s2;
+    const float t1 = a * c, t2 = b * b, t3 = a + c, t4 = t3 * t3;
+    const float rr = t1 - t2;
+    const float kt = 0.04f * t4;
+    out[(size_t)y * W + x] = rr - kt;
+}
+
+// ---------------------------------------------------------------------------------------
+// HOG window histograms: 64x16 output tile, window radius r <= 7.
+constexpr int GT_W = 64, GT_H = 16, GR_MAX = 7;
+constexpr int GX_MAX = GT_W + 2 * GR_MAX, GY_MAX = GT_H + 2 * GR_MAX;
+__constant__ int c_hog_cos[8] = {15396, 12551, 8192, 2845, -2845, -8192, -12551, -15396};
+__constant__ int c_hog_sin[8] = {5604, 10531, 14189, 16135, 16135, 14189, 10531, 5604};
+
+__global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g, int H, int W,
+                                                  int pitch, int r, int row0, int row1,
+                                                  uint16_t* __restrict__ hist) {
+    __shared__ uint8_t sbin[GY_MAX][GX_MAX];
+    __shared__ uint8_t smag[GY_MAX][GX_MAX];
+    __shared__ uint16_t vsum[GT_H][GX_MAX][9];
+    __shared__ __attribute__((aligned(16))) uint16_t otile[GT_H][GT_W][10];
+    const int x0 = blockIdx.x * GT_W, y0 = row0 + blockIdx.y * GT_H;
+    const int nx = GT_W + 2 * r, ny = GT_H + 2 * r;
+    for (int i = threadIdx.x; i < nx * ny; i += 256) {
+        const int ty = i / nx, tx = i % nx;
+        const int yy = clampi(y0 - r + ty, 0, H - 1);
+        const int xx = clampi(x0 - r + tx, 0, W - 1);
+        int gx, gy;
+        sobel(g, H, W, pitch, xx, yy, gx, gy);
+        const int m = (abs(gx) + abs(gy)) >> 3;
+        if (gy < 0 || (gy == 0 && gx < 0)) { gx = -gx; gy = -gy; }
+        int b = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b += (c_hog_cos[k] * gy - c_hog_sin[k] * gx >= 0);
+        sbin[ty][tx] = (uint8_t)b;
+        smag[ty][tx] = (uint8_t)m;
+    }
+    __syncthreads();
+    // vertical window sums: task = (column, bin)
+    for (int task = threadIdx.x; task < nx * 9; task += 256) {
+        const int tx = task / 9, b = task % 9;
+        uint32_t s = 0;
+        for (int j = 0; j < 2 * r + 1; ++j) s += sbin[j][tx] == b ? smag[j][tx] : 0u;
+        vsum[0][tx][b] = (uint16_t)s;
+        for (int oy = 1; oy < GT_H; ++oy) {
+            const int ja = oy + 2 * r, jd = oy - 1;
+            s += (sbin[ja][tx] == b ? smag[ja][tx] : 0u);
+            s -= (sbin[jd][tx] == b ? smag[jd][tx] : 0u);
+            vsum[oy][tx][b] = (uint16_t)s;
+        }
+    }
+    __syncthreads();
+    // horizontal window sums: task = (row, bin)
+    for (int task = threadIdx.x; task < GT_H * 10; task += 256) {
+        const int oy = task / 10, b = task % 10;
+        if (b == 9) {
+            for (int ox = 0; ox < GT_W; ++ox) otile[oy][ox][9] = 0;
+            continue;
+        }
+        uint32_t s = 0;
+        for (int i = 0; i < 2 * r + 1; ++i) s += vsum[oy][i][b];
+        otile[oy][0][b] = (uint16_t)s;
+        for (int ox = 1; ox < GT_W; ++ox) {
+            s += vsum[oy][ox + 2 * r][b];
+            s -= vsum[oy][ox - 1][b];
+            otile[oy][ox][b] = (uint16_t)s;
+        }
+    }
+    __syncthreads();
+    // coalesced copy-out: each tile row is 64 px * 20 B = 320 dwords, contiguous in HBM
+    const int wv = min(GT_W, W - x0);
+    for (int i = threadIdx.x; i < GT_H * GT_W * 5; i += 256) {
+        const int oy = i / (GT_W * 5), rem = i % (GT_W * 5);
+        const int y = y0 + oy;
+        if (y >= row1 || rem >= wv * 5) continue;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&otile[oy][0][0]);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(hist + ((size_t)y * W + x0) * 10);
+        dst[rem] = src[rem];
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Post-processing of one f32 disparity value (shared by the median kernels and k_post).
+__device__ __forceinline__ void post_one(const PostParams& pp, size_t i, float d) {
+    if (pp.mode == POST_DEPTH) {
+        // depth_map.py:925-936 — NumPy-2 keeps float32 throughout
+        const float fxb = (float)(700 * 0.08);
+        const float den = d + (float)1e-6;
+        const float depth = fxb / den;
+        float dc = depth < pp.minf ? pp.minf : depth;
+        dc = dc > pp.maxf ? pp.maxf : dc;
+        const bool valid = (d > pp.min_disp_global) && (dc >= pp.minf) && (dc <= pp.maxf);
+        pp.out_a[i] = valid ? dc : 0.0f;
+        float t = dc - pp.minf;
+        t = t / pp.rangef;
+        t = t * 255.0f;
+        pp.out_u8[i] = (uint8_t)(int)t;
+    } else if (pp.mode == POST_SCALED) {
+        // fused_depth_map.py:1010-1024
+        const float lo = (float)pp.min_disp, hi = (float)(pp.min_disp + pp.num_disp - 1);
+        float c = d < lo ? lo : d;
+        c = c > hi ? hi : c;
+        float t = c - lo;
+        t = t / (float)pp.num_disp;
+        t = t * 255.0f;
+        const uint8_t u = (uint8_t)(int)t;
+        pp.out_u8[i] = u;
+        pp.out_a[i] = (float)u;
+        pp.out_b[i] = (d > (float)(pp.min_disp + 1) && d < hi) ? 1.0f : 0.0f;
+    }
+}
+
+// Median-of-25 on packed pairs: lane value = (row y, row y+1) of one column.
+typedef short s2 __attribute__((ext_vector_type(2)));
+constexpr int MT_W = 64, MT_H = 8;   // 64 x 8 outputs; thread = one column x two rows
+
+__global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ in, int H, int W,
+                                                    int row0, int row1, float* __restrict__ disp,
+                                                    PostParams pp) {
+    __shared__ int16_t tile[MT_H + 4][MT_W + 4];
+    const int x0 = blockIdx.x * MT_W, y0 = row0 + blockIdx.y * MT_H;
+    for (int i = threadIdx.x; i < (MT_H + 4) * (MT_W + 4); i += 256) {
+        const int ty = i / (MT_W + 4), tx = i % (MT_W + 4);
+        tile[ty][tx] = in[(size_t)clampi(y0 - 2 + ty, 0, H - 1) * W + clampi(x0 - 2 + tx, 0, W - 1)];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x % MT_W, pr = threadIdx.x / MT_W;   // pr in 0..3 -> rows 2pr, 2pr+1
+    s2 v[25];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            s2 p;
+            p.x = tile[2 * pr + j][tx + i];
+            p.y = tile[2 * pr + 1 + j][tx + i];
+            v[j * 5 + i] = p;
+        }
+#pragma unroll
+    for (int c = 0; c < SV_MED25_NCMP; ++c) {
+        const int a = SV_MED25_NET[c][0], b = SV_MED25_NET[c][1], use = SV_MED25_NET[c][2];
+        const s2 lo = __builtin_elementwise_min(v[a], v[b]);
+        const s2 hi = __builtin_elementwise_max(v[a], v[b]);
+        if (use & 1) v[a] = lo;
+        if (use & 2) v[b] = hi;
+    }
+    const s2 m = v[SV_MED25_OUT];
+    const int x = x0 + tx;
+    if (x >= W) return;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int y = y0 + 2 * pr + h;
+        if (y >= row1) continue;
+        const float d = (float)(h == 0 ? m.x : m.y) / 16.0f;
+        const size_t i = (size_t)y * W + x;
+        disp[i] = d;
+        post_one(pp, i, d);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_median_f32(const float* __restrict__ in, int H, int W,
+                                                    float* __restrict__ out) {
+    __shared__ float tile[MT_H + 4][MT_W + 4];
+    const int x0 = blockIdx.x * MT_W, y0 = blockIdx.y * MT_H;
+    for (int i = threadIdx.x; i < (MT_H + 4) * (MT_W + 4); i += 256) {
+        const int ty = i / (MT_W + 4), tx = i % (MT_W + 4);
+        tile[ty][tx] = in[(size_t)clampi(y0 - 2 + ty, 0, H - 1) * W + clampi(x0 - 2 + tx, 0, W - 1)];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x % MT_W, pr = threadIdx.x / MT_W;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        float v[25];
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+#pragma unroll
+            for (int i = 0; i < 5; ++i) v[j * 5 + i] = tile[2 * pr + h + j][tx + i];
+#pragma unroll
+        for (int c = 0; c < SV_MED25_NCMP; ++c) {
+            const int a = SV_MED25_NET[c][0], b = SV_MED25_NET[c][1], use = SV_MED25_NET[c][2];
+            const float lo = fminf(v[a], v[b]), hi = fmaxf(v[a], v[b]);
+            if (use & 1) v[a] = lo;
+            if (use & 2) v[b] = hi;
+        }
+        const int x = x0 + tx, y = y0 + 2 * pr + h;
+        if (x < W && y < H) out[(size_t)y * W + x] = v[SV_MED25_OUT];
+    }
+}
+
+__global__ void k_post(const float* __restrict__ disp, int n, PostParams pp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) post_one(pp, (size_t)i, disp[i]);
+}
+
+}  // namespace
+
+int launch_gray(const uint8_t* bgr, int H, int W, int pitch, uint8_t* gray, hipStream_t s) {
+    hipLaunchKernelGGL(k_gray, dim3((W + 255) / 256, H), dim3(256), 0, s, bgr, H, W, pitch, gray);
+    return (int)hipGetLastError();
+}
+
+int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_harris, dim3((W + HT - 1) / HT, (H + HT - 1) / HT), dim3(256), 0, s, g, H,
+                       W, pitch, out);
+    return (int)hipGetLastError();
+}
+
+int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0, int row1,
+                    uint16_t* hist, hipStream_t s) {
+    const int r = win / 2;
+    if (r > GR_MAX) return (int)hipErrorInvalidValue;
+    if (row0 < 0) row0 = 0;
+    if (row1 > H) row1 = H;
+    if (row1 <= row0) return 0;
+    hipLaunchKernelGGL(k_hog_hist, dim3((W + GT_W - 1) / GT_W, (row1 - row0 + GT_H - 1) / GT_H),
+                       dim3(256), 0, s, g, H, W, pitch, r, row0, row1, hist);
+    return (int)hipGetLastError();
+}
+
+int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float* disp,
+                      const PostParams& pp, hipStream_t s) {
+    if (row1 <= row0) return 0;
+    hipLaunchKernelGGL(k_median_i16, dim3((W + MT_W - 1) / MT_W, (row1 - row0 + MT_H - 1) / MT_H),
+                       dim3(256), 0, s, in, H, W, row0, row1, disp, pp);
+    return (int)hipGetLastError();
+}
+
+int launch_median_f32(const float* in, int H, int W, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_median_f32, dim3((W + MT_W - 1) / MT_W, (H + MT_H - 1) / MT_H), dim3(256),
+                       0, s, in, H, W, out);
+    return (int)hipGetLastError();
+}
+
+int launch_post(const float* disp, int n, const PostParams& pp, hipStream_t s) {
+    if (n <= 0 || pp.mode == POST_NONE) return 0;
+    hipLaunchKernelGGL(k_post, dim3((n + 255) / 256), dim3(256), 0, s, disp, n, pp);
+    return (int)hipGetLastError();
+}
+
+}  // namespace sv

@@ -1,0 +1,63 @@
+// Internal declarations shared by the HIP kernel files and the C-ABI (sv_capi.cpp).
+// gfx950 (CDNA4, wave64) only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sv {
+
+enum Cost { COST_SAD = 0, COST_SSD = 1, COST_HOG = 2 };
+
+// Disparity lanes: each wave is split into groups of LPG lanes (16/32/64); every lane of a
+// group owns DPL consecutive disparities of the same output pixel, so one group covers
+// LPG*DPL candidates and the per-pixel argmin is an in-lane min3 chain plus a
+// log2(LPG)-step DPP reduction.
+struct MatchPlan {
+    int dpl;     // disparities per lane: 4, 6 or 8
+    int lpg;     // lanes per group: 16, 32 or 64
+    int ndw;     // dwords per column pack: ceil(win/4) (SAD/SSD), 5 for HOG
+    int dbits;   // argmin key index bits
+};
+
+struct MatchParams {
+    const uint8_t* L;      // left gray (device), row pitch `pitch` bytes
+    const uint8_t* R;      // right gray
+    const uint16_t* HL;    // HOG window histograms [H][W][10] (cost == HOG)
+    const uint16_t* HR;
+    int H, W, pitch;
+    int minD, D, r;        // r = win/2 (0 for HOG: the window lives in the histograms)
+    int win;
+    int X0, X1;            // matched column band [X0, X1)
+    int row0, row1;        // output rows [row0, row1)
+    int lpg, lpg_log2, dbits;
+    int16_t* out;
+    int opitch;            // elements
+};
+
+// Host-side launchers (return hipError_t as int).
+int plan_match(int num_disp, int win, int cost, MatchPlan* plan);
+size_t match_lds_bytes(const MatchPlan& p, int r, int cost);
+int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t s);
+int launch_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v, hipStream_t s);
+
+int launch_gray(const uint8_t* bgr, int H, int W, int pitch, uint8_t* gray, hipStream_t s);
+int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStream_t s);
+int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0, int row1,
+                    uint16_t* hist, hipStream_t s);
+
+// Post-processing modes for the median kernel.
+enum PostMode { POST_NONE = 0, POST_DEPTH = 1, POST_SCALED = 2 };
+struct PostParams {
+    int mode;
+    float minf, maxf, rangef, min_disp_global;   // POST_DEPTH (depth_map.py:915-937)
+    int min_disp, num_disp;                       // POST_SCALED (fused_depth_map.py:1010-1029)
+    float* out_a;      // DEPTH: depth_final        SCALED: disparity_normalized (f32)
+    uint8_t* out_u8;   // DEPTH: depth_normalized   SCALED: disparity_normalized (u8)
+    float* out_b;      // SCALED: confidence
+};
+int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float* disp,
+                      const PostParams& pp, hipStream_t s);
+int launch_median_f32(const float* in, int H, int W, float* out, hipStream_t s);
+int launch_post(const float* disp, int n, const PostParams& pp, hipStream_t s);
+
+}  // namespace sv

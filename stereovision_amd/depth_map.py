@@ -1,0 +1,72 @@
+"""Drop-in for the reference's ``depth_map.py`` disparity path.
+
+``create_depth_map(left_img, right_img, stereo_calib=None, min_depth=0.3, max_depth=2.0)``
+keeps the reference's name, arguments, module globals and return tuple
+(depth_map.py:837-946):
+
+    returns (depth_final float32 HxW, disparity float32 HxW, depth_colormap uint8 HxWx3)
+
+and its never-raise convention for per-frame failures (print, then zero arrays,
+depth_map.py:941-946).  The numeric body — BGR->gray, the disparity engine (which
+replaces cv2.StereoSGBM), medianBlur(5), depth = 56/(d+1e-6), clip, mask and
+u8 normalisation — runs in one pass of the gfx950 kernels (include/stereovision_amd.h,
+``sv_depth_map``).  A missing HIP library or GPU is NOT a per-frame failure: it raises
+:class:`stereovision_amd.engine.EngineUnavailable` before any compute (no CPU fallback).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import colormap
+from .engine import get_engine
+from .preamble import ensure_same_size as _ensure_same_size
+from .preamble import to_engine_image
+
+# Matching parameters — module globals read at call time, as in depth_map.py:31-33.
+MIN_DISP = 16 * 0
+NUM_DISP = 16 * 20
+WINDOW_SIZE = 7
+# Cost function of the north_star engine that replaces StereoSGBM: "sad" | "ssd" | "hog".
+COST = "sad"
+
+
+def ensure_same_size(left_img, right_img):
+    """depth_map.py:39-71."""
+    return _ensure_same_size(left_img, right_img, verbose=True)
+
+
+def _gray_pair(engine, left_img, right_img):
+    gl = to_engine_image(left_img)
+    gr = to_engine_image(right_img)
+    if gl.ndim != gr.ndim:   # one BGR, one gray: convert the BGR one on the GPU
+        gl = engine.gray(gl) if gl.ndim == 3 else gl
+        gr = engine.gray(gr) if gr.ndim == 3 else gr
+    return gl, gr
+
+
+def create_depth_map(left_img, right_img, stereo_calib=None, min_depth=0.3, max_depth=2.0):
+    """depth_map.py:837-946 on the MI355X engine.
+
+    ``stereo_calib`` is accepted for signature compatibility; as in the reference it does
+    not change the result (its 'calibration_data' key is never produced, so fx = 700,
+    depth_map.py:915-920).
+    """
+    left_img, right_img = ensure_same_size(left_img, right_img)
+    engine = get_engine()          # raises loudly when the HIP path is unavailable
+    h, w = np.asarray(left_img).shape[:2]
+    try:
+        gl, gr = _gray_pair(engine, left_img, right_img)
+        if gl.shape[:2] != gr.shape[:2]:
+            print(f"ERROR: shapes differ after conversion: {gl.shape} vs {gr.shape}")
+            gl, gr = _ensure_same_size(gl, gr)
+            h, w = gl.shape[:2]
+        depth_final, disparity, depth_normalized = engine.depth_map(
+            gl, gr, MIN_DISP, NUM_DISP, WINDOW_SIZE, float(min_depth), float(max_depth),
+            min_disp_global=MIN_DISP, cost=COST)
+        depth_colormap = colormap.apply(depth_normalized, "turbo")
+        return depth_final, disparity, depth_colormap
+    except Exception as e:  # the reference's per-frame error convention (:941-946)
+        print(f"Error creating depth map: {e}")
+        empty_uint8 = np.zeros((h, w), dtype=np.uint8)
+        empty_colormap = colormap.apply(empty_uint8, "turbo")
+        return np.zeros((h, w), dtype=np.float32), np.zeros((h, w), dtype=np.float32), empty_colormap

@@ -1,0 +1,390 @@
+"""ctypes binding of libsvhip.so (include/stereovision_amd.h).
+
+The product path: NumPy arrays in, NumPy arrays out, all arithmetic in the gfx950 HIP
+kernels.  There is no CPU fallback — if the library or a GPU is missing,
+:func:`get_engine` raises :class:`EngineUnavailable` loudly.
+
+ctypes releases the GIL for the duration of every foreign call, so an Engine can be
+driven from the reference's ThreadPoolExecutor workers (fused_depth_map.py:2591-2598)
+while the main thread keeps working.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SV_LIB_PATH", os.path.join(_HERE, "lib", "libsvhip.so"))
+
+COSTS = {"sad": 0, "ssd": 1, "hog": 2}
+POST_NONE, POST_DEPTH, POST_SCALED = 0, 1, 2
+KERNELS = {"gray": 0, "harris": 1, "hog": 2, "match": 3, "median": 4, "post": 5}
+
+# Every symbol include/stereovision_amd.h declares (checked by tests/test_capi.py).
+EXPORTED = [
+    "sv_version", "sv_last_error", "sv_device_count", "sv_create", "sv_destroy",
+    "sv_synchronize", "sv_stream", "sv_plan", "sv_gray", "sv_disparity", "sv_median5_f32",
+    "sv_depth_post", "sv_scaled_post", "sv_depth_map", "sv_stereo_scaled", "sv_harris",
+    "sv_hog_hist", "sv_gray_dev", "sv_disparity_dev", "sv_median_post_dev",
+    "sv_depth_map_dev", "sv_harris_dev", "sv_hog_hist_dev", "sv_profile_enable",
+    "sv_profile_read", "sv_profile_reset",
+]
+
+
+class SVError(RuntimeError):
+    """A libsvhip call returned a nonzero status."""
+
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} failed ({code}): {msg}")
+        self.code = code
+
+
+class EngineUnavailable(SVError):
+    """libsvhip.so is missing or no HIP device is visible: the HIP path cannot run."""
+
+    def __init__(self, msg: str):
+        RuntimeError.__init__(self, msg)
+        self.code = -19
+
+
+_c_int = ctypes.c_int
+_c_float = ctypes.c_float
+_vp = ctypes.c_void_p
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+_i16p = np.ctypeslib.ndpointer(np.int16, flags="C_CONTIGUOUS")
+_u16p = np.ctypeslib.ndpointer(np.uint16, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+
+
+class _NullableF32:
+    """ndpointer that also accepts None (for optional outputs)."""
+
+    @classmethod
+    def from_param(cls, obj):
+        if obj is None:
+            return None
+        return _f32p.from_param(obj)
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def _declare(lib):
+    sig = {
+        "sv_version": ([], _c_int),
+        "sv_last_error": ([], ctypes.c_char_p),
+        "sv_device_count": ([ctypes.POINTER(_c_int)], _c_int),
+        "sv_create": ([_c_int, ctypes.POINTER(_vp)], _c_int),
+        "sv_destroy": ([_vp], None),
+        "sv_synchronize": ([_vp], _c_int),
+        "sv_stream": ([_vp], _vp),
+        "sv_plan": ([_c_int, _c_int, _c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),
+                     ctypes.POINTER(_c_int)], _c_int),
+        "sv_gray": ([_vp, _u8p, _c_int, _c_int, _c_int, _u8p], _c_int),
+        "sv_disparity": ([_vp, _u8p, _u8p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                          _c_int, _c_int, _i16p, _NullableF32], _c_int),
+        "sv_median5_f32": ([_vp, _f32p, _c_int, _c_int, _f32p], _c_int),
+        "sv_depth_post": ([_vp, _f32p, _c_int, _c_float, _c_float, _c_float, _c_float, _f32p,
+                           _u8p], _c_int),
+        "sv_scaled_post": ([_vp, _f32p, _c_int, _c_int, _c_int, _f32p, _u8p, _f32p], _c_int),
+        "sv_depth_map": ([_vp, _u8p, _u8p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                          _c_int, _c_int, _c_float, _c_float, _c_float, _c_float, _f32p, _f32p,
+                          _u8p], _c_int),
+        "sv_stereo_scaled": ([_vp, _u8p, _u8p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                              _c_int, _c_int, _f32p, _f32p, _u8p, _f32p], _c_int),
+        "sv_harris": ([_vp, _u8p, _c_int, _c_int, _c_int, _f32p], _c_int),
+        "sv_hog_hist": ([_vp, _u8p, _c_int, _c_int, _c_int, _c_int, _u16p], _c_int),
+        "sv_gray_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp], _c_int),
+        "sv_disparity_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                              _c_int, _c_int, _c_int, _vp, _c_int, _vp], _c_int),
+        "sv_median_post_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                _c_float, _c_float, _c_float, _c_int, _c_int, _vp, _vp, _vp,
+                                _vp, _vp], _c_int),
+        "sv_depth_map_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                              _c_int, _c_float, _c_float, _c_float, _c_float, _vp, _vp, _vp,
+                              _vp], _c_int),
+        "sv_harris_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp], _c_int),
+        "sv_hog_hist_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
+                            _c_int),
+        "sv_profile_enable": ([_vp, _c_int], _c_int),
+        "sv_profile_read": ([_vp, _c_int, ctypes.POINTER(ctypes.c_double),
+                             ctypes.POINTER(ctypes.c_longlong)], _c_int),
+        "sv_profile_reset": ([_vp], _c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load libsvhip.so (raises EngineUnavailable when it is not built)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise EngineUnavailable(
+                f"libsvhip.so not found at {p}: build it with `python -c 'import "
+                f"__graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+        lib = ctypes.CDLL(p)
+        _declare(lib)
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def last_error() -> str:
+    return load_library().sv_last_error().decode(errors="replace")
+
+
+def _check(fn: str, rc: int):
+    if rc != 0:
+        raise SVError(fn, rc, last_error())
+
+
+def device_count() -> int:
+    n = _c_int(0)
+    rc = load_library().sv_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def plan(num_disp: int, win: int, cost: str | int = "sad") -> dict:
+    dpl, lpg, lds = _c_int(), _c_int(), _c_int()
+    _check("sv_plan", load_library().sv_plan(num_disp, win, _cost(cost), ctypes.byref(dpl),
+                                              ctypes.byref(lpg), ctypes.byref(lds)))
+    return {"dpl": dpl.value, "lpg": lpg.value, "lds_bytes": lds.value}
+
+
+def _cost(cost) -> int:
+    if isinstance(cost, str):
+        try:
+            return COSTS[cost.lower()]
+        except KeyError:
+            raise ValueError(f"unknown cost {cost!r}; expected one of {sorted(COSTS)}") from None
+    return int(cost)
+
+
+def _image(a: np.ndarray) -> tuple[np.ndarray, int, int, int]:
+    a = np.ascontiguousarray(a)
+    if a.dtype != np.uint8:
+        raise TypeError(f"expected uint8 image, got {a.dtype}")
+    if a.ndim == 2:
+        return a, a.shape[0], a.shape[1], 1
+    if a.ndim == 3 and a.shape[2] == 3:
+        return a, a.shape[0], a.shape[1], 3
+    raise ValueError(f"expected HxW or HxWx3 image, got shape {a.shape}")
+
+
+class Engine:
+    """One libsvhip context (device + stream + cached buffers)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        n = device_count()
+        if n <= 0:
+            raise EngineUnavailable("no HIP device visible: the MI355X path cannot run")
+        h = _vp()
+        rc = self.lib.sv_create(device, ctypes.byref(h))
+        if rc != 0:
+            raise EngineUnavailable(f"sv_create({device}) failed ({rc}): {last_error()}")
+        self._h = h
+        self.device = device
+
+    # -- lifetime -------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.sv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self) -> int:
+        return self.lib.sv_stream(self._h) or 0
+
+    def synchronize(self):
+        _check("sv_synchronize", self.lib.sv_synchronize(self._h))
+
+    # -- host-memory entry points -----------------------------------------------------
+    def gray(self, bgr: np.ndarray) -> np.ndarray:
+        bgr, H, W, C = _image(bgr)
+        if C != 3:
+            raise ValueError("gray() expects an HxWx3 BGR image")
+        out = np.empty((H, W), np.uint8)
+        _check("sv_gray", self.lib.sv_gray(self._h, bgr, H, W, W * 3, out))
+        return out
+
+    def disparity(self, left, right, min_disp: int, num_disp: int, win: int, cost="sad",
+                  harris: bool = False):
+        """int16 x16 disparity (StereoSGBM.compute convention) [+ Harris of the left]."""
+        left, H, W, C = _image(left)
+        right, H2, W2, C2 = _image(right)
+        if (H, W, C) != (H2, W2, C2):
+            raise ValueError("left/right shapes differ")
+        d16 = np.empty((H, W), np.int16)
+        hr = np.empty((H, W), np.float32) if harris else None
+        _check("sv_disparity", self.lib.sv_disparity(self._h, left, right, H, W, C, W * C,
+                                                     int(min_disp), int(num_disp), int(win),
+                                                     _cost(cost), d16, hr))
+        return (d16, hr) if harris else d16
+
+    def median5(self, a: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(a, np.float32)
+        out = np.empty_like(a)
+        _check("sv_median5_f32", self.lib.sv_median5_f32(self._h, a, a.shape[0], a.shape[1], out))
+        return out
+
+    def depth_post(self, disparity, min_depth: float, max_depth: float, min_disp_global=0):
+        d = np.ascontiguousarray(disparity, np.float32)
+        df = np.empty_like(d)
+        nm = np.empty(d.shape, np.uint8)
+        _check("sv_depth_post", self.lib.sv_depth_post(
+            self._h, d, d.size, np.float32(min_depth), np.float32(max_depth),
+            np.float32(float(max_depth) - float(min_depth)), np.float32(min_disp_global), df, nm))
+        return df, nm
+
+    def scaled_post(self, disparity, min_disp: int, num_disp: int):
+        d = np.ascontiguousarray(disparity, np.float32)
+        dn = np.empty_like(d)
+        du = np.empty(d.shape, np.uint8)
+        cf = np.empty_like(d)
+        _check("sv_scaled_post", self.lib.sv_scaled_post(self._h, d, d.size, int(min_disp),
+                                                         int(num_disp), dn, du, cf))
+        return dn, du, cf
+
+    def depth_map(self, left, right, min_disp: int, num_disp: int, win: int, min_depth: float,
+                  max_depth: float, min_disp_global=None, cost="sad"):
+        """Numeric body of depth_map.create_depth_map: (depth_final, disparity, depth_u8)."""
+        left, H, W, C = _image(left)
+        right, H2, W2, C2 = _image(right)
+        if (H, W, C) != (H2, W2, C2):
+            raise ValueError("left/right shapes differ")
+        mdg = min_disp if min_disp_global is None else min_disp_global
+        depth = np.empty((H, W), np.float32)
+        disp = np.empty((H, W), np.float32)
+        norm = np.empty((H, W), np.uint8)
+        _check("sv_depth_map", self.lib.sv_depth_map(
+            self._h, left, right, H, W, C, W * C, int(min_disp), int(num_disp), int(win),
+            _cost(cost), np.float32(min_depth), np.float32(max_depth),
+            np.float32(float(max_depth) - float(min_depth)), np.float32(mdg), depth, disp, norm))
+        return depth, disp, norm
+
+    def stereo_scaled(self, left, right, min_disp: int, num_disp: int, win: int, cost="sad"):
+        """Numeric body of create_depth_map_stereo_scaled:
+        (disparity_normalized f32, disparity f32, normalized u8, confidence f32)."""
+        left, H, W, C = _image(left)
+        right, H2, W2, C2 = _image(right)
+        if (H, W, C) != (H2, W2, C2):
+            raise ValueError("left/right shapes differ")
+        dn = np.empty((H, W), np.float32)
+        disp = np.empty((H, W), np.float32)
+        du = np.empty((H, W), np.uint8)
+        cf = np.empty((H, W), np.float32)
+        _check("sv_stereo_scaled", self.lib.sv_stereo_scaled(
+            self._h, left, right, H, W, C, W * C, int(min_disp), int(num_disp), int(win),
+            _cost(cost), dn, disp, du, cf))
+        return dn, disp, du, cf
+
+    def harris(self, gray: np.ndarray) -> np.ndarray:
+        gray, H, W, C = _image(gray)
+        if C != 1:
+            raise ValueError("harris() expects a gray image")
+        out = np.empty((H, W), np.float32)
+        _check("sv_harris", self.lib.sv_harris(self._h, gray, H, W, W, out))
+        return out
+
+    def hog_hist(self, gray: np.ndarray, win: int) -> np.ndarray:
+        """[9, H, W] uint16 window histograms (the device layout is [H][W][10])."""
+        gray, H, W, C = _image(gray)
+        if C != 1:
+            raise ValueError("hog_hist() expects a gray image")
+        out = np.empty((H, W, 10), np.uint16)
+        _check("sv_hog_hist", self.lib.sv_hog_hist(self._h, gray, H, W, W, int(win), out))
+        return np.ascontiguousarray(out[:, :, :9].transpose(2, 0, 1))
+
+    # -- device-memory entry points (integer device pointers) ---------------------------
+    def gray_dev(self, d_bgr: int, H: int, W: int, pitch: int, d_gray: int, stream: int = 0):
+        _check("sv_gray_dev", self.lib.sv_gray_dev(self._h, d_bgr, H, W, pitch, d_gray,
+                                                   stream or None))
+
+    def disparity_dev(self, d_left: int, d_right: int, H: int, W: int, pitch: int,
+                      min_disp: int, num_disp: int, win: int, cost, row0: int, row1: int,
+                      d_out16: int, out_pitch: int, stream: int = 0):
+        _check("sv_disparity_dev", self.lib.sv_disparity_dev(
+            self._h, d_left, d_right, H, W, pitch, int(min_disp), int(num_disp), int(win),
+            _cost(cost), int(row0), int(row1), d_out16, out_pitch, stream or None))
+
+    def median_post_dev(self, d_disp16: int, H: int, W: int, row0: int, row1: int, mode: int,
+                        d_disparity: int, d_out_a: int = 0, d_out_u8: int = 0, d_out_b: int = 0,
+                        min_depth=0.0, max_depth=0.0, min_disp_global=0.0, min_disp=0,
+                        num_disp=0, stream: int = 0):
+        _check("sv_median_post_dev", self.lib.sv_median_post_dev(
+            self._h, d_disp16, H, W, int(row0), int(row1), int(mode), np.float32(min_depth),
+            np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
+            np.float32(min_disp_global), int(min_disp), int(num_disp), d_disparity,
+            d_out_a or None, d_out_u8 or None, d_out_b or None, stream or None))
+
+    def depth_map_dev(self, d_left: int, d_right: int, H: int, W: int, pitch: int,
+                      min_disp: int, num_disp: int, win: int, min_depth: float,
+                      max_depth: float, d_depth: int, d_disp: int, d_norm: int, cost="sad",
+                      min_disp_global=None, stream: int = 0):
+        mdg = min_disp if min_disp_global is None else min_disp_global
+        _check("sv_depth_map_dev", self.lib.sv_depth_map_dev(
+            self._h, d_left, d_right, H, W, pitch, int(min_disp), int(num_disp), int(win),
+            _cost(cost), np.float32(min_depth), np.float32(max_depth),
+            np.float32(float(max_depth) - float(min_depth)), np.float32(mdg), d_depth, d_disp,
+            d_norm, stream or None))
+
+    def harris_dev(self, d_gray: int, H: int, W: int, pitch: int, d_out: int, stream: int = 0):
+        _check("sv_harris_dev", self.lib.sv_harris_dev(self._h, d_gray, H, W, pitch, d_out,
+                                                       stream or None))
+
+    def hog_hist_dev(self, d_gray: int, H: int, W: int, pitch: int, win: int, row0: int,
+                     row1: int, d_out: int, stream: int = 0):
+        _check("sv_hog_hist_dev", self.lib.sv_hog_hist_dev(self._h, d_gray, H, W, pitch, win,
+                                                           row0, row1, d_out, stream or None))
+
+    # -- profiling ------------------------------------------------------------------------
+    def profile(self, on: bool = True):
+        _check("sv_profile_enable", self.lib.sv_profile_enable(self._h, 1 if on else 0))
+
+    def profile_reset(self):
+        _check("sv_profile_reset", self.lib.sv_profile_reset(self._h))
+
+    def profile_read(self, kernel: str | int) -> tuple[float, int]:
+        k = KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
+        ms = ctypes.c_double()
+        n = ctypes.c_longlong()
+        _check("sv_profile_read", self.lib.sv_profile_read(self._h, k, ctypes.byref(ms),
+                                                           ctypes.byref(n)))
+        return ms.value, n.value
+
+
+_engines: dict[int, Engine] = {}
+_engines_lock = threading.Lock()
+
+
+def get_engine(device: int | None = None) -> Engine:
+    """Process-wide cached Engine per device (SV_DEVICE env var picks the default)."""
+    if device is None:
+        device = int(os.environ.get("SV_DEVICE", "0"))
+    with _engines_lock:
+        eng = _engines.get(device)
+        if eng is None:
+            eng = Engine(device)
+            _engines[device] = eng
+        return eng

@@ -5,72 +5,102 @@
 // HOG winner-take-all engine specified in DESIGN.md ("Semantics").  Output: int16 = d*16,
 // invalid = (minD-1)*16 outside the matched band [X0, X1).
 //
-// Work decomposition (one wave = one output row y, 256 output columns):
-//   * the wave is split into G = 64/LPG groups of LPG lanes; group g walks the segment
-//     [xs, xs+S) of S = 4*LPG columns left to right;
+// Work decomposition (one wave = ROWS output rows (1 or 2), one run of output columns):
+//   * the wave is split into G = 64/LPG groups of LPG lanes; group g walks its segment of
+//     S columns left to right;
 //   * lane l of a group owns the DPL consecutive disparities d = minD + l*DPL + k, so the
 //     LPG*DPL candidates of one pixel sit across one group, and the argmin is an in-lane
 //     min3 chain over (cost << dbits | d) keys + a DPP row reduction (first-min tie-break);
-//   * image data is staged ONCE per wave in LDS as "column packs": the win bytes of one
-//     column, rows y-r..y+r, packed 4 per dword (zero padded).  One v_sad_u8 then sums 4
-//     vertical taps, so a column's vertical window costs ceil(win/4) VALU ops;
+//   * image data is staged ONCE per wave in LDS as "column packs": the window rows of one
+//     column packed 4 bytes per dword (zero padded).  One v_sad_u8 sums 4 vertical taps;
 //   * the horizontal window is a running sum along x: per step the group adds the column
 //     entering the window and subtracts the column leaving it;
 //   * the right-image column a lane needs for disparity k at step t is the column it
 //     loaded for k-1 at step t-1, so each lane keeps a DPL-deep register ring and loads
-//     ONE new right pack per step (plus one for the leaving column) — LDS traffic is
-//     2 R + 2 L reads per step per lane for DPL cost cells;
-//   * right packs are stored with a 1-in-8 slot gap (rphys) so the 16 lanes of a group,
-//     whose columns are DPL apart, hit distinct LDS banks on ds_read_b128.
-// SSD uses the same skeleton with v_dot4_u32_u8: sum (L-R)^2 = sum L^2 + sum R^2 - 2 sum L*R
-// (squares precomputed per pack).  HOG reads 9-bin window histograms (u16) as packs and
-// compares them with v_sad_u16; it has no running window (r = 0 in the skeleton).
+//     ONE new right pack per step (plus one for the leaving column);
+//   * right packs are stored with a 1-in-DPL slot gap (rslot) so the 16 lanes of a group,
+//     whose columns are DPL apart, hit distinct LDS banks, and a lane's reads inside a
+//     DPL-step chunk use static offsets;
+//   * the per-pixel DPP reductions of a DPL-step chunk are batched (independent chains)
+//     before one coalesced store per lane.
+// Cost kinds:
+//   SAD   1 row/wave, pack = ceil(win/4) byte dwords, ceil(win/4) v_sad_u8 per column cell;
+//   SAD2  2 rows/wave (rows y, y+1) for 5 <= win <= 9: a pack holds the 2r shared middle
+//         rows + row y-r and row y+r+1 as single-byte dwords, so the two cells of a column
+//         cost ceil(2r/4) + 2 v_sad_u8 instead of 2*ceil(win/4) (win 9: 4 instead of 6);
+//   SSD   v_dot4_u32_u8: sum (L-R)^2 = sum L^2 + sum R^2 - 2 sum L*R (squares per pack);
+//   HOG   9-bin u16 window histograms as packs compared with v_sad_u16 (no running window).
 #include "sv_internal.h"
 
 namespace sv {
 namespace {
 
-constexpr int WAVE_COLS = 256;
-constexpr int ROWS_PER_BLOCK = 4;
+constexpr int ROWS_PER_BLOCK = 4;     // waves per 256-thread block
+constexpr int COST_SAD2 = 3;          // internal kind: SAD, two output rows per wave
+
+// Segment width per lane group: 4*LPG columns rounded up to a multiple of DPL so that
+// every group of a wave shares the same right-pack slot phase (rslot).
+__host__ __device__ __forceinline__ int seg_width(int lpg, int dpl) { return (4 * lpg + dpl - 1) / dpl * dpl; }
+__host__ __device__ __forceinline__ int wave_cols(int lpg, int dpl) { return (64 / lpg) * seg_width(lpg, dpl); }
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
-__device__ __forceinline__ int rphys(int i) { return i + (i >> 3); }
 
-template <int COST> struct PackQ { static constexpr int Q = (COST == COST_SAD) ? 1 : 2; };
+// A column pack holds NW live dwords inside a 16*Q-byte LDS slot.  ND is the kind's width
+// parameter: byte dwords (SAD, SSD), shared dwords (SAD2), unused (HOG).
+template <int COST, int ND> struct PackCfg {
+    static constexpr int NW = COST == COST_SAD ? ND : COST == COST_SSD ? ND + 1 : COST == COST_SAD2 ? ND + 2 : 5;
+    static constexpr int Q = (NW + 3) / 4;
+    static constexpr int ROWS = COST == COST_SAD2 ? 2 : 1;
+};
+template <int NW> struct Pk { uint32_t w[NW]; };
 
-template <int Q>
-__device__ __forceinline__ void load_pack(const uint4* p, uint4 (&v)[Q]) {
+template <int NW>
+__device__ __forceinline__ Pk<NW> ld(const uint4* p) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(p, 16));
+    Pk<NW> v;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) v[q] = p[q];
+    for (int i = 0; i < NW; ++i) v.w[i] = q[i];
+    return v;
 }
 
-// Per-cell column cost added to `acc`.
-template <int COST, int NDW, int Q>
-__device__ __forceinline__ uint32_t vcol(const uint4 (&l)[Q], const uint4 (&r)[Q], uint32_t acc) {
+// Column cost(s) of one (left pack, right pack) pair.  ROWS = 1: returns acc + cost.
+// SAD2: acc[0] += cost(row y), acc[1] += cost(row y+1) (SUB: -=).
+template <int COST, int ND, int NW, bool SUB>
+__device__ __forceinline__ void vcol(const Pk<NW>& l, const Pk<NW>& r, uint32_t* acc) {
     if constexpr (COST == COST_SAD) {
-        acc = __builtin_amdgcn_sad_u8(l[0].x, r[0].x, acc);
-        if constexpr (NDW > 1) acc = __builtin_amdgcn_sad_u8(l[0].y, r[0].y, acc);
-        if constexpr (NDW > 2) acc = __builtin_amdgcn_sad_u8(l[0].z, r[0].z, acc);
-        if constexpr (NDW > 3) acc = __builtin_amdgcn_sad_u8(l[0].w, r[0].w, acc);
-        return acc;
+        if constexpr (!SUB) {
+#pragma unroll
+            for (int i = 0; i < ND; ++i) acc[0] = __builtin_amdgcn_sad_u8(l.w[i], r.w[i], acc[0]);
+        } else {
+            uint32_t v = 0u;
+#pragma unroll
+            for (int i = 0; i < ND; ++i) v = __builtin_amdgcn_sad_u8(l.w[i], r.w[i], v);
+            acc[0] -= v;
+        }
+    } else if constexpr (COST == COST_SAD2) {
+        uint32_t s = 0u;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) s = __builtin_amdgcn_sad_u8(l.w[i], r.w[i], s);
+        const uint32_t v0 = __builtin_amdgcn_sad_u8(l.w[ND], r.w[ND], s);
+        const uint32_t v1 = __builtin_amdgcn_sad_u8(l.w[ND + 1], r.w[ND + 1], s);
+        if constexpr (!SUB) { acc[0] += v0; acc[1] += v1; }
+        else { acc[0] -= v0; acc[1] -= v1; }
     } else if constexpr (COST == COST_SSD) {
-        uint32_t dot = __builtin_amdgcn_udot4(l[0].x, r[0].x, 0u, false);
-        if constexpr (NDW > 1) dot = __builtin_amdgcn_udot4(l[0].y, r[0].y, dot, false);
-        if constexpr (NDW > 2) dot = __builtin_amdgcn_udot4(l[0].z, r[0].z, dot, false);
-        if constexpr (NDW > 3) dot = __builtin_amdgcn_udot4(l[0].w, r[0].w, dot, false);
-        return acc + (l[1].x + r[1].x) - (dot << 1);
-    } else {  // HOG: 9 u16 bins in 5 dwords
-        acc = __builtin_amdgcn_sad_u16(l[0].x, r[0].x, acc);
-        acc = __builtin_amdgcn_sad_u16(l[0].y, r[0].y, acc);
-        acc = __builtin_amdgcn_sad_u16(l[0].z, r[0].z, acc);
-        acc = __builtin_amdgcn_sad_u16(l[0].w, r[0].w, acc);
-        acc = __builtin_amdgcn_sad_u16(l[1].x, r[1].x, acc);
-        return acc;
+        uint32_t dot = 0u;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) dot = __builtin_amdgcn_udot4(l.w[i], r.w[i], dot, false);
+        const uint32_t v = (l.w[ND] + r.w[ND]) - (dot << 1);
+        if constexpr (!SUB) acc[0] += v; else acc[0] -= v;
+    } else {  // HOG: 9 u16 bins in 5 dwords; the cost IS the cell value
+        uint32_t v = 0u;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) v = __builtin_amdgcn_sad_u16(l.w[i], r.w[i], v);
+        acc[0] = v;
     }
 }
 
-// Build one column pack for logical column c around row y (replicate-clamped).
-template <int COST, int Q>
+// Build one column pack for logical column c around output row y (replicate-clamped).
+template <int COST, int ND>
 __device__ __forceinline__ void build_pack(const MatchParams& a, const uint8_t* img,
                                            const uint16_t* hist, int c, int y, uint4* dst) {
     const int cc = clampi(c, 0, a.W - 1);
@@ -78,69 +108,161 @@ __device__ __forceinline__ void build_pack(const MatchParams& a, const uint8_t* 
         const uint32_t* src = reinterpret_cast<const uint32_t*>(hist + ((size_t)y * a.W + cc) * 10);
         dst[0] = make_uint4(src[0], src[1], src[2], src[3]);
         dst[1] = make_uint4(src[4], 0u, 0u, 0u);
+    } else if constexpr (COST == COST_SAD2) {
+        // rows y-r .. y+r+1: j = 0 -> word ND (row y only), j = 2r+1 -> word ND+1 (row y+1
+        // only), j in [1, 2r] -> shared word (j-1)/4
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        const int last = 2 * a.r + 1;
+        for (int j = 0; j <= last; ++j) {
+            const int yy = clampi(y - a.r + j, 0, a.H - 1);
+            const uint32_t v = img[(size_t)yy * a.pitch + cc];
+            const int q = j == 0 ? ND : j == last ? ND + 1 : (j - 1) >> 2;
+            const uint32_t sh = (j == 0 || j == last) ? v : v << (8 * ((j - 1) & 3));
+            w[0] |= q == 0 ? sh : 0u;
+            w[1] |= q == 1 ? sh : 0u;
+            w[2] |= q == 2 ? sh : 0u;
+            w[3] |= q == 3 ? sh : 0u;
+        }
+        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
     } else {
-        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, sq = 0;
+        uint32_t w[5] = {0u, 0u, 0u, 0u, 0u};
+        uint32_t sq = 0;
         for (int j = 0; j < a.win; ++j) {
             const int yy = clampi(y - a.r + j, 0, a.H - 1);
             const uint32_t v = img[(size_t)yy * a.pitch + cc];
             sq += v * v;
             const uint32_t sh = v << (8 * (j & 3));
             const int q = j >> 2;
-            w0 |= q == 0 ? sh : 0u;
-            w1 |= q == 1 ? sh : 0u;
-            w2 |= q == 2 ? sh : 0u;
-            w3 |= q == 3 ? sh : 0u;
+            w[0] |= q == 0 ? sh : 0u;
+            w[1] |= q == 1 ? sh : 0u;
+            w[2] |= q == 2 ? sh : 0u;
+            w[3] |= q == 3 ? sh : 0u;
         }
-        dst[0] = make_uint4(w0, w1, w2, w3);
-        if constexpr (Q > 1) dst[1] = make_uint4(sq, 0u, 0u, 0u);
+        if constexpr (COST == COST_SSD) w[ND] = sq;
+        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        if constexpr (PackCfg<COST, ND>::Q > 1) dst[1] = make_uint4(w[4], 0u, 0u, 0u);
     }
 }
 
-// min over the LPG lanes of a group; the result is exact in the group's LAST lane
-// (in every lane for LPG = 16).
-__device__ __forceinline__ uint32_t group_min(uint32_t v, int lpg) {
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, (int)v, 0x121, 0xF, 0xF, false));  // row_ror:1
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, (int)v, 0x122, 0xF, 0xF, false));  // row_ror:2
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, (int)v, 0x124, 0xF, 0xF, false));  // row_ror:4
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, (int)v, 0x128, 0xF, 0xF, false));  // row_ror:8
-    if (lpg >= 32)  // row_bcast:15 into rows 1 and 3
-        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x142, 0xA, 0xF, false));
-    if (lpg == 64)  // row_bcast:31 into rows 2 and 3
-        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x143, 0xC, 0xF, false));
-    return v;
+// Logical right-pack index i -> LDS slot: one empty slot after every DPL packs, phased by
+// c0 so that every DPL-step chunk of a lane's "entering column" reads is DPL consecutive
+// slots (static ds_read offsets) and the 16 lanes of a group, DPL packs apart, land DPL+1
+// slots apart (DPL+1 odd -> distinct 16-byte bank groups for ds_read_b128).
+__device__ __forceinline__ int rslot(int i, int c0, int dpl) { return i + (i + c0) / dpl; }
+
+template <int COST, int ND, int DPL>
+__device__ __forceinline__ void match_chunk(
+    const int cut, const int dbits, const uint4* __restrict__ rnb,
+    const uint4* __restrict__ rob, const uint4* __restrict__ lnb, const uint4* __restrict__ lob,
+    Pk<PackCfg<COST, ND>::NW> (&rn)[DPL], Pk<PackCfg<COST, ND>::NW> (&ro)[DPL],
+    uint32_t (&h)[DPL][PackCfg<COST, ND>::ROWS], const uint32_t (&mk)[DPL],
+    uint32_t (&bk)[PackCfg<COST, ND>::ROWS][DPL]) {
+    constexpr int NW = PackCfg<COST, ND>::NW;
+    constexpr int Q = PackCfg<COST, ND>::Q;
+    constexpr int ROWS = PackCfg<COST, ND>::ROWS;
+    constexpr bool RUN = COST != COST_HOG;            // running horizontal window
+#pragma unroll
+    for (int u = 0; u < DPL; ++u) {
+        // ring slot u receives this step's entering right column; its previous content
+        // (k = DPL-1 of the last step) is dead.  Static offsets inside the chunk; `cut` is
+        // the wave-uniform phase of the old ring's slot gap.
+        rn[u] = ld<NW>(rnb + u * Q);
+        const Pk<NW> L = ld<NW>(lnb + u * Q);
+        Pk<NW> LO;
+        if constexpr (RUN) {
+            ro[u] = ld<NW>(rob + (u + (u >= cut ? 1 : 0)) * Q);
+            LO = ld<NW>(lob + u * Q);
+        }
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) {
+            const int sk = (u - k + DPL) % DPL;
+            vcol<COST, ND, NW, false>(L, rn[sk], h[k]);
+            if constexpr (RUN) vcol<COST, ND, NW, true>(LO, ro[sk], h[k]);
+        }
+#pragma unroll
+        for (int q = 0; q < ROWS; ++q) {
+            uint32_t b = 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = 0; k < DPL; ++k) b = min(b, (h[k][q] << dbits) | mk[k]);
+            bk[q][u] = b;
+        }
+        // one scheduling region per step: without it hipcc hoists every step's LDS reads
+        // to the top of the chunk and the register file doubles
+        __builtin_amdgcn_sched_barrier(0);
+    }
 }
 
-template <int COST, int NDW, int DPL>
-__global__ __launch_bounds__(256) void k_match(MatchParams a) {
-    constexpr int Q = PackQ<COST>::Q;
+// Batched per-pixel reductions of one chunk, branch-free per LPG so the independent DPP
+// chains interleave.
+// The min lands in the group's LAST lane (every lane for LPG = 16): row_ror within 16-lane
+// rows, then row_bcast:15 / row_bcast:31 across rows.
+template <int LPG, int N>
+__device__ __forceinline__ void reduce_batch(uint32_t* v) {
+#define SV_ROR_STEP(CTRL)                                                                     \
+    _Pragma("unroll") for (int i = 0; i < N; ++i)                                             \
+        v[i] = min(v[i], (uint32_t)__builtin_amdgcn_update_dpp(0u, (int)v[i], CTRL, 0xF, 0xF, false));
+    SV_ROR_STEP(0x121)  // row_ror:1
+    SV_ROR_STEP(0x122)  // row_ror:2
+    SV_ROR_STEP(0x124)  // row_ror:4
+    SV_ROR_STEP(0x128)  // row_ror:8
+#undef SV_ROR_STEP
+    if constexpr (LPG >= 32) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            v[i] = min(v[i], (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v[i], 0x142, 0xA, 0xF, false));
+    }
+    if constexpr (LPG == 64) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            v[i] = min(v[i], (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v[i], 0x143, 0xC, 0xF, false));
+    }
+}
+
+// Occupancy target: LDS admits ~3 blocks/CU for the common configs (D <= 128, win <= 11),
+// so cap registers at 3 waves/SIMD (<= 168 VGPRs); the widest packs get 2 waves/SIMD.
+template <int COST, int ND> struct Occ {
+    static constexpr int W = (COST == COST_SAD || COST == COST_SAD2 || ND <= 3) ? 3 : 2;
+};
+
+template <int COST, int ND, int DPL>
+__global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a) {
+    constexpr int NW = PackCfg<COST, ND>::NW;
+    constexpr int Q = PackCfg<COST, ND>::Q;
+    constexpr int ROWS = PackCfg<COST, ND>::ROWS;
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int LPG = a.lpg;
-    const int S = 4 * LPG;                 // segment width per group
+    const int S = seg_width(LPG, DPL);      // segment width per group
+    const int WC = wave_cols(LPG, DPL);
     const int r = a.r;
     const int W2 = 2 * r + 1;
-    const int NL = WAVE_COLS + 4 * r + DPL;
-    const int NRlog = WAVE_COLS + 4 * r + LPG * DPL + DPL;
-    const int NRphys = NRlog + (NRlog >> 3) + 1;
+    const int c0 = (DPL - (4 * r + 1) % DPL) % DPL;      // (iR0 + W2 + c0) % DPL == 0
+    const int NL = WC + 4 * r + DPL + 1;
+    const int NRlog = WC + 4 * r + LPG * DPL + DPL;
+    const int NRphys = NRlog + (NRlog + c0) / DPL + 1;
     uint4* Lp = smem + (size_t)wid * (NL + NRphys) * Q;
     uint4* Rp = Lp + (size_t)NL * Q;
 
-    const int y = a.row0 + (int)blockIdx.y * ROWS_PER_BLOCK + wid;
+    const int y = a.row0 + ((int)blockIdx.y * ROWS_PER_BLOCK + wid) * ROWS;
     const int yc = min(y, a.row1 - 1);
-    const int xw = a.X0 + (int)blockIdx.x * WAVE_COLS;
+    const int xw = a.X0 + (int)blockIdx.x * WC;
     const int cL0 = xw - 3 * r - 1;
     const int cR0 = cL0 - a.minD - (LPG * DPL - 1);
 
-    for (int i = lane; i < NL; i += 64) build_pack<COST, Q>(a, a.L, a.HL, cL0 + i, yc, Lp + (size_t)i * Q);
+    for (int i = lane; i < NL; i += 64) build_pack<COST, ND>(a, a.L, a.HL, cL0 + i, yc, Lp + (size_t)i * Q);
     for (int i = lane; i < NRlog; i += 64)
-        build_pack<COST, Q>(a, a.R, a.HR, cR0 + i, yc, Rp + (size_t)rphys(i) * Q);
+        build_pack<COST, ND>(a, a.R, a.HR, cR0 + i, yc, Rp + (size_t)rslot(i, c0, DPL) * Q);
 
-    if (blockIdx.x == 0 && y < a.row1) {  // columns outside the matched band are invalid
+    if (blockIdx.x == 0) {  // columns outside the matched band are invalid
         const int16_t inv = (int16_t)((a.minD - 1) * 16);
-        int16_t* orow = a.out + (size_t)y * a.opitch;
-        for (int x = lane; x < a.X0; x += 64) orow[x] = inv;
-        for (int x = a.X1 + lane; x < a.W; x += 64) orow[x] = inv;
+#pragma unroll
+        for (int q = 0; q < ROWS; ++q) {
+            if (y + q >= a.row1) break;
+            int16_t* orow = a.out + (size_t)(y + q) * a.opitch;
+            for (int x = lane; x < a.X0; x += 64) orow[x] = inv;
+            for (int x = a.X1 + lane; x < a.W; x += 64) orow[x] = inv;
+        }
     }
     __syncthreads();
     if (y >= a.row1) return;
@@ -148,13 +270,11 @@ __global__ __launch_bounds__(256) void k_match(MatchParams a) {
     const int g = lane >> a.lpg_log2;
     const int l = lane & (LPG - 1);
     const int xs = xw + g * S;
-    const int iL0 = g * S + 2 * r + 1;
-    const int iR0 = g * S + 2 * r + (LPG - l) * DPL;
-    const int T = (S + 2 * r + DPL - 1) / DPL * DPL;
+    const int iL0 = g * S + 2 * r + 1;                   // L index of the window's first column
+    const int iR0 = g * S + 2 * r + (LPG - l) * DPL;   // R index of (first column, k = 0)
     const uint32_t dmask = (1u << a.dbits) - 1u;
     const int dbits = a.dbits;
-    const bool emitter = (l == LPG - 1);
-    int16_t* orow = a.out + (size_t)y * a.opitch;
+    const int j = l - (LPG - 16);                        // emitting lane -> step within a chunk
 
     uint32_t mk[DPL];
 #pragma unroll
@@ -162,48 +282,70 @@ __global__ __launch_bounds__(256) void k_match(MatchParams a) {
         const int idx = l * DPL + k;
         mk[k] = idx < a.D ? (uint32_t)idx : 0xFFFFFFFFu;
     }
-    uint4 rn[DPL][Q];
-    uint4 ro[DPL][Q];
+    uint32_t h[DPL][ROWS], bk[ROWS][DPL];
 #pragma unroll
-    for (int j = 1; j < DPL; ++j) {
-        load_pack<Q>(Rp + (size_t)rphys(iR0 - j) * Q, rn[DPL - j]);
-        if constexpr (COST != COST_HOG) load_pack<Q>(Rp + (size_t)rphys(iR0 - j - W2) * Q, ro[DPL - j]);
-    }
-    uint32_t h[DPL];
+    for (int k = 0; k < DPL; ++k)
 #pragma unroll
-    for (int k = 0; k < DPL; ++k) h[k] = 0u;
+        for (int q = 0; q < ROWS; ++q) h[k][q] = 0u;
 
-    for (int t0 = 0; t0 < T; t0 += DPL) {
+    // ---- prologue: window of output column xs = the W2 columns xs-r .. xs+r, added directly
+    for (int t = 0; t < W2; ++t) {
+        const Pk<NW> L = ld<NW>(Lp + (size_t)(iL0 + t) * Q);
 #pragma unroll
-        for (int u = 0; u < DPL; ++u) {
-            const int t = t0 + u;
-            load_pack<Q>(Rp + (size_t)rphys(iR0 + t) * Q, rn[u]);
-            uint4 ln[Q];
-            load_pack<Q>(Lp + (size_t)(iL0 + t) * Q, ln);
-            if constexpr (COST == COST_HOG) {
+        for (int k = 0; k < DPL; ++k)
+            vcol<COST, ND, NW, false>(L, ld<NW>(Rp + (size_t)rslot(iR0 + t - k, c0, DPL) * Q), h[k]);
+    }
+    {
+        const bool emit0 = j == 0 && xs < a.X1;
 #pragma unroll
-                for (int k = 0; k < DPL; ++k) h[k] = vcol<COST, NDW, Q>(ln, rn[(u - k + DPL) % DPL], 0u);
-            } else {
-                load_pack<Q>(Rp + (size_t)rphys(iR0 + t - W2) * Q, ro[u]);
+        for (int q = 0; q < ROWS; ++q) {
+            uint32_t b = 0xFFFFFFFFu;
 #pragma unroll
-                for (int k = 0; k < DPL; ++k) h[k] = vcol<COST, NDW, Q>(ln, rn[(u - k + DPL) % DPL], h[k]);
-                if (t >= W2) {
-                    uint4 lo[Q];
-                    load_pack<Q>(Lp + (size_t)(iL0 + t - W2) * Q, lo);
+            for (int k = 0; k < DPL; ++k) b = min(b, (h[k][q] << dbits) | mk[k]);
+            if (LPG == 16) reduce_batch<16, 1>(&b);
+            else if (LPG == 32) reduce_batch<32, 1>(&b);
+            else reduce_batch<64, 1>(&b);
+            if (emit0 && y + q < a.row1)
+                a.out[(size_t)(y + q) * a.opitch + xs] = (int16_t)(((int)(b & dmask) + a.minD) * 16);
+        }
+    }
+
+    // ---- main loop: step t' adds column xs+r+1+t' and drops column xs-r+t' (output
+    // xs+1+t'), in chunks of DPL steps with static ring slots and static LDS offsets.
+    // c0 aligns chunk starts with the right-pack slot gaps (see rslot); the leaving
+    // column's reads trail by W2 packs, so their gap phase is (-W2) mod DPL for every lane.
+    const int phi = (DPL - W2 % DPL) % DPL;
+    const int cut = DPL - phi;                           // old slot offsets u >= cut skip a gap
+    const int iN = iR0 + W2;                             // R index of the entering column, t' = 0
+    Pk<NW> rn[DPL], ro[DPL];
 #pragma unroll
-                    for (int k = 0; k < DPL; ++k) h[k] -= vcol<COST, NDW, Q>(lo, ro[(u - k + DPL) % DPL], 0u);
-                }
-            }
-            if (t >= 2 * r) {
-                uint32_t best = 0xFFFFFFFFu;
+    for (int s = 1; s < DPL; ++s) {                      // virtual steps t' = s - DPL
+        rn[s] = ld<NW>(Rp + (size_t)rslot(iN - (DPL - s), c0, DPL) * Q);
+        if constexpr (COST != COST_HOG) ro[s] = ld<NW>(Rp + (size_t)rslot(iR0 - (DPL - s), c0, DPL) * Q);
+    }
+    const uint4* rn0 = Rp + (size_t)rslot(iN, c0, DPL) * Q;
+    const uint4* ro0 = Rp + (size_t)rslot(iR0, c0, DPL) * Q;
+    const uint4* ln0 = Lp + (size_t)(iL0 + W2) * Q;
+    const uint4* lo0 = Lp + (size_t)iL0 * Q;
+    const int T = (S - 1 + DPL - 1) / DPL * DPL;
+
+    for (int t0 = 0, c = 0; t0 < T; t0 += DPL, ++c) {
+        match_chunk<COST, ND, DPL>(cut, dbits, rn0 + (size_t)c * (DPL + 1) * Q, ro0 + (size_t)c * (DPL + 1) * Q,
+                                   ln0 + (size_t)t0 * Q, lo0 + (size_t)t0 * Q, rn, ro, h, mk, bk);
+        const int e = t0 + j + 1;
+        const int x = xs + e;
+        const bool emit = j >= 0 && j < DPL && e < S && x < a.X1;
+        // ROWS*DPL independent group reductions (ILP instead of a serial DPP chain per step)
+        if (LPG == 16) reduce_batch<16, ROWS * DPL>(&bk[0][0]);
+        else if (LPG == 32) reduce_batch<32, ROWS * DPL>(&bk[0][0]);
+        else reduce_batch<64, ROWS * DPL>(&bk[0][0]);
 #pragma unroll
-                for (int k = 0; k < DPL; ++k) best = min(best, (h[k] << dbits) | mk[k]);
-                best = group_min(best, LPG);
-                const int e = t - 2 * r;
-                const int x = xs + e;
-                if (emitter && e < S && x < a.X1)
-                    orow[x] = (int16_t)(((int)(best & dmask) + a.minD) * 16);
-            }
+        for (int q = 0; q < ROWS; ++q) {
+            uint32_t v = bk[q][0];
+#pragma unroll
+            for (int u = 1; u < DPL; ++u) v = (j == u) ? bk[q][u] : v;
+            if (emit && y + q < a.row1)
+                a.out[(size_t)(y + q) * a.opitch + x] = (int16_t)(((int)(v & dmask) + a.minD) * 16);
         }
     }
 }
@@ -214,32 +356,40 @@ __global__ void k_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v) {
     if (x < W && y < H) out[(size_t)y * opitch + x] = v;
 }
 
-template <int COST, int NDW, int DPL>
+template <int COST, int ND, int DPL>
 int launch_one(const MatchParams& a, size_t lds, hipStream_t s) {
-    auto fn = k_match<COST, NDW, DPL>;
+    auto fn = k_match<COST, ND, DPL>;
     if (lds > 65536) {  // opt in to > 64 KiB of dynamic LDS (per device, cheap host call)
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return (int)e;
     }
-    dim3 grid((a.X1 - a.X0 + WAVE_COLS - 1) / WAVE_COLS, (a.row1 - a.row0 + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
+    const int wc = wave_cols(a.lpg, DPL);
+    const int rows_per_block = ROWS_PER_BLOCK * PackCfg<COST, ND>::ROWS;
+    dim3 grid((a.X1 - a.X0 + wc - 1) / wc, (a.row1 - a.row0 + rows_per_block - 1) / rows_per_block);
     hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, a);
     return (int)hipGetLastError();
 }
 
-template <int COST, int NDW>
+template <int COST, int ND>
 int launch_dpl(const MatchParams& a, const MatchPlan& p, size_t lds, hipStream_t s) {
     switch (p.dpl) {
-        case 4: return launch_one<COST, NDW, 4>(a, lds, s);
-        case 6: return launch_one<COST, NDW, 6>(a, lds, s);
-        case 8: return launch_one<COST, NDW, 8>(a, lds, s);
+        case 4: return launch_one<COST, ND, 4>(a, lds, s);
+        case 6: return launch_one<COST, ND, 6>(a, lds, s);
+        case 8: return launch_one<COST, ND, 8>(a, lds, s);
     }
     return (int)hipErrorInvalidValue;
 }
 
 template <int COST>
-int launch_ndw(const MatchParams& a, const MatchPlan& p, size_t lds, hipStream_t s) {
+int launch_nd(const MatchParams& a, const MatchPlan& p, size_t lds, hipStream_t s) {
     if constexpr (COST == COST_HOG) {
         return launch_dpl<COST, 5>(a, p, lds, s);
+    } else if constexpr (COST == COST_SAD2) {
+        switch (p.ndw) {
+            case 1: return launch_dpl<COST, 1>(a, p, lds, s);
+            case 2: return launch_dpl<COST, 2>(a, p, lds, s);
+        }
+        return (int)hipErrorInvalidValue;
     } else {
         switch (p.ndw) {
             case 1: return launch_dpl<COST, 1>(a, p, lds, s);
@@ -249,6 +399,11 @@ int launch_ndw(const MatchParams& a, const MatchPlan& p, size_t lds, hipStream_t
         }
         return (int)hipErrorInvalidValue;
     }
+}
+
+// Kind actually launched for a public cost: SAD with 5 <= win <= 9 runs two rows per wave.
+int kind_of(int cost, int win) {
+    return (cost == COST_SAD && win >= 5 && win <= 9) ? COST_SAD2 : cost;
 }
 
 }  // namespace
@@ -263,7 +418,8 @@ int plan_match(int num_disp, int win, int cost, MatchPlan* plan) {
     if (i == 7) return -22;
     plan->dpl = menu[i][0];
     plan->lpg = menu[i][1];
-    plan->ndw = cost == COST_HOG ? 5 : (win + 3) / 4;
+    const int kind = kind_of(cost, win);
+    plan->ndw = kind == COST_HOG ? 5 : kind == COST_SAD2 ? (win - 1 + 3) / 4 : (win + 3) / 4;
     int n = plan->dpl * plan->lpg - 1, bits = 0;
     while (n > 0) { ++bits; n >>= 1; }
     plan->dbits = bits < 1 ? 1 : bits;
@@ -275,10 +431,14 @@ int plan_match(int num_disp, int win, int cost, MatchPlan* plan) {
 }
 
 size_t match_lds_bytes(const MatchPlan& p, int r, int cost) {
-    const int Q = cost == COST_SAD ? 1 : 2;
-    const int NL = WAVE_COLS + 4 * r + p.dpl;
-    const int NRlog = WAVE_COLS + 4 * r + p.lpg * p.dpl + p.dpl;
-    const int NRphys = NRlog + (NRlog >> 3) + 1;
+    const int kind = kind_of(cost, 2 * r + 1);
+    const int nw = kind == COST_SAD ? p.ndw : kind == COST_SSD ? p.ndw + 1 : kind == COST_SAD2 ? p.ndw + 2 : 5;
+    const int Q = (nw + 3) / 4;
+    const int c0 = (p.dpl - (4 * r + 1) % p.dpl) % p.dpl;
+    const int wc = wave_cols(p.lpg, p.dpl);
+    const int NL = wc + 4 * r + p.dpl + 1;
+    const int NRlog = wc + 4 * r + p.lpg * p.dpl + p.dpl;
+    const int NRphys = NRlog + (NRlog + c0) / p.dpl + 1;
     return (size_t)ROWS_PER_BLOCK * (NL + NRphys) * Q * 16;
 }
 
@@ -295,10 +455,11 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
                                (int16_t)((a.minD - 1) * 16), s);
     const size_t lds = match_lds_bytes(p, a.r, cost);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-    switch (cost) {
-        case COST_SAD: return launch_ndw<COST_SAD>(a, p, lds, s);
-        case COST_SSD: return launch_ndw<COST_SSD>(a, p, lds, s);
-        case COST_HOG: return launch_ndw<COST_HOG>(a, p, lds, s);
+    switch (kind_of(cost, a.win)) {
+        case COST_SAD: return launch_nd<COST_SAD>(a, p, lds, s);
+        case COST_SAD2: return launch_nd<COST_SAD2>(a, p, lds, s);
+        case COST_SSD: return launch_nd<COST_SSD>(a, p, lds, s);
+        case COST_HOG: return launch_nd<COST_HOG>(a, p, lds, s);
     }
     return (int)hipErrorInvalidValue;
 }

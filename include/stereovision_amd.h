@@ -113,6 +113,13 @@ int sv_stereo_scaled(sv_ctx* ctx, const uint8_t* left, const uint8_t* right, int
 
 int sv_harris(sv_ctx* ctx, const uint8_t* gray, int H, int W, int stride, float* out);
 
+/* Row band [row0, row1) of the disparity map (halo rows read from the full frame, so the
+ * bands of a row-tiled multi-GPU split reassemble bit-exactly); only those rows of
+ * disp16 (HxW) are written. */
+int sv_disparity_rows(sv_ctx* ctx, const uint8_t* left, const uint8_t* right, int H, int W,
+                      int channels, int stride, int min_disp, int num_disp, int win, int cost,
+                      int row0, int row1, int16_t* disp16);
+
 /* out: [H][W][10] uint16 (9 bins + 1 zero pad) window histograms */
 int sv_hog_hist(sv_ctx* ctx, const uint8_t* gray, int H, int W, int stride, int win,
                 uint16_t* out);
@@ -146,6 +153,12 @@ int sv_harris_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, f
                   void* stream);
 int sv_hog_hist_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, int win,
                     int row0, int row1, uint16_t* d_out, void* stream);
+
+/* ---- device memory helpers (synchronous on the context stream) -------------------- */
+int sv_dev_alloc(sv_ctx* ctx, uint64_t bytes, void** out);
+int sv_dev_free(sv_ctx* ctx, void* p);
+int sv_copy_to_device(sv_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+int sv_copy_to_host(sv_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 
 /* ---- profiling: HIP events around every kernel this context launches -------------- */
 int sv_profile_enable(sv_ctx* ctx, int on);

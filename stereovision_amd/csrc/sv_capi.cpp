@@ -486,6 +486,59 @@ int sv_disparity(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, in
     return collect(c, o, 2);
 }
 
+int sv_disparity_rows(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels,
+                      int stride, int min_disp, int num_disp, int win, int cost, int row0, int row1,
+                      int16_t* disp16) {
+    SV_ENTER(c);
+    if (!disp16) return fail(SV_EINVAL, "null disparity output");
+    if (row0 < 0) row0 = 0;
+    if (row1 > H) row1 = H;
+    if (row1 <= row0) return 0;
+    sv::MatchPlan plan;
+    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    rc = stage_pair(c, left, right, H, W, channels, stride);
+    if (rc) return rc;
+    SV_HIP(c->d16.ensure((size_t)H * W * sizeof(int16_t)));
+    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
+                           win, cost, row0, row1, c->d16.as<int16_t>(), W, c->stream);
+    if (rc) return rc;
+    const size_t off = (size_t)row0 * W;
+    Out o[] = {{disp16 + off, c->d16.as<int16_t>() + off, (size_t)(row1 - row0) * W * sizeof(int16_t)}};
+    return collect(c, o, 1);
+}
+
+int sv_dev_alloc(sv_ctx* c, uint64_t bytes, void** out) {
+    SV_ENTER(c);
+    if (!out || bytes == 0) return fail(SV_EINVAL, "bad allocation request");
+    *out = nullptr;
+    SV_HIP(hipMalloc(out, (size_t)bytes));
+    return 0;
+}
+
+int sv_dev_free(sv_ctx* c, void* p) {
+    SV_ENTER(c);
+    if (p) SV_HIP(hipFree(p));
+    return 0;
+}
+
+int sv_copy_to_device(sv_ctx* c, void* dst, const void* src, uint64_t bytes) {
+    SV_ENTER(c);
+    if (!dst || !src) return fail(SV_EINVAL, "null pointer");
+    SV_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, c->stream));
+    SV_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int sv_copy_to_host(sv_ctx* c, void* dst, const void* src, uint64_t bytes) {
+    SV_ENTER(c);
+    if (!dst || !src) return fail(SV_EINVAL, "null pointer");
+    SV_HIP(hipStreamSynchronize(c->stream));   // results of enqueued device work
+    SV_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, c->stream));
+    SV_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
 int sv_median5_f32(sv_ctx* c, const float* in, int H, int W, float* out) {
     SV_ENTER(c);
     if (check_image(in, H, W) || !out) return fail(SV_EINVAL, "bad median arguments");

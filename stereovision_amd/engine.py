@@ -30,7 +30,8 @@ EXPORTED = [
     "sv_depth_post", "sv_scaled_post", "sv_depth_map", "sv_stereo_scaled", "sv_harris",
     "sv_hog_hist", "sv_gray_dev", "sv_disparity_dev", "sv_median_post_dev",
     "sv_depth_map_dev", "sv_harris_dev", "sv_hog_hist_dev", "sv_profile_enable",
-    "sv_profile_read", "sv_profile_reset",
+    "sv_profile_read", "sv_profile_reset", "sv_disparity_rows", "sv_dev_alloc", "sv_dev_free",
+    "sv_copy_to_device", "sv_copy_to_host",
 ]
 
 
@@ -110,6 +111,12 @@ def _declare(lib):
         "sv_harris_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp], _c_int),
         "sv_hog_hist_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
                             _c_int),
+        "sv_disparity_rows": ([_vp, _u8p, _u8p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                               _c_int, _c_int, _c_int, _c_int, _i16p], _c_int),
+        "sv_dev_alloc": ([_vp, ctypes.c_uint64, ctypes.POINTER(_vp)], _c_int),
+        "sv_dev_free": ([_vp, _vp], _c_int),
+        "sv_copy_to_device": ([_vp, _vp, _vp, ctypes.c_uint64], _c_int),
+        "sv_copy_to_host": ([_vp, _vp, _vp, ctypes.c_uint64], _c_int),
         "sv_profile_enable": ([_vp, _c_int], _c_int),
         "sv_profile_read": ([_vp, _c_int, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_longlong)], _c_int),
@@ -241,6 +248,39 @@ class Engine:
                                                      int(min_disp), int(num_disp), int(win),
                                                      _cost(cost), d16, hr))
         return (d16, hr) if harris else d16
+
+    def disparity_rows(self, left, right, min_disp: int, num_disp: int, win: int, row0: int,
+                       row1: int, cost="sad", out: np.ndarray | None = None) -> np.ndarray:
+        """Rows [row0, row1) of the int16 x16 disparity (a row-tiled shard); other rows of
+        ``out`` are left untouched."""
+        left, H, W, C = _image(left)
+        right, H2, W2, C2 = _image(right)
+        if (H, W, C) != (H2, W2, C2):
+            raise ValueError("left/right shapes differ")
+        if out is None:
+            out = np.zeros((H, W), np.int16)
+        _check("sv_disparity_rows", self.lib.sv_disparity_rows(
+            self._h, left, right, H, W, C, W * C, int(min_disp), int(num_disp), int(win),
+            _cost(cost), int(row0), int(row1), out))
+        return out
+
+    # -- device buffers (torch-free zero-copy use) ------------------------------------
+    def dev_alloc(self, nbytes: int) -> int:
+        p = _vp()
+        _check("sv_dev_alloc", self.lib.sv_dev_alloc(self._h, int(nbytes), ctypes.byref(p)))
+        return p.value
+
+    def dev_free(self, ptr: int):
+        _check("sv_dev_free", self.lib.sv_dev_free(self._h, ptr))
+
+    def to_device(self, ptr: int, a: np.ndarray):
+        a = np.ascontiguousarray(a)
+        _check("sv_copy_to_device", self.lib.sv_copy_to_device(self._h, ptr, a.ctypes.data, a.nbytes))
+
+    def to_host(self, ptr: int, shape, dtype) -> np.ndarray:
+        out = np.empty(shape, dtype)
+        _check("sv_copy_to_host", self.lib.sv_copy_to_host(self._h, out.ctypes.data, ptr, out.nbytes))
+        return out
 
     def median5(self, a: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(a, np.float32)

@@ -185,3 +185,145 @@ def test_vga_stream_config_with_harris(engine):
         d16, hr = engine.disparity(L, R, 0, 64, 9, harris=True)
         np.testing.assert_array_equal(d16, C.disparity16(L, R, 0, 64, 9, 0))
         assert np.abs(hr - C.harris(L)).max() <= HARRIS_TOL
+
+
+# ---- row tiling, device API, golden fixtures, torch-first runtime ------------------------
+GOLDEN = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "golden_v1.npz")
+
+
+def test_golden_fixtures_on_gpu(engine):
+    g = np.load(GOLDEN)
+    names = sorted({k.split("_")[0] for k in g.files if k.endswith("_params")})
+    for n in names:
+        L, R = g[f"{n}_left"], g[f"{n}_right"]
+        mn, D, win = (int(v) for v in g[f"{n}_params"])
+        for cname in ("sad", "ssd", "hog"):
+            np.testing.assert_array_equal(engine.disparity(L, R, mn, D, win, cname), g[f"{n}_d16_{cname}"])
+        depth, disp, norm = engine.depth_map(L, R, mn, D, win, 0.3, 2.0)
+        np.testing.assert_array_equal(disp, g[f"{n}_disparity"])
+        np.testing.assert_array_equal(depth, g[f"{n}_depth_final"])
+        np.testing.assert_array_equal(norm, g[f"{n}_depth_norm"])
+        assert np.abs(engine.harris(L) - g[f"{n}_harris"]).max() <= HARRIS_TOL
+        np.testing.assert_array_equal(engine.hog_hist(L, win), g[f"{n}_hog"])
+    np.testing.assert_array_equal(engine.gray(g["gray_bgr"]), g["gray_out"])
+
+
+@pytest.mark.parametrize("cost,win", [("sad", 9), ("sad", 11), ("ssd", 7), ("hog", 15)])
+def test_row_bands_reassemble_bit_exactly_on_gpu(engine, cost, win):
+    L, R, _ = stereo_pair(131, 700, 128, seed=21)
+    full = engine.disparity(L, R, 0, 128, win, cost)
+    for world in (2, 3, 8):
+        out = np.zeros_like(full)
+        for k in range(world):
+            r0, r1 = 131 * k // world, 131 * (k + 1) // world
+            engine.disparity_rows(L, R, 0, 128, win, r0, r1, cost, out=out)
+        np.testing.assert_array_equal(out, full)
+
+
+def test_device_api_band_pipeline(engine):
+    """sv_disparity_dev + sv_median_post_dev over row bands == the host depth_map path."""
+    H, W, D, win = 70, 400, 64, 9
+    L, R, _ = stereo_pair(H, W, D, seed=5)
+    e_depth, e_disp, e_norm = engine.depth_map(L, R, 0, D, win, 0.3, 2.0)
+    dL, dR = engine.dev_alloc(H * W), engine.dev_alloc(H * W)
+    d16 = engine.dev_alloc(H * W * 2)
+    ddisp, ddepth, dnorm = engine.dev_alloc(H * W * 4), engine.dev_alloc(H * W * 4), engine.dev_alloc(H * W)
+    try:
+        engine.to_device(dL, L)
+        engine.to_device(dR, R)
+        for k in range(3):
+            r0, r1 = H * k // 3, H * (k + 1) // 3
+            h0, h1 = max(0, r0 - 2), min(H, r1 + 2)
+            engine.disparity_dev(dL, dR, H, W, W, 0, D, win, "sad", h0, h1, d16, W)
+            engine.median_post_dev(d16, H, W, r0, r1, 1, ddisp, ddepth, dnorm,
+                                   min_depth=0.3, max_depth=2.0, min_disp_global=0)
+        np.testing.assert_array_equal(engine.to_host(ddisp, (H, W), np.float32), e_disp)
+        np.testing.assert_array_equal(engine.to_host(ddepth, (H, W), np.float32), e_depth)
+        np.testing.assert_array_equal(engine.to_host(dnorm, (H, W), np.uint8), e_norm)
+        # whole device path in one call
+        engine.depth_map_dev(dL, dR, H, W, W, 0, D, win, 0.3, 2.0, ddepth, ddisp, dnorm)
+        np.testing.assert_array_equal(engine.to_host(ddepth, (H, W), np.float32), e_depth)
+    finally:
+        for p in (dL, dR, d16, ddisp, ddepth, dnorm):
+            engine.dev_free(p)
+
+
+def test_profiling_counters(engine):
+    L, R = _pair(40, 300, 64, seed=1)
+    engine.profile(True)
+    engine.profile_reset()
+    for _ in range(3):
+        engine.depth_map(L, R, 0, 64, 9, 0.3, 2.0)
+    engine.profile(False)
+    ms, n = engine.profile_read("match")
+    assert n == 3 and ms > 0
+    ms, n = engine.profile_read("median")
+    assert n == 3 and ms > 0
+
+
+def test_thread_pool_usage_like_reference(engine):
+    """fused_depth_map.py:2591-2598 submits the stereo call to a ThreadPoolExecutor."""
+    from concurrent.futures import ThreadPoolExecutor
+    from stereovision_amd import fused_depth_map as FDM
+    L, R = _pair(60, 300, 96, seed=8)
+    bl, br = to_bgr(L), to_bgr(R)
+    exp = O.create_depth_map_stereo_scaled(bl, br, 0, 96, 5)
+    with ThreadPoolExecutor(max_workers=2) as ex:
+        futs = [ex.submit(FDM.create_depth_map_stereo_scaled, bl.copy(), br.copy(), 0, 96, 5)
+                for _ in range(6)]
+        for f in futs:
+            dn, disp, cmap, conf = f.result(timeout=30)
+            np.testing.assert_array_equal(disp, exp[1])
+            np.testing.assert_array_equal(conf, exp[3])
+
+
+def test_dropin_create_depth_map_end_to_end(engine, monkeypatch):
+    from stereovision_amd import depth_map as DM
+    monkeypatch.setattr(DM, "NUM_DISP", 64)
+    monkeypatch.setattr(DM, "WINDOW_SIZE", 9)
+    L, R = _pair(50, 320, 64, seed=9)
+    depth, disp, cmap = DM.create_depth_map(to_bgr(L), to_bgr(R), None, 0.2, 4.0)
+    e = O.create_depth_map(to_bgr(L), to_bgr(R), 0, 64, 9, 0.2, 4.0)
+    np.testing.assert_array_equal(depth, e[0])
+    np.testing.assert_array_equal(disp, e[1])
+    assert cmap.shape == (50, 320, 3)
+    # reference default globals (NUM_DISP=320, WINDOW_SIZE=7) on a frame wide enough
+    monkeypatch.setattr(DM, "NUM_DISP", 320)
+    monkeypatch.setattr(DM, "WINDOW_SIZE", 7)
+    L, R = _pair(30, 700, 320, seed=10)
+    depth, disp, cmap = DM.create_depth_map(L, R)
+    np.testing.assert_array_equal(disp, O.disparity_f32(C.disparity16(L, R, 0, 320, 7, 0)))
+
+
+def test_torch_first_runtime_and_row_tiled_module():
+    """bench.py / distributed.py import torch first (libsvhip then binds to torch's HIP
+    runtime); run that configuration in a fresh process and check RowTiledDepthMap bands."""
+    import subprocess, sys, textwrap, os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent("""
+        import sys; sys.path[:0] = [%r, %r]
+        import torch, numpy as np
+        import sv_oracle as O, sv_oracle_c as C
+        from stereovision_amd.distributed import RowTiledDepthMap
+        from stereovision_amd.synthetic import stereo_pair
+        H, W, D, win = 97, 500, 64, 9
+        L, R, _ = stereo_pair(H, W, D, seed=3)
+        dL, dR = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+        ref = O.disparity_f32(C.disparity16(L, R, 0, D, win, 0))
+        ref_depth, _ = O.depth_post(ref, 0.3, 2.0)
+        for world in (1, 2, 4):
+            disp = np.zeros((H, W), np.float32); depth = np.zeros((H, W), np.float32)
+            for k in range(world):
+                rt = RowTiledDepthMap(H, W, D, win, rank=k, world=world)
+                bd, ba, bu, bb = rt.compute(dL, dR)
+                torch.cuda.synchronize()
+                disp[rt.r0:rt.r1] = bd.cpu().numpy(); depth[rt.r0:rt.r1] = ba.cpu().numpy()
+            assert np.array_equal(disp, ref), world
+            assert np.array_equal(depth, ref_depth), world
+        maps = open('/proc/self/maps').read()
+        assert '/torch/lib/libamdhip64.so' in maps and '/opt/rocm' not in ''.join(
+            l for l in maps.splitlines() if 'libamdhip64' in l)
+        print('ok')
+    """ % (root, os.path.join(root, "oracle")))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

@@ -109,15 +109,28 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed loop")
+    ap.add_argument("--mode", default="frames", choices=["frames", "rowtile"],
+                    help="frames: independent frames per rank (C4, weak scaling); rowtile: "
+                         "one frame row-tiled across ranks + RCCL row gather (C5, strong)")
+    ap.add_argument("--gather", action="store_true",
+                    help="frames mode: gather every step's disparity maps to rank 0 (RCCL)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo rehearses N>1 with several ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = local if world > 1 else 0
+    ndev = torch.cuda.device_count()
+    dev = local % max(1, ndev) if world > 1 else 0
     torch.cuda.set_device(dev)
+    gloo = args.dist_backend == "gloo"
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    comm_dev = "cpu" if gloo else f"cuda:{dev}"
 
     H, W, D, win = args.height, args.width, args.num_disp, args.win
     F = max(1, args.frames)
@@ -133,11 +146,35 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     pL = [dL[i].data_ptr() for i in range(F)]
     pR = [dR[i].data_ptr() for i in range(F)]
+    rowtile = args.mode == "rowtile"
+    if rowtile:
+        from stereovision_amd.distributed import RowTiledDepthMap, gather_rows
+        L0, R0 = stereo_batch(1, H, W, D, seed=4242)      # the SAME frame on every rank
+        dL = torch.from_numpy(L0).to(f"cuda:{dev}")
+        dR = torch.from_numpy(R0).to(f"cuda:{dev}")
+        tile = RowTiledDepthMap(H, W, D, win, cost=args.cost, device=dev,
+                                rank=rank, world=world)
+
+    def gather(t):
+        if world == 1:
+            return
+        src = t.to(comm_dev) if gloo else t
+        if rowtile:
+            gather_rows(src, H)
+        else:
+            out = torch.empty((world,) + tuple(src.shape), dtype=src.dtype, device=src.device)
+            dist.all_gather_into_tensor(out, src.unsqueeze(0).contiguous())
 
     def step(i):
+        if rowtile:
+            band_disp, _, _, _ = tile.compute(dL[0], dR[0])
+            gather(band_disp)
+            return
         f = i % F
         eng.depth_map_dev(pL[f], pR[f], H, W, W, 0, D, win, 0.3, 2.0, depth.data_ptr(),
                           disp.data_ptr(), norm.data_ptr(), cost=args.cost, stream=stream)
+        if args.gather:
+            gather(disp)
 
     for i in range(args.warmup):
         step(i)
@@ -161,17 +198,19 @@ def main():
     med_ms, med_n = eng.profile_read("median")
 
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    frames = world * args.steps
+    frames = args.steps if rowtile else world * args.steps
     value = frames / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
     npx = H * W
+    if rowtile:       # per-launch work is one band (+ median halo rows) of the frame
+        npx = (tile.h1 - tile.h0) * W
     k_avg_s = (match_ms / match_n) * 1e-3 if match_n else None
     k_bytes = 4 * npx                          # 2 u8 images read + int16 map written
-    frame_bytes = 11 * npx                     # 2 u8 in; depth f32 + disparity f32 + u8 out
+    frame_bytes = 11 * H * W                   # 2 u8 in; depth f32 + disparity f32 + u8 out
     taps = npx * D * win * win
     roofline = None
     if k_avg_s:
@@ -192,12 +231,15 @@ def main():
         "metric": "disparity frames/sec + HBM GB/s, 1920x1080 D=128 win=9, 1/2/4/8 GPU",
         "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "scaling": "strong" if rowtile else "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic rectified pairs (stereovision_amd.synthetic, seeds per rank)",
         "config": {"workload": f"{W}x{H} D={D} win={win} {args.cost.upper()} depth_map path "
                                "(disparity + median5 + depth post), gray inputs resident in HBM",
                    "height": H, "width": W, "num_disp": D, "win": win, "cost": args.cost,
-                   "frames_resident_per_rank": F, "parallelism": f"frame-sharded x{world}"},
+                   "frames_resident_per_rank": 1 if rowtile else F,
+                   "parallelism": (f"row-tiled x{world} + RCCL row gather" if rowtile else
+                                   f"frame-sharded x{world}" + (" + RCCL gather" if args.gather else "")),
+                   "dist_backend": args.dist_backend if world > 1 else None},
         "hbm_gbs_frame_path": round(frame_bytes * value / 1e9, 2),
         "roofline": roofline,
         "cpu_baseline": None,

@@ -91,7 +91,20 @@ struct sv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
-    DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin;
+    DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut;
+    // cached post-processing table: key = (mode, params, range); `lut_ev` marks its build
+    struct LutKey {
+        int mode = -1, min_disp = 0, num_disp = 0, m0 = 0, n = 0;
+        float minf = 0, maxf = 0, rangef = 0, mdg = 0;
+        bool operator==(const LutKey& o) const {
+            return mode == o.mode && min_disp == o.min_disp && num_disp == o.num_disp && m0 == o.m0 &&
+                   n == o.n && std::memcmp(&minf, &o.minf, sizeof(float)) == 0 &&
+                   std::memcmp(&maxf, &o.maxf, sizeof(float)) == 0 &&
+                   std::memcmp(&rangef, &o.rangef, sizeof(float)) == 0 &&
+                   std::memcmp(&mdg, &o.mdg, sizeof(float)) == 0;
+        }
+    } lut_key;
+    hipEvent_t lut_ev = nullptr;
     HostBuf hin, hout;
     bool prof = false;
     std::vector<EvPair> pending;
@@ -199,6 +212,42 @@ int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int 
         a.HR = c->hog[1].as<uint16_t>();
     }
     SV_LAUNCH(c, SV_K_MATCH, s, sv::launch_match(a, plan, cost, s));
+    return 0;
+}
+
+// Attach the cached post-processing table for the median kernel (built on first use of a
+// parameter set; covers every int16 x16 value a map with this (min_disp, num_disp) holds).
+int attach_lut(sv_ctx* c, sv::PostParams& pp, hipStream_t s) {
+    pp.lut_n = 0;
+    if (pp.mode == SV_POST_NONE || pp.num_disp <= 0 || pp.num_disp > 512) return 0;
+    sv_ctx::LutKey k;
+    k.mode = pp.mode;
+    k.min_disp = pp.min_disp;
+    k.num_disp = pp.num_disp;
+    k.m0 = (pp.min_disp - 1) * 16;
+    k.n = (pp.num_disp + 1) * 16;
+    k.minf = pp.minf;
+    k.maxf = pp.maxf;
+    k.rangef = pp.rangef;
+    k.mdg = pp.min_disp_global;
+    const size_t n = (size_t)k.n;
+    float* la = c->lut.as<float>();
+    if (!(k == c->lut_key) || !c->lut_ev) {
+        SV_HIP(c->lut.ensure(n * (2 * sizeof(float) + 1)));
+        la = c->lut.as<float>();
+        if (!c->lut_ev) SV_HIP(hipEventCreateWithFlags(&c->lut_ev, hipEventDisableTiming));
+        int e = sv::launch_post_lut(pp, k.m0, k.n, la, reinterpret_cast<uint8_t*>(la + 2 * n), la + n, s);
+        if (e) return hipfail(e, "launch_post_lut");
+        SV_HIP(hipEventRecord(c->lut_ev, s));
+        c->lut_key = k;
+    } else {
+        SV_HIP(hipStreamWaitEvent(s, c->lut_ev, 0));   // built earlier, maybe on another stream
+    }
+    pp.lut_a = la;
+    pp.lut_b = la + n;
+    pp.lut_u8 = reinterpret_cast<const uint8_t*>(la + 2 * n);
+    pp.lut_m0 = k.m0;
+    pp.lut_n = k.n;
     return 0;
 }
 
@@ -344,7 +393,8 @@ void sv_destroy(sv_ctx* c) {
         c->prof_drain();
         for (auto e : c->pool) (void)hipEventDestroy(e);
         DevBuf* bufs[] = {&c->img[0], &c->img[1], &c->gray[0], &c->gray[1], &c->d16, &c->fa, &c->fb,
-                          &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin};
+                          &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->lut};
+        if (c->lut_ev) (void)hipEventDestroy(c->lut_ev);
         for (auto* b : bufs) b->release();
         c->hin.release();
         c->hout.release();
@@ -406,6 +456,8 @@ int sv_median_post_dev(sv_ctx* c, const int16_t* d_disp16, int H, int W, int row
     hipStream_t s = pick(c, stream);
     sv::PostParams pp = make_post(mode, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
                                   d_out_a, d_out_u8, d_out_b);
+    int lrc = attach_lut(c, pp, s);
+    if (lrc) return lrc;
     SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(d_disp16, H, W, row0, row1, d_disparity, pp, s));
     return 0;
 }
@@ -424,6 +476,8 @@ int sv_depth_map_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, i
     if (rc) return rc;
     sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
                                   num_disp, d_depth, d_norm, nullptr);
+    rc = attach_lut(c, pp, s);
+    if (rc) return rc;
     SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, d_disparity, pp, s));
     return 0;
 }
@@ -613,6 +667,8 @@ int sv_depth_map(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, in
     if (rc) return rc;
     sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
                                   num_disp, c->fb.as<float>(), c->u8.as<uint8_t>(), nullptr);
+    rc = attach_lut(c, pp, c->stream);
+    if (rc) return rc;
     SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
               sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fa.as<float>(), pp, c->stream));
     Out o[] = {{depth_final, c->fb.p, n * sizeof(float)},
@@ -643,6 +699,8 @@ int sv_stereo_scaled(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H
     if (rc) return rc;
     sv::PostParams pp = make_post(SV_POST_SCALED, 0.f, 0.f, 0.f, 0.f, min_disp, num_disp, c->fb.as<float>(),
                                   c->u8.as<uint8_t>(), c->fc.as<float>());
+    rc = attach_lut(c, pp, c->stream);
+    if (rc) return rc;
     SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
               sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fa.as<float>(), pp, c->stream));
     Out o[] = {{disparity_normalized, c->fb.p, n * sizeof(float)},

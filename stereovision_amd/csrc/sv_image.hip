@@ -228,10 +228,18 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
     for (int h = 0; h < 2; ++h) {
         const int y = y0 + 2 * pr + h;
         if (y >= row1) continue;
-        const float d = (float)(h == 0 ? m.x : m.y) / 16.0f;
+        const int mv = h == 0 ? m.x : m.y;
+        const float d = (float)mv / 16.0f;
         const size_t i = (size_t)y * W + x;
         disp[i] = d;
-        post_one(pp, i, d);
+        const int li = mv - pp.lut_m0;
+        if (pp.mode != POST_NONE && li >= 0 && li < pp.lut_n) {   // table lookup (exact)
+            pp.out_a[i] = pp.lut_a[li];
+            pp.out_u8[i] = pp.lut_u8[li];
+            if (pp.mode == POST_SCALED) pp.out_b[i] = pp.lut_b[li];
+        } else {
+            post_one(pp, i, d);
+        }
     }
 }
 
@@ -267,6 +275,11 @@ __global__ __launch_bounds__(256) void k_median_f32(const float* __restrict__ in
 __global__ void k_post(const float* __restrict__ disp, int n, PostParams pp) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) post_one(pp, (size_t)i, disp[i]);
+}
+
+__global__ void k_post_lut(PostParams pp, int m0, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) post_one(pp, (size_t)i, (float)(m0 + i) / 16.0f);
 }
 
 }  // namespace
@@ -305,6 +318,18 @@ int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float
 int launch_median_f32(const float* in, int H, int W, float* out, hipStream_t s) {
     hipLaunchKernelGGL(k_median_f32, dim3((W + MT_W - 1) / MT_W, (H + MT_H - 1) / MT_H), dim3(256),
                        0, s, in, H, W, out);
+    return (int)hipGetLastError();
+}
+
+int launch_post_lut(const PostParams& pp, int m0, int n, float* lut_a, uint8_t* lut_u8,
+                    float* lut_b, hipStream_t s) {
+    if (n <= 0 || pp.mode == POST_NONE) return 0;
+    PostParams q = pp;
+    q.out_a = lut_a;
+    q.out_u8 = lut_u8;
+    q.out_b = lut_b;
+    q.lut_n = 0;
+    hipLaunchKernelGGL(k_post_lut, dim3((n + 255) / 256), dim3(256), 0, s, q, m0, n);
     return (int)hipGetLastError();
 }
 

@@ -54,10 +54,20 @@ struct PostParams {
     float* out_a;      // DEPTH: depth_final        SCALED: disparity_normalized (f32)
     uint8_t* out_u8;   // DEPTH: depth_normalized   SCALED: disparity_normalized (u8)
     float* out_b;      // SCALED: confidence
+    // Optional lookup table of the post-processing as a function of the int16 x16 median
+    // value m in [lut_m0, lut_m0 + lut_n), built by launch_post_lut with the same f32 ops
+    // (bit-identical to evaluating post_one per pixel; replaces two IEEE divisions).
+    const float* lut_a;
+    const uint8_t* lut_u8;
+    const float* lut_b;
+    int lut_m0, lut_n;
 };
 int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float* disp,
                       const PostParams& pp, hipStream_t s);
 int launch_median_f32(const float* in, int H, int W, float* out, hipStream_t s);
 int launch_post(const float* disp, int n, const PostParams& pp, hipStream_t s);
+// Evaluates the post-processing of pp.mode for m = m0 .. m0+n-1 (d = m/16) into the tables.
+int launch_post_lut(const PostParams& pp, int m0, int n, float* lut_a, uint8_t* lut_u8,
+                    float* lut_b, hipStream_t s);
 
 }  // namespace sv

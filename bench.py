@@ -5,7 +5,10 @@ Workload (BASELINE.json metric): 1920x1080 rectified synthetic pairs, D=128, 9x9
 window, the whole device path of depth_map.create_depth_map per frame:
     disparity (k_match) -> medianBlur 5 + depth post (k_median_i16, fused)
 Inputs are gray u8 pairs already resident in HBM (8 distinct frames per rank, cycled);
-outputs are depth f32, disparity f32 and depth u8 per frame.  One step = one frame pair.
+outputs are depth f32, disparity f32 and depth u8 per frame.  One step = one batch of
+--batch frame pairs (default 8) through sv_depth_map_batch_dev: one k_match and one
+k_median_i16 launch over the whole batch (grid.z = frame), which keeps all 256 CUs busy
+instead of leaving a partial last wave of blocks per frame.  --batch 1 = one call per frame.
 
 Multi-GPU: one process per GPU (torch.distributed.run), frames sharded across ranks with
 no collective in the data path (weak scaling); value = frames of all ranks / max time.
@@ -106,6 +109,9 @@ def main():
     ap.add_argument("--win", type=int, default=9)
     ap.add_argument("--cost", default="sad", choices=["sad", "ssd", "hog"])
     ap.add_argument("--frames", type=int, default=8, help="distinct resident frames per rank")
+    ap.add_argument("--batch", type=int, default=8,
+                    help="frames mode: frames per step, one launch per kernel over the batch "
+                         "(sv_depth_map_batch_dev); 1 = one frame per call (latency mode)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed loop")
@@ -134,12 +140,14 @@ def main():
 
     H, W, D, win = args.height, args.width, args.num_disp, args.win
     F = max(1, args.frames)
+    B = max(1, min(args.batch, F))
+    F = (F // B) * B
     L, R = stereo_batch(F, H, W, D, seed=1000 * rank)
     dL = torch.from_numpy(L).to(f"cuda:{dev}")
     dR = torch.from_numpy(R).to(f"cuda:{dev}")
-    depth = torch.empty((H, W), dtype=torch.float32, device=f"cuda:{dev}")
-    disp = torch.empty((H, W), dtype=torch.float32, device=f"cuda:{dev}")
-    norm = torch.empty((H, W), dtype=torch.uint8, device=f"cuda:{dev}")
+    depth = torch.empty((B, H, W), dtype=torch.float32, device=f"cuda:{dev}")
+    disp = torch.empty((B, H, W), dtype=torch.float32, device=f"cuda:{dev}")
+    norm = torch.empty((B, H, W), dtype=torch.uint8, device=f"cuda:{dev}")
     torch.cuda.synchronize()
 
     eng = get_engine(dev)
@@ -170,9 +178,14 @@ def main():
             band_disp, _, _, _ = tile.compute(dL[0], dR[0])
             gather(band_disp)
             return
-        f = i % F
-        eng.depth_map_dev(pL[f], pR[f], H, W, W, 0, D, win, 0.3, 2.0, depth.data_ptr(),
-                          disp.data_ptr(), norm.data_ptr(), cost=args.cost, stream=stream)
+        f = (i * B) % F
+        if B == 1:
+            eng.depth_map_dev(pL[f], pR[f], H, W, W, 0, D, win, 0.3, 2.0, depth.data_ptr(),
+                              disp.data_ptr(), norm.data_ptr(), cost=args.cost, stream=stream)
+        else:
+            eng.depth_map_batch_dev(pL[f], pR[f], B, H, W, W, H * W, 0, D, win, 0.3, 2.0,
+                                    depth.data_ptr(), disp.data_ptr(), norm.data_ptr(),
+                                    cost=args.cost, stream=stream)
         if args.gather:
             gather(disp)
 
@@ -202,10 +215,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    frames = args.steps if rowtile else world * args.steps
+    frames = args.steps if rowtile else world * args.steps * B
     value = frames / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
-    npx = H * W
+    npx = H * W * (1 if rowtile else B)
     if rowtile:       # per-launch work is one band (+ median halo rows) of the frame
         npx = (tile.h1 - tile.h0) * W
     k_avg_s = (match_ms / match_n) * 1e-3 if match_n else None
@@ -237,6 +250,7 @@ def main():
                                "(disparity + median5 + depth post), gray inputs resident in HBM",
                    "height": H, "width": W, "num_disp": D, "win": win, "cost": args.cost,
                    "frames_resident_per_rank": 1 if rowtile else F,
+                   "frames_per_step": 1 if rowtile else B,
                    "parallelism": (f"row-tiled x{world} + RCCL row gather" if rowtile else
                                    f"frame-sharded x{world}" + (" + RCCL gather" if args.gather else "")),
                    "dist_backend": args.dist_backend if world > 1 else None},

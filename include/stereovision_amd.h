@@ -149,6 +149,29 @@ int sv_depth_map_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
                      float max_depth, float depth_range, float min_disp_global, float* d_depth,
                      float* d_disparity, uint8_t* d_norm, void* stream);
 
+/* ---- frame batches (one launch per kernel over grid.z) ------------------------------
+ * A batch of n_frames equally-shaped gray pairs, frame z at d_left/d_right + z*frame_stride
+ * bytes.  Replaces the reference's per-frame loop over the same calls (depth_map.py:837-946
+ * called once per captured frame, fused_depth_map.py:2591-2598) when frames are queued:
+ * one launch per kernel fills the GPU even for small frames.  Outputs are dense per frame
+ * (frame z of an H x W output at + z*H*W elements) except sv_disparity_batch_dev's int16
+ * map, which takes an explicit out_pitch / out_frame_stride (elements).  The context's
+ * internal scratch (sv_depth_map_batch_dev) assumes calls on one context use one stream. */
+int sv_disparity_batch_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
+                           int n_frames, int H, int W, int pitch, int64_t frame_stride,
+                           int min_disp, int num_disp, int win, int cost, int16_t* d_disp16,
+                           int out_pitch, int64_t out_frame_stride, void* stream);
+int sv_median_post_batch_dev(sv_ctx* ctx, const int16_t* d_disp16, int n_frames, int H, int W,
+                             int mode, float min_depth, float max_depth, float depth_range,
+                             float min_disp_global, int min_disp, int num_disp,
+                             float* d_disparity, float* d_out_a, uint8_t* d_out_u8,
+                             float* d_out_b, void* stream);
+int sv_depth_map_batch_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
+                           int n_frames, int H, int W, int pitch, int64_t frame_stride,
+                           int min_disp, int num_disp, int win, int cost, float min_depth,
+                           float max_depth, float depth_range, float min_disp_global,
+                           float* d_depth, float* d_disparity, uint8_t* d_norm, void* stream);
+
 int sv_harris_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, float* d_out,
                   void* stream);
 int sv_hog_hist_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, int win,

@@ -171,9 +171,20 @@ int check_match(int H, int W, int min_disp, int num_disp, int win, int cost, sv:
 }
 
 // Enqueue disparity for rows [row0,row1) of gray device images.
+// nf > 1: a batch of frames, frame z at L/R + z*fs_in bytes and out + z*fs_out elements
+// (one launch over grid.z; HOG runs frame by frame through its histogram scratch).
 int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, int pitch,
                       int min_disp, int num_disp, int win, int cost, int row0, int row1,
-                      int16_t* out, int opitch, hipStream_t s) {
+                      int16_t* out, int opitch, hipStream_t s, int nf = 1, long long fs_in = 0,
+                      long long fs_out = 0) {
+    if (nf > 1 && cost == SV_COST_HOG) {
+        for (int z = 0; z < nf; ++z) {
+            int rc = enqueue_disparity(c, L + z * fs_in, R + z * fs_in, H, W, pitch, min_disp, num_disp,
+                                       win, cost, row0, row1, out + z * fs_out, opitch, s);
+            if (rc) return rc;
+        }
+        return 0;
+    }
     sv::MatchPlan plan;
     int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
     if (rc) return rc;
@@ -202,6 +213,10 @@ int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int 
     a.dbits = plan.dbits;
     a.out = out;
     a.opitch = opitch;
+    a.nf = nf < 1 ? 1 : nf;
+    a.fs_in = fs_in;
+    a.fs_out = fs_out;
+    a.fs_hist = 0;
     if (cost == SV_COST_HOG && a.X1 > a.X0) {
         const size_t hb = (size_t)H * W * 10 * sizeof(uint16_t);
         SV_HIP(c->hog[0].ensure(hb));
@@ -479,6 +494,67 @@ int sv_depth_map_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, i
     rc = attach_lut(c, pp, s);
     if (rc) return rc;
     SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, d_disparity, pp, s));
+    return 0;
+}
+
+int sv_disparity_batch_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, int n_frames, int H,
+                           int W, int pitch, int64_t frame_stride, int min_disp, int num_disp, int win,
+                           int cost, int16_t* d_disp16, int out_pitch, int64_t out_frame_stride,
+                           void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_left, H, W) || check_image(d_right, H, W) || !d_disp16 || n_frames < 0)
+        return fail(SV_EINVAL, "bad disparity arguments");
+    if (pitch < W || out_pitch < W) return fail(SV_EINVAL, "pitch smaller than width");
+    if (n_frames > 1 && (frame_stride < (int64_t)pitch * H || out_frame_stride < (int64_t)out_pitch * H))
+        return fail(SV_EINVAL, "frame stride smaller than a frame");
+    if (n_frames == 0) return 0;
+    return enqueue_disparity(c, d_left, d_right, H, W, pitch, min_disp, num_disp, win, cost, 0, H, d_disp16,
+                             out_pitch, pick(c, stream), n_frames, frame_stride, out_frame_stride);
+}
+
+int sv_median_post_batch_dev(sv_ctx* c, const int16_t* d_disp16, int n_frames, int H, int W, int mode,
+                             float min_depth, float max_depth, float depth_range, float min_disp_global,
+                             int min_disp, int num_disp, float* d_disparity, float* d_out_a,
+                             uint8_t* d_out_u8, float* d_out_b, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_disp16, H, W) || !d_disparity || n_frames < 0) return fail(SV_EINVAL, "bad median arguments");
+    if (mode == SV_POST_DEPTH && (!d_out_a || !d_out_u8)) return fail(SV_EINVAL, "depth post outputs missing");
+    if (mode == SV_POST_SCALED && (!d_out_a || !d_out_u8 || !d_out_b || num_disp <= 0))
+        return fail(SV_EINVAL, "scaled post outputs missing");
+    if (n_frames == 0) return 0;
+    hipStream_t s = pick(c, stream);
+    sv::PostParams pp = make_post(mode, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
+                                  d_out_a, d_out_u8, d_out_b);
+    int rc = attach_lut(c, pp, s);
+    if (rc) return rc;
+    const long long fs = (long long)H * W;
+    SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(d_disp16, H, W, 0, H, d_disparity, pp, s, n_frames, fs, fs));
+    return 0;
+}
+
+int sv_depth_map_batch_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, int n_frames, int H, int W,
+                           int pitch, int64_t frame_stride, int min_disp, int num_disp, int win, int cost,
+                           float min_depth, float max_depth, float depth_range, float min_disp_global,
+                           float* d_depth, float* d_disparity, uint8_t* d_norm, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_left, H, W) || check_image(d_right, H, W) || !d_depth || !d_disparity || !d_norm ||
+        n_frames < 0)
+        return fail(SV_EINVAL, "bad depth-map arguments");
+    if (pitch < W) return fail(SV_EINVAL, "pitch smaller than width");
+    if (n_frames > 1 && frame_stride < (int64_t)pitch * H) return fail(SV_EINVAL, "frame stride smaller than a frame");
+    if (n_frames == 0) return 0;
+    hipStream_t s = pick(c, stream);
+    const long long fs = (long long)H * W;
+    SV_HIP(c->d16.ensure((size_t)n_frames * fs * sizeof(int16_t)));
+    int rc = enqueue_disparity(c, d_left, d_right, H, W, pitch, min_disp, num_disp, win, cost, 0, H,
+                               c->d16.as<int16_t>(), W, s, n_frames, frame_stride, fs);
+    if (rc) return rc;
+    sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                                  num_disp, d_depth, d_norm, nullptr);
+    rc = attach_lut(c, pp, s);
+    if (rc) return rc;
+    SV_LAUNCH(c, SV_K_MEDIAN, s,
+              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, d_disparity, pp, s, n_frames, fs, fs));
     return 0;
 }
 

@@ -194,8 +194,16 @@ constexpr int MT_W = 64, MT_H = 8;   // 64 x 8 outputs; thread = one column x tw
 
 __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ in, int H, int W,
                                                     int row0, int row1, float* __restrict__ disp,
-                                                    PostParams pp) {
+                                                    PostParams pp, long long fs_in, long long fs_out) {
     __shared__ int16_t tile[MT_H + 4][MT_W + 4];
+    if (blockIdx.z) {   // frame batch
+        in += blockIdx.z * fs_in;
+        const long long o = blockIdx.z * fs_out;
+        disp += o;
+        if (pp.out_a) pp.out_a += o;
+        if (pp.out_u8) pp.out_u8 += o;
+        if (pp.out_b) pp.out_b += o;
+    }
     const int x0 = blockIdx.x * MT_W, y0 = row0 + blockIdx.y * MT_H;
     for (int i = threadIdx.x; i < (MT_H + 4) * (MT_W + 4); i += 256) {
         const int ty = i / (MT_W + 4), tx = i % (MT_W + 4);
@@ -308,10 +316,10 @@ int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0
 }
 
 int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float* disp,
-                      const PostParams& pp, hipStream_t s) {
-    if (row1 <= row0) return 0;
-    hipLaunchKernelGGL(k_median_i16, dim3((W + MT_W - 1) / MT_W, (row1 - row0 + MT_H - 1) / MT_H),
-                       dim3(256), 0, s, in, H, W, row0, row1, disp, pp);
+                      const PostParams& pp, hipStream_t s, int nf, long long fs_in, long long fs_out) {
+    if (row1 <= row0 || nf <= 0) return 0;
+    hipLaunchKernelGGL(k_median_i16, dim3((W + MT_W - 1) / MT_W, (row1 - row0 + MT_H - 1) / MT_H, nf),
+                       dim3(256), 0, s, in, H, W, row0, row1, disp, pp, fs_in, fs_out);
     return (int)hipGetLastError();
 }
 

@@ -32,6 +32,10 @@ struct MatchParams {
     int lpg, lpg_log2, dbits;
     int16_t* out;
     int opitch;            // elements
+    // frame batch (grid.z): frame z reads L/R + z*fs_in bytes, HL/HR + z*fs_hist elements
+    // and writes out + z*fs_out elements
+    int nf;
+    long long fs_in, fs_out, fs_hist;
 };
 
 // Host-side launchers (return hipError_t as int).
@@ -62,8 +66,10 @@ struct PostParams {
     const float* lut_b;
     int lut_m0, lut_n;
 };
+// nf frames (grid.z): frame z reads in + z*fs_in and writes disp/out_* + z*fs_out elements.
 int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float* disp,
-                      const PostParams& pp, hipStream_t s);
+                      const PostParams& pp, hipStream_t s, int nf = 1, long long fs_in = 0,
+                      long long fs_out = 0);
 int launch_median_f32(const float* in, int H, int W, float* out, hipStream_t s);
 int launch_post(const float* disp, int n, const PostParams& pp, hipStream_t s);
 // Evaluates the post-processing of pp.mode for m = m0 .. m0+n-1 (d = m/16) into the tables.

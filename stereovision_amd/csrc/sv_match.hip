@@ -230,6 +230,15 @@ __global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a
     constexpr int Q = PackCfg<COST, ND>::Q;
     constexpr int ROWS = PackCfg<COST, ND>::ROWS;
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    if (blockIdx.z) {   // frame batch
+        a.L += blockIdx.z * a.fs_in;
+        a.R += blockIdx.z * a.fs_in;
+        a.out += blockIdx.z * a.fs_out;
+        if constexpr (COST == COST_HOG) {
+            a.HL += blockIdx.z * a.fs_hist;
+            a.HR += blockIdx.z * a.fs_hist;
+        }
+    }
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int LPG = a.lpg;
@@ -365,7 +374,8 @@ int launch_one(const MatchParams& a, size_t lds, hipStream_t s) {
     }
     const int wc = wave_cols(a.lpg, DPL);
     const int rows_per_block = ROWS_PER_BLOCK * PackCfg<COST, ND>::ROWS;
-    dim3 grid((a.X1 - a.X0 + wc - 1) / wc, (a.row1 - a.row0 + rows_per_block - 1) / rows_per_block);
+    dim3 grid((a.X1 - a.X0 + wc - 1) / wc, (a.row1 - a.row0 + rows_per_block - 1) / rows_per_block,
+              a.nf > 1 ? a.nf : 1);
     hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, a);
     return (int)hipGetLastError();
 }
@@ -450,9 +460,14 @@ int launch_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v, hipStream
 
 int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t s) {
     if (a.row1 <= a.row0) return 0;
-    if (a.X1 <= a.X0)
-        return launch_fill_i16(a.out + (size_t)a.row0 * a.opitch, a.opitch, a.row1 - a.row0, a.W,
-                               (int16_t)((a.minD - 1) * 16), s);
+    if (a.X1 <= a.X0) {
+        for (int z = 0; z < (a.nf > 1 ? a.nf : 1); ++z) {
+            int e = launch_fill_i16(a.out + z * a.fs_out + (size_t)a.row0 * a.opitch, a.opitch,
+                                    a.row1 - a.row0, a.W, (int16_t)((a.minD - 1) * 16), s);
+            if (e) return e;
+        }
+        return 0;
+    }
     const size_t lds = match_lds_bytes(p, a.r, cost);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
     switch (kind_of(cost, a.win)) {

@@ -31,7 +31,8 @@ EXPORTED = [
     "sv_hog_hist", "sv_gray_dev", "sv_disparity_dev", "sv_median_post_dev",
     "sv_depth_map_dev", "sv_harris_dev", "sv_hog_hist_dev", "sv_profile_enable",
     "sv_profile_read", "sv_profile_reset", "sv_disparity_rows", "sv_dev_alloc", "sv_dev_free",
-    "sv_copy_to_device", "sv_copy_to_host",
+    "sv_copy_to_device", "sv_copy_to_host", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
+    "sv_depth_map_batch_dev",
 ]
 
 
@@ -117,6 +118,15 @@ def _declare(lib):
         "sv_dev_free": ([_vp, _vp], _c_int),
         "sv_copy_to_device": ([_vp, _vp, _vp, ctypes.c_uint64], _c_int),
         "sv_copy_to_host": ([_vp, _vp, _vp, ctypes.c_uint64], _c_int),
+        "sv_disparity_batch_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, ctypes.c_int64,
+                                    _c_int, _c_int, _c_int, _c_int, _vp, _c_int, ctypes.c_int64,
+                                    _vp], _c_int),
+        "sv_median_post_batch_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                      _c_float, _c_float, _c_float, _c_int, _c_int, _vp, _vp,
+                                      _vp, _vp, _vp], _c_int),
+        "sv_depth_map_batch_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
+                                    ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                    _c_float, _c_float, _c_float, _vp, _vp, _vp, _vp], _c_int),
         "sv_profile_enable": ([_vp, _c_int], _c_int),
         "sv_profile_read": ([_vp, _c_int, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_longlong)], _c_int),
@@ -388,6 +398,38 @@ class Engine:
             _cost(cost), np.float32(min_depth), np.float32(max_depth),
             np.float32(float(max_depth) - float(min_depth)), np.float32(mdg), d_depth, d_disp,
             d_norm, stream or None))
+
+    # -- frame batches (one launch per kernel over all frames) ------------------------------
+    def disparity_batch_dev(self, d_left: int, d_right: int, n_frames: int, H: int, W: int,
+                            pitch: int, frame_stride: int, min_disp: int, num_disp: int,
+                            win: int, cost, d_out16: int, out_pitch: int,
+                            out_frame_stride: int, stream: int = 0):
+        _check("sv_disparity_batch_dev", self.lib.sv_disparity_batch_dev(
+            self._h, d_left, d_right, int(n_frames), H, W, pitch, int(frame_stride),
+            int(min_disp), int(num_disp), int(win), _cost(cost), d_out16, out_pitch,
+            int(out_frame_stride), stream or None))
+
+    def median_post_batch_dev(self, d_disp16: int, n_frames: int, H: int, W: int, mode: int,
+                              d_disparity: int, d_out_a: int = 0, d_out_u8: int = 0,
+                              d_out_b: int = 0, min_depth=0.0, max_depth=0.0,
+                              min_disp_global=0.0, min_disp=0, num_disp=0, stream: int = 0):
+        _check("sv_median_post_batch_dev", self.lib.sv_median_post_batch_dev(
+            self._h, d_disp16, int(n_frames), H, W, int(mode), np.float32(min_depth),
+            np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
+            np.float32(min_disp_global), int(min_disp), int(num_disp), d_disparity,
+            d_out_a or None, d_out_u8 or None, d_out_b or None, stream or None))
+
+    def depth_map_batch_dev(self, d_left: int, d_right: int, n_frames: int, H: int, W: int,
+                            pitch: int, frame_stride: int, min_disp: int, num_disp: int,
+                            win: int, min_depth: float, max_depth: float, d_depth: int,
+                            d_disp: int, d_norm: int, cost="sad", min_disp_global=None,
+                            stream: int = 0):
+        mdg = min_disp if min_disp_global is None else min_disp_global
+        _check("sv_depth_map_batch_dev", self.lib.sv_depth_map_batch_dev(
+            self._h, d_left, d_right, int(n_frames), H, W, pitch, int(frame_stride),
+            int(min_disp), int(num_disp), int(win), _cost(cost), np.float32(min_depth),
+            np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
+            np.float32(mdg), d_depth, d_disp, d_norm, stream or None))
 
     def harris_dev(self, d_gray: int, H: int, W: int, pitch: int, d_out: int, stream: int = 0):
         _check("sv_harris_dev", self.lib.sv_harris_dev(self._h, d_gray, H, W, pitch, d_out,

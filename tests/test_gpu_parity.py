@@ -248,6 +248,73 @@ def test_device_api_band_pipeline(engine):
             engine.dev_free(p)
 
 
+@pytest.mark.parametrize("cost,win", [("sad", 9), ("sad", 11), ("ssd", 5), ("hog", 7)])
+def test_frame_batch_matches_single_frames(engine, cost, win):
+    """sv_*_batch_dev (one launch over grid.z) == the per-frame oracle, frame by frame,
+    with a padded input frame stride and a padded output pitch."""
+    nf, H, W, D = 3, 37, 300, 64
+    pitch, fstride = W + 16, (W + 16) * H + 64
+    pairs = [stereo_pair(H, W, D, seed=40 + z)[:2] for z in range(nf)]
+    hL = np.zeros(nf * fstride, np.uint8)
+    hR = np.zeros(nf * fstride, np.uint8)
+    for z, (L, R) in enumerate(pairs):
+        hL[z * fstride: z * fstride + pitch * H].reshape(H, pitch)[:, :W] = L
+        hR[z * fstride: z * fstride + pitch * H].reshape(H, pitch)[:, :W] = R
+    opitch, ofs = W + 8, (W + 8) * H + 40
+    dL, dR = engine.dev_alloc(hL.nbytes), engine.dev_alloc(hR.nbytes)
+    d16 = engine.dev_alloc(nf * ofs * 2)
+    try:
+        engine.to_device(dL, hL)
+        engine.to_device(dR, hR)
+        engine.disparity_batch_dev(dL, dR, nf, H, W, pitch, fstride, 0, D, win, cost, d16, opitch, ofs)
+        out = engine.to_host(d16, (nf * ofs,), np.int16)
+        for z, (L, R) in enumerate(pairs):
+            got = out[z * ofs: z * ofs + opitch * H].reshape(H, opitch)[:, :W]
+            ref = C.disparity16(L, R, 0, D, win, {"sad": 0, "ssd": 1, "hog": 2}[cost])
+            np.testing.assert_array_equal(got, ref, err_msg=f"frame {z}")
+    finally:
+        for p in (dL, dR, d16):
+            engine.dev_free(p)
+
+
+def test_depth_map_batch_dev_and_scaled_batch(engine):
+    nf, H, W, D, win = 4, 45, 320, 64, 9
+    pairs = [stereo_pair(H, W, D, seed=60 + z)[:2] for z in range(nf)]
+    hL = np.stack([p[0] for p in pairs])
+    hR = np.stack([p[1] for p in pairs])
+    n = nf * H * W
+    dL, dR = engine.dev_alloc(n), engine.dev_alloc(n)
+    ddepth, ddisp, dnorm, dconf = (engine.dev_alloc(n * 4), engine.dev_alloc(n * 4),
+                                   engine.dev_alloc(n), engine.dev_alloc(n * 4))
+    d16 = engine.dev_alloc(n * 2)
+    try:
+        engine.to_device(dL, hL)
+        engine.to_device(dR, hR)
+        engine.depth_map_batch_dev(dL, dR, nf, H, W, W, H * W, 0, D, win, 0.3, 2.0, ddepth, ddisp, dnorm)
+        depth = engine.to_host(ddepth, (nf, H, W), np.float32)
+        disp = engine.to_host(ddisp, (nf, H, W), np.float32)
+        norm = engine.to_host(dnorm, (nf, H, W), np.uint8)
+        for z, (L, R) in enumerate(pairs):
+            e = O.create_depth_map(L, R, 0, D, win, 0.3, 2.0)
+            np.testing.assert_array_equal(depth[z], e[0], err_msg=f"frame {z}")
+            np.testing.assert_array_equal(disp[z], e[1], err_msg=f"frame {z}")
+            np.testing.assert_array_equal(norm[z], e[2], err_msg=f"frame {z}")
+        # scaled post over the same batch of int16 maps (app 2)
+        engine.disparity_batch_dev(dL, dR, nf, H, W, W, H * W, 0, D, win, "sad", d16, W, H * W)
+        engine.median_post_batch_dev(d16, nf, H, W, 2, ddisp, ddepth, dnorm, dconf, min_disp=0, num_disp=D)
+        a = engine.to_host(ddepth, (nf, H, W), np.float32)
+        u8 = engine.to_host(dnorm, (nf, H, W), np.uint8)
+        conf = engine.to_host(dconf, (nf, H, W), np.float32)
+        for z, (L, R) in enumerate(pairs):
+            e = O.create_depth_map_stereo_scaled(L, R, 0, D, win)
+            np.testing.assert_array_equal(a[z], e[0], err_msg=f"frame {z}")
+            np.testing.assert_array_equal(u8[z], e[2], err_msg=f"frame {z}")
+            np.testing.assert_array_equal(conf[z], e[3], err_msg=f"frame {z}")
+    finally:
+        for p in (dL, dR, ddepth, ddisp, dnorm, dconf, d16):
+            engine.dev_free(p)
+
+
 def test_profiling_counters(engine):
     L, R = _pair(40, 300, 64, seed=1)
     engine.profile(True)

@@ -231,7 +231,8 @@ def main():
         roofline = {
             "kernel": "k_match", "bound": "hbm", "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": pmc_traffic(f"{W}x{H}_D{D}_w{win}_{args.cost}"),
+            "traffic": pmc_traffic(f"{W}x{H}_D{D}_w{win}_{args.cost}" +
+                                   (f"_b{B}" if B > 1 and not rowtile else "")),
             "bytes_per_launch": k_bytes, "avg_launch_us": round(k_avg_s * 1e6, 2),
             "launches": match_n,
             "valu": {"achieved_taps_per_s": taps / k_avg_s, "peak_taps_per_s": VALU_TAP_PEAK,

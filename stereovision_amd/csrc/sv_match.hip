@@ -144,11 +144,116 @@ __device__ __forceinline__ void build_pack(const MatchParams& a, const uint8_t* 
     }
 }
 
+// ---- vectorised pack building: one lane = 4 consecutive in-bounds columns -------------
+// Each window row is read as ONE dword (4 columns) and 4 rows x 4 columns are transposed
+// with v_perm_b32 into the 4 columns' pack words (8 perms per 16 bytes), instead of one
+// clamped byte load + shift/select chain per (row, column).
+__device__ __forceinline__ void transpose4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t (&o)[4]) {
+    const uint32_t t0 = __builtin_amdgcn_perm(b, a, 0x05010400u);   // a0 b0 a1 b1
+    const uint32_t t1 = __builtin_amdgcn_perm(b, a, 0x07030602u);   // a2 b2 a3 b3
+    const uint32_t t2 = __builtin_amdgcn_perm(d, c, 0x05010400u);   // c0 d0 c1 d1
+    const uint32_t t3 = __builtin_amdgcn_perm(d, c, 0x07030602u);   // c2 d2 c3 d3
+    o[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);              // a0 b0 c0 d0
+    o[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);
+    o[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+    o[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+}
+
+// Pack words of the 4 columns cg..cg+3 (all inside [0, W), 4-byte aligned rows) around
+// output row y; same layout as build_pack.
+template <int COST, int ND>
+__device__ __forceinline__ void build_group(const MatchParams& a, const uint8_t* img, int cg, int y,
+                                            uint32_t (&w)[PackCfg<COST, ND>::NW][4]) {
+    const int r = a.r;
+    auto row = [&](int j) -> uint32_t {
+        const int yy = clampi(y - r + j, 0, a.H - 1);
+        return *reinterpret_cast<const uint32_t*>(img + (size_t)yy * a.pitch + cg);
+    };
+    constexpr int J0 = COST == COST_SAD2 ? 1 : 0;            // first shared row
+    const int nsh = COST == COST_SAD2 ? 2 * r : a.win;       // shared (transposed) rows
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+        uint32_t d[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) d[t] = (4 * q + t < nsh) ? row(J0 + 4 * q + t) : 0u;
+        transpose4(d[0], d[1], d[2], d[3], w[q]);
+    }
+    if constexpr (COST == COST_SAD2) {
+        const uint32_t s0 = row(0), s1 = row(2 * r + 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            w[ND][k] = (s0 >> (8 * k)) & 0xFFu;
+            w[ND + 1][k] = (s1 >> (8 * k)) & 0xFFu;
+        }
+    } else if constexpr (COST == COST_SSD) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t sq = 0u;
+#pragma unroll
+            for (int q = 0; q < ND; ++q) sq = __builtin_amdgcn_udot4(w[q][k], w[q][k], sq, false);
+            w[ND][k] = sq;
+        }
+    }
+}
+
 // Logical right-pack index i -> LDS slot: one empty slot after every DPL packs, phased by
 // c0 so that every DPL-step chunk of a lane's "entering column" reads is DPL consecutive
 // slots (static ds_read offsets) and the 16 lanes of a group, DPL packs apart, land DPL+1
 // slots apart (DPL+1 odd -> distinct 16-byte bank groups for ds_read_b128).
 __device__ __forceinline__ int rslot(int i, int c0, int dpl) { return i + (i + c0) / dpl; }
+
+// All column packs of one wave: L packs i -> column cL0 + i (slot i), R packs i -> column
+// cR0 + i (slot rslot(i)).  Interior 4-column groups take the vectorised path; groups
+// touching the image border (replicate clamp), HOG, and unaligned images take build_pack.
+template <int COST, int ND, int DPL>
+__device__ __forceinline__ void build_all_packs(const MatchParams& a, int y, int cL0, int NL, int cR0,
+                                                int NRlog, int c0, uint4* Lp, uint4* Rp, int lane) {
+    constexpr int NW = PackCfg<COST, ND>::NW;
+    constexpr int Q = PackCfg<COST, ND>::Q;
+    bool aligned = ((reinterpret_cast<uintptr_t>(a.L) | reinterpret_cast<uintptr_t>(a.R) |
+                     (uintptr_t)a.pitch) & 3u) == 0;
+    if constexpr (COST == COST_HOG) aligned = false;
+    if (!aligned) {
+        for (int i = lane; i < NL; i += 64) build_pack<COST, ND>(a, a.L, a.HL, cL0 + i, y, Lp + (size_t)i * Q);
+        for (int i = lane; i < NRlog; i += 64)
+            build_pack<COST, ND>(a, a.R, a.HR, cR0 + i, y, Rp + (size_t)rslot(i, c0, DPL) * Q);
+        return;
+    }
+    if constexpr (COST != COST_HOG) {
+    const int aL = cL0 & ~3, aR = cR0 & ~3;                  // floor to a multiple of 4
+    const int gL = (cL0 + NL - aL + 3) >> 2, gR = (cR0 + NRlog - aR + 3) >> 2;
+    for (int gi = lane; gi < gL + gR; gi += 64) {
+        const bool right = gi >= gL;
+        const int cg = right ? aR + 4 * (gi - gL) : aL + 4 * gi;
+        const int cfirst = right ? cR0 : cL0, n = right ? NRlog : NL;
+        const uint8_t* img = right ? a.R : a.L;
+        uint4* base = right ? Rp : Lp;
+        if (cg >= 0 && cg + 4 <= a.W) {
+            uint32_t w[NW][4];
+            build_group<COST, ND>(a, img, cg, y, w);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int idx = cg + k - cfirst;
+                if (idx < 0 || idx >= n) continue;
+                uint32_t v[4 * Q];
+#pragma unroll
+                for (int i = 0; i < 4 * Q; ++i) v[i] = i < NW ? w[i < NW ? i : 0][k] : 0u;
+                uint4* dst = base + (size_t)(right ? rslot(idx, c0, DPL) : idx) * Q;
+#pragma unroll
+                for (int i = 0; i < Q; ++i) dst[i] = make_uint4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int idx = cg + k - cfirst;
+                if (idx < 0 || idx >= n) continue;
+                build_pack<COST, ND>(a, img, nullptr, cg + k, y,
+                                     base + (size_t)(right ? rslot(idx, c0, DPL) : idx) * Q);
+            }
+        }
+    }
+    }
+}
 
 template <int COST, int ND, int DPL>
 __device__ __forceinline__ void match_chunk(
@@ -259,9 +364,7 @@ __global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a
     const int cL0 = xw - 3 * r - 1;
     const int cR0 = cL0 - a.minD - (LPG * DPL - 1);
 
-    for (int i = lane; i < NL; i += 64) build_pack<COST, ND>(a, a.L, a.HL, cL0 + i, yc, Lp + (size_t)i * Q);
-    for (int i = lane; i < NRlog; i += 64)
-        build_pack<COST, ND>(a, a.R, a.HR, cR0 + i, yc, Rp + (size_t)rslot(i, c0, DPL) * Q);
+    build_all_packs<COST, ND, DPL>(a, yc, cL0, NL, cR0, NRlog, c0, Lp, Rp, lane);
 
     if (blockIdx.x == 0) {  // columns outside the matched band are invalid
         const int16_t inv = (int16_t)((a.minD - 1) * 16);

@@ -55,7 +55,9 @@ enum sv_status {
     SV_ENOMEM = -12,
     SV_ENODEV = -19,
     SV_EINVAL = -22,
-    SV_ERANGE = -34   /* parameters whose argmin key would overflow 32 bits */
+    SV_ERANGE = -34   /* parameters whose argmin key would overflow 32 bits: (cmax << dbits)
+                         >= 2^32, or ((2 cmax + 2) << dbits) >= 2^32 when num_disp leaves
+                         padding disparities in the lane plan (cmax = largest window cost) */
 };
 
 /* post-processing modes of sv_median_post_dev */

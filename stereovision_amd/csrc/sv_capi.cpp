@@ -211,6 +211,7 @@ int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int 
     a.lpg = plan.lpg;
     a.lpg_log2 = plan.lpg == 16 ? 4 : plan.lpg == 32 ? 5 : 6;
     a.dbits = plan.dbits;
+    a.pad_key = (uint32_t)((sv::max_cost(win, cost) + 1) << plan.dbits);
     a.out = out;
     a.opitch = opitch;
     a.nf = nf < 1 ? 1 : nf;

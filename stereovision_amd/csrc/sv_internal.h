@@ -36,10 +36,12 @@ struct MatchParams {
     // and writes out + z*fs_out elements
     int nf;
     long long fs_in, fs_out, fs_hist;
+    uint32_t pad_key;      // (max_cost + 1) << dbits: key offset of padding disparities
 };
 
 // Host-side launchers (return hipError_t as int).
 int plan_match(int num_disp, int win, int cost, MatchPlan* plan);
+uint64_t max_cost(int win, int cost);   // largest window cost of a (win, cost) pair
 size_t match_lds_bytes(const MatchPlan& p, int r, int cost);
 int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t s);
 int launch_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v, hipStream_t s);

@@ -63,40 +63,38 @@ __device__ __forceinline__ Pk<NW> ld(const uint4* p) {
     return v;
 }
 
-// Column cost(s) of one (left pack, right pack) pair.  ROWS = 1: returns acc + cost.
-// SAD2: acc[0] += cost(row y), acc[1] += cost(row y+1) (SUB: -=).
-template <int COST, int ND, int NW, bool SUB>
-__device__ __forceinline__ void vcol(const Pk<NW>& l, const Pk<NW>& r, uint32_t* acc) {
+// Column cost(s) of one (left pack, right pack) pair: v[0] (and v[1] = row y+1 for SAD2).
+template <int COST, int ND, int NW>
+__device__ __forceinline__ void ccol(const Pk<NW>& l, const Pk<NW>& r, uint32_t* v) {
     if constexpr (COST == COST_SAD) {
-        if constexpr (!SUB) {
+        uint32_t a = 0u;
 #pragma unroll
-            for (int i = 0; i < ND; ++i) acc[0] = __builtin_amdgcn_sad_u8(l.w[i], r.w[i], acc[0]);
-        } else {
-            uint32_t v = 0u;
-#pragma unroll
-            for (int i = 0; i < ND; ++i) v = __builtin_amdgcn_sad_u8(l.w[i], r.w[i], v);
-            acc[0] -= v;
-        }
+        for (int i = 0; i < ND; ++i) a = __builtin_amdgcn_sad_u8(l.w[i], r.w[i], a);
+        v[0] = a;
     } else if constexpr (COST == COST_SAD2) {
         uint32_t s = 0u;
 #pragma unroll
         for (int i = 0; i < ND; ++i) s = __builtin_amdgcn_sad_u8(l.w[i], r.w[i], s);
-        const uint32_t v0 = __builtin_amdgcn_sad_u8(l.w[ND], r.w[ND], s);
-        const uint32_t v1 = __builtin_amdgcn_sad_u8(l.w[ND + 1], r.w[ND + 1], s);
-        if constexpr (!SUB) { acc[0] += v0; acc[1] += v1; }
-        else { acc[0] -= v0; acc[1] -= v1; }
+        v[0] = __builtin_amdgcn_sad_u8(l.w[ND], r.w[ND], s);
+        v[1] = __builtin_amdgcn_sad_u8(l.w[ND + 1], r.w[ND + 1], s);
     } else if constexpr (COST == COST_SSD) {
         uint32_t dot = 0u;
 #pragma unroll
         for (int i = 0; i < ND; ++i) dot = __builtin_amdgcn_udot4(l.w[i], r.w[i], dot, false);
-        const uint32_t v = (l.w[ND] + r.w[ND]) - (dot << 1);
-        if constexpr (!SUB) acc[0] += v; else acc[0] -= v;
+        v[0] = (l.w[ND] + r.w[ND]) - (dot << 1);
     } else {  // HOG: 9 u16 bins in 5 dwords; the cost IS the cell value
-        uint32_t v = 0u;
+        uint32_t a = 0u;
 #pragma unroll
-        for (int i = 0; i < 5; ++i) v = __builtin_amdgcn_sad_u16(l.w[i], r.w[i], v);
-        acc[0] = v;
+        for (int i = 0; i < 5; ++i) a = __builtin_amdgcn_sad_u16(l.w[i], r.w[i], a);
+        v[0] = a;
     }
+}
+
+// h + d * m (m = 1 << dbits, |d| < 2^23: one column's cost difference) as ONE
+// v_mad_i32_i24.  Through the mul24 intrinsic LLVM does not factor the per-step updates
+// into running diff sums (which `h += d << s` in plain C gets: an extra add per cell).
+__device__ __forceinline__ uint32_t shl_add(uint32_t d, int m, uint32_t h) {
+    return h + (uint32_t)__mul24((int)d, m);
 }
 
 // Build one column pack for logical column c around output row y (replicate-clamped).
@@ -281,14 +279,23 @@ __device__ __forceinline__ void match_chunk(
 #pragma unroll
         for (int k = 0; k < DPL; ++k) {
             const int sk = (u - k + DPL) % DPL;
-            vcol<COST, ND, NW, false>(L, rn[sk], h[k]);
-            if constexpr (RUN) vcol<COST, ND, NW, true>(LO, ro[sk], h[k]);
+            uint32_t vn[ROWS];
+            ccol<COST, ND, NW>(L, rn[sk], vn);
+            if constexpr (RUN) {
+                // running keys: h = (window cost << dbits) + base; one shift-add per cell
+                uint32_t vo[ROWS];
+                ccol<COST, ND, NW>(LO, ro[sk], vo);
+#pragma unroll
+                for (int q = 0; q < ROWS; ++q) h[k][q] = shl_add(vn[q] - vo[q], 1 << dbits, h[k][q]);
+            } else {
+                h[k][0] = (vn[0] << dbits) | mk[k];
+            }
         }
 #pragma unroll
         for (int q = 0; q < ROWS; ++q) {
             uint32_t b = 0xFFFFFFFFu;
 #pragma unroll
-            for (int k = 0; k < DPL; ++k) b = min(b, (h[k][q] << dbits) | mk[k]);
+            for (int k = 0; k < DPL; ++k) b = min(b, h[k][q]);
             bk[q][u] = b;
         }
         // one scheduling region per step: without it hipcc hoists every step's LDS reads
@@ -388,24 +395,32 @@ __global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a
     const int dbits = a.dbits;
     const int j = l - (LPG - 16);                        // emitting lane -> step within a chunk
 
+    // argmin keys (cost << dbits) | idx.  Running kinds keep the key itself in h, starting
+    // from its base: idx, or for padding disparities (idx >= D) idx + (cmax + 1) << dbits so
+    // they can never win (plan_match checks the range).  HOG forms keys with mk.
     uint32_t mk[DPL];
+    uint32_t h[DPL][ROWS], bk[ROWS][DPL];
 #pragma unroll
     for (int k = 0; k < DPL; ++k) {
         const int idx = l * DPL + k;
         mk[k] = idx < a.D ? (uint32_t)idx : 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = 0; q < ROWS; ++q) h[k][q] = idx < a.D ? (uint32_t)idx : a.pad_key | (uint32_t)idx;
     }
-    uint32_t h[DPL][ROWS], bk[ROWS][DPL];
-#pragma unroll
-    for (int k = 0; k < DPL; ++k)
-#pragma unroll
-        for (int q = 0; q < ROWS; ++q) h[k][q] = 0u;
 
     // ---- prologue: window of output column xs = the W2 columns xs-r .. xs+r, added directly
     for (int t = 0; t < W2; ++t) {
         const Pk<NW> L = ld<NW>(Lp + (size_t)(iL0 + t) * Q);
 #pragma unroll
-        for (int k = 0; k < DPL; ++k)
-            vcol<COST, ND, NW, false>(L, ld<NW>(Rp + (size_t)rslot(iR0 + t - k, c0, DPL) * Q), h[k]);
+        for (int k = 0; k < DPL; ++k) {
+            uint32_t vn[ROWS];
+            ccol<COST, ND, NW>(L, ld<NW>(Rp + (size_t)rslot(iR0 + t - k, c0, DPL) * Q), vn);
+            if constexpr (COST == COST_HOG) h[k][0] = (vn[0] << dbits) | mk[k];
+            else {
+#pragma unroll
+                for (int q = 0; q < ROWS; ++q) h[k][q] += vn[q] << dbits;
+            }
+        }
     }
     {
         const bool emit0 = j == 0 && xs < a.X1;
@@ -413,7 +428,7 @@ __global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a
         for (int q = 0; q < ROWS; ++q) {
             uint32_t b = 0xFFFFFFFFu;
 #pragma unroll
-            for (int k = 0; k < DPL; ++k) b = min(b, (h[k][q] << dbits) | mk[k]);
+            for (int k = 0; k < DPL; ++k) b = min(b, h[k][q]);
             if (LPG == 16) reduce_batch<16, 1>(&b);
             else if (LPG == 32) reduce_batch<32, 1>(&b);
             else reduce_batch<64, 1>(&b);
@@ -521,6 +536,12 @@ int kind_of(int cost, int win) {
 
 }  // namespace
 
+uint64_t max_cost(int win, int cost) {
+    return cost == COST_SAD ? (uint64_t)win * win * 255
+         : cost == COST_SSD ? (uint64_t)win * win * 255 * 255
+                            : (uint64_t)9 * win * win * 255;
+}
+
 int plan_match(int num_disp, int win, int cost, MatchPlan* plan) {
     static const int menu[][2] = {{4, 16}, {6, 16}, {8, 16}, {6, 32}, {8, 32}, {6, 64}, {8, 64}};
     if (num_disp <= 0 || win < 1 || (win & 1) == 0 || win > 15) return -22;
@@ -536,10 +557,11 @@ int plan_match(int num_disp, int win, int cost, MatchPlan* plan) {
     int n = plan->dpl * plan->lpg - 1, bits = 0;
     while (n > 0) { ++bits; n >>= 1; }
     plan->dbits = bits < 1 ? 1 : bits;
-    uint64_t cmax = cost == COST_SAD ? (uint64_t)win * win * 255
-                  : cost == COST_SSD ? (uint64_t)win * win * 255 * 255
-                                     : (uint64_t)9 * win * win * 255;
+    const uint64_t cmax = max_cost(win, cost);
     if ((cmax << plan->dbits) >= (1ull << 32)) return -34;  // ERANGE: key would overflow
+    // padding disparities (idx >= D) carry keys above (cmax + 1) << dbits
+    if (num_disp < plan->dpl * plan->lpg && cost != COST_HOG && (((2 * cmax + 2) << plan->dbits) >= (1ull << 32)))
+        return -34;
     return 0;
 }
 

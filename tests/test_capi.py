@@ -68,6 +68,16 @@ def test_key_range_is_checked():
     assert ei.value.code == -34
 
 
+def test_key_range_with_padding_disparities():
+    # D=256 fills the (8 x 32) lane plan exactly: (cmax << 8) fits
+    assert E.plan(256, 15, "ssd")["dpl"] * E.plan(256, 15, "ssd")["lpg"] == 256
+    # D=200 leaves padding disparities whose keys start at (cmax + 1) << 8: overflows
+    with pytest.raises(E.SVError) as ei:
+        E.plan(200, 15, "ssd")
+    assert ei.value.code == -34
+    E.plan(200, 15, "sad")
+
+
 def test_engine_fails_loudly_without_gpu():
     if E.device_count() > 0:
         pytest.skip("a GPU is visible")

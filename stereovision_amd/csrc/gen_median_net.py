@@ -105,6 +105,84 @@ def verify01(net, out_slot, n_real=25):
     return True
 
 
+def build_sel(n_real: int, n: int, lo_pads: int, ranks: list[int]):
+    """Batcher on n wires: `lo_pads` -inf pads below the real inputs (wires lo_pads ..
+    lo_pads+n_real-1), +inf pads above; constant-folded, pruned to the wires that end up
+    holding the given ranks (0-indexed among the real inputs), returned in rank order."""
+    order = {"-": 0, "r": 1, "+": 2}
+    kind = ["-"] * lo_pads + ["r"] * n_real + ["+"] * (n - lo_pads - n_real)
+    ops = []
+    for a, b in batcher_pairs(n):
+        if kind[a] == "r" and kind[b] == "r":
+            ops.append(("cmp", a, b))
+        elif order[kind[a]] > order[kind[b]]:
+            ops.append(("swap", a, b))
+            kind[a], kind[b] = kind[b], kind[a]
+    slot = list(range(n))
+    cmps = []
+    for op, a, b in ops:
+        if op == "swap":
+            slot[a], slot[b] = slot[b], slot[a]
+        else:
+            cmps.append((slot[a], slot[b]))
+    outs = [slot[lo_pads + k] for k in ranks]
+    live = set(outs)
+    kept = []
+    for a, b in reversed(cmps):
+        need_a, need_b = a in live, b in live
+        if need_a or need_b:
+            kept.append((a, b, int(need_a) | (int(need_b) << 1)))
+            live.add(a)
+            live.add(b)
+    kept.reverse()
+    assert all(lo_pads <= w < lo_pads + n_real for w in live), "network reads a pad wire"
+    # renumber real wires to 0..n_real-1
+    net = [(a - lo_pads, b - lo_pads, u) for a, b, u in kept]
+    return net, [o - lo_pads for o in outs]
+
+
+def run_sel(net, outs, vals):
+    v = list(vals)
+    for a, b, _ in net:
+        x, y = v[a], v[b]
+        v[a], v[b] = (x, y) if x <= y else (y, x)
+    return [v[o] for o in outs]
+
+
+def verify01_sel(net, outs, n_real, ranks):
+    """0-1 principle: output j must equal the ranks[j]-th smallest for all 2^n_real
+    binary inputs (bit-sliced, 64 inputs per word)."""
+    low = []
+    for i in range(6):
+        m = 0
+        for t in range(64):
+            if (t >> i) & 1:
+                m |= 1 << t
+        low.append(m)
+    full = (1 << 64) - 1
+    popc = [bin(t).count("1") for t in range(64)]
+    for hi in range(1 << (n_real - 6)):
+        v = low + [full if (hi >> (i - 6)) & 1 else 0 for i in range(6, n_real)]
+        for a, b, _ in net:
+            x, y = v[a], v[b]
+            v[a], v[b] = x & y, x | y
+        ones_hi = bin(hi).count("1")
+        for o, k in zip(outs, ranks):
+            # k-th smallest (0-indexed) is 1 iff the number of zeros <= k
+            exp = 0
+            for t in range(64):
+                zeros = n_real - ones_hi - popc[t]
+                if zeros <= k:
+                    exp |= 1 << t
+            if v[o] != exp:
+                return False
+    return True
+
+
+# optimal 9-comparator sorting network for 5 inputs (Knuth, TAOCP 5.3.4)
+SORT5 = [(0, 1), (3, 4), (2, 4), (2, 3), (1, 4), (0, 3), (0, 2), (1, 3), (1, 2)]
+
+
 def main(check: bool = True):
     net, out_slot = build()
     rng = random.Random(0)
@@ -113,6 +191,23 @@ def main(check: bool = True):
         assert run(net, out_slot, vals) == sorted(vals)[12]
     if check:
         assert verify01(net, out_slot), "0-1 principle check failed"
+    # SEL20: sorted ranks 7..12 of 20 values (the shared 4x5 rows of two vertically
+    # adjacent 5x5 windows: the 13th of 25 lies in ranks 7..12 of the shared 20 or among
+    # the 5 rows unique to the window -> median = 6th of (6 sorted + 5 sorted))
+    ranks = list(range(7, 13))
+    sel, sel_out = build_sel(20, 32, 6, ranks)
+    for _ in range(2000):
+        vals = [rng.randint(-40, 40) for _ in range(20)]
+        assert run_sel(sel, sel_out, vals) == sorted(vals)[7:13]
+    for _ in range(2000):
+        vals = [rng.randint(-9, 9) for _ in range(5)]
+        v = list(vals)
+        for a, b in SORT5:
+            if v[a] > v[b]:
+                v[a], v[b] = v[b], v[a]
+        assert v == sorted(vals)
+    if check:
+        assert verify01_sel(sel, sel_out, 20, ranks), "SEL20 0-1 check failed"
     here = os.path.dirname(os.path.abspath(__file__))
     lines = [
         "// Generated by gen_median_net.py — do not edit.",
@@ -130,9 +225,24 @@ def main(check: bool = True):
     for a, b, u in net:
         lines.append(f"  {{{a}, {b}, {u}}},")
     lines.append("};")
+    lines += [
+        "",
+        f"// Ranks 7..12 (sorted) of 20 values: {len(sel)} comparators ({sum(2 if c[2] == 3 else 1 for c in sel)}",
+        "// min/max ops), pruned Batcher on 32 wires (6 -inf + 6 +inf pads folded). Verified",
+        "// exhaustively with the 0-1 principle over all 2^20 binary inputs.",
+        f"#define SV_SEL20_NCMP {len(sel)}",
+        "static constexpr unsigned char SV_SEL20_OUT[6] = {" + ", ".join(map(str, sel_out)) + "};",
+        "static constexpr unsigned char SV_SEL20_NET[SV_SEL20_NCMP][3] = {",
+    ]
+    for a, b, u in sel:
+        lines.append(f"  {{{a}, {b}, {u}}},")
+    lines.append("};")
+    lines += ["", "// optimal 9-comparator sort of 5 values",
+              "static constexpr unsigned char SV_SORT5_NET[9][2] = {" +
+              ", ".join(f"{{{a}, {b}}}" for a, b in SORT5) + "};"]
     with open(os.path.join(here, "sv_median_net.h"), "w") as f:
         f.write("\n".join(lines) + "\n")
-    print(f"{len(net)} comparators, output wire {out_slot}")
+    print(f"{len(net)} comparators, output wire {out_slot}; SEL20 {len(sel)} comparators")
 
 
 if __name__ == "__main__":

@@ -315,6 +315,42 @@ def test_depth_map_batch_dev_and_scaled_batch(engine):
             engine.dev_free(p)
 
 
+@pytest.mark.parametrize("H,W", [(1, 1), (1, 70), (2, 3), (3, 65), (5, 64), (17, 130), (33, 63), (70, 129)])
+def test_median_post_ragged_maps_and_bands(engine, H, W):
+    """k_median_i16 (4 rows per lane, shared-rank selection) on arbitrary int16 x16 maps:
+    every ragged size, full frame and 3 row bands, depth and scaled post, vs the oracle."""
+    rng = np.random.default_rng(H * 7919 + W)
+    D = 64
+    d16 = (rng.integers(-1, D, (H, W)) * 16).astype(np.int16)
+    # runs of equal values to exercise ties
+    d16[:, ::3] = d16[:, :1]
+    disp = O.disparity_f32(d16)
+    e_depth, e_norm = O.depth_post(disp, 0.3, 2.0, 0)
+    e_sn, e_su8, e_conf = O.scaled_post(disp, 0, D)
+    n = H * W
+    d_in = engine.dev_alloc(n * 2)
+    bufs = [engine.dev_alloc(n * 4) for _ in range(3)] + [engine.dev_alloc(n)]
+    try:
+        engine.to_device(d_in, d16)
+        for bands in (1, 3):
+            for k in range(bands):
+                r0, r1 = H * k // bands, H * (k + 1) // bands
+                engine.median_post_dev(d_in, H, W, r0, r1, 1, bufs[0], bufs[1], bufs[3],
+                                       min_depth=0.3, max_depth=2.0, min_disp_global=0,
+                                       min_disp=0, num_disp=D)
+            np.testing.assert_array_equal(engine.to_host(bufs[0], (H, W), np.float32), disp)
+            np.testing.assert_array_equal(engine.to_host(bufs[1], (H, W), np.float32), e_depth)
+            np.testing.assert_array_equal(engine.to_host(bufs[3], (H, W), np.uint8), e_norm)
+        engine.median_post_dev(d_in, H, W, 0, H, 2, bufs[0], bufs[1], bufs[3], bufs[2],
+                               min_disp=0, num_disp=D)
+        np.testing.assert_array_equal(engine.to_host(bufs[1], (H, W), np.float32), e_sn)
+        np.testing.assert_array_equal(engine.to_host(bufs[3], (H, W), np.uint8), e_su8)
+        np.testing.assert_array_equal(engine.to_host(bufs[2], (H, W), np.float32), e_conf)
+    finally:
+        for p in [d_in] + bufs:
+            engine.dev_free(p)
+
+
 def test_profiling_counters(engine):
     L, R = _pair(40, 300, 64, seed=1)
     engine.profile(True)

@@ -330,6 +330,28 @@ __device__ __forceinline__ void reduce_batch(uint32_t* v) {
     }
 }
 
+// Reduce-scatter of 16 keys over the 16 lanes of a row (LPG = 16, ROWS * DPL = 16):
+// on return lane l's v[0] is the min over the row of key index l.  Four butterfly steps
+// with XOR partners 15, 7, 3, 1 (row_mirror, row_half_mirror, quad perms); at each step a
+// lane keeps the half of its keys selected by the partner bit and sends the other half:
+// 8+4+2+1 fused v_min_u32_dpp plus 2 selects each, instead of 16 x 4 row_ror steps.
+__device__ __forceinline__ void reduce_scatter16(uint32_t (&v)[16], int l) {
+#define SV_RS_STEP(HALF, BIT, CTRL)                                                            \
+    {                                                                                          \
+        const bool hi = (l & (BIT)) != 0;                                                      \
+        _Pragma("unroll") for (int k = 0; k < (HALF); ++k) {                                   \
+            const uint32_t send = hi ? v[k] : v[k + (HALF)];                                   \
+            const uint32_t keep = hi ? v[k + (HALF)] : v[k];                                   \
+            v[k] = min(keep, (uint32_t)__builtin_amdgcn_update_dpp(0u, (int)send, CTRL, 0xF, 0xF, false)); \
+        }                                                                                      \
+    }
+    SV_RS_STEP(8, 8, 0x140)   // row_mirror:      partner l ^ 15
+    SV_RS_STEP(4, 4, 0x141)   // row_half_mirror: partner l ^ 7
+    SV_RS_STEP(2, 2, 0x1B)    // quad_perm 3210:  partner l ^ 3
+    SV_RS_STEP(1, 1, 0xB1)    // quad_perm 1032:  partner l ^ 1
+#undef SV_RS_STEP
+}
+
 // Occupancy target: LDS admits ~3 blocks/CU for the common configs (D <= 128, win <= 11),
 // so cap registers at 3 waves/SIMD (<= 168 VGPRs); the widest packs get 2 waves/SIMD.
 template <int COST, int ND> struct Occ {
@@ -459,6 +481,18 @@ __global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a
     for (int t0 = 0, c = 0; t0 < T; t0 += DPL, ++c) {
         match_chunk<COST, ND, DPL>(cut, dbits, rn0 + (size_t)c * (DPL + 1) * Q, ro0 + (size_t)c * (DPL + 1) * Q,
                                    ln0 + (size_t)t0 * Q, lo0 + (size_t)t0 * Q, rn, ro, h, mk, bk);
+        if constexpr (ROWS * DPL == 16) {
+            if (LPG == 16) {   // reduce-scatter: lane l ends with key (row l / DPL, step l % DPL)
+                uint32_t v[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = bk[i / DPL][i % DPL];
+                reduce_scatter16(v, l);
+                const int q = l / DPL, e = t0 + l % DPL + 1, x = xs + e;
+                if (e < S && x < a.X1 && y + q < a.row1)
+                    a.out[(size_t)(y + q) * a.opitch + x] = (int16_t)(((int)(v[0] & dmask) + a.minD) * 16);
+                continue;
+            }
+        }
         const int e = t0 + j + 1;
         const int x = xs + e;
         const bool emit = j >= 0 && j < DPL && e < S && x < a.X1;

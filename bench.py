@@ -39,7 +39,7 @@ from stereovision_amd.engine import get_engine  # noqa: E402
 from stereovision_amd.synthetic import stereo_batch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-VALU_TAP_PEAK = 157.3e12       # v_sad_u8 taps/s (4 taps x 256 CU x 64 x 2.4 GHz)
+VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2   # 256 CU x 4 SIMD, one wave64 VALU instr per 2 cycles
 
 
 def log(*a):
@@ -87,15 +87,14 @@ def cpu_baseline(H, W, D, win, cost, seconds):
     }
 
 
-def pmc_traffic(workload_key):
-    """HBM bytes per k_match launch from the committed rocprofv3 PMC summary, if any."""
+def pmc_entry(workload_key):
+    """k_match PMC figures per launch from the committed rocprofv3 summary, if any."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
-            d = json.load(f)
-        return d.get(workload_key, {}).get("hbm_bytes_per_launch")
+            return json.load(f).get(workload_key, {})
     except (OSError, ValueError):
-        return None
+        return {}
 
 
 def main():
@@ -224,20 +223,27 @@ def main():
     k_avg_s = (match_ms / match_n) * 1e-3 if match_n else None
     k_bytes = 4 * npx                          # 2 u8 images read + int16 map written
     frame_bytes = 11 * H * W                   # 2 u8 in; depth f32 + disparity f32 + u8 out
-    taps = npx * D * win * win
     roofline = None
     if k_avg_s:
         achieved = k_bytes / k_avg_s / 1e9
+        pmc = pmc_entry(f"{W}x{H}_D{D}_w{win}_{args.cost}" + (f"_b{B}" if B > 1 and not rowtile else ""))
+        insts = pmc.get("valu_insts_per_launch")
         roofline = {
             "kernel": "k_match", "bound": "hbm", "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": pmc_traffic(f"{W}x{H}_D{D}_w{win}_{args.cost}" +
-                                   (f"_b{B}" if B > 1 and not rowtile else "")),
+            "traffic": pmc.get("hbm_bytes_per_launch"),
             "bytes_per_launch": k_bytes, "avg_launch_us": round(k_avg_s * 1e6, 2),
             "launches": match_n,
-            "valu": {"achieved_taps_per_s": taps / k_avg_s, "peak_taps_per_s": VALU_TAP_PEAK,
-                     "frac": round(taps / k_avg_s / VALU_TAP_PEAK, 4),
-                     "cells_per_s": npx * D / k_avg_s},
+            # what actually bounds k_match: VALU issue.  SQ_INSTS_VALU per
+            # launch (rocprofv3 PMC, profiles/) over the live launch time, against the
+            # full-rate issue peak (1 wave64 instruction / 2 cycles / SIMD); v_sad_u8 and the
+            # other VOP3 integer ops issue at half that rate (profiles/r01_valu_rate.txt).
+            "valu": {"unit": "wave-instr/s",
+                     "achieved": round(insts / k_avg_s) if insts else None,
+                     "peak": VALU_ISSUE_PEAK,
+                     "frac": round(insts / k_avg_s / VALU_ISSUE_PEAK, 4) if insts else None,
+                     "insts_per_launch": insts,
+                     "cells_per_s": round(npx * D / k_avg_s)},
             "median_post_avg_us": round(med_ms / med_n * 1e3, 2) if med_n else None,
         }
 

@@ -410,9 +410,14 @@ __global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a
 
     const int g = lane >> a.lpg_log2;
     const int l = lane & (LPG - 1);
+    // disparity slot of the lane inside its group: lanes of odd 16-lane rows are rotated by
+    // 8, which makes the per-step right-pack ds_read_b128 conflict-free across the two
+    // groups that share a b128 lane group (the min over a group does not depend on the
+    // order; emission uses the physical lane)
+    const int sl = l ^ (((lane >> 4) & 1) << 3);
     const int xs = xw + g * S;
     const int iL0 = g * S + 2 * r + 1;                   // L index of the window's first column
-    const int iR0 = g * S + 2 * r + (LPG - l) * DPL;   // R index of (first column, k = 0)
+    const int iR0 = g * S + 2 * r + (LPG - sl) * DPL;  // R index of (first column, k = 0)
     const uint32_t dmask = (1u << a.dbits) - 1u;
     const int dbits = a.dbits;
     const int j = l - (LPG - 16);                        // emitting lane -> step within a chunk
@@ -424,7 +429,7 @@ __global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a
     uint32_t h[DPL][ROWS], bk[ROWS][DPL];
 #pragma unroll
     for (int k = 0; k < DPL; ++k) {
-        const int idx = l * DPL + k;
+        const int idx = sl * DPL + k;
         mk[k] = idx < a.D ? (uint32_t)idx : 0xFFFFFFFFu;
 #pragma unroll
         for (int q = 0; q < ROWS; ++q) h[k][q] = idx < a.D ? (uint32_t)idx : a.pad_key | (uint32_t)idx;

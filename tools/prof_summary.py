@@ -39,10 +39,12 @@ if agg:
         if "k_match" in k and "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             fetch = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]) * 1024
             write = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * 1024
+            valu = d.get("SQ_INSTS_VALU")
             pmc[key] = {"hbm_bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch),
                         "write_bytes": round(write), "tag": tag,
-                        "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024, no gfx950 x2 read correction "
-                                "(narrow loads; see DESIGN.md)"}
+                        "valu_insts_per_launch": round(sum(valu) / len(valu)) if valu else None,
+                        "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024, uncorrected: the x2 gfx950 read correction "
+                                "applies to 16-B/lane streams; k_match reads dwords (uncalibrated, DESIGN.md)"}
     json.dump(pmc, open(pmc_path, "w"), indent=1)
 out = os.path.join(root, "profiles", f"{tag}_summary.md")
 open(out, "w").write("\n".join(lines) + "\n")

@@ -114,6 +114,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed loop")
+    ap.add_argument("--profile-every", type=int, default=4,
+                    help="bracket the kernels of every N-th timed step with HIP events (each "
+                         "event record costs a few us of queue time; 1 = every step)")
     ap.add_argument("--mode", default="frames", choices=["frames", "rowtile"],
                     help="frames: independent frames per rank (C4, weak scaling); rowtile: "
                          "one frame row-tiled across ranks + RCCL row gather (C5, strong)")
@@ -191,14 +194,19 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    eng.profile(not args.no_profile)
+    eng.profile(False)
     eng.profile_reset()
+    every = max(1, args.profile_every)
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if not args.no_profile and every > 1:
+            eng.profile(i % every == 0)        # host-side toggle, no GPU work
+        elif i == 0:
+            eng.profile(not args.no_profile)
         step(i)
     torch.cuda.synchronize()
     if world > 1:

@@ -105,6 +105,7 @@ struct sv_ctx {
         }
     } lut_key;
     hipEvent_t lut_ev = nullptr;
+    hipStream_t lut_stream = nullptr;   // stream the table was built on
     HostBuf hin, hout;
     bool prof = false;
     std::vector<EvPair> pending;
@@ -256,8 +257,9 @@ int attach_lut(sv_ctx* c, sv::PostParams& pp, hipStream_t s) {
         if (e) return hipfail(e, "launch_post_lut");
         SV_HIP(hipEventRecord(c->lut_ev, s));
         c->lut_key = k;
-    } else {
-        SV_HIP(hipStreamWaitEvent(s, c->lut_ev, 0));   // built earlier, maybe on another stream
+        c->lut_stream = s;
+    } else if (s != c->lut_stream) {
+        SV_HIP(hipStreamWaitEvent(s, c->lut_ev, 0));   // built earlier on another stream
     }
     pp.lut_a = la;
     pp.lut_b = la + n;

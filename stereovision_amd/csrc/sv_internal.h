@@ -37,6 +37,7 @@ struct MatchParams {
     int nf;
     long long fs_in, fs_out, fs_hist;
     uint32_t pad_key;      // (max_cost + 1) << dbits: key offset of padding disparities
+    int segm;              // segment length in LPG units (set by launch_match)
 };
 
 // Host-side launchers (return hipError_t as int).

@@ -32,25 +32,43 @@
 //   HOG   9-bin u16 window histograms as packs compared with v_sad_u16 (no running window).
 #include "sv_internal.h"
 
+#include <cstdlib>
+
 namespace sv {
 namespace {
 
-constexpr int ROWS_PER_BLOCK = 4;     // waves per 256-thread block
 constexpr int COST_SAD2 = 3;          // internal kind: SAD, two output rows per wave
+constexpr int COST_SAD4 = 4;          // internal kind: SAD, four output rows per wave
 
 // Segment width per lane group: 4*LPG columns rounded up to a multiple of DPL so that
 // every group of a wave shares the same right-pack slot phase (rslot).
-__host__ __device__ __forceinline__ int seg_width(int lpg, int dpl) { return (4 * lpg + dpl - 1) / dpl * dpl; }
-__host__ __device__ __forceinline__ int wave_cols(int lpg, int dpl) { return (64 / lpg) * seg_width(lpg, dpl); }
+// `sm` = segment length in units of LPG columns (4; 2 for the 4-row kind, whose 32-byte
+// packs would otherwise limit the LDS to 1.5 waves per SIMD).
+__host__ __device__ __forceinline__ int seg_width(int lpg, int dpl, int sm = 4) { return (sm * lpg + dpl - 1) / dpl * dpl; }
+__host__ __device__ __forceinline__ int wave_cols(int lpg, int dpl, int sm = 4) { return (64 / lpg) * seg_width(lpg, dpl, sm); }
+int seg_mult(int kind) {
+    static const int sm4 = [] {
+        const char* e = std::getenv("SV_SAD4_SEG");
+        const int v = e ? std::atoi(e) : 2;
+        return v >= 1 && v <= 8 ? v : 2;
+    }();
+    return kind == COST_SAD4 ? sm4 : 4;
+}
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
 
 // A column pack holds NW live dwords inside a 16*Q-byte LDS slot.  ND is the kind's width
 // parameter: byte dwords (SAD, SSD), shared dwords (SAD2), unused (HOG).
 template <int COST, int ND> struct PackCfg {
-    static constexpr int NW = COST == COST_SAD ? ND : COST == COST_SSD ? ND + 1 : COST == COST_SAD2 ? ND + 2 : 5;
+    // ND is the kind's width parameter: byte dwords (SAD, SSD), shared dwords (SAD2), the
+    // window radius r (SAD4: ceil((2r-2)/4) common dwords + 4 per-row dwords)
+    static constexpr int NW = COST == COST_SAD ? ND : COST == COST_SSD ? ND + 1 : COST == COST_SAD2 ? ND + 2
+                            : COST == COST_SAD4 ? (2 * ND - 2 + 3) / 4 + 4 : 5;
     static constexpr int Q = (NW + 3) / 4;
-    static constexpr int ROWS = COST == COST_SAD2 ? 2 : 1;
+    static constexpr int ROWS = COST == COST_SAD2 ? 2 : COST == COST_SAD4 ? 4 : 1;
+    // waves per block: the 4-row kind's packs take 32 B of LDS, one wave per block lets
+    // the LDS hold as many waves as the register file does
+    static constexpr int WPB = COST == COST_SAD4 ? 1 : 4;
 };
 template <int NW> struct Pk { uint32_t w[NW]; };
 
@@ -77,6 +95,13 @@ __device__ __forceinline__ void ccol(const Pk<NW>& l, const Pk<NW>& r, uint32_t*
         for (int i = 0; i < ND; ++i) s = __builtin_amdgcn_sad_u8(l.w[i], r.w[i], s);
         v[0] = __builtin_amdgcn_sad_u8(l.w[ND], r.w[ND], s);
         v[1] = __builtin_amdgcn_sad_u8(l.w[ND + 1], r.w[ND + 1], s);
+    } else if constexpr (COST == COST_SAD4) {
+        constexpr int NC = NW - 4;
+        uint32_t s = 0u;
+#pragma unroll
+        for (int i = 0; i < NC; ++i) s = __builtin_amdgcn_sad_u8(l.w[i], r.w[i], s);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = __builtin_amdgcn_sad_u8(l.w[NC + q], r.w[NC + q], s);
     } else if constexpr (COST == COST_SSD) {
         uint32_t dot = 0u;
 #pragma unroll
@@ -122,6 +147,32 @@ __device__ __forceinline__ void build_pack(const MatchParams& a, const uint8_t* 
             w[3] |= q == 3 ? sh : 0u;
         }
         dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    } else if constexpr (COST == COST_SAD4) {
+        // rows y-r .. y+r+3 (j = 0 .. 2r+3): j in [3, 2r] -> common word (j-3)/4; the 3
+        // rows of output q outside the common block -> byte positions of word ND+q
+        constexpr int NC = PackCfg<COST, ND>::NW - 4;
+        uint32_t w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        const int r = ND;
+        for (int j = 0; j <= 2 * r + 3; ++j) {
+            const int yy = clampi(y - r + j, 0, a.H - 1);
+            const uint32_t v = img[(size_t)yy * a.pitch + cc];
+            if (j >= 3 && j <= 2 * r) {
+                const int q = (j - 3) >> 2;
+                const uint32_t sh = v << (8 * ((j - 3) & 3));
+#pragma unroll
+                for (int i = 0; i < NC; ++i) w[i] |= q == i ? sh : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                // custom rows of output q: j = q .. 2 (before the common block), then
+                // j = 2r+1 .. 2r+q (after it); byte position = order within the 3
+                const int pos = j <= 2 ? j - q : (j >= 2 * r + 1 ? (3 - q) + (j - 2 * r - 1) : -1);
+                const bool in = j <= 2 ? (j >= q) : (j >= 2 * r + 1 && j <= 2 * r + q);
+                w[NC + q] |= in ? v << (8 * pos) : 0u;
+            }
+        }
+        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
     } else {
         uint32_t w[5] = {0u, 0u, 0u, 0u, 0u};
         uint32_t sq = 0;
@@ -162,11 +213,35 @@ __device__ __forceinline__ void transpose4(uint32_t a, uint32_t b, uint32_t c, u
 template <int COST, int ND>
 __device__ __forceinline__ void build_group(const MatchParams& a, const uint8_t* img, int cg, int y,
                                             uint32_t (&w)[PackCfg<COST, ND>::NW][4]) {
-    const int r = a.r;
+    const int r = COST == COST_SAD4 ? ND : a.r;
     auto row = [&](int j) -> uint32_t {
         const int yy = clampi(y - r + j, 0, a.H - 1);
         return *reinterpret_cast<const uint32_t*>(img + (size_t)yy * a.pitch + cg);
     };
+    if constexpr (COST == COST_SAD4) {
+        constexpr int R = ND, NC = PackCfg<COST, ND>::NW - 4, NCR = 2 * R - 2;
+        uint32_t rw[2 * R + 4];
+#pragma unroll
+        for (int j = 0; j < 2 * R + 4; ++j) rw[j] = row(j);
+#pragma unroll
+        for (int m = 0; m < NC; ++m) {
+            uint32_t d[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) d[t] = 4 * m + t < NCR ? rw[3 + 4 * m + t] : 0u;
+            transpose4(d[0], d[1], d[2], d[3], w[m]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t d[3];
+            int n = 0;
+#pragma unroll
+            for (int j = q; j <= 2; ++j) d[n++] = rw[j];
+#pragma unroll
+            for (int j = 2 * R + 1; j <= 2 * R + q; ++j) d[n++] = rw[j];
+            transpose4(d[0], d[1], d[2], 0u, w[NC + q]);
+        }
+        return;
+    }
     constexpr int J0 = COST == COST_SAD2 ? 1 : 0;            // first shared row
     const int nsh = COST == COST_SAD2 ? 2 * r : a.win;       // shared (transposed) rows
 #pragma unroll
@@ -355,11 +430,11 @@ __device__ __forceinline__ void reduce_scatter16(uint32_t (&v)[16], int l) {
 // Occupancy target: LDS admits ~3 blocks/CU for the common configs (D <= 128, win <= 11),
 // so cap registers at 3 waves/SIMD (<= 168 VGPRs); the widest packs get 2 waves/SIMD.
 template <int COST, int ND> struct Occ {
-    static constexpr int W = (COST == COST_SAD || COST == COST_SAD2 || ND <= 3) ? 3 : 2;
+    static constexpr int W = COST == COST_SAD4 ? 2 : (COST == COST_SAD || COST == COST_SAD2 || ND <= 3) ? 3 : 2;
 };
 
 template <int COST, int ND, int DPL>
-__global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a) {
+__global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) void k_match(MatchParams a) {
     constexpr int NW = PackCfg<COST, ND>::NW;
     constexpr int Q = PackCfg<COST, ND>::Q;
     constexpr int ROWS = PackCfg<COST, ND>::ROWS;
@@ -376,8 +451,8 @@ __global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int LPG = a.lpg;
-    const int S = seg_width(LPG, DPL);      // segment width per group
-    const int WC = wave_cols(LPG, DPL);
+    const int S = seg_width(LPG, DPL, a.segm);      // segment width per group
+    const int WC = wave_cols(LPG, DPL, a.segm);
     const int r = a.r;
     const int W2 = 2 * r + 1;
     const int c0 = (DPL - (4 * r + 1) % DPL) % DPL;      // (iR0 + W2 + c0) % DPL == 0
@@ -387,7 +462,7 @@ __global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a
     uint4* Lp = smem + (size_t)wid * (NL + NRphys) * Q;
     uint4* Rp = Lp + (size_t)NL * Q;
 
-    const int y = a.row0 + ((int)blockIdx.y * ROWS_PER_BLOCK + wid) * ROWS;
+    const int y = a.row0 + ((int)blockIdx.y * PackCfg<COST, ND>::WPB + wid) * ROWS;
     const int yc = min(y, a.row1 - 1);
     const int xw = a.X0 + (int)blockIdx.x * WC;
     const int cL0 = xw - 3 * r - 1;
@@ -486,15 +561,18 @@ __global__ __launch_bounds__(256, (Occ<COST, ND>::W)) void k_match(MatchParams a
     for (int t0 = 0, c = 0; t0 < T; t0 += DPL, ++c) {
         match_chunk<COST, ND, DPL>(cut, dbits, rn0 + (size_t)c * (DPL + 1) * Q, ro0 + (size_t)c * (DPL + 1) * Q,
                                    ln0 + (size_t)t0 * Q, lo0 + (size_t)t0 * Q, rn, ro, h, mk, bk);
-        if constexpr (ROWS * DPL == 16) {
+        if constexpr (ROWS * DPL == 16 || ROWS * DPL == 32) {
             if (LPG == 16) {   // reduce-scatter: lane l ends with key (row l / DPL, step l % DPL)
-                uint32_t v[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] = bk[i / DPL][i % DPL];
-                reduce_scatter16(v, l);
-                const int q = l / DPL, e = t0 + l % DPL + 1, x = xs + e;
-                if (e < S && x < a.X1 && y + q < a.row1)
-                    a.out[(size_t)(y + q) * a.opitch + x] = (int16_t)(((int)(v[0] & dmask) + a.minD) * 16);
+                for (int half = 0; half < ROWS * DPL / 16; ++half) {
+                    uint32_t v[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) v[i] = bk[(16 * half + i) / DPL][i % DPL];
+                    reduce_scatter16(v, l);
+                    const int q = (16 * half) / DPL + l / DPL, e = t0 + l % DPL + 1, x = xs + e;
+                    if (e < S && x < a.X1 && y + q < a.row1)
+                        a.out[(size_t)(y + q) * a.opitch + x] = (int16_t)(((int)(v[0] & dmask) + a.minD) * 16);
+                }
                 continue;
             }
         }
@@ -529,11 +607,11 @@ int launch_one(const MatchParams& a, size_t lds, hipStream_t s) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return (int)e;
     }
-    const int wc = wave_cols(a.lpg, DPL);
-    const int rows_per_block = ROWS_PER_BLOCK * PackCfg<COST, ND>::ROWS;
+    const int wc = wave_cols(a.lpg, DPL, a.segm);
+    const int rows_per_block = PackCfg<COST, ND>::WPB * PackCfg<COST, ND>::ROWS;
     dim3 grid((a.X1 - a.X0 + wc - 1) / wc, (a.row1 - a.row0 + rows_per_block - 1) / rows_per_block,
               a.nf > 1 ? a.nf : 1);
-    hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL(fn, grid, dim3(64 * PackCfg<COST, ND>::WPB), lds, s, a);
     return (int)hipGetLastError();
 }
 
@@ -557,6 +635,13 @@ int launch_nd(const MatchParams& a, const MatchPlan& p, size_t lds, hipStream_t 
             case 2: return launch_dpl<COST, 2>(a, p, lds, s);
         }
         return (int)hipErrorInvalidValue;
+    } else if constexpr (COST == COST_SAD4) {
+        switch (p.ndw) {   // = r
+            case 2: return launch_dpl<COST, 2>(a, p, lds, s);
+            case 3: return launch_dpl<COST, 3>(a, p, lds, s);
+            case 4: return launch_dpl<COST, 4>(a, p, lds, s);
+        }
+        return (int)hipErrorInvalidValue;
     } else {
         switch (p.ndw) {
             case 1: return launch_dpl<COST, 1>(a, p, lds, s);
@@ -568,9 +653,15 @@ int launch_nd(const MatchParams& a, const MatchPlan& p, size_t lds, hipStream_t 
     }
 }
 
-// Kind actually launched for a public cost: SAD with 5 <= win <= 9 runs two rows per wave.
+// Kind actually launched for a public cost: SAD with 5 <= win <= 9 runs four rows per wave
+// (SV_SAD_ROWS=2 selects the two-row kind, for A/B measurements).
 int kind_of(int cost, int win) {
-    return (cost == COST_SAD && win >= 5 && win <= 9) ? COST_SAD2 : cost;
+    static const int rows = [] {
+        const char* e = std::getenv("SV_SAD_ROWS");
+        return (e && std::atoi(e) == 2) ? 2 : 4;
+    }();
+    if (cost == COST_SAD && win >= 5 && win <= 9) return rows == 2 ? COST_SAD2 : COST_SAD4;
+    return cost;
 }
 
 }  // namespace
@@ -592,7 +683,8 @@ int plan_match(int num_disp, int win, int cost, MatchPlan* plan) {
     plan->dpl = menu[i][0];
     plan->lpg = menu[i][1];
     const int kind = kind_of(cost, win);
-    plan->ndw = kind == COST_HOG ? 5 : kind == COST_SAD2 ? (win - 1 + 3) / 4 : (win + 3) / 4;
+    plan->ndw = kind == COST_HOG ? 5 : kind == COST_SAD2 ? (win - 1 + 3) / 4 : kind == COST_SAD4 ? win / 2
+              : (win + 3) / 4;
     int n = plan->dpl * plan->lpg - 1, bits = 0;
     while (n > 0) { ++bits; n >>= 1; }
     plan->dbits = bits < 1 ? 1 : bits;
@@ -606,14 +698,16 @@ int plan_match(int num_disp, int win, int cost, MatchPlan* plan) {
 
 size_t match_lds_bytes(const MatchPlan& p, int r, int cost) {
     const int kind = kind_of(cost, 2 * r + 1);
-    const int nw = kind == COST_SAD ? p.ndw : kind == COST_SSD ? p.ndw + 1 : kind == COST_SAD2 ? p.ndw + 2 : 5;
+    const int nw = kind == COST_SAD ? p.ndw : kind == COST_SSD ? p.ndw + 1 : kind == COST_SAD2 ? p.ndw + 2
+                 : kind == COST_SAD4 ? (2 * p.ndw - 2 + 3) / 4 + 4 : 5;
+    const int wpb = kind == COST_SAD4 ? 1 : 4;
     const int Q = (nw + 3) / 4;
     const int c0 = (p.dpl - (4 * r + 1) % p.dpl) % p.dpl;
-    const int wc = wave_cols(p.lpg, p.dpl);
+    const int wc = wave_cols(p.lpg, p.dpl, seg_mult(kind));
     const int NL = wc + 4 * r + p.dpl + 1;
     const int NRlog = wc + 4 * r + p.lpg * p.dpl + p.dpl;
     const int NRphys = NRlog + (NRlog + c0) / p.dpl + 1;
-    return (size_t)ROWS_PER_BLOCK * (NL + NRphys) * Q * 16;
+    return (size_t)wpb * (NL + NRphys) * Q * 16;
 }
 
 int launch_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v, hipStream_t s) {
@@ -634,11 +728,14 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
     }
     const size_t lds = match_lds_bytes(p, a.r, cost);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+    MatchParams b = a;
+    b.segm = seg_mult(kind_of(cost, a.win));
     switch (kind_of(cost, a.win)) {
-        case COST_SAD: return launch_nd<COST_SAD>(a, p, lds, s);
-        case COST_SAD2: return launch_nd<COST_SAD2>(a, p, lds, s);
-        case COST_SSD: return launch_nd<COST_SSD>(a, p, lds, s);
-        case COST_HOG: return launch_nd<COST_HOG>(a, p, lds, s);
+        case COST_SAD: return launch_nd<COST_SAD>(b, p, lds, s);
+        case COST_SAD2: return launch_nd<COST_SAD2>(b, p, lds, s);
+        case COST_SAD4: return launch_nd<COST_SAD4>(b, p, lds, s);
+        case COST_SSD: return launch_nd<COST_SSD>(b, p, lds, s);
+        case COST_HOG: return launch_nd<COST_HOG>(b, p, lds, s);
     }
     return (int)hipErrorInvalidValue;
 }

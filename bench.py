@@ -270,6 +270,13 @@ def main():
                                    f"frame-sharded x{world}" + (" + RCCL gather" if args.gather else "")),
                    "dist_backend": args.dist_backend if world > 1 else None},
         "hbm_gbs_frame_path": round(frame_bytes * value / 1e9, 2),
+        # BASELINE.md's fixed roofline formulas, per GPU: 6*H*W algorithmic bytes and
+        # H*W*D*win^2 SAD taps per frame against 8.0e12 B/s and 157.3e12 taps/s.  The
+        # taps fraction exceeds 1 because running window sums do O(1) work per tap column.
+        "baseline_roofline": {
+            "fps_per_gpu": round(value / world, 2),
+            "achieved_hbm_frac": round(6 * H * W * value / world / 8.0e12, 5),
+            "achieved_valu_frac": round(H * W * D * win * win * value / world / 157.3e12, 4)},
         "roofline": roofline,
         "cpu_baseline": None,
     }

@@ -640,6 +640,9 @@ int launch_nd(const MatchParams& a, const MatchPlan& p, size_t lds, hipStream_t 
             case 2: return launch_dpl<COST, 2>(a, p, lds, s);
             case 3: return launch_dpl<COST, 3>(a, p, lds, s);
             case 4: return launch_dpl<COST, 4>(a, p, lds, s);
+            case 5: return launch_dpl<COST, 5>(a, p, lds, s);
+            case 6: return launch_dpl<COST, 6>(a, p, lds, s);
+            case 7: return launch_dpl<COST, 7>(a, p, lds, s);
         }
         return (int)hipErrorInvalidValue;
     } else {
@@ -653,14 +656,18 @@ int launch_nd(const MatchParams& a, const MatchPlan& p, size_t lds, hipStream_t 
     }
 }
 
-// Kind actually launched for a public cost: SAD with 5 <= win <= 9 runs four rows per wave
-// (SV_SAD_ROWS=2 selects the two-row kind, for A/B measurements).
+// Kind actually launched for a public cost: SAD with win >= 5 runs four rows per wave
+// (SV_SAD_ROWS=2 / 1 select the two-row kind for 5 <= win <= 9 / the one-row kind, for A/B
+// measurements).
 int kind_of(int cost, int win) {
     static const int rows = [] {
         const char* e = std::getenv("SV_SAD_ROWS");
-        return (e && std::atoi(e) == 2) ? 2 : 4;
+        const int v = e ? std::atoi(e) : 4;
+        return v == 1 || v == 2 ? v : 4;
     }();
-    if (cost == COST_SAD && win >= 5 && win <= 9) return rows == 2 ? COST_SAD2 : COST_SAD4;
+    if (cost == COST_SAD && rows == 1) return COST_SAD;
+    if (cost == COST_SAD && win >= 5 && win <= 9 && rows == 2) return COST_SAD2;
+    if (cost == COST_SAD && win >= 5) return COST_SAD4;
     return cost;
 }
 

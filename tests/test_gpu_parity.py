@@ -52,6 +52,20 @@ def test_disparity_ragged_shapes(engine, H, W):
                                       O.disparity16(L, R, 0, D, win))
 
 
+@pytest.mark.parametrize("win", [5, 7, 9, 11, 13, 15])
+@pytest.mark.parametrize("H", [1, 2, 3, 5, 6, 7, 13])
+def test_four_row_kind_every_height_and_window(engine, win, H):
+    """The 4-rows-per-wave SAD kind (win >= 5): heights that leave 1-3 rows in the last
+    wave, every supported window radius, a negative min_disp."""
+    rng = np.random.default_rng(win * 100 + H)
+    W = 173
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    for min_disp, D in [(0, 48), (-5, 64)]:
+        np.testing.assert_array_equal(engine.disparity(L, R, min_disp, D, win),
+                                      O.disparity16(L, R, min_disp, D, win))
+
+
 def test_disparity_image_narrower_than_band(engine):
     L, R = _pair(20, 50, 64, seed=3)
     got = engine.disparity(L, R, 0, 64, 5)

@@ -42,15 +42,15 @@ constexpr int COST_SAD4 = 4;          // internal kind: SAD, four output rows pe
 
 // Segment width per lane group: 4*LPG columns rounded up to a multiple of DPL so that
 // every group of a wave shares the same right-pack slot phase (rslot).
-// `sm` = segment length in units of LPG columns (4; 2 for the 4-row kind, whose 32-byte
-// packs would otherwise limit the LDS to 1.5 waves per SIMD).
+// `sm` = segment length in units of LPG columns (4; SV_SAD4_SEG overrides it for the
+// 4-row kind, for A/B measurements).
 __host__ __device__ __forceinline__ int seg_width(int lpg, int dpl, int sm = 4) { return (sm * lpg + dpl - 1) / dpl * dpl; }
 __host__ __device__ __forceinline__ int wave_cols(int lpg, int dpl, int sm = 4) { return (64 / lpg) * seg_width(lpg, dpl, sm); }
 int seg_mult(int kind) {
     static const int sm4 = [] {
         const char* e = std::getenv("SV_SAD4_SEG");
-        const int v = e ? std::atoi(e) : 2;
-        return v >= 1 && v <= 8 ? v : 2;
+        const int v = e ? std::atoi(e) : 4;
+        return v >= 1 && v <= 8 ? v : 4;
     }();
     return kind == COST_SAD4 ? sm4 : 4;
 }
@@ -66,19 +66,60 @@ template <int COST, int ND> struct PackCfg {
                             : COST == COST_SAD4 ? (2 * ND - 2 + 3) / 4 + 4 : 5;
     static constexpr int Q = (NW + 3) / 4;
     static constexpr int ROWS = COST == COST_SAD2 ? 2 : COST == COST_SAD4 ? 4 : 1;
-    // waves per block: the 4-row kind's packs take 32 B of LDS, one wave per block lets
-    // the LDS hold as many waves as the register file does
+    // waves per block: the 4-row kind's packs are large, one wave per block lets the LDS
+    // hold as many waves as the register file does
     static constexpr int WPB = COST == COST_SAD4 ? 1 : 4;
+    // SPLIT (4-row kind with <= 2 common words): the common words live in a separate
+    // 8-byte-per-slot array, the 4 per-row words in the 16-byte array: 24 B per pack
+    // instead of a 32-byte slot, so a 4-LPG segment still fits 2 waves per SIMD in LDS
+    static constexpr int NC = COST == COST_SAD4 ? NW - 4 : 0;
+    static constexpr bool SPLIT = COST == COST_SAD4 && NC <= 2;
+    static constexpr int QX = SPLIT ? 1 : Q;          // uint4 per slot in the main array
+    static constexpr int SLOT_BYTES = 16 * QX + (SPLIT ? 8 : 0);
 };
 template <int NW> struct Pk { uint32_t w[NW]; };
 
-template <int NW>
-__device__ __forceinline__ Pk<NW> ld(const uint4* p) {
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(p, 16));
-    Pk<NW> v;
+// Pointer to a column-pack slot (main array + the split common-word array).
+template <int COST, int ND, typename X, typename C> struct PackPtrT {
+    X* x;
+    C* c;
+    __device__ __forceinline__ PackPtrT operator+(int s) const {
+        return {x + s * PackCfg<COST, ND>::QX, PackCfg<COST, ND>::SPLIT ? c + s : c};
+    }
+};
+template <int COST, int ND> using PackPtr = PackPtrT<COST, ND, const uint4, const uint2>;
+template <int COST, int ND> using PackOut = PackPtrT<COST, ND, uint4, uint2>;
+
+template <int COST, int ND>
+__device__ __forceinline__ Pk<PackCfg<COST, ND>::NW> ld(PackPtr<COST, ND> p) {
+    using P = PackCfg<COST, ND>;
+    Pk<P::NW> v;
+    if constexpr (P::SPLIT) {
+        const uint2 c = *p.c;
+        v.w[0] = c.x;
+        if constexpr (P::NC > 1) v.w[1] = c.y;
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(p.x, 16));
 #pragma unroll
-    for (int i = 0; i < NW; ++i) v.w[i] = q[i];
+        for (int i = 0; i < 4; ++i) v.w[P::NC + i] = q[i];
+    } else {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(p.x, 16));
+#pragma unroll
+        for (int i = 0; i < P::NW; ++i) v.w[i] = q[i];
+    }
     return v;
+}
+
+// Store the NW words w[0..NW) of one pack.
+template <int COST, int ND>
+__device__ __forceinline__ void put(PackOut<COST, ND> p, const uint32_t (&w)[8]) {
+    using P = PackCfg<COST, ND>;
+    if constexpr (P::SPLIT) {
+        *p.c = make_uint2(w[0], P::NC > 1 ? w[1] : 0u);
+        p.x[0] = make_uint4(w[P::NC], w[P::NC + 1], w[P::NC + 2], w[P::NC + 3]);
+    } else {
+        p.x[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        if constexpr (P::Q > 1) p.x[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
 }
 
 // Column cost(s) of one (left pack, right pack) pair: v[0] (and v[1] = row y+1 for SAD2).
@@ -125,12 +166,12 @@ __device__ __forceinline__ uint32_t shl_add(uint32_t d, int m, uint32_t h) {
 // Build one column pack for logical column c around output row y (replicate-clamped).
 template <int COST, int ND>
 __device__ __forceinline__ void build_pack(const MatchParams& a, const uint8_t* img,
-                                           const uint16_t* hist, int c, int y, uint4* dst) {
+                                           const uint16_t* hist, int c, int y, PackOut<COST, ND> dst) {
     const int cc = clampi(c, 0, a.W - 1);
     if constexpr (COST == COST_HOG) {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(hist + ((size_t)y * a.W + cc) * 10);
-        dst[0] = make_uint4(src[0], src[1], src[2], src[3]);
-        dst[1] = make_uint4(src[4], 0u, 0u, 0u);
+        const uint32_t w[8] = {src[0], src[1], src[2], src[3], src[4], 0u, 0u, 0u};
+        put<COST, ND>(dst, w);
     } else if constexpr (COST == COST_SAD2) {
         // rows y-r .. y+r+1: j = 0 -> word ND (row y only), j = 2r+1 -> word ND+1 (row y+1
         // only), j in [1, 2r] -> shared word (j-1)/4
@@ -146,7 +187,8 @@ __device__ __forceinline__ void build_pack(const MatchParams& a, const uint8_t* 
             w[2] |= q == 2 ? sh : 0u;
             w[3] |= q == 3 ? sh : 0u;
         }
-        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        const uint32_t o[8] = {w[0], w[1], w[2], w[3], 0u, 0u, 0u, 0u};
+        put<COST, ND>(dst, o);
     } else if constexpr (COST == COST_SAD4) {
         // rows y-r .. y+r+3 (j = 0 .. 2r+3): j in [3, 2r] -> common word (j-3)/4; the 3
         // rows of output q outside the common block -> byte positions of word ND+q
@@ -171,8 +213,7 @@ __device__ __forceinline__ void build_pack(const MatchParams& a, const uint8_t* 
                 w[NC + q] |= in ? v << (8 * pos) : 0u;
             }
         }
-        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
-        dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+        put<COST, ND>(dst, w);
     } else {
         uint32_t w[5] = {0u, 0u, 0u, 0u, 0u};
         uint32_t sq = 0;
@@ -188,8 +229,8 @@ __device__ __forceinline__ void build_pack(const MatchParams& a, const uint8_t* 
             w[3] |= q == 3 ? sh : 0u;
         }
         if constexpr (COST == COST_SSD) w[ND] = sq;
-        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
-        if constexpr (PackCfg<COST, ND>::Q > 1) dst[1] = make_uint4(w[4], 0u, 0u, 0u);
+        const uint32_t o[8] = {w[0], w[1], w[2], w[3], w[4], 0u, 0u, 0u};
+        put<COST, ND>(dst, o);
     }
 }
 
@@ -280,16 +321,16 @@ __device__ __forceinline__ int rslot(int i, int c0, int dpl) { return i + (i + c
 // touching the image border (replicate clamp), HOG, and unaligned images take build_pack.
 template <int COST, int ND, int DPL>
 __device__ __forceinline__ void build_all_packs(const MatchParams& a, int y, int cL0, int NL, int cR0,
-                                                int NRlog, int c0, uint4* Lp, uint4* Rp, int lane) {
+                                                int NRlog, int c0, PackOut<COST, ND> Lp,
+                                                PackOut<COST, ND> Rp, int lane) {
     constexpr int NW = PackCfg<COST, ND>::NW;
-    constexpr int Q = PackCfg<COST, ND>::Q;
     bool aligned = ((reinterpret_cast<uintptr_t>(a.L) | reinterpret_cast<uintptr_t>(a.R) |
                      (uintptr_t)a.pitch) & 3u) == 0;
     if constexpr (COST == COST_HOG) aligned = false;
     if (!aligned) {
-        for (int i = lane; i < NL; i += 64) build_pack<COST, ND>(a, a.L, a.HL, cL0 + i, y, Lp + (size_t)i * Q);
+        for (int i = lane; i < NL; i += 64) build_pack<COST, ND>(a, a.L, a.HL, cL0 + i, y, Lp + i);
         for (int i = lane; i < NRlog; i += 64)
-            build_pack<COST, ND>(a, a.R, a.HR, cR0 + i, y, Rp + (size_t)rslot(i, c0, DPL) * Q);
+            build_pack<COST, ND>(a, a.R, a.HR, cR0 + i, y, Rp + rslot(i, c0, DPL));
         return;
     }
     if constexpr (COST != COST_HOG) {
@@ -300,7 +341,7 @@ __device__ __forceinline__ void build_all_packs(const MatchParams& a, int y, int
         const int cg = right ? aR + 4 * (gi - gL) : aL + 4 * gi;
         const int cfirst = right ? cR0 : cL0, n = right ? NRlog : NL;
         const uint8_t* img = right ? a.R : a.L;
-        uint4* base = right ? Rp : Lp;
+        const PackOut<COST, ND> base = right ? Rp : Lp;
         if (cg >= 0 && cg + 4 <= a.W) {
             uint32_t w[NW][4];
             build_group<COST, ND>(a, img, cg, y, w);
@@ -308,20 +349,17 @@ __device__ __forceinline__ void build_all_packs(const MatchParams& a, int y, int
             for (int k = 0; k < 4; ++k) {
                 const int idx = cg + k - cfirst;
                 if (idx < 0 || idx >= n) continue;
-                uint32_t v[4 * Q];
+                uint32_t v[8];
 #pragma unroll
-                for (int i = 0; i < 4 * Q; ++i) v[i] = i < NW ? w[i < NW ? i : 0][k] : 0u;
-                uint4* dst = base + (size_t)(right ? rslot(idx, c0, DPL) : idx) * Q;
-#pragma unroll
-                for (int i = 0; i < Q; ++i) dst[i] = make_uint4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+                for (int i = 0; i < 8; ++i) v[i] = i < NW ? w[i < NW ? i : 0][k] : 0u;
+                put<COST, ND>(base + (right ? rslot(idx, c0, DPL) : idx), v);
             }
         } else {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int idx = cg + k - cfirst;
                 if (idx < 0 || idx >= n) continue;
-                build_pack<COST, ND>(a, img, nullptr, cg + k, y,
-                                     base + (size_t)(right ? rslot(idx, c0, DPL) : idx) * Q);
+                build_pack<COST, ND>(a, img, nullptr, cg + k, y, base + (right ? rslot(idx, c0, DPL) : idx));
             }
         }
     }
@@ -330,13 +368,12 @@ __device__ __forceinline__ void build_all_packs(const MatchParams& a, int y, int
 
 template <int COST, int ND, int DPL>
 __device__ __forceinline__ void match_chunk(
-    const int cut, const int dbits, const uint4* __restrict__ rnb,
-    const uint4* __restrict__ rob, const uint4* __restrict__ lnb, const uint4* __restrict__ lob,
+    const int cut, const int dbits, PackPtr<COST, ND> rnb, PackPtr<COST, ND> rob, PackPtr<COST, ND> lnb,
+    PackPtr<COST, ND> lob,
     Pk<PackCfg<COST, ND>::NW> (&rn)[DPL], Pk<PackCfg<COST, ND>::NW> (&ro)[DPL],
     uint32_t (&h)[DPL][PackCfg<COST, ND>::ROWS], const uint32_t (&mk)[DPL],
     uint32_t (&bk)[PackCfg<COST, ND>::ROWS][DPL]) {
     constexpr int NW = PackCfg<COST, ND>::NW;
-    constexpr int Q = PackCfg<COST, ND>::Q;
     constexpr int ROWS = PackCfg<COST, ND>::ROWS;
     constexpr bool RUN = COST != COST_HOG;            // running horizontal window
 #pragma unroll
@@ -344,12 +381,12 @@ __device__ __forceinline__ void match_chunk(
         // ring slot u receives this step's entering right column; its previous content
         // (k = DPL-1 of the last step) is dead.  Static offsets inside the chunk; `cut` is
         // the wave-uniform phase of the old ring's slot gap.
-        rn[u] = ld<NW>(rnb + u * Q);
-        const Pk<NW> L = ld<NW>(lnb + u * Q);
+        rn[u] = ld<COST, ND>(rnb + u);
+        const Pk<NW> L = ld<COST, ND>(lnb + u);
         Pk<NW> LO;
         if constexpr (RUN) {
-            ro[u] = ld<NW>(rob + (u + (u >= cut ? 1 : 0)) * Q);
-            LO = ld<NW>(lob + u * Q);
+            ro[u] = ld<COST, ND>(rob + (u + (u >= cut ? 1 : 0)));
+            LO = ld<COST, ND>(lob + u);
         }
 #pragma unroll
         for (int k = 0; k < DPL; ++k) {
@@ -436,7 +473,6 @@ template <int COST, int ND> struct Occ {
 template <int COST, int ND, int DPL>
 __global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) void k_match(MatchParams a) {
     constexpr int NW = PackCfg<COST, ND>::NW;
-    constexpr int Q = PackCfg<COST, ND>::Q;
     constexpr int ROWS = PackCfg<COST, ND>::ROWS;
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     if (blockIdx.z) {   // frame batch
@@ -449,7 +485,7 @@ __global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) 
         }
     }
     const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
+    const int wid = PackCfg<COST, ND>::WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
     const int LPG = a.lpg;
     const int S = seg_width(LPG, DPL, a.segm);      // segment width per group
     const int WC = wave_cols(LPG, DPL, a.segm);
@@ -459,8 +495,14 @@ __global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) 
     const int NL = WC + 4 * r + DPL + 1;
     const int NRlog = WC + 4 * r + LPG * DPL + DPL;
     const int NRphys = NRlog + (NRlog + c0) / DPL + 1;
-    uint4* Lp = smem + (size_t)wid * (NL + NRphys) * Q;
-    uint4* Rp = Lp + (size_t)NL * Q;
+    // per-wave LDS region: [L main | R main | L common | R common] (common arrays: SPLIT)
+    using P = PackCfg<COST, ND>;
+    uint4* wbase = reinterpret_cast<uint4*>(reinterpret_cast<char*>(smem) + (size_t)wid * (NL + NRphys) * P::SLOT_BYTES);
+    uint2* cbase = reinterpret_cast<uint2*>(wbase + (size_t)(NL + NRphys) * P::QX);
+    const PackOut<COST, ND> Lw{wbase, cbase};
+    const PackOut<COST, ND> Rw{wbase + (size_t)NL * P::QX, cbase + NL};
+    const PackPtr<COST, ND> Lp{Lw.x, Lw.c};
+    const PackPtr<COST, ND> Rp{Rw.x, Rw.c};
 
     const int y = a.row0 + ((int)blockIdx.y * PackCfg<COST, ND>::WPB + wid) * ROWS;
     const int yc = min(y, a.row1 - 1);
@@ -468,7 +510,7 @@ __global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) 
     const int cL0 = xw - 3 * r - 1;
     const int cR0 = cL0 - a.minD - (LPG * DPL - 1);
 
-    build_all_packs<COST, ND, DPL>(a, yc, cL0, NL, cR0, NRlog, c0, Lp, Rp, lane);
+    build_all_packs<COST, ND, DPL>(a, yc, cL0, NL, cR0, NRlog, c0, Lw, Rw, lane);
 
     if (blockIdx.x == 0) {  // columns outside the matched band are invalid
         const int16_t inv = (int16_t)((a.minD - 1) * 16);
@@ -512,11 +554,11 @@ __global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) 
 
     // ---- prologue: window of output column xs = the W2 columns xs-r .. xs+r, added directly
     for (int t = 0; t < W2; ++t) {
-        const Pk<NW> L = ld<NW>(Lp + (size_t)(iL0 + t) * Q);
+        const Pk<NW> L = ld<COST, ND>(Lp + (iL0 + t));
 #pragma unroll
         for (int k = 0; k < DPL; ++k) {
             uint32_t vn[ROWS];
-            ccol<COST, ND, NW>(L, ld<NW>(Rp + (size_t)rslot(iR0 + t - k, c0, DPL) * Q), vn);
+            ccol<COST, ND, NW>(L, ld<COST, ND>(Rp + rslot(iR0 + t - k, c0, DPL)), vn);
             if constexpr (COST == COST_HOG) h[k][0] = (vn[0] << dbits) | mk[k];
             else {
 #pragma unroll
@@ -549,18 +591,18 @@ __global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) 
     Pk<NW> rn[DPL], ro[DPL];
 #pragma unroll
     for (int s = 1; s < DPL; ++s) {                      // virtual steps t' = s - DPL
-        rn[s] = ld<NW>(Rp + (size_t)rslot(iN - (DPL - s), c0, DPL) * Q);
-        if constexpr (COST != COST_HOG) ro[s] = ld<NW>(Rp + (size_t)rslot(iR0 - (DPL - s), c0, DPL) * Q);
+        rn[s] = ld<COST, ND>(Rp + rslot(iN - (DPL - s), c0, DPL));
+        if constexpr (COST != COST_HOG) ro[s] = ld<COST, ND>(Rp + rslot(iR0 - (DPL - s), c0, DPL));
     }
-    const uint4* rn0 = Rp + (size_t)rslot(iN, c0, DPL) * Q;
-    const uint4* ro0 = Rp + (size_t)rslot(iR0, c0, DPL) * Q;
-    const uint4* ln0 = Lp + (size_t)(iL0 + W2) * Q;
-    const uint4* lo0 = Lp + (size_t)iL0 * Q;
+    const PackPtr<COST, ND> rn0 = Rp + rslot(iN, c0, DPL);
+    const PackPtr<COST, ND> ro0 = Rp + rslot(iR0, c0, DPL);
+    const PackPtr<COST, ND> ln0 = Lp + (iL0 + W2);
+    const PackPtr<COST, ND> lo0 = Lp + iL0;
     const int T = (S - 1 + DPL - 1) / DPL * DPL;
 
     for (int t0 = 0, c = 0; t0 < T; t0 += DPL, ++c) {
-        match_chunk<COST, ND, DPL>(cut, dbits, rn0 + (size_t)c * (DPL + 1) * Q, ro0 + (size_t)c * (DPL + 1) * Q,
-                                   ln0 + (size_t)t0 * Q, lo0 + (size_t)t0 * Q, rn, ro, h, mk, bk);
+        match_chunk<COST, ND, DPL>(cut, dbits, rn0 + c * (DPL + 1), ro0 + c * (DPL + 1), ln0 + t0, lo0 + t0, rn,
+                                   ro, h, mk, bk);
         if constexpr (ROWS * DPL == 16 || ROWS * DPL == 32) {
             if (LPG == 16) {   // reduce-scatter: lane l ends with key (row l / DPL, step l % DPL)
 #pragma unroll
@@ -708,13 +750,14 @@ size_t match_lds_bytes(const MatchPlan& p, int r, int cost) {
     const int nw = kind == COST_SAD ? p.ndw : kind == COST_SSD ? p.ndw + 1 : kind == COST_SAD2 ? p.ndw + 2
                  : kind == COST_SAD4 ? (2 * p.ndw - 2 + 3) / 4 + 4 : 5;
     const int wpb = kind == COST_SAD4 ? 1 : 4;
+    const bool split = kind == COST_SAD4 && nw - 4 <= 2;
     const int Q = (nw + 3) / 4;
     const int c0 = (p.dpl - (4 * r + 1) % p.dpl) % p.dpl;
     const int wc = wave_cols(p.lpg, p.dpl, seg_mult(kind));
     const int NL = wc + 4 * r + p.dpl + 1;
     const int NRlog = wc + 4 * r + p.lpg * p.dpl + p.dpl;
     const int NRphys = NRlog + (NRlog + c0) / p.dpl + 1;
-    return (size_t)wpb * (NL + NRphys) * Q * 16;
+    return (size_t)wpb * (NL + NRphys) * (split ? 24 : Q * 16);
 }
 
 int launch_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v, hipStream_t s) {

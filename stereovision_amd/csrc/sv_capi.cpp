@@ -824,6 +824,12 @@ int sv_hog_hist(sv_ctx* c, const uint8_t* gray, int H, int W, int stride, int wi
 int sv_profile_enable(sv_ctx* c, int on) {
     SV_ENTER(c);
     c->prof = on != 0;
+    // create the events up front: hipEventCreate inside a timed loop costs host time
+    while (c->prof && c->pool.size() + 2 * c->pending.size() < 1024) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) break;
+        c->pool.push_back(e);
+    }
     return 0;
 }
 

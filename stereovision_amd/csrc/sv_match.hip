@@ -46,13 +46,18 @@ constexpr int COST_SAD4 = 4;          // internal kind: SAD, four output rows pe
 // 4-row kind, for A/B measurements).
 __host__ __device__ __forceinline__ int seg_width(int lpg, int dpl, int sm = 4) { return (sm * lpg + dpl - 1) / dpl * dpl; }
 __host__ __device__ __forceinline__ int wave_cols(int lpg, int dpl, int sm = 4) { return (64 / lpg) * seg_width(lpg, dpl, sm); }
-int seg_mult(int kind) {
+// 4-row kind: full-length segments when the common words are split into their own array
+// (24-B packs, r <= 5); half-length for the 32-B packs of r 6..7, which would otherwise
+// hold the LDS to 1.5 waves per SIMD.
+int seg_mult(int kind, int r) {
     static const int sm4 = [] {
         const char* e = std::getenv("SV_SAD4_SEG");
-        const int v = e ? std::atoi(e) : 4;
-        return v >= 1 && v <= 8 ? v : 4;
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 1 && v <= 8 ? v : 0;
     }();
-    return kind == COST_SAD4 ? sm4 : 4;
+    if (kind != COST_SAD4) return 4;
+    if (sm4) return sm4;
+    return (2 * r - 2 + 3) / 4 <= 2 ? 4 : 2;
 }
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
@@ -753,7 +758,7 @@ size_t match_lds_bytes(const MatchPlan& p, int r, int cost) {
     const bool split = kind == COST_SAD4 && nw - 4 <= 2;
     const int Q = (nw + 3) / 4;
     const int c0 = (p.dpl - (4 * r + 1) % p.dpl) % p.dpl;
-    const int wc = wave_cols(p.lpg, p.dpl, seg_mult(kind));
+    const int wc = wave_cols(p.lpg, p.dpl, seg_mult(kind, r));
     const int NL = wc + 4 * r + p.dpl + 1;
     const int NRlog = wc + 4 * r + p.lpg * p.dpl + p.dpl;
     const int NRphys = NRlog + (NRlog + c0) / p.dpl + 1;
@@ -779,7 +784,7 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
     const size_t lds = match_lds_bytes(p, a.r, cost);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
     MatchParams b = a;
-    b.segm = seg_mult(kind_of(cost, a.win));
+    b.segm = seg_mult(kind_of(cost, a.win), a.r);
     switch (kind_of(cost, a.win)) {
         case COST_SAD: return launch_nd<COST_SAD>(b, p, lds, s);
         case COST_SAD2: return launch_nd<COST_SAD2>(b, p, lds, s);

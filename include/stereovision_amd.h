@@ -20,6 +20,14 @@
  *   sv_stereo_scaled                 the whole numeric body of create_depth_map_stereo_scaled
  *                                    (fused_depth_map.py:976-1029) minus colormap/putText
  *   sv_harris, sv_hog_hist           north_star stages with no reference counterpart
+ *   sv_init_undistort_rectify_map    cv2.initUndistortRectifyMap(K, dist, R, P, size, CV_16SC2)
+ *                                    depth_map.py:636-641, fused_depth_map.py:402-407
+ *   sv_remap / sv_remap_dev          cv2.remap(img, map1, map2, cv2.INTER_LINEAR)
+ *                                    depth_map.py:815-826, fused_depth_map.py:480-491
+ *   sv_resize_linear                 cv2.resize(img, size) INTER_LINEAR (fused_depth_map.py:474-476)
+ *   sv_rectify_pair                  the two remap calls of apply_stereo_rectification
+ *                                    (depth_map.py:779-834, fused_depth_map.py:444-500) with
+ *                                    the maps resident on the device
  *
  * Conventions
  *   - plain pointers and sizes only; images are row-major uint8, `stride` in bytes;
@@ -66,7 +74,8 @@ enum sv_post { SV_POST_NONE = 0, SV_POST_DEPTH = 1, SV_POST_SCALED = 2 };
 /* kernel ids for the profiling counters */
 enum sv_kernel {
     SV_K_GRAY = 0, SV_K_HARRIS = 1, SV_K_HOG = 2, SV_K_MATCH = 3, SV_K_MEDIAN = 4, SV_K_POST = 5,
-    SV_NKERNELS = 6
+    SV_K_REMAP = 6, SV_K_UNDISTORT = 7, SV_K_RESIZE = 8,
+    SV_NKERNELS = 9
 };
 
 int sv_version(void);
@@ -178,6 +187,48 @@ int sv_harris_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, f
                   void* stream);
 int sv_hog_hist_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, int win,
                     int row0, int row1, uint16_t* d_out, void* stream);
+
+/* ---- rectification ---------------------------------------
+ * K: 3x3 camera matrix, row-major doubles.  dist: ndist in {0, 4, 5, 8, 12, 14} OpenCV
+ * distCoeffs (k1 k2 p1 p2 [k3 [k4 k5 k6 [s1 s2 s3 s4 [tx ty]]]]; a nonzero tilt is
+ * SV_EINVAL).  R: 3x3 rectification rotation or NULL (identity).  P: new camera matrix,
+ * 3 x p_cols row-major (p_cols 3 or 4; NULL = K).  Maps (CV_16SC2 + CV_16UC1 layout, dense
+ * H x W): map1 = int16 (x, y) pairs of the source pixel, map2 = (y & 31) * 32 + (x & 31) of
+ * the 1/32-pixel fraction.  Rounding of the f64 source position follows cvRound. */
+int sv_init_undistort_rectify_map(sv_ctx* ctx, const double* K, const double* dist, int ndist,
+                                  const double* R, const double* P, int p_cols, int H, int W,
+                                  int16_t* map1, uint16_t* map2);
+int sv_init_undistort_rectify_map_dev(sv_ctx* ctx, const double* K, const double* dist, int ndist,
+                                      const double* R, const double* P, int p_cols, int H, int W,
+                                      int16_t* d_map1, uint16_t* d_map2, void* stream);
+
+/* remap INTER_LINEAR, BORDER_CONSTANT 0: src sH x sW x channels (1 or 3) u8 with row pitch
+ * `stride` bytes; map1/map2 (map2 nullable = integer maps) and dst are H x W.  Host memory. */
+int sv_remap(sv_ctx* ctx, const uint8_t* src, int sH, int sW, int channels, int stride,
+             const int16_t* map1, const uint16_t* map2, int H, int W, uint8_t* dst);
+/* Device version over a batch of n_frames sources (frame z at d_src + z*src_frame_stride,
+ * output at d_dst + z*dst_frame_stride), one launch.  gray_out (channels == 3 only) writes
+ * cvtColor(remap(src), BGR2GRAY) instead of the BGR result: the rectified gray image the
+ * matcher reads, in one pass. */
+int sv_remap_dev(sv_ctx* ctx, const uint8_t* d_src, int sH, int sW, int channels, int src_pitch,
+                 int64_t src_frame_stride, const int16_t* d_map1, const uint16_t* d_map2, int H, int W,
+                 int gray_out, uint8_t* d_dst, int dst_pitch, int64_t dst_frame_stride, int n_frames,
+                 void* stream);
+/* apply_stereo_rectification with device-resident maps: host left/right (sH x sW x channels,
+ * row pitch `stride`) -> host rectified left/right (H x W x channels, dense). */
+int sv_rectify_pair(sv_ctx* ctx, const int16_t* d_map1_left, const uint16_t* d_map2_left,
+                    const int16_t* d_map1_right, const uint16_t* d_map2_right, int H, int W,
+                    const uint8_t* left, const uint8_t* right, int sH, int sW, int channels, int stride,
+                    uint8_t* out_left, uint8_t* out_right);
+
+/* cv2.resize(src, (dW, dH)) INTER_LINEAR for u8 gray/BGR (fused_depth_map.py:474-476 and
+ * :2498-2507, depth_map.py:757-776, ensure_same_size depth_map.py:39-71): OpenCV's
+ * fixed-point two-pass bilinear; an exact 2x downscale is OpenCV's INTER_AREA fast path. */
+int sv_resize_linear(sv_ctx* ctx, const uint8_t* src, int sH, int sW, int channels, int stride,
+                     uint8_t* dst, int dH, int dW);
+int sv_resize_linear_dev(sv_ctx* ctx, const uint8_t* d_src, int sH, int sW, int channels,
+                         int src_pitch, int64_t src_frame_stride, uint8_t* d_dst, int dH, int dW,
+                         int dst_pitch, int64_t dst_frame_stride, int n_frames, void* stream);
 
 /* ---- device memory helpers (synchronous on the context stream) -------------------- */
 int sv_dev_alloc(sv_ctx* ctx, uint64_t bytes, void** out);

@@ -91,7 +91,7 @@ struct sv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
-    DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut;
+    DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut, rmap1, rmap2, rdst[2];
     // cached post-processing table: key = (mode, params, range); `lut_ev` marks its build
     struct LutKey {
         int mode = -1, min_disp = 0, num_disp = 0, m0 = 0, n = 0;
@@ -363,6 +363,61 @@ struct Guard {
     Guard guard_(ctx);                                                      \
     if (guard_.rc) return guard_.rc
 
+
+// initUndistortRectifyMap's setup: ir = inv(P[:, :3] * R) with OpenCV's Matx33d product and
+// cofactor inverse (the same operation order as oracle/sv_rectify_oracle.py).
+int make_undistort(const double* K, const double* dist, int ndist, const double* R, const double* P,
+                   int p_cols, int H, int W, sv::UndistortParams* out) {
+    if (!K || H <= 0 || W <= 0) return fail(SV_EINVAL, "bad map arguments");
+    if (H > 32767 || W > 32767) return fail(SV_EINVAL, "map size beyond the int16 coordinate range");
+    if (!(ndist == 0 || ndist == 4 || ndist == 5 || ndist == 8 || ndist == 12 || ndist == 14) ||
+        (ndist > 0 && !dist))
+        return fail(SV_EINVAL, "distCoeffs must have 0, 4, 5, 8, 12 or 14 elements");
+    if (ndist == 14 && (dist[12] != 0.0 || dist[13] != 0.0))
+        return fail(SV_EINVAL, "tilted sensor model (tauX, tauY != 0) is not supported");
+    if (P && p_cols != 3 && p_cols != 4) return fail(SV_EINVAL, "P must be 3x3 or 3x4");
+    double A[9], Rm[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, M[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) A[i * 3 + j] = P ? P[i * p_cols + j] : K[i * 3 + j];
+    if (R) std::memcpy(Rm, R, sizeof(Rm));
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            M[i * 3 + j] = (A[i * 3 + 0] * Rm[0 * 3 + j] + A[i * 3 + 1] * Rm[1 * 3 + j]) + A[i * 3 + 2] * Rm[2 * 3 + j];
+    auto a = [&](int i, int j) { return M[i * 3 + j]; };
+    const double det = a(0, 0) * (a(1, 1) * a(2, 2) - a(2, 1) * a(1, 2)) -
+                       a(0, 1) * (a(1, 0) * a(2, 2) - a(2, 0) * a(1, 2)) +
+                       a(0, 2) * (a(1, 0) * a(2, 1) - a(2, 0) * a(1, 1));
+    if (det == 0.0) return fail(SV_EINVAL, "singular newCameraMatrix * R");
+    const double d = 1.0 / det;
+    double* b = out->ir;
+    b[0] = (a(1, 1) * a(2, 2) - a(1, 2) * a(2, 1)) * d;
+    b[1] = (a(0, 2) * a(2, 1) - a(0, 1) * a(2, 2)) * d;
+    b[2] = (a(0, 1) * a(1, 2) - a(0, 2) * a(1, 1)) * d;
+    b[3] = (a(1, 2) * a(2, 0) - a(1, 0) * a(2, 2)) * d;
+    b[4] = (a(0, 0) * a(2, 2) - a(0, 2) * a(2, 0)) * d;
+    b[5] = (a(0, 2) * a(1, 0) - a(0, 0) * a(1, 2)) * d;
+    b[6] = (a(1, 0) * a(2, 1) - a(1, 1) * a(2, 0)) * d;
+    b[7] = (a(0, 1) * a(2, 0) - a(0, 0) * a(2, 1)) * d;
+    b[8] = (a(0, 0) * a(1, 1) - a(0, 1) * a(1, 0)) * d;
+    out->fx = K[0];
+    out->fy = K[4];
+    out->u0 = K[2];
+    out->v0 = K[5];
+    for (int i = 0; i < 12; ++i) out->k[i] = i < ndist ? dist[i] : 0.0;
+    out->H = H;
+    out->W = W;
+    return 0;
+}
+
+int check_remap(const void* src, int sH, int sW, int channels, int pitch, const void* map1, int H, int W,
+                const void* dst) {
+    if (!src || !map1 || !dst || sH <= 0 || sW <= 0 || H <= 0 || W <= 0)
+        return fail(SV_EINVAL, "bad remap arguments");
+    if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
+    if (pitch < sW * channels) return fail(SV_EINVAL, "source pitch smaller than a row");
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -411,7 +466,8 @@ void sv_destroy(sv_ctx* c) {
         c->prof_drain();
         for (auto e : c->pool) (void)hipEventDestroy(e);
         DevBuf* bufs[] = {&c->img[0], &c->img[1], &c->gray[0], &c->gray[1], &c->d16, &c->fa, &c->fb,
-                          &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->lut};
+                          &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->lut,
+                          &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1]};
         if (c->lut_ev) (void)hipEventDestroy(c->lut_ev);
         for (auto* b : bufs) b->release();
         c->hin.release();
@@ -817,6 +873,156 @@ int sv_hog_hist(sv_ctx* c, const uint8_t* gray, int H, int W, int stride, int wi
     SV_LAUNCH(c, SV_K_HOG, c->stream,
               sv::launch_hog_hist(c->gray[0].as<uint8_t>(), H, W, W, win, 0, H, c->hog[0].as<uint16_t>(), c->stream));
     Out o[] = {{out, c->hog[0].p, n * 10 * sizeof(uint16_t)}};
+    return collect(c, o, 1);
+}
+
+// ---------------------------------------------------------------- rectification
+int sv_init_undistort_rectify_map_dev(sv_ctx* c, const double* K, const double* dist, int ndist, const double* R,
+                                      const double* P, int p_cols, int H, int W, int16_t* d_map1,
+                                      uint16_t* d_map2, void* stream) {
+    SV_ENTER(c);
+    if (!d_map1 || !d_map2) return fail(SV_EINVAL, "null map outputs");
+    sv::UndistortParams up;
+    int rc = make_undistort(K, dist, ndist, R, P, p_cols, H, W, &up);
+    if (rc) return rc;
+    hipStream_t s = pick(c, stream);
+    SV_LAUNCH(c, SV_K_UNDISTORT, s, sv::launch_undistort_map(up, reinterpret_cast<short2*>(d_map1), d_map2, s));
+    return 0;
+}
+
+int sv_init_undistort_rectify_map(sv_ctx* c, const double* K, const double* dist, int ndist, const double* R,
+                                  const double* P, int p_cols, int H, int W, int16_t* map1, uint16_t* map2) {
+    SV_ENTER(c);
+    if (!map1 || !map2) return fail(SV_EINVAL, "null map outputs");
+    sv::UndistortParams up;
+    int rc = make_undistort(K, dist, ndist, R, P, p_cols, H, W, &up);
+    if (rc) return rc;
+    const size_t n = (size_t)H * W;
+    SV_HIP(c->rmap1.ensure(n * 4));
+    SV_HIP(c->rmap2.ensure(n * 2));
+    SV_LAUNCH(c, SV_K_UNDISTORT, c->stream,
+              sv::launch_undistort_map(up, c->rmap1.as<short2>(), c->rmap2.as<uint16_t>(), c->stream));
+    Out o[] = {{map1, c->rmap1.p, n * 4}, {map2, c->rmap2.p, n * 2}};
+    return collect(c, o, 2);
+}
+
+int sv_remap_dev(sv_ctx* c, const uint8_t* d_src, int sH, int sW, int channels, int src_pitch,
+                 int64_t src_frame_stride, const int16_t* d_map1, const uint16_t* d_map2, int H, int W,
+                 int gray_out, uint8_t* d_dst, int dst_pitch, int64_t dst_frame_stride, int n_frames,
+                 void* stream) {
+    SV_ENTER(c);
+    int rc = check_remap(d_src, sH, sW, channels, src_pitch, d_map1, H, W, d_dst);
+    if (rc) return rc;
+    if (gray_out && channels != 3) return fail(SV_EINVAL, "gray_out needs a 3-channel source");
+    const int ob = (channels == 3 && !gray_out) ? 3 : 1;
+    if (dst_pitch < W * ob) return fail(SV_EINVAL, "destination pitch smaller than a row");
+    if (n_frames < 0) return fail(SV_EINVAL, "negative frame count");
+    if (n_frames > 1 && (src_frame_stride < (int64_t)src_pitch * sH || dst_frame_stride < (int64_t)dst_pitch * H))
+        return fail(SV_EINVAL, "frame stride smaller than a frame");
+    if (n_frames == 0) return 0;
+    hipStream_t s = pick(c, stream);
+    SV_LAUNCH(c, SV_K_REMAP, s,
+              sv::launch_remap(d_src, sH, sW, channels, src_pitch, src_frame_stride,
+                               reinterpret_cast<const short2*>(d_map1), d_map2, H, W, gray_out != 0, d_dst,
+                               dst_pitch, dst_frame_stride, n_frames, s));
+    return 0;
+}
+
+// Stage host images (any stride) and host/device maps, remap on the context stream.
+static int remap_host_common(sv_ctx* c, const uint8_t* const* srcs, int nimg, int sH, int sW, int channels,
+                             int stride, const short2* const* dmap1, const uint16_t* const* dmap2, int H, int W,
+                             uint8_t* const* outs) {
+    const size_t row = (size_t)sW * channels, n = row * sH;
+    SV_HIP(c->hin.ensure(nimg * n));
+    for (int k = 0; k < nimg; ++k) {
+        SV_HIP(c->img[k].ensure(n));
+        uint8_t* dst = c->hin.as<uint8_t>() + k * n;
+        if ((size_t)stride == row) {
+            std::memcpy(dst, srcs[k], n);
+        } else {
+            for (int y = 0; y < sH; ++y) std::memcpy(dst + y * row, srcs[k] + (size_t)y * stride, row);
+        }
+        SV_HIP(hipMemcpyAsync(c->img[k].p, dst, n, hipMemcpyHostToDevice, c->stream));
+    }
+    const size_t on = (size_t)H * W * channels;
+    Out o[2];
+    for (int k = 0; k < nimg; ++k) {
+        SV_HIP(c->rdst[k].ensure(on));
+        SV_LAUNCH(c, SV_K_REMAP, c->stream,
+                  sv::launch_remap(c->img[k].as<uint8_t>(), sH, sW, channels, (int)row, 0, dmap1[k], dmap2[k], H, W,
+                                   false, c->rdst[k].as<uint8_t>(), W * channels, 0, 1, c->stream));
+        o[k] = {outs[k], c->rdst[k].p, on};
+    }
+    return collect(c, o, nimg);
+}
+
+int sv_remap(sv_ctx* c, const uint8_t* src, int sH, int sW, int channels, int stride, const int16_t* map1,
+             const uint16_t* map2, int H, int W, uint8_t* dst) {
+    SV_ENTER(c);
+    int rc = check_remap(src, sH, sW, channels, stride, map1, H, W, dst);
+    if (rc) return rc;
+    const size_t n = (size_t)H * W;
+    SV_HIP(c->rmap1.ensure(n * 4));
+    SV_HIP(c->rmap2.ensure(n * 2));
+    SV_HIP(hipMemcpyAsync(c->rmap1.p, map1, n * 4, hipMemcpyHostToDevice, c->stream));
+    if (map2) SV_HIP(hipMemcpyAsync(c->rmap2.p, map2, n * 2, hipMemcpyHostToDevice, c->stream));
+    const short2* m1[1] = {c->rmap1.as<short2>()};
+    const uint16_t* m2[1] = {map2 ? c->rmap2.as<uint16_t>() : nullptr};
+    const uint8_t* srcs[1] = {src};
+    uint8_t* outs[1] = {dst};
+    return remap_host_common(c, srcs, 1, sH, sW, channels, stride, m1, m2, H, W, outs);
+}
+
+int sv_rectify_pair(sv_ctx* c, const int16_t* d_map1_left, const uint16_t* d_map2_left,
+                    const int16_t* d_map1_right, const uint16_t* d_map2_right, int H, int W, const uint8_t* left,
+                    const uint8_t* right, int sH, int sW, int channels, int stride, uint8_t* out_left,
+                    uint8_t* out_right) {
+    SV_ENTER(c);
+    int rc = check_remap(left, sH, sW, channels, stride, d_map1_left, H, W, out_left);
+    if (!rc) rc = check_remap(right, sH, sW, channels, stride, d_map1_right, H, W, out_right);
+    if (rc) return rc;
+    const short2* m1[2] = {reinterpret_cast<const short2*>(d_map1_left), reinterpret_cast<const short2*>(d_map1_right)};
+    const uint16_t* m2[2] = {d_map2_left, d_map2_right};
+    const uint8_t* srcs[2] = {left, right};
+    uint8_t* outs[2] = {out_left, out_right};
+    return remap_host_common(c, srcs, 2, sH, sW, channels, stride, m1, m2, H, W, outs);
+}
+
+int sv_resize_linear_dev(sv_ctx* c, const uint8_t* d_src, int sH, int sW, int channels, int src_pitch,
+                         int64_t src_frame_stride, uint8_t* d_dst, int dH, int dW, int dst_pitch,
+                         int64_t dst_frame_stride, int n_frames, void* stream) {
+    SV_ENTER(c);
+    if (!d_src || !d_dst || sH <= 0 || sW <= 0 || dH <= 0 || dW <= 0 || n_frames < 0)
+        return fail(SV_EINVAL, "bad resize arguments");
+    if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
+    if (src_pitch < sW * channels || dst_pitch < dW * channels) return fail(SV_EINVAL, "pitch smaller than a row");
+    if (n_frames > 1 && (src_frame_stride < (int64_t)src_pitch * sH || dst_frame_stride < (int64_t)dst_pitch * dH))
+        return fail(SV_EINVAL, "frame stride smaller than a frame");
+    if (n_frames == 0) return 0;
+    hipStream_t s = pick(c, stream);
+    SV_LAUNCH(c, SV_K_RESIZE, s,
+              sv::launch_resize_linear(d_src, sH, sW, channels, src_pitch, src_frame_stride, d_dst, dH, dW,
+                                       dst_pitch, dst_frame_stride, n_frames, s));
+    return 0;
+}
+
+int sv_resize_linear(sv_ctx* c, const uint8_t* src, int sH, int sW, int channels, int stride, uint8_t* dst,
+                     int dH, int dW) {
+    SV_ENTER(c);
+    if (!src || !dst || sH <= 0 || sW <= 0 || dH <= 0 || dW <= 0) return fail(SV_EINVAL, "bad resize arguments");
+    if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
+    const size_t row = (size_t)sW * channels, n = row * sH;
+    if (stride < (int)row) return fail(SV_EINVAL, "stride smaller than a row");
+    SV_HIP(c->hin.ensure(n));
+    for (int y = 0; y < sH; ++y) std::memcpy(c->hin.as<uint8_t>() + y * row, src + (size_t)y * stride, row);
+    SV_HIP(c->img[0].ensure(n));
+    const size_t on = (size_t)dH * dW * channels;
+    SV_HIP(c->rdst[0].ensure(on));
+    SV_HIP(hipMemcpyAsync(c->img[0].p, c->hin.p, n, hipMemcpyHostToDevice, c->stream));
+    SV_LAUNCH(c, SV_K_RESIZE, c->stream,
+              sv::launch_resize_linear(c->img[0].as<uint8_t>(), sH, sW, channels, (int)row, 0,
+                                       c->rdst[0].as<uint8_t>(), dH, dW, dW * channels, 0, 1, c->stream));
+    Out o[] = {{dst, c->rdst[0].p, on}};
     return collect(c, o, 1);
 }
 

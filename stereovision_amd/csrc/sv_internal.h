@@ -52,6 +52,22 @@ int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStre
 int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0, int row1,
                     uint16_t* hist, hipStream_t s);
 
+// Rectification (sv_rectify.hip).  ir = inv(P[:, :3] * R) row-major; k = k1 k2 p1 p2 k3 k4
+// k5 k6 s1 s2 s3 s4 (OpenCV distCoeffs order, zero-padded).
+struct UndistortParams {
+    double ir[9];
+    double fx, fy, u0, v0;
+    double k[12];
+    int H, W;
+};
+int launch_undistort_map(const UndistortParams& p, short2* map1, uint16_t* map2, hipStream_t s);
+int launch_remap(const uint8_t* src, int sH, int sW, int channels, int spitch, long long sfs,
+                 const short2* map1, const uint16_t* map2, int H, int W, bool gray_out, uint8_t* dst,
+                 int dpitch, long long dfs, int nf, hipStream_t s);
+
+int launch_resize_linear(const uint8_t* src, int sH, int sW, int cn, int spitch, long long sfs, uint8_t* dst,
+                         int dH, int dW, int dpitch, long long dfs, int nf, hipStream_t s);
+
 // Post-processing modes for the median kernel.
 enum PostMode { POST_NONE = 0, POST_DEPTH = 1, POST_SCALED = 2 };
 struct PostParams {

@@ -18,9 +18,13 @@ from __future__ import annotations
 import numpy as np
 
 from . import colormap
+from . import rectify as _rectify
 from .engine import get_engine
 from .preamble import ensure_same_size as _ensure_same_size
+from .preamble import resize_linear as _resize_linear
 from .preamble import to_engine_image
+
+STEREO_CALIBRATION_FILE = "output/stereo_calibration_data.pkl"   # depth_map.py:22
 
 # Matching parameters — module globals read at call time, as in depth_map.py:31-33.
 MIN_DISP = 16 * 0
@@ -33,6 +37,24 @@ COST = "sad"
 def ensure_same_size(left_img, right_img):
     """depth_map.py:39-71."""
     return _ensure_same_size(left_img, right_img, verbose=True)
+
+
+def load_stereo_calibration(path=None):
+    """depth_map.py:591-668: calibration file -> stereoRectify(alpha=0) -> CV_16SC2 maps
+    (computed on the GPU; the dict also carries the maps resident in HBM)."""
+    return _rectify.load_stereo_calibration(path or STEREO_CALIBRATION_FILE)
+
+
+def resize_to_target(frame, target_size):
+    """depth_map.py:757-776 (cv2.resize INTER_LINEAR on the GPU)."""
+    if frame.shape[1] == target_size[0] and frame.shape[0] == target_size[1]:
+        return frame
+    return _resize_linear(frame, target_size[0], target_size[1])
+
+
+def apply_stereo_rectification(left_img, right_img, stereo_calib):
+    """depth_map.py:779-834: resize to the calibration size, both INTER_LINEAR remaps."""
+    return _rectify.apply_stereo_rectification(left_img, right_img, stereo_calib)
 
 
 def _gray_pair(engine, left_img, right_img):

@@ -21,7 +21,8 @@ LIB_PATH = os.environ.get("SV_LIB_PATH", os.path.join(_HERE, "lib", "libsvhip.so
 
 COSTS = {"sad": 0, "ssd": 1, "hog": 2}
 POST_NONE, POST_DEPTH, POST_SCALED = 0, 1, 2
-KERNELS = {"gray": 0, "harris": 1, "hog": 2, "match": 3, "median": 4, "post": 5}
+KERNELS = {"gray": 0, "harris": 1, "hog": 2, "match": 3, "median": 4, "post": 5, "remap": 6,
+           "undistort": 7, "resize": 8}
 
 # Every symbol include/stereovision_amd.h declares (checked by tests/test_capi.py).
 EXPORTED = [
@@ -32,7 +33,8 @@ EXPORTED = [
     "sv_depth_map_dev", "sv_harris_dev", "sv_hog_hist_dev", "sv_profile_enable",
     "sv_profile_read", "sv_profile_reset", "sv_disparity_rows", "sv_dev_alloc", "sv_dev_free",
     "sv_copy_to_device", "sv_copy_to_host", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
-    "sv_depth_map_batch_dev",
+    "sv_depth_map_batch_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
+    "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
 ]
 
 
@@ -59,6 +61,25 @@ _u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
 _i16p = np.ctypeslib.ndpointer(np.int16, flags="C_CONTIGUOUS")
 _u16p = np.ctypeslib.ndpointer(np.uint16, flags="C_CONTIGUOUS")
 _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+
+
+class _NullableF64:
+    """ndpointer that also accepts None (optional matrices)."""
+
+    @classmethod
+    def from_param(cls, obj):
+        if obj is None:
+            return None
+        return _f64p.from_param(obj)
+
+
+class _NullableU16:
+    @classmethod
+    def from_param(cls, obj):
+        if obj is None:
+            return None
+        return _u16p.from_param(obj)
 
 
 class _NullableF32:
@@ -127,6 +148,22 @@ def _declare(lib):
         "sv_depth_map_batch_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
                                     ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
                                     _c_float, _c_float, _c_float, _vp, _vp, _vp, _vp], _c_int),
+        "sv_init_undistort_rectify_map": ([_vp, _f64p, _NullableF64, _c_int, _NullableF64,
+                                           _NullableF64, _c_int, _c_int, _c_int, _i16p, _u16p],
+                                          _c_int),
+        "sv_init_undistort_rectify_map_dev": ([_vp, _f64p, _NullableF64, _c_int, _NullableF64,
+                                               _NullableF64, _c_int, _c_int, _c_int, _vp, _vp, _vp],
+                                              _c_int),
+        "sv_remap": ([_vp, _u8p, _c_int, _c_int, _c_int, _c_int, _i16p, _NullableU16, _c_int,
+                      _c_int, _u8p], _c_int),
+        "sv_remap_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, ctypes.c_int64, _vp, _vp,
+                          _c_int, _c_int, _c_int, _vp, _c_int, ctypes.c_int64, _c_int, _vp], _c_int),
+        "sv_rectify_pair": ([_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _u8p, _u8p, _c_int, _c_int,
+                             _c_int, _c_int, _u8p, _u8p], _c_int),
+        "sv_resize_linear": ([_vp, _u8p, _c_int, _c_int, _c_int, _c_int, _u8p, _c_int, _c_int],
+                             _c_int),
+        "sv_resize_linear_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, ctypes.c_int64, _vp,
+                                  _c_int, _c_int, _c_int, ctypes.c_int64, _c_int, _vp], _c_int),
         "sv_profile_enable": ([_vp, _c_int], _c_int),
         "sv_profile_read": ([_vp, _c_int, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_longlong)], _c_int),
@@ -439,6 +476,96 @@ class Engine:
                      row1: int, d_out: int, stream: int = 0):
         _check("sv_hog_hist_dev", self.lib.sv_hog_hist_dev(self._h, d_gray, H, W, pitch, win,
                                                            row0, row1, d_out, stream or None))
+
+    # -- rectification (initUndistortRectifyMap / remap) ------------------------------------
+    @staticmethod
+    def _map_params(K, dist, R, P):
+        K = np.ascontiguousarray(np.asarray(K, np.float64).reshape(3, 3))
+        d = None if dist is None else np.ascontiguousarray(np.asarray(dist, np.float64).ravel())
+        nd = 0 if d is None else int(d.size)
+        if nd == 0:
+            d = None
+        Rm = None if R is None else np.ascontiguousarray(np.asarray(R, np.float64).reshape(3, 3))
+        Pm = None
+        pc = 3
+        if P is not None:
+            Pm = np.asarray(P, np.float64)
+            pc = Pm.size // 3
+            Pm = np.ascontiguousarray(Pm.reshape(3, pc))
+        return K, d, nd, Rm, Pm, pc
+
+    def init_undistort_rectify_map(self, K, dist, R, P, width: int, height: int):
+        """cv2.initUndistortRectifyMap(K, dist, R, P, (width, height), CV_16SC2) ->
+        (map1 int16 [H, W, 2], map2 uint16 [H, W])."""
+        K, d, nd, Rm, Pm, pc = self._map_params(K, dist, R, P)
+        m1 = np.empty((height, width, 2), np.int16)
+        m2 = np.empty((height, width), np.uint16)
+        _check("sv_init_undistort_rectify_map", self.lib.sv_init_undistort_rectify_map(
+            self._h, K, d, nd, Rm, Pm, pc, int(height), int(width), m1, m2))
+        return m1, m2
+
+    def init_undistort_rectify_map_dev(self, K, dist, R, P, width: int, height: int, d_map1: int,
+                                       d_map2: int, stream: int = 0):
+        K, d, nd, Rm, Pm, pc = self._map_params(K, dist, R, P)
+        _check("sv_init_undistort_rectify_map_dev", self.lib.sv_init_undistort_rectify_map_dev(
+            self._h, K, d, nd, Rm, Pm, pc, int(height), int(width), d_map1, d_map2, stream or None))
+
+    def remap(self, src, map1, map2) -> np.ndarray:
+        """cv2.remap(src, map1, map2, cv2.INTER_LINEAR) (BORDER_CONSTANT 0), uint8 gray/BGR."""
+        src, sH, sW, C = _image(src)
+        m1 = np.ascontiguousarray(map1, np.int16)
+        if m1.ndim != 3 or m1.shape[2] != 2:
+            raise ValueError(f"map1 must be HxWx2 int16 (CV_16SC2), got {m1.shape}")
+        H, W = m1.shape[:2]
+        m2 = None
+        if map2 is not None and np.asarray(map2).size:
+            m2 = np.ascontiguousarray(map2, np.uint16)
+            if m2.shape != (H, W):
+                raise ValueError(f"map2 shape {m2.shape} != {(H, W)}")
+        out = np.empty((H, W, C) if C == 3 else (H, W), np.uint8)
+        _check("sv_remap", self.lib.sv_remap(self._h, src, sH, sW, C, sW * C, m1, m2, H, W, out))
+        return out
+
+    def remap_dev(self, d_src: int, sH: int, sW: int, channels: int, src_pitch: int,
+                  d_map1: int, d_map2: int, H: int, W: int, d_dst: int, dst_pitch: int,
+                  gray_out: bool = False, n_frames: int = 1, src_frame_stride: int = 0,
+                  dst_frame_stride: int = 0, stream: int = 0):
+        _check("sv_remap_dev", self.lib.sv_remap_dev(
+            self._h, d_src, sH, sW, channels, src_pitch, int(src_frame_stride), d_map1,
+            d_map2 or None, H, W, 1 if gray_out else 0, d_dst, dst_pitch, int(dst_frame_stride),
+            int(n_frames), stream or None))
+
+    def resize(self, src, width: int, height: int) -> np.ndarray:
+        """cv2.resize(src, (width, height)) with INTER_LINEAR, uint8 gray/BGR."""
+        src, sH, sW, C = _image(src)
+        if (sH, sW) == (height, width):
+            return src.copy()
+        out = np.empty((height, width, C) if C == 3 else (height, width), np.uint8)
+        _check("sv_resize_linear", self.lib.sv_resize_linear(self._h, src, sH, sW, C, sW * C, out,
+                                                             int(height), int(width)))
+        return out
+
+    def resize_dev(self, d_src: int, sH: int, sW: int, channels: int, src_pitch: int, d_dst: int,
+                   dH: int, dW: int, dst_pitch: int, n_frames: int = 1, src_frame_stride: int = 0,
+                   dst_frame_stride: int = 0, stream: int = 0):
+        _check("sv_resize_linear_dev", self.lib.sv_resize_linear_dev(
+            self._h, d_src, sH, sW, channels, src_pitch, int(src_frame_stride), d_dst, dH, dW,
+            dst_pitch, int(dst_frame_stride), int(n_frames), stream or None))
+
+    def rectify_pair(self, dmaps, left, right):
+        """Both remaps of apply_stereo_rectification with device-resident maps
+        (``dmaps`` = (d_map1_l, d_map2_l, d_map1_r, d_map2_r, H, W))."""
+        left, sH, sW, C = _image(left)
+        right, sH2, sW2, C2 = _image(right)
+        if (sH, sW, C) != (sH2, sW2, C2):
+            raise ValueError("left/right shapes differ")
+        m1l, m2l, m1r, m2r, H, W = dmaps
+        shape = (H, W, C) if C == 3 else (H, W)
+        ol = np.empty(shape, np.uint8)
+        orr = np.empty(shape, np.uint8)
+        _check("sv_rectify_pair", self.lib.sv_rectify_pair(
+            self._h, m1l, m2l, m1r, m2r, H, W, left, right, sH, sW, C, sW * C, ol, orr))
+        return ol, orr
 
     # -- profiling ------------------------------------------------------------------------
     def profile(self, on: bool = True):

@@ -23,8 +23,11 @@ import traceback
 import numpy as np
 
 from . import colormap
+from . import rectify as _rectify
 from .engine import get_engine
 from .preamble import ensure_same_size, to_engine_image
+
+STEREO_CALIBRATION_FILE = "output/stereo_calibration_data.pkl"   # fused_depth_map.py:61
 
 PROCESSING_SCALE = 0.33
 MIN_DISP_BASE = 0
@@ -44,6 +47,18 @@ def scaled_stereo_params(processing_scale: float = None, num_disp_base: int = No
     if window_size_scaled % 2 == 0:
         window_size_scaled += 1
     return num_disp_scaled, window_size_scaled
+
+
+def load_stereo_calibration_with_scaling(scale_factor=1.0, path=None):
+    """fused_depth_map.py:307-441: camera matrices scaled by ``scale_factor``,
+    stereoRectify(alpha=0, CALIB_ZERO_DISPARITY) at int(w*s) x int(h*s), maps on the GPU."""
+    return _rectify.load_stereo_calibration_with_scaling(scale_factor,
+                                                         path or STEREO_CALIBRATION_FILE)
+
+
+def apply_stereo_rectification(left_img, right_img, stereo_calib):
+    """fused_depth_map.py:444-500: resize to img_size_proc, both INTER_LINEAR remaps."""
+    return _rectify.apply_stereo_rectification(left_img, right_img, stereo_calib)
 
 
 def create_depth_map_stereo_scaled(left_img, right_img, min_disp, num_disp, window_size):

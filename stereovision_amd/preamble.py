@@ -11,48 +11,28 @@ from __future__ import annotations
 
 import numpy as np
 
-try:  # optional: exact cv2.resize when available
-    import cv2  # type: ignore
-except Exception:  # pragma: no cover
-    cv2 = None
 
-
-def _resize_linear(img: np.ndarray, w: int, h: int) -> np.ndarray:
-    """Bilinear resize with half-pixel centres (cv2.INTER_LINEAR geometry; not its
-    fixed-point rounding — only used when cv2 is absent and sizes differ)."""
-    H, W = img.shape[:2]
-    ys = np.clip((np.arange(h) + 0.5) * (H / h) - 0.5, 0, H - 1)
-    xs = np.clip((np.arange(w) + 0.5) * (W / w) - 0.5, 0, W - 1)
-    y0 = np.floor(ys).astype(int)
-    x0 = np.floor(xs).astype(int)
-    y1 = np.minimum(y0 + 1, H - 1)
-    x1 = np.minimum(x0 + 1, W - 1)
-    fy = (ys - y0)[:, None]
-    fx = (xs - x0)[None, :]
-    a = img.astype(np.float32)
-    if a.ndim == 3:
-        fy = fy[..., None]
-        fx = fx[..., None]
-    top = a[y0][:, x0] * (1 - fx) + a[y0][:, x1] * fx
-    bot = a[y1][:, x0] * (1 - fx) + a[y1][:, x1] * fx
-    out = top * (1 - fy) + bot * fy
-    if np.issubdtype(img.dtype, np.integer):
-        out = np.clip(np.rint(out), np.iinfo(img.dtype).min, np.iinfo(img.dtype).max)
-    return out.astype(img.dtype)
+def resize_linear(img: np.ndarray, w: int, h: int) -> np.ndarray:
+    """cv2.resize(img, (w, h)) INTER_LINEAR on the GPU (k_resize_linear, OpenCV's fixed-point
+    bilinear).  uint8 gray/BGR frames only — the reference's camera frames; there is no
+    host fallback."""
+    img = np.asarray(img)
+    if img.dtype != np.uint8:
+        raise TypeError(f"resize: uint8 frames only, got {img.dtype}")
+    from .engine import get_engine
+    return get_engine().resize(img, int(w), int(h))
 
 
 def ensure_same_size(left_img, right_img, verbose: bool = False):
+    """depth_map.py:39-71 / fused_depth_map.py:506-537: both images resized (INTER_LINEAR)
+    to the smaller common size when their sizes differ."""
     h1, w1 = left_img.shape[:2]
     h2, w2 = right_img.shape[:2]
     if (h1, w1) == (h2, w2):
         return left_img, right_img
     h_min, w_min = min(h1, h2), min(w1, w2)
-    if cv2 is not None:
-        left_r = cv2.resize(left_img, (w_min, h_min))
-        right_r = cv2.resize(right_img, (w_min, h_min))
-    else:
-        left_r = _resize_linear(left_img, w_min, h_min)
-        right_r = _resize_linear(right_img, w_min, h_min)
+    left_r = resize_linear(left_img, w_min, h_min)
+    right_r = resize_linear(right_img, w_min, h_min)
     if verbose:
         print(f"Resized: {w1}x{h1} and {w2}x{h2} -> {w_min}x{h_min}")
     return left_r, right_r

@@ -116,13 +116,12 @@ def test_preamble_non_uint8_inputs_follow_reference():
         preamble.to_engine_image(np.zeros((4, 4, 4), np.uint8))
 
 
-def test_ensure_same_size():
+def test_ensure_same_size_passthrough():
     a = np.zeros((10, 20), np.uint8)
-    b = np.zeros((12, 16), np.uint8)
-    x, y = preamble.ensure_same_size(a, b)
-    assert x.shape == y.shape == (10, 16)
     x, y = preamble.ensure_same_size(a, a)
     assert x is a and y is a
+    with pytest.raises(TypeError):          # no host resize path: uint8 frames go to the GPU
+        preamble.resize_linear(np.zeros((4, 4), np.float32), 2, 2)
 
 
 def test_colormaps():

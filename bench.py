@@ -36,7 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from stereovision_amd.engine import get_engine  # noqa: E402
-from stereovision_amd.synthetic import stereo_batch  # noqa: E402
+from stereovision_amd.synthetic import stereo_batch, synthetic_calibration  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2   # 256 CU x 4 SIMD, one wave64 VALU instr per 2 cycles
@@ -87,6 +87,56 @@ def cpu_baseline(H, W, D, win, cost, seconds):
     }
 
 
+def make_rectifier(eng, W, H):
+    """Device-resident CV_16SC2 maps of a synthetic calibration (stereoRectify alpha=0)."""
+    from stereovision_amd import calib
+    from stereovision_amd.rectify import StereoRectifier
+    c = synthetic_calibration(W, H)
+    R1, R2, P1, P2, _, _, _ = calib.stereo_rectify(c["mtx_left"], c["dist_left"], c["mtx_right"],
+                                                   c["dist_right"], (W, H), c["R"], c["T"], alpha=0)
+    return StereoRectifier.from_calibration(c["mtx_left"], c["dist_left"], R1, P1, c["mtx_right"],
+                                            c["dist_right"], R2, P2, (W, H), eng)
+
+
+def hbm_entry(name, bytes_per_launch, ms, n):
+    if not n:
+        return None
+    s = ms / n * 1e-3
+    gbs = bytes_per_launch / s / 1e9
+    return {"kernel": name, "bound": "hbm", "avg_launch_us": round(s * 1e6, 2),
+            "bytes_per_launch": bytes_per_launch, "achieved": round(gbs, 1), "unit": "GB/s",
+            "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4), "launches": n}
+
+
+def aux_kernels(eng, dev, H, W, B, stream, med_ms, med_n, reps=20):
+    """HBM rooflines of the memory-bound kernels around k_match, measured after the timed
+    region (not part of `value`): k_median_i16 from the timed steps, and k_remap (the
+    rectify+gray stage in front of the path) over a batch of B raw 1080p BGR frames."""
+    out = {"k_median_i16": hbm_entry("k_median_i16", 11 * H * W * B, med_ms, med_n)}
+    rect = make_rectifier(eng, W, H)
+    src = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=f"cuda:{dev}")
+    dst = torch.empty((B, H, W), dtype=torch.uint8, device=f"cuda:{dev}")
+    m1, m2 = rect.device_maps[0], rect.device_maps[1]
+    for _ in range(3):
+        eng.remap_dev(src.data_ptr(), H, W, 3, 3 * W, m1, m2, H, W, dst.data_ptr(), W,
+                      gray_out=True, n_frames=B, src_frame_stride=3 * H * W,
+                      dst_frame_stride=H * W, stream=stream)
+    torch.cuda.synchronize()
+    eng.profile_reset()
+    eng.profile(True)
+    for _ in range(reps):
+        eng.remap_dev(src.data_ptr(), H, W, 3, 3 * W, m1, m2, H, W, dst.data_ptr(), W,
+                      gray_out=True, n_frames=B, src_frame_stride=3 * H * W,
+                      dst_frame_stride=H * W, stream=stream)
+    torch.cuda.synchronize()
+    eng.profile(False)
+    ms, n = eng.profile_read("remap")
+    # algorithmic bytes per output pixel: 6 (map1 + map2) + 3 (BGR source) + 1 (gray out)
+    out["k_remap_bgr2gray"] = hbm_entry("k_remap<3,gray>", 10 * H * W * B, ms, n)
+    rect.close()
+    return out
+
+
 def pmc_entry(workload_key):
     """k_match PMC figures per launch from the committed rocprofv3 summary, if any."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -122,6 +172,10 @@ def main():
                          "one frame row-tiled across ranks + RCCL row gather (C5, strong)")
     ap.add_argument("--gather", action="store_true",
                     help="frames mode: gather every step's disparity maps to rank 0 (RCCL)")
+    ap.add_argument("--rectify", action="store_true",
+                    help="camera pipeline: raw BGR frames resident in HBM -> rectify+gray "
+                         "(k_remap, calibrated CV_16SC2 maps) -> disparity -> median/post")
+    ap.add_argument("--no-aux", action="store_true", help="skip the aux-kernel rooflines")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo rehearses N>1 with several ranks on one GPU")
     args = ap.parse_args()
@@ -157,6 +211,15 @@ def main():
     pL = [dL[i].data_ptr() for i in range(F)]
     pR = [dR[i].data_ptr() for i in range(F)]
     rowtile = args.mode == "rowtile"
+    rectify = args.rectify and not rowtile
+    if rectify:      # raw camera frames: BGR, unrectified; gray intermediates per batch
+        rect = make_rectifier(eng, W, H)
+        bL = torch.from_numpy(np.repeat(L[..., None], 3, axis=3)).to(f"cuda:{dev}")
+        bR = torch.from_numpy(np.repeat(R[..., None], 3, axis=3)).to(f"cuda:{dev}")
+        gL = torch.empty((B, H, W), dtype=torch.uint8, device=f"cuda:{dev}")
+        gR = torch.empty((B, H, W), dtype=torch.uint8, device=f"cuda:{dev}")
+        m1l, m2l, m1r, m2r, _, _ = rect.device_maps
+        torch.cuda.synchronize()
     if rowtile:
         from stereovision_amd.distributed import RowTiledDepthMap, gather_rows
         L0, R0 = stereo_batch(1, H, W, D, seed=4242)      # the SAME frame on every rank
@@ -181,7 +244,15 @@ def main():
             gather(band_disp)
             return
         f = (i * B) % F
-        if B == 1:
+        if rectify:
+            for src, m1, m2, g in ((bL, m1l, m2l, gL), (bR, m1r, m2r, gR)):
+                eng.remap_dev(src[f].data_ptr(), H, W, 3, 3 * W, m1, m2, H, W, g.data_ptr(), W,
+                              gray_out=True, n_frames=B, src_frame_stride=3 * H * W,
+                              dst_frame_stride=H * W, stream=stream)
+            eng.depth_map_batch_dev(gL.data_ptr(), gR.data_ptr(), B, H, W, W, H * W, 0, D, win,
+                                    0.3, 2.0, depth.data_ptr(), disp.data_ptr(), norm.data_ptr(),
+                                    cost=args.cost, stream=stream)
+        elif B == 1:
             eng.depth_map_dev(pL[f], pR[f], H, W, W, 0, D, win, 0.3, 2.0, depth.data_ptr(),
                               disp.data_ptr(), norm.data_ptr(), cost=args.cost, stream=stream)
         else:
@@ -216,6 +287,7 @@ def main():
     eng.profile(False)
     match_ms, match_n = eng.profile_read("match")
     med_ms, med_n = eng.profile_read("median")
+    remap_ms, remap_n = eng.profile_read("remap")
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=comm_dev)
@@ -231,6 +303,8 @@ def main():
     k_avg_s = (match_ms / match_n) * 1e-3 if match_n else None
     k_bytes = 4 * npx                          # 2 u8 images read + int16 map written
     frame_bytes = 11 * H * W                   # 2 u8 in; depth f32 + disparity f32 + u8 out
+    if rectify:
+        frame_bytes = 11 * H * W + 2 * 10 * H * W   # + per camera: map 6 B, BGR 3 B, gray 1 B
     roofline = None
     if k_avg_s:
         achieved = k_bytes / k_avg_s / 1e9
@@ -261,8 +335,11 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong" if rowtile else "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic rectified pairs (stereovision_amd.synthetic, seeds per rank)",
-        "config": {"workload": f"{W}x{H} D={D} win={win} {args.cost.upper()} depth_map path "
-                               "(disparity + median5 + depth post), gray inputs resident in HBM",
+        "config": {"workload": (f"{W}x{H} D={D} win={win} {args.cost.upper()} camera pipeline: "
+                                "raw BGR frames resident in HBM -> rectify+gray (k_remap) -> "
+                                "disparity -> median5 + depth post" if rectify else
+                                f"{W}x{H} D={D} win={win} {args.cost.upper()} depth_map path "
+                                "(disparity + median5 + depth post), gray inputs resident in HBM"),
                    "height": H, "width": W, "num_disp": D, "win": win, "cost": args.cost,
                    "frames_resident_per_rank": 1 if rowtile else F,
                    "frames_per_step": 1 if rowtile else B,
@@ -278,8 +355,18 @@ def main():
             "achieved_hbm_frac": round(6 * H * W * value / world / 8.0e12, 5),
             "achieved_valu_frac": round(H * W * D * win * win * value / world / 157.3e12, 4)},
         "roofline": roofline,
+        "aux_kernels": None,
         "cpu_baseline": None,
     }
+    if rectify and remap_n:
+        result["aux_kernels"] = {
+            "k_remap_bgr2gray": hbm_entry("k_remap<3,gray>", 10 * H * W * B, remap_ms, remap_n)}
+        rect.close()
+    elif rank == 0 and world == 1 and not rowtile and not args.no_aux:
+        try:
+            result["aux_kernels"] = aux_kernels(eng, dev, H, W, B, stream, med_ms, med_n)
+        except Exception as e:  # reported, never required
+            log(f"aux kernels failed: {e}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(H, W, D, win, args.cost, args.cpu_seconds)

@@ -64,3 +64,30 @@ def stereo_batch(n: int, H: int, W: int, num_disp: int, seed: int = 0, min_disp:
     for i in range(n):
         L[i], R[i], _ = stereo_pair(H, W, num_disp, seed + i, min_disp)
     return L, R
+
+
+def synthetic_calibration(width: int, height: int, seed: int = 0) -> dict:
+    """A plausible stereo calibration in the reference's file schema
+    (stereo_calibration.py:276-297): two ~70-degree-FOV cameras with radial/tangential
+    distortion, a 8 cm baseline and a ~1 degree relative rotation."""
+    rng = np.random.default_rng(seed)
+    f = 0.7 * width
+
+    def cam(df, dc):
+        return np.array([[f + df[0], 0, width / 2 + dc[0]], [0, f + df[1], height / 2 + dc[1]],
+                         [0, 0, 1.0]])
+
+    r = rng.normal(size=3)
+    r *= np.deg2rad(1.0) / np.linalg.norm(r)
+    theta = np.linalg.norm(r)
+    k = r / theta
+    kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    R = np.cos(theta) * np.eye(3) + (1 - np.cos(theta)) * np.outer(k, k) + np.sin(theta) * kx
+    return {
+        "mtx_left": cam(rng.normal(size=2) * 0.005 * f, rng.normal(size=2) * 0.01 * width),
+        "dist_left": np.array([[-0.12, 0.05, 0.001, -0.0008, -0.01]]),
+        "mtx_right": cam(rng.normal(size=2) * 0.005 * f, rng.normal(size=2) * 0.01 * width),
+        "dist_right": np.array([[-0.10, 0.04, -0.0005, 0.0009, -0.008]]),
+        "R": R, "T": np.array([[-0.08], [0.001], [0.0005]]),
+        "img_size": (int(width), int(height)),
+    }

@@ -6,9 +6,9 @@ cd "$R" || exit 2
 mkdir -p gpurun_out
 step() {
   local name=$1 secs=$2; shift 2
-  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  timeout -k 10 "$secs" "$@" > "$R/gpurun_out/$name.log" 2>&1
   local rc=$?
-  echo "== $name rc=$rc"; tail -n 3 "gpurun_out/$name.log"
+  echo "== $name rc=$rc"; tail -n 3 "$R/gpurun_out/$name.log"
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 step bench_default 300 python bench.py --steps 100 --no-cpu-baseline

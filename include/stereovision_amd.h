@@ -25,6 +25,11 @@
  *   sv_remap / sv_remap_dev          cv2.remap(img, map1, map2, cv2.INTER_LINEAR)
  *                                    depth_map.py:815-826, fused_depth_map.py:480-491
  *   sv_resize_linear                 cv2.resize(img, size) INTER_LINEAR (fused_depth_map.py:474-476)
+ *   sv_frame_stats                   image statistics of detect_camera_occlusion
+ *                                    (fused_depth_map.py:131-301)
+ *   sv_select_count/ranks            order statistics of np.percentile in
+ *                                    calibrate_midas_to_stereo / normalize_to_stereo_range
+ *                                    (fused_depth_map.py:1169-1257, 1503-1554)
  *   sv_rectify_pair                  the two remap calls of apply_stereo_rectification
  *                                    (depth_map.py:779-834, fused_depth_map.py:444-500) with
  *                                    the maps resident on the device
@@ -74,8 +79,9 @@ enum sv_post { SV_POST_NONE = 0, SV_POST_DEPTH = 1, SV_POST_SCALED = 2 };
 /* kernel ids for the profiling counters */
 enum sv_kernel {
     SV_K_GRAY = 0, SV_K_HARRIS = 1, SV_K_HOG = 2, SV_K_MATCH = 3, SV_K_MEDIAN = 4, SV_K_POST = 5,
-    SV_K_REMAP = 6, SV_K_UNDISTORT = 7, SV_K_RESIZE = 8,
-    SV_NKERNELS = 9
+    SV_K_REMAP = 6, SV_K_UNDISTORT = 7, SV_K_RESIZE = 8, SV_K_STATS = 9, SV_K_SELECT = 10,
+    SV_K_AFFINE = 11,
+    SV_NKERNELS = 12
 };
 
 int sv_version(void);
@@ -229,6 +235,43 @@ int sv_resize_linear(sv_ctx* ctx, const uint8_t* src, int sH, int sW, int channe
 int sv_resize_linear_dev(sv_ctx* ctx, const uint8_t* d_src, int sH, int sW, int channels,
                          int src_pitch, int64_t src_frame_stride, uint8_t* d_dst, int dH, int dW,
                          int dst_pitch, int64_t dst_frame_stride, int n_frames, void* stream);
+
+/* ---- reductions around the path ----------------------------
+ * Image statistics of detect_camera_occlusion (fused_depth_map.py:131-301) for one image
+ * or a pair (img1 nullable): per 48x48 block of compute_block_homogeneity
+ * (bh = max(1, H/48) x bw = max(1, W/48) blocks, partial edge tiles excluded as in the
+ * reference) the exact sum and sum of squares of the gray values, and the 256-bin
+ * histogram of the whole image (cv2.calcHist).  channels 3 = BGR, converted with the
+ * cvtColor BGR2GRAY fixed point first.  Outputs per image: block_sum/block_sq [bh*bw],
+ * hist [256]; the pair's second image follows the first. */
+int sv_frame_stats(sv_ctx* ctx, const uint8_t* img0, const uint8_t* img1, int H, int W, int channels,
+                   int stride, uint32_t* block_sum, uint32_t* block_sq, uint32_t* hist);
+int sv_frame_stats_dev(sv_ctx* ctx, const uint8_t* d_img0, const uint8_t* d_img1, int H, int W,
+                       int channels, int pitch, uint32_t* d_block_sum, uint32_t* d_block_sq,
+                       uint32_t* d_hist, void* stream);
+
+/* Order statistics of a float32 device array for np.percentile (calibrate_midas_to_stereo
+ * fused_depth_map.py:1169-1257, normalize_to_stereo_range :1503-1554) with the reference's
+ * masks as predicates: mask_mode 0 = all elements, 1 = elements > 0 (stereo_disparity > 0),
+ * 2 = elements whose d_mask value > thr (stereo_confidence > 0.7).  sv_select_count gives
+ * the number of selected elements and of NaNs among them (np.percentile returns nan if
+ * any); sv_select_ranks gives the values of the given 0-based ranks of the ascending
+ * sorted selection (nranks <= 4; radix select in three passes of 11/11/10 bits).  Both
+ * block until the result is on the host. */
+int sv_select_count(sv_ctx* ctx, const float* d_x, int64_t n, int mask_mode, const float* d_mask,
+                    float thr, int64_t* selected, int64_t* nans);
+int sv_select_ranks(sv_ctx* ctx, const float* d_x, int64_t n, int mask_mode, const float* d_mask,
+                    float thr, const int64_t* ranks, int nranks, float* values);
+/* Elementwise epilogues: mode 0: out = fc + ((x - fa) / fb) * fd in float32, op by op;
+ * mode 1: out = float32(float64(x) * ds + doff); mode 2: out = fc. */
+int sv_affine_f32_dev(sv_ctx* ctx, const float* d_x, int64_t n, int mode, float fa, float fb,
+                      float fc, float fd, double ds, double doff, float* d_out, void* stream);
+
+/* cv2.resize(x, (dW, dH), INTER_LINEAR) of a float32 HxW map (calibrate_midas_to_stereo,
+ * fused_depth_map.py:1216-1217): OpenCV's float path, S0*b0 + S1*b1 without contraction.
+ * Pitches in bytes. */
+int sv_resize_linear_f32_dev(sv_ctx* ctx, const float* d_src, int sH, int sW, int src_pitch,
+                             float* d_dst, int dH, int dW, int dst_pitch, void* stream);
 
 /* ---- device memory helpers (synchronous on the context stream) -------------------- */
 int sv_dev_alloc(sv_ctx* ctx, uint64_t bytes, void** out);

@@ -91,7 +91,7 @@ struct sv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
-    DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut, rmap1, rmap2, rdst[2];
+    DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut, rmap1, rmap2, rdst[2], stats, sel;
     // cached post-processing table: key = (mode, params, range); `lut_ev` marks its build
     struct LutKey {
         int mode = -1, min_disp = 0, num_disp = 0, m0 = 0, n = 0;
@@ -467,7 +467,7 @@ void sv_destroy(sv_ctx* c) {
         for (auto e : c->pool) (void)hipEventDestroy(e);
         DevBuf* bufs[] = {&c->img[0], &c->img[1], &c->gray[0], &c->gray[1], &c->d16, &c->fa, &c->fb,
                           &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->lut,
-                          &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1]};
+                          &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1], &c->stats, &c->sel};
         if (c->lut_ev) (void)hipEventDestroy(c->lut_ev);
         for (auto* b : bufs) b->release();
         c->hin.release();
@@ -1002,7 +1002,18 @@ int sv_resize_linear_dev(sv_ctx* c, const uint8_t* d_src, int sH, int sW, int ch
     hipStream_t s = pick(c, stream);
     SV_LAUNCH(c, SV_K_RESIZE, s,
               sv::launch_resize_linear(d_src, sH, sW, channels, src_pitch, src_frame_stride, d_dst, dH, dW,
-                                       dst_pitch, dst_frame_stride, n_frames, s));
+                                       dst_pitch, dst_frame_stride, n_frames, false, s));
+    return 0;
+}
+
+int sv_resize_linear_f32_dev(sv_ctx* c, const float* d_src, int sH, int sW, int src_pitch, float* d_dst, int dH,
+                             int dW, int dst_pitch, void* stream) {
+    SV_ENTER(c);
+    if (!d_src || !d_dst || sH <= 0 || sW <= 0 || dH <= 0 || dW <= 0) return fail(SV_EINVAL, "bad resize arguments");
+    if (src_pitch < sW * 4 || dst_pitch < dW * 4) return fail(SV_EINVAL, "pitch smaller than a row");
+    hipStream_t s = pick(c, stream);
+    SV_LAUNCH(c, SV_K_RESIZE, s,
+              sv::launch_resize_linear(d_src, sH, sW, 1, src_pitch, 0, d_dst, dH, dW, dst_pitch, 0, 1, true, s));
     return 0;
 }
 
@@ -1021,9 +1032,201 @@ int sv_resize_linear(sv_ctx* c, const uint8_t* src, int sH, int sW, int channels
     SV_HIP(hipMemcpyAsync(c->img[0].p, c->hin.p, n, hipMemcpyHostToDevice, c->stream));
     SV_LAUNCH(c, SV_K_RESIZE, c->stream,
               sv::launch_resize_linear(c->img[0].as<uint8_t>(), sH, sW, channels, (int)row, 0,
-                                       c->rdst[0].as<uint8_t>(), dH, dW, dW * channels, 0, 1, c->stream));
+                                       c->rdst[0].as<uint8_t>(), dH, dW, dW * channels, 0, 1, false, c->stream));
     Out o[] = {{dst, c->rdst[0].p, on}};
     return collect(c, o, 1);
+}
+
+// ---------------------------------------------------------------- reductions
+static void stats_blocks(int H, int W, int* bh, int* bw) {
+    *bh = H / 48 > 0 ? H / 48 : 1;
+    *bw = W / 48 > 0 ? W / 48 : 1;
+}
+
+int sv_frame_stats_dev(sv_ctx* c, const uint8_t* d_img0, const uint8_t* d_img1, int H, int W, int channels,
+                       int pitch, uint32_t* d_block_sum, uint32_t* d_block_sq, uint32_t* d_hist, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_img0, H, W) || !d_block_sum || !d_block_sq || !d_hist)
+        return fail(SV_EINVAL, "bad frame-stats arguments");
+    if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
+    if (pitch < W * channels) return fail(SV_EINVAL, "pitch smaller than a row");
+    hipStream_t s = pick(c, stream);
+    const int nimg = d_img1 ? 2 : 1;
+    SV_HIP(hipMemsetAsync(d_hist, 0, (size_t)nimg * 256 * sizeof(uint32_t), s));
+    sv::FrameStatsArgs a{};
+    a.img0 = d_img0;
+    a.img1 = d_img1;
+    a.H = H;
+    a.W = W;
+    a.pitch = pitch;
+    a.cn = channels;
+    stats_blocks(H, W, &a.bh, &a.bw);
+    a.block_sum = d_block_sum;
+    a.block_sq = d_block_sq;
+    a.hist = d_hist;
+    SV_LAUNCH(c, SV_K_STATS, s, sv::launch_frame_stats(a, nimg, s));
+    return 0;
+}
+
+int sv_frame_stats(sv_ctx* c, const uint8_t* img0, const uint8_t* img1, int H, int W, int channels, int stride,
+                   uint32_t* block_sum, uint32_t* block_sq, uint32_t* hist) {
+    SV_ENTER(c);
+    if (check_image(img0, H, W) || !block_sum || !block_sq || !hist) return fail(SV_EINVAL, "bad frame-stats arguments");
+    if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
+    const size_t row = (size_t)W * channels, n = row * H;
+    if (stride < (int)row) return fail(SV_EINVAL, "stride smaller than a row");
+    const int nimg = img1 ? 2 : 1;
+    int bh, bw;
+    stats_blocks(H, W, &bh, &bw);
+    const size_t nb = (size_t)bh * bw;
+    SV_HIP(c->hin.ensure(nimg * n));
+    const uint8_t* src[2] = {img0, img1};
+    for (int k = 0; k < nimg; ++k) {
+        SV_HIP(c->img[k].ensure(n));
+        uint8_t* dst = c->hin.as<uint8_t>() + k * n;
+        for (int y = 0; y < H; ++y) std::memcpy(dst + y * row, src[k] + (size_t)y * stride, row);
+        SV_HIP(hipMemcpyAsync(c->img[k].p, dst, n, hipMemcpyHostToDevice, c->stream));
+    }
+    SV_HIP(c->stats.ensure(nimg * (2 * nb + 256) * sizeof(uint32_t)));
+    uint32_t* d = c->stats.as<uint32_t>();
+    SV_HIP(hipMemsetAsync(d + 2 * nimg * nb, 0, (size_t)nimg * 256 * sizeof(uint32_t), c->stream));
+    sv::FrameStatsArgs a{};
+    a.img0 = c->img[0].as<uint8_t>();
+    a.img1 = nimg == 2 ? c->img[1].as<uint8_t>() : nullptr;
+    a.H = H;
+    a.W = W;
+    a.pitch = (int)row;
+    a.cn = channels;
+    a.bh = bh;
+    a.bw = bw;
+    a.block_sum = d;
+    a.block_sq = d + nimg * nb;
+    a.hist = d + 2 * nimg * nb;
+    SV_LAUNCH(c, SV_K_STATS, c->stream, sv::launch_frame_stats(a, nimg, c->stream));
+    Out o[] = {{block_sum, a.block_sum, nimg * nb * 4}, {block_sq, a.block_sq, nimg * nb * 4},
+               {hist, a.hist, (size_t)nimg * 256 * 4}};
+    return collect(c, o, 3);
+}
+
+static int check_select(const float* d_x, int64_t n, int mask_mode, const float* d_mask) {
+    if (!d_x || n < 0) return fail(SV_EINVAL, "bad select arguments");
+    if (mask_mode < 0 || mask_mode > 2) return fail(SV_EINVAL, "mask_mode must be 0, 1 or 2");
+    if (mask_mode == 2 && !d_mask) return fail(SV_EINVAL, "mask_mode 2 needs a mask array");
+    return 0;
+}
+
+// One select pass over the context stream: ghist[nranks][2048] back on the host.
+static int select_pass(sv_ctx* c, sv::SelectArgs& a, uint32_t* hist_host, unsigned long long* counts_host) {
+    const size_t hb = (size_t)sv::kMaxRanks * 2048 * sizeof(uint32_t);
+    SV_HIP(c->sel.ensure(hb + 2 * sizeof(unsigned long long)));
+    a.ghist = c->sel.as<uint32_t>();
+    a.counts = counts_host ? reinterpret_cast<unsigned long long*>(c->sel.as<uint8_t>() + hb) : nullptr;
+    SV_HIP(hipMemsetAsync(c->sel.p, 0, hb + 2 * sizeof(unsigned long long), c->stream));
+    SV_LAUNCH(c, SV_K_SELECT, c->stream, sv::launch_select_hist(a, c->stream));
+    SV_HIP(c->hout.ensure(hb + 16));
+    SV_HIP(hipMemcpyAsync(c->hout.p, c->sel.p, hb + 16, hipMemcpyDeviceToHost, c->stream));
+    SV_HIP(hipStreamSynchronize(c->stream));
+    std::memcpy(hist_host, c->hout.p, (size_t)a.nranks * 2048 * sizeof(uint32_t));
+    if (counts_host) std::memcpy(counts_host, c->hout.as<uint8_t>() + hb, 16);
+    return 0;
+}
+
+int sv_select_count(sv_ctx* c, const float* d_x, int64_t n, int mask_mode, const float* d_mask, float thr,
+                    int64_t* selected, int64_t* nans) {
+    SV_ENTER(c);
+    int rc = check_select(d_x, n, mask_mode, d_mask);
+    if (rc) return rc;
+    sv::SelectArgs a{};
+    a.x = d_x;
+    a.mask = d_mask;
+    a.thr = thr;
+    a.mask_mode = mask_mode;
+    a.n = (size_t)n;
+    a.shift = 21;
+    a.bits = 11;
+    a.nranks = 1;
+    std::vector<uint32_t> h(2048);
+    unsigned long long cnt[2] = {0, 0};
+    if (n > 0) {
+        rc = select_pass(c, a, h.data(), cnt);
+        if (rc) return rc;
+    }
+    if (selected) *selected = (int64_t)cnt[0];
+    if (nans) *nans = (int64_t)cnt[1];
+    return 0;
+}
+
+int sv_select_ranks(sv_ctx* c, const float* d_x, int64_t n, int mask_mode, const float* d_mask, float thr,
+                    const int64_t* ranks, int nranks, float* values) {
+    SV_ENTER(c);
+    int rc = check_select(d_x, n, mask_mode, d_mask);
+    if (rc) return rc;
+    if (!ranks || !values || nranks < 1 || nranks > sv::kMaxRanks) return fail(SV_EINVAL, "1..4 ranks");
+    sv::SelectArgs a{};
+    a.x = d_x;
+    a.mask = d_mask;
+    a.thr = thr;
+    a.mask_mode = mask_mode;
+    a.n = (size_t)n;
+    uint32_t prefix[sv::kMaxRanks] = {};
+    int64_t rem[sv::kMaxRanks];
+    for (int r = 0; r < nranks; ++r) {
+        if (ranks[r] < 0) return fail(SV_EINVAL, "negative rank");
+        rem[r] = ranks[r];
+    }
+    std::vector<uint32_t> h((size_t)sv::kMaxRanks * 2048);
+    unsigned long long cnt[2] = {0, 0};
+    const int shifts[3] = {21, 10, 0}, bits[3] = {11, 11, 10};
+    for (int p = 0; p < 3; ++p) {
+        a.shift = shifts[p];
+        a.bits = bits[p];
+        a.nranks = p == 0 ? 1 : nranks;          // pass 0: one histogram serves every rank
+        for (int r = 0; r < nranks; ++r) a.prefix[r] = p == 0 ? 0u : prefix[r];
+        rc = select_pass(c, a, h.data(), p == 0 ? cnt : nullptr);
+        if (rc) return rc;
+        if (p == 0) {
+            for (int r = 0; r < nranks; ++r)
+                if ((unsigned long long)rem[r] >= cnt[0]) return fail(SV_ERANGE, "rank beyond the selection");
+        }
+        for (int r = 0; r < nranks; ++r) {
+            const uint32_t* hr = h.data() + (p == 0 ? 0 : r) * 2048;
+            int64_t acc = 0;
+            int d = 0;
+            for (; d < (1 << bits[p]); ++d) {
+                if (acc + (int64_t)hr[d] > rem[r]) break;
+                acc += hr[d];
+            }
+            if (d == (1 << bits[p])) return fail(SV_EHIP, "select: histogram inconsistent (data changed?)");
+            rem[r] -= acc;
+            prefix[r] = (prefix[r] << bits[p]) | (uint32_t)d;
+        }
+    }
+    for (int r = 0; r < nranks; ++r) {
+        const uint32_t k = prefix[r];
+        const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+        std::memcpy(&values[r], &u, sizeof(float));
+    }
+    return 0;
+}
+
+int sv_affine_f32_dev(sv_ctx* c, const float* d_x, int64_t n, int mode, float fa, float fb, float fc, float fd,
+                      double ds, double doff, float* d_out, void* stream) {
+    SV_ENTER(c);
+    if (!d_x || !d_out || n < 0 || mode < 0 || mode > 2) return fail(SV_EINVAL, "bad affine arguments");
+    hipStream_t s = pick(c, stream);
+    sv::AffineArgs a{};
+    a.x = d_x;
+    a.out = d_out;
+    a.n = (size_t)n;
+    a.mode = mode;
+    a.fa = fa;
+    a.fb = fb;
+    a.fc = fc;
+    a.fd = fd;
+    a.ds = ds;
+    a.doff = doff;
+    SV_LAUNCH(c, SV_K_AFFINE, s, sv::launch_affine_f32(a, s));
+    return 0;
 }
 
 // ---------------------------------------------------------------- profiling

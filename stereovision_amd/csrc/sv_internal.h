@@ -65,8 +65,48 @@ int launch_remap(const uint8_t* src, int sH, int sW, int channels, int spitch, l
                  const short2* map1, const uint16_t* map2, int H, int W, bool gray_out, uint8_t* dst,
                  int dpitch, long long dfs, int nf, hipStream_t s);
 
-int launch_resize_linear(const uint8_t* src, int sH, int sW, int cn, int spitch, long long sfs, uint8_t* dst,
-                         int dH, int dW, int dpitch, long long dfs, int nf, hipStream_t s);
+// u8 (f32 = false) or float32 images; pitches and frame strides in bytes.
+int launch_resize_linear(const void* src, int sH, int sW, int cn, int spitch, long long sfs, void* dst,
+                         int dH, int dW, int dpitch, long long dfs, int nf, bool f32, hipStream_t s);
+
+// Reductions (sv_stats.hip).
+struct FrameStatsArgs {
+    const uint8_t* img0;
+    const uint8_t* img1;      // grid.z = 2: the second image of the pair
+    int H, W, pitch, cn;
+    int bh, bw;               // blocks of compute_block_homogeneity: max(1, H/48) x max(1, W/48)
+    uint32_t* block_sum;      // [nimg][bh][bw]
+    uint32_t* block_sq;
+    uint32_t* hist;           // [nimg][256], accumulated with atomics (zero it first)
+};
+int launch_frame_stats(const FrameStatsArgs& a, int nimg, hipStream_t s);
+
+enum SelectMask { SEL_ALL = 0, SEL_POSITIVE = 1, SEL_MASK_GT = 2 };
+constexpr int kMaxRanks = 4;
+struct SelectArgs {
+    const float* x;
+    const float* mask;        // SEL_MASK_GT: element i selected iff mask[i] > thr
+    float thr;
+    int mask_mode;
+    size_t n;
+    int shift, bits;          // digit = (key >> shift) & ((1 << bits) - 1)
+    int nranks;
+    uint32_t prefix[kMaxRanks];   // key >> (shift + bits) of each rank's target
+    uint32_t* ghist;          // [nranks][2048]
+    unsigned long long* counts;   // pass 0: [selected, nan]
+};
+int launch_select_hist(const SelectArgs& a, hipStream_t s);
+
+enum AffineMode { AFF_F32 = 0, AFF_F64 = 1, AFF_FILL = 2 };
+struct AffineArgs {
+    const float* x;
+    float* out;
+    size_t n;
+    int mode;
+    float fa, fb, fc, fd;     // AFF_F32: fc + ((x - fa) / fb) * fd;  AFF_FILL: fc
+    double ds, doff;          // AFF_F64: float(double(x) * ds + doff)
+};
+int launch_affine_f32(const AffineArgs& a, hipStream_t s);
 
 // Post-processing modes for the median kernel.
 enum PostMode { POST_NONE = 0, POST_DEPTH = 1, POST_SCALED = 2 };

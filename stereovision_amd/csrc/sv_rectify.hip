@@ -181,59 +181,78 @@ __global__ __launch_bounds__(256) void k_remap(RemapArgs a) {
 // to the image; the vertical pass rounds as the scalar FixedPtCast<int, uchar, 22>.
 // An exact 2x downscale takes OpenCV's INTER_AREA fast path (2x2 mean, +2 >> 2).
 struct ResizeArgs {
-    const uint8_t* src;
-    int sH, sW, spitch, cn;
-    uint8_t* dst;
+    const void* src;
+    int sH, sW, spitch, cn;   // pitches in bytes
+    void* dst;
     int dH, dW, dpitch;
     double scale_x, scale_y;
-    long long sfs, dfs;
+    long long sfs, dfs;       // frame strides in bytes
     int area2;
 };
 
 __device__ __forceinline__ void resize_coord(int d, double scale, int n, bool clamp_frac, int& s0,
-                                             int& s1, int& a0, int& a1) {
-    float f = (float)((d + 0.5) * scale - 0.5);
+                                             int& s1, float& f) {
+    f = (float)((d + 0.5) * scale - 0.5);
     int s = (int)floorf(f);
     f -= (float)s;
     if (clamp_frac) {   // x: OpenCV clamps the column and zeroes the fraction
         if (s < 0) f = 0.f, s = 0;
         if (s >= n - 1) f = 0.f, s = n - 1;
     }
-    a0 = (int)__builtin_rintf((1.f - f) * 2048.f);
-    a1 = (int)__builtin_rintf(f * 2048.f);
     s0 = min(max(s, 0), n - 1);
     s1 = min(max(s + 1, 0), n - 1);
 }
 
+// T = uint8_t: fixed point (2^11 coefficients, (h0 b0 + h1 b1 + 2^21) >> 22);
+// T = float: OpenCV's float path, S0*b0 + S1*b1 in f32 without contraction.
+template <typename T>
 __global__ __launch_bounds__(256) void k_resize_linear(ResizeArgs a) {
     const int dx = blockIdx.x * blockDim.x + threadIdx.x;
     const int dy = blockIdx.y;
     if (dx >= a.dW) return;
-    const uint8_t* src = a.src + blockIdx.z * a.sfs;
-    uint8_t* d = a.dst + blockIdx.z * a.dfs + (size_t)dy * a.dpitch + (size_t)dx * a.cn;
+    const uint8_t* src = static_cast<const uint8_t*>(a.src) + blockIdx.z * a.sfs;
+    T* d = reinterpret_cast<T*>(static_cast<uint8_t*>(a.dst) + blockIdx.z * a.dfs + (size_t)dy * a.dpitch) +
+           (size_t)dx * a.cn;
     if (a.area2) {
-        const uint8_t* p = src + (size_t)(2 * dy) * a.spitch + (size_t)(2 * dx) * a.cn;
-        for (int c = 0; c < a.cn; ++c)
-            d[c] = (uint8_t)((p[c] + p[c + a.cn] + p[a.spitch + c] + p[a.spitch + c + a.cn] + 2) >> 2);
+        const T* p = reinterpret_cast<const T*>(src + (size_t)(2 * dy) * a.spitch) + (size_t)(2 * dx) * a.cn;
+        const T* p1 = reinterpret_cast<const T*>(reinterpret_cast<const uint8_t*>(p) + a.spitch);
+        for (int c = 0; c < a.cn; ++c) {
+            if constexpr (sizeof(T) == 1)
+                d[c] = (T)((p[c] + p[c + a.cn] + p1[c] + p1[c + a.cn] + 2) >> 2);
+            else
+                d[c] = (((p[c] + p[c + a.cn]) + p1[c]) + p1[c + a.cn]) * 0.25f;
+        }
         return;
     }
-    int x0, x1, ax0, ax1, y0, y1, by0, by1;
-    resize_coord(dx, a.scale_x, a.sW, true, x0, x1, ax0, ax1);
-    resize_coord(dy, a.scale_y, a.sH, false, y0, y1, by0, by1);
-    const uint8_t* r0 = src + (size_t)y0 * a.spitch;
-    const uint8_t* r1 = src + (size_t)y1 * a.spitch;
-    for (int c = 0; c < a.cn; ++c) {
-        const int h0 = r0[x0 * a.cn + c] * ax0 + r0[x1 * a.cn + c] * ax1;
-        const int h1 = r1[x0 * a.cn + c] * ax0 + r1[x1 * a.cn + c] * ax1;
-        const int v = (h0 * by0 + h1 * by1 + (1 << 21)) >> 22;
-        d[c] = (uint8_t)min(max(v, 0), 255);
+    int x0, x1, y0, y1;
+    float fx, fy;
+    resize_coord(dx, a.scale_x, a.sW, true, x0, x1, fx);
+    resize_coord(dy, a.scale_y, a.sH, false, y0, y1, fy);
+    const T* r0 = reinterpret_cast<const T*>(src + (size_t)y0 * a.spitch);
+    const T* r1 = reinterpret_cast<const T*>(src + (size_t)y1 * a.spitch);
+    if constexpr (sizeof(T) == 1) {
+        const int ax0 = (int)__builtin_rintf((1.f - fx) * 2048.f), ax1 = (int)__builtin_rintf(fx * 2048.f);
+        const int by0 = (int)__builtin_rintf((1.f - fy) * 2048.f), by1 = (int)__builtin_rintf(fy * 2048.f);
+        for (int c = 0; c < a.cn; ++c) {
+            const int h0 = r0[x0 * a.cn + c] * ax0 + r0[x1 * a.cn + c] * ax1;
+            const int h1 = r1[x0 * a.cn + c] * ax0 + r1[x1 * a.cn + c] * ax1;
+            const int v = (h0 * by0 + h1 * by1 + (1 << 21)) >> 22;
+            d[c] = (T)min(max(v, 0), 255);
+        }
+    } else {
+        const float ax0 = 1.f - fx, ax1 = fx, by0 = 1.f - fy, by1 = fy;
+        for (int c = 0; c < a.cn; ++c) {
+            const float h0 = r0[x0 * a.cn + c] * ax0 + r0[x1 * a.cn + c] * ax1;
+            const float h1 = r1[x0 * a.cn + c] * ax0 + r1[x1 * a.cn + c] * ax1;
+            d[c] = h0 * by0 + h1 * by1;
+        }
     }
 }
 
 }  // namespace
 
-int launch_resize_linear(const uint8_t* src, int sH, int sW, int cn, int spitch, long long sfs, uint8_t* dst,
-                         int dH, int dW, int dpitch, long long dfs, int nf, hipStream_t s) {
+int launch_resize_linear(const void* src, int sH, int sW, int cn, int spitch, long long sfs, void* dst,
+                         int dH, int dW, int dpitch, long long dfs, int nf, bool f32, hipStream_t s) {
     if (dH <= 0 || dW <= 0 || nf <= 0) return 0;
     ResizeArgs a;
     a.src = src;
@@ -252,7 +271,10 @@ int launch_resize_linear(const uint8_t* src, int sH, int sW, int cn, int spitch,
     a.scale_y = 1. / inv_y;
     a.area2 = (a.scale_x == 2.0 && a.scale_y == 2.0) ? 1 : 0;
     dim3 grid((dW + 255) / 256, dH, nf);
-    hipLaunchKernelGGL(k_resize_linear, grid, dim3(256), 0, s, a);
+    if (f32)
+        hipLaunchKernelGGL(k_resize_linear<float>, grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_resize_linear<uint8_t>, grid, dim3(256), 0, s, a);
     return (int)hipGetLastError();
 }
 

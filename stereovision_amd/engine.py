@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("SV_LIB_PATH", os.path.join(_HERE, "lib", "libsvhip.so
 COSTS = {"sad": 0, "ssd": 1, "hog": 2}
 POST_NONE, POST_DEPTH, POST_SCALED = 0, 1, 2
 KERNELS = {"gray": 0, "harris": 1, "hog": 2, "match": 3, "median": 4, "post": 5, "remap": 6,
-           "undistort": 7, "resize": 8}
+           "undistort": 7, "resize": 8, "stats": 9, "select": 10, "affine": 11}
 
 # Every symbol include/stereovision_amd.h declares (checked by tests/test_capi.py).
 EXPORTED = [
@@ -35,6 +35,8 @@ EXPORTED = [
     "sv_copy_to_device", "sv_copy_to_host", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
     "sv_depth_map_batch_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
     "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
+    "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
+    "sv_select_ranks", "sv_affine_f32_dev",
 ]
 
 
@@ -62,6 +64,8 @@ _i16p = np.ctypeslib.ndpointer(np.int16, flags="C_CONTIGUOUS")
 _u16p = np.ctypeslib.ndpointer(np.uint16, flags="C_CONTIGUOUS")
 _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
 _f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+_u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
 
 
 class _NullableF64:
@@ -164,6 +168,18 @@ def _declare(lib):
                              _c_int),
         "sv_resize_linear_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, ctypes.c_int64, _vp,
                                   _c_int, _c_int, _c_int, ctypes.c_int64, _c_int, _vp], _c_int),
+        "sv_resize_linear_f32_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int,
+                                      _vp], _c_int),
+        "sv_frame_stats": ([_vp, _u8p, _vp, _c_int, _c_int, _c_int, _c_int, _u32p, _u32p, _u32p],
+                           _c_int),
+        "sv_frame_stats_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
+                               _c_int),
+        "sv_select_count": ([_vp, _vp, ctypes.c_int64, _c_int, _vp, _c_float,
+                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)], _c_int),
+        "sv_select_ranks": ([_vp, _vp, ctypes.c_int64, _c_int, _vp, _c_float, _i64p, _c_int, _f32p],
+                            _c_int),
+        "sv_affine_f32_dev": ([_vp, _vp, ctypes.c_int64, _c_int, _c_float, _c_float, _c_float, _c_float,
+                               ctypes.c_double, ctypes.c_double, _vp, _vp], _c_int),
         "sv_profile_enable": ([_vp, _c_int], _c_int),
         "sv_profile_read": ([_vp, _c_int, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_longlong)], _c_int),
@@ -249,12 +265,34 @@ class Engine:
             raise EngineUnavailable(f"sv_create({device}) failed ({rc}): {last_error()}")
         self._h = h
         self.device = device
+        self._scratch: dict[str, tuple[int, int]] = {}
 
     # -- lifetime -------------------------------------------------------------------
     def close(self):
         if getattr(self, "_h", None):
+            for p, _ in self._scratch.values():
+                self.lib.sv_dev_free(self._h, p)
+            self._scratch = {}
             self.lib.sv_destroy(self._h)
             self._h = None
+
+    def scratch(self, name: str, nbytes: int) -> int:
+        """A grow-only device buffer owned by this engine (for host-array entry points)."""
+        p, cap = self._scratch.get(name, (0, 0))
+        if cap < nbytes:
+            if p:
+                self.dev_free(p)
+            p = self.dev_alloc(max(int(nbytes), 256))
+            self._scratch[name] = (p, max(int(nbytes), 256))
+        return p
+
+    def upload(self, name: str, a: np.ndarray) -> int:
+        """Copy a host array into the named scratch buffer; returns its device pointer."""
+        a = np.ascontiguousarray(a)
+        p = self.scratch(name, a.nbytes)
+        if a.nbytes:
+            self.to_device(p, a)
+        return p
 
     def __del__(self):  # pragma: no cover - best effort
         try:
@@ -551,6 +589,59 @@ class Engine:
         _check("sv_resize_linear_dev", self.lib.sv_resize_linear_dev(
             self._h, d_src, sH, sW, channels, src_pitch, int(src_frame_stride), d_dst, dH, dW,
             dst_pitch, int(dst_frame_stride), int(n_frames), stream or None))
+
+    def resize_f32_dev(self, d_src: int, sH: int, sW: int, d_dst: int, dH: int, dW: int,
+                       stream: int = 0):
+        _check("sv_resize_linear_f32_dev", self.lib.sv_resize_linear_f32_dev(
+            self._h, d_src, sH, sW, sW * 4, d_dst, dH, dW, dW * 4, stream or None))
+
+    # -- reductions (occlusion statistics, percentile order statistics) ------------------
+    def frame_stats(self, img0, img1=None):
+        """Per-48x48-block (sum, sum of squares) and the 256-bin histogram of one gray/BGR
+        image or a pair -> (block_sum [n, bh, bw], block_sq [n, bh, bw], hist [n, 256])."""
+        img0, H, W, C = _image(img0)
+        n = 1
+        if img1 is not None:
+            img1, H2, W2, C2 = _image(img1)
+            if (H2, W2, C2) != (H, W, C):
+                raise ValueError("frame_stats: the two images differ in shape")
+            n = 2
+        bh, bw = max(1, H // 48), max(1, W // 48)
+        bs = np.empty((n, bh, bw), np.uint32)
+        bq = np.empty((n, bh, bw), np.uint32)
+        hist = np.empty((n, 256), np.uint32)
+        _check("sv_frame_stats", self.lib.sv_frame_stats(
+            self._h, img0, img1.ctypes.data if img1 is not None else None, H, W, C, W * C, bs, bq,
+            hist))
+        return bs, bq, hist
+
+    def frame_stats_dev(self, d_img0: int, d_img1: int, H: int, W: int, channels: int, pitch: int,
+                        d_block_sum: int, d_block_sq: int, d_hist: int, stream: int = 0):
+        _check("sv_frame_stats_dev", self.lib.sv_frame_stats_dev(
+            self._h, d_img0, d_img1 or None, H, W, channels, pitch, d_block_sum, d_block_sq, d_hist,
+            stream or None))
+
+    def select_count(self, d_x: int, n: int, mask_mode: int = 0, d_mask: int = 0,
+                     thr: float = 0.0) -> tuple[int, int]:
+        sel, nan = ctypes.c_int64(), ctypes.c_int64()
+        _check("sv_select_count", self.lib.sv_select_count(
+            self._h, d_x, int(n), int(mask_mode), d_mask or None, np.float32(thr), ctypes.byref(sel),
+            ctypes.byref(nan)))
+        return sel.value, nan.value
+
+    def select_ranks(self, d_x: int, n: int, ranks, mask_mode: int = 0, d_mask: int = 0,
+                     thr: float = 0.0) -> np.ndarray:
+        r = np.ascontiguousarray(np.asarray(ranks, np.int64).ravel())
+        out = np.empty(r.size, np.float32)
+        _check("sv_select_ranks", self.lib.sv_select_ranks(
+            self._h, d_x, int(n), int(mask_mode), d_mask or None, np.float32(thr), r, r.size, out))
+        return out
+
+    def affine_f32_dev(self, d_x: int, n: int, mode: int, d_out: int, fa=0.0, fb=1.0, fc=0.0,
+                       fd=0.0, ds=1.0, doff=0.0, stream: int = 0):
+        _check("sv_affine_f32_dev", self.lib.sv_affine_f32_dev(
+            self._h, d_x, int(n), int(mode), np.float32(fa), np.float32(fb), np.float32(fc),
+            np.float32(fd), float(ds), float(doff), d_out, stream or None))
 
     def rectify_pair(self, dmaps, left, right):
         """Both remaps of apply_stereo_rectification with device-resident maps

@@ -24,6 +24,8 @@ import numpy as np
 
 from . import colormap
 from . import rectify as _rectify
+from .fusion import (calibrate_midas_to_stereo, detect_camera_occlusion,  # noqa: F401
+                     normalize_to_stereo_range)
 from .engine import get_engine
 from .preamble import ensure_same_size, to_engine_image
 

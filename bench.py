@@ -134,6 +134,29 @@ def aux_kernels(eng, dev, H, W, B, stream, med_ms, med_n, reps=20):
     # algorithmic bytes per output pixel: 6 (map1 + map2) + 3 (BGR source) + 1 (gray out)
     out["k_remap_bgr2gray"] = hbm_entry("k_remap<3,gray>", 10 * H * W * B, ms, n)
     rect.close()
+    # occlusion statistics of a rectified gray pair (1 B/px per image read once)
+    nb = max(1, H // 48) * max(1, W // 48)
+    st = torch.zeros(2 * (2 * nb + 256), dtype=torch.int32, device=f"cuda:{dev}")
+    p0 = dst[0].data_ptr()
+    p1 = dst[1].data_ptr()
+    sp = st.data_ptr()
+    eng.profile_reset()
+    eng.profile(True)
+    for _ in range(reps):
+        eng.frame_stats_dev(p0, p1, H, W, 1, W, sp, sp + 8 * nb, sp + 16 * nb, stream=stream)
+    torch.cuda.synchronize()
+    eng.profile(False)
+    ms, n = eng.profile_read("stats")
+    out["k_frame_stats"] = hbm_entry("k_frame_stats", 2 * H * W, ms, n)
+    # one radix-select pass over a float32 disparity map (4 B/px)
+    d = torch.rand((H, W), dtype=torch.float32, device=f"cuda:{dev}")
+    eng.profile_reset()
+    eng.profile(True)
+    for _ in range(reps):
+        eng.select_count(d.data_ptr(), H * W, 1)
+    eng.profile(False)
+    ms, n = eng.profile_read("select")
+    out["k_select_hist"] = hbm_entry("k_select_hist", 4 * H * W, ms, n)
     return out
 
 

@@ -46,8 +46,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_baseline_sgbm(H, W, D, win, seconds):
+    """SGBM mode: the NumPy SGBM-3WAY oracle (single process) on horizontal strips of the
+    frame (full width, the whole disparity range), scaled to frames/s by the strip share."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sv_sgbm_oracle as SG  # test infrastructure, used here only as the CPU baseline
+    L, R = stereo_batch(1, H, W, D, seed=4242)
+    rows = max(8, min(H, 64))
+    n, t0 = 0, time.perf_counter()
+    while True:
+        y0 = (n * rows) % max(1, H - rows + 1)
+        SG.sgbm(L[0, y0:y0 + rows], R[0, y0:y0 + rows], 0, D, win)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds or n >= 50:
+            break
+    fps = n * rows / H / dt
+    return {"value": round(fps, 4), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} strips of {rows}x{W} (D={D}, win={win}) of the NumPy SGBM-3WAY oracle "
+                      f"in {dt:.1f} s, scaled by {rows}/{H} rows to frames/s; single process"}
+
+
 def cpu_baseline(H, W, D, win, cost, seconds):
     """C oracle (the port) timed on this host: whole app-1 path per frame."""
+    if cost == "sgbm":
+        return cpu_baseline_sgbm(H, W, D, win, seconds)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import sv_oracle_c as C  # test infrastructure, used here only as the CPU baseline
     lib = C.lib()
@@ -179,7 +202,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--num-disp", type=int, default=128)
     ap.add_argument("--win", type=int, default=9)
-    ap.add_argument("--cost", default="sad", choices=["sad", "ssd", "hog"])
+    ap.add_argument("--cost", default="sad", choices=["sad", "ssd", "hog", "sgbm"],
+                    help="sad/ssd/hog: the north_star WTA engine; sgbm: the SGBM-3WAY mode")
     ap.add_argument("--frames", type=int, default=8, help="distinct resident frames per rank")
     ap.add_argument("--batch", type=int, default=8,
                     help="frames mode: frames per step, one launch per kernel over the batch "
@@ -308,9 +332,10 @@ def main():
     elapsed = time.perf_counter() - t0
 
     eng.profile(False)
-    match_ms, match_n = eng.profile_read("match")
+    match_ms, match_n = eng.profile_read("sgbm" if args.cost == "sgbm" else "match")
     med_ms, med_n = eng.profile_read("median")
     remap_ms, remap_n = eng.profile_read("remap")
+    k_name = "sgbm pipeline (k_sgbm_*)" if args.cost == "sgbm" else "k_match"
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=comm_dev)
@@ -334,7 +359,7 @@ def main():
         pmc = pmc_entry(f"{W}x{H}_D{D}_w{win}_{args.cost}" + (f"_b{B}" if B > 1 and not rowtile else ""))
         insts = pmc.get("valu_insts_per_launch")
         roofline = {
-            "kernel": "k_match", "bound": "hbm", "achieved": round(achieved, 2),
+            "kernel": k_name, "bound": "hbm", "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": pmc.get("hbm_bytes_per_launch"),
             "bytes_per_launch": k_bytes, "avg_launch_us": round(k_avg_s * 1e6, 2),

@@ -60,7 +60,12 @@ extern "C" {
 
 typedef struct sv_ctx sv_ctx;
 
-enum sv_cost { SV_COST_SAD = 0, SV_COST_SSD = 1, SV_COST_HOG = 2 };
+/* SAD / SSD / HOG: the north_star winner-take-all engine.  SGBM: OpenCV's SGBM-3WAY
+ * algorithm restated (the reference's own matcher), with the reference's parameters
+ * P1 = 24 win^2, P2 = 96 win^2, disp12MaxDiff 1, uniquenessRatio 10, speckle 100 / 32,
+ * preFilterCap 63 (depth_map.py:894-906) when selected through the generic entry points;
+ * sv_sgbm / sv_sgbm_dev take every parameter.  SGBM is frame-only (no row bands). */
+enum sv_cost { SV_COST_SAD = 0, SV_COST_SSD = 1, SV_COST_HOG = 2, SV_COST_SGBM = 3 };
 
 enum sv_status {
     SV_OK = 0,
@@ -80,8 +85,8 @@ enum sv_post { SV_POST_NONE = 0, SV_POST_DEPTH = 1, SV_POST_SCALED = 2 };
 enum sv_kernel {
     SV_K_GRAY = 0, SV_K_HARRIS = 1, SV_K_HOG = 2, SV_K_MATCH = 3, SV_K_MEDIAN = 4, SV_K_POST = 5,
     SV_K_REMAP = 6, SV_K_UNDISTORT = 7, SV_K_RESIZE = 8, SV_K_STATS = 9, SV_K_SELECT = 10,
-    SV_K_AFFINE = 11,
-    SV_NKERNELS = 12
+    SV_K_AFFINE = 11, SV_K_SGBM = 12, SV_K_SPECKLE = 13,
+    SV_NKERNELS = 14
 };
 
 int sv_version(void);
@@ -235,6 +240,22 @@ int sv_resize_linear(sv_ctx* ctx, const uint8_t* src, int sH, int sW, int channe
 int sv_resize_linear_dev(sv_ctx* ctx, const uint8_t* d_src, int sH, int sW, int channels,
                          int src_pitch, int64_t src_frame_stride, uint8_t* d_dst, int dH, int dW,
                          int dst_pitch, int64_t dst_frame_stride, int n_frames, void* stream);
+
+/* ---- SGBM-3WAY mode -----------------------------------------
+ * cv2.StereoSGBM_create(minDisparity, numDisparities, blockSize, P1, P2, disp12MaxDiff,
+ * preFilterCap, uniquenessRatio, speckleWindowSize, speckleRange, MODE_SGBM_3WAY)
+ * .compute(left, right) (depth_map.py:894-909): int16 x16 map, invalid = (minD-1)*16.
+ * Semantics in oracle/sv_sgbm_oracle.py (one stripe; int32 aggregation).  Limits:
+ * num_disp <= 512, block_size odd <= 15, P2 < 349525, P1 < P2 (P2 = max(P2, P1+1)).
+ * disp12MaxDiff < 0 disables the left-right check; speckleWindowSize <= 0 the filter. */
+int sv_sgbm(sv_ctx* ctx, const uint8_t* left, const uint8_t* right, int H, int W, int channels,
+            int stride, int min_disp, int num_disp, int block_size, int P1, int P2,
+            int disp12_max_diff, int pre_filter_cap, int uniqueness_ratio,
+            int speckle_window_size, int speckle_range, int16_t* disp16);
+int sv_sgbm_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int H, int W, int pitch,
+                int min_disp, int num_disp, int block_size, int P1, int P2, int disp12_max_diff,
+                int pre_filter_cap, int uniqueness_ratio, int speckle_window_size,
+                int speckle_range, int16_t* d_disp16, int out_pitch, void* stream);
 
 /* ---- reductions around the path ----------------------------
  * Image statistics of detect_camera_occlusion (fused_depth_map.py:131-301) for one image

@@ -91,7 +91,8 @@ struct sv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
-    DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut, rmap1, rmap2, rdst[2], stats, sel;
+    DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut, rmap1, rmap2, rdst[2], stats, sel,
+        sg_hsum, sg_c, sg_l, sg_band, cc_parent, cc_size;
     // cached post-processing table: key = (mode, params, range); `lut_ev` marks its build
     struct LutKey {
         int mode = -1, min_disp = 0, num_disp = 0, m0 = 0, n = 0;
@@ -165,9 +166,79 @@ int check_match(int H, int W, int min_disp, int num_disp, int win, int cost, sv:
     if (num_disp <= 0 || num_disp > 512) return fail(SV_EINVAL, "num_disp must be in [1, 512]");
     if (win < 1 || win > 15 || (win & 1) == 0) return fail(SV_EINVAL, "win must be odd in [1, 15]");
     if (min_disp < -4096 || min_disp > 4096) return fail(SV_EINVAL, "min_disp out of range");
+    if (cost == SV_COST_SGBM) return 0;   // no lane plan: sv_sgbm.hip sizes itself
     int rc = sv::plan_match(num_disp, win, cost, plan);
     if (rc == -34) return fail(SV_ERANGE, "cost range too large for the argmin key");
     if (rc != 0) return fail(SV_EINVAL, "unsupported (num_disp, win, cost)");
+    return 0;
+}
+
+
+struct SgbmParams {
+    int P1, P2, disp12, cap, uniq, speckle_win, speckle_range;
+};
+
+SgbmParams sgbm_reference_params(int win) {
+    // depth_map.py:894-906 / fused_depth_map.py:988-1000
+    return {8 * 3 * win * win, 32 * 3 * win * win, 1, 63, 10, 100, 32};
+}
+
+// Enqueue the whole SGBM-3WAY pipeline for one frame (buffers grown in the context).
+int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, int pitch, int min_disp,
+                 int num_disp, int win, SgbmParams p, int16_t* out, int opitch, hipStream_t s) {
+    if (sv::sgbm_dpl(num_disp) < 0) return fail(SV_EINVAL, "num_disp must be in [1, 512]");
+    if (W > 16384) return fail(SV_EINVAL, "SGBM: width beyond 16384");
+    if (p.P1 < 0 || p.P2 < 0) return fail(SV_EINVAL, "negative P1/P2");
+    if (p.P2 <= p.P1) p.P2 = p.P1 + 1;                       // OpenCV: P2 = max(P2, P1 + 1)
+    if (p.P2 >= 349525) return fail(SV_ERANGE, "SGBM: P2 too large for the 32-bit argmin key");
+    p.cap = (p.cap > 15 ? p.cap : 15) | 1;                   // OpenCV's ftzero
+    if (p.cap > 127) return fail(SV_EINVAL, "preFilterCap must be <= 127");
+    sv::SgbmArgs a{};
+    a.L = L;
+    a.R = R;
+    a.H = H;
+    a.W = W;
+    a.pitch = pitch;
+    a.minD = min_disp;
+    a.D = num_disp;
+    a.r = win / 2;
+    const int maxd = min_disp + num_disp;
+    a.X0 = maxd > 0 ? maxd : 0;
+    int X1 = W + (min_disp < 0 ? min_disp : 0);
+    if (X1 > W) X1 = W;
+    a.Wb = X1 > a.X0 ? X1 - a.X0 : 0;
+    a.cap = p.cap;
+    a.P1 = p.P1;
+    a.P2 = p.P2;
+    a.uniq = p.uniq < 0 ? 10 : p.uniq;
+    a.disp12 = p.disp12;
+    const long long cmax = (long long)(2 * p.cap + 63) * win * win;   // max window cost
+    if (cmax > 65535) return fail(SV_EINVAL, "SGBM: window cost beyond 16 bits (lower preFilterCap/blockSize)");
+    a.l32 = (cmax > 32767 || p.P2 > 32768) ? 1 : 0;
+    const int dpl = sv::sgbm_dpl(num_disp);
+    a.Dp = (num_disp + dpl - 1) / dpl * dpl;
+    const size_t vol = (size_t)H * a.Wb * a.Dp;
+    SV_HIP(c->sg_hsum.ensure(vol * 2 + 256));
+    SV_HIP(c->sg_c.ensure(vol * 2 + 256));
+    SV_HIP(c->sg_l.ensure(vol * (a.l32 ? 8 : 2) + 256));
+    SV_HIP(c->sg_band.ensure((size_t)H * a.Wb * 8 + 256));
+    a.hsum = c->sg_hsum.as<uint16_t>();
+    a.C = c->sg_c.as<uint16_t>();
+    // int16 paths: L_lr reuses the hsum volume (dead after the window-row sums)
+    a.Llr = a.l32 ? c->sg_l.p : c->sg_hsum.p;
+    a.Lrl = a.l32 ? (void*)(c->sg_l.as<int32_t>() + vol) : c->sg_l.p;
+    a.band = c->sg_band.p;
+    a.out = out;
+    a.opitch = opitch;
+    SV_LAUNCH(c, SV_K_SGBM, s, sv::launch_sgbm(a, s));
+    if (p.speckle_win > 0) {
+        const size_t n = (size_t)H * W;
+        SV_HIP(c->cc_parent.ensure(n * 4));
+        SV_HIP(c->cc_size.ensure(n * 4));
+        SV_LAUNCH(c, SV_K_SPECKLE, s,
+                  sv::launch_speckles(out, H, W, opitch, (min_disp - 1) * 16, p.speckle_win, 16 * p.speckle_range,
+                                      c->cc_parent.as<int>(), c->cc_size.as<int>(), s));
+    }
     return 0;
 }
 
@@ -192,6 +263,15 @@ int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int 
     if (row0 < 0) row0 = 0;
     if (row1 > H) row1 = H;
     if (row1 <= row0) return 0;
+    if (cost == SV_COST_SGBM) {   // the top-down path crosses rows: whole frames only
+        if (row0 != 0 || row1 != H) return fail(SV_EINVAL, "SGBM cannot compute a row band (use frames)");
+        for (int z = 0; z < (nf < 1 ? 1 : nf); ++z) {
+            rc = enqueue_sgbm(c, L + z * fs_in, R + z * fs_in, H, W, pitch, min_disp, num_disp, win,
+                              sgbm_reference_params(win), out + z * fs_out, opitch, s);
+            if (rc) return rc;
+        }
+        return 0;
+    }
     sv::MatchParams a{};
     a.L = L;
     a.R = R;
@@ -467,7 +547,9 @@ void sv_destroy(sv_ctx* c) {
         for (auto e : c->pool) (void)hipEventDestroy(e);
         DevBuf* bufs[] = {&c->img[0], &c->img[1], &c->gray[0], &c->gray[1], &c->d16, &c->fa, &c->fb,
                           &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->lut,
-                          &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1], &c->stats, &c->sel};
+                          &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1], &c->stats, &c->sel,
+                          &c->sg_hsum, &c->sg_c, &c->sg_l, &c->sg_band, &c->cc_parent,
+                          &c->cc_size};
         if (c->lut_ev) (void)hipEventDestroy(c->lut_ev);
         for (auto* b : bufs) b->release();
         c->hin.release();
@@ -1227,6 +1309,41 @@ int sv_affine_f32_dev(sv_ctx* c, const float* d_x, int64_t n, int mode, float fa
     a.doff = doff;
     SV_LAUNCH(c, SV_K_AFFINE, s, sv::launch_affine_f32(a, s));
     return 0;
+}
+
+// ---------------------------------------------------------------- SGBM-3WAY mode
+int sv_sgbm_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, int H, int W, int pitch, int min_disp,
+                int num_disp, int block_size, int P1, int P2, int disp12_max_diff, int pre_filter_cap,
+                int uniqueness_ratio, int speckle_window_size, int speckle_range, int16_t* d_disp16, int out_pitch,
+                void* stream) {
+    SV_ENTER(c);
+    sv::MatchPlan plan;
+    int rc = check_match(H, W, min_disp, num_disp, block_size, SV_COST_SGBM, &plan);
+    if (rc) return rc;
+    if (check_image(d_left, H, W) || check_image(d_right, H, W) || !d_disp16 || pitch < W || out_pitch < W)
+        return fail(SV_EINVAL, "bad SGBM arguments");
+    SgbmParams p{P1, P2, disp12_max_diff, pre_filter_cap, uniqueness_ratio, speckle_window_size, speckle_range};
+    return enqueue_sgbm(c, d_left, d_right, H, W, pitch, min_disp, num_disp, block_size, p, d_disp16, out_pitch,
+                        pick(c, stream));
+}
+
+int sv_sgbm(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels, int stride,
+            int min_disp, int num_disp, int block_size, int P1, int P2, int disp12_max_diff, int pre_filter_cap,
+            int uniqueness_ratio, int speckle_window_size, int speckle_range, int16_t* disp16) {
+    SV_ENTER(c);
+    if (!disp16) return fail(SV_EINVAL, "null disparity output");
+    sv::MatchPlan plan;
+    int rc = check_match(H, W, min_disp, num_disp, block_size, SV_COST_SGBM, &plan);
+    if (rc) return rc;
+    rc = stage_pair(c, left, right, H, W, channels, stride);
+    if (rc) return rc;
+    SV_HIP(c->d16.ensure((size_t)H * W * sizeof(int16_t)));
+    SgbmParams p{P1, P2, disp12_max_diff, pre_filter_cap, uniqueness_ratio, speckle_window_size, speckle_range};
+    rc = enqueue_sgbm(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
+                      block_size, p, c->d16.as<int16_t>(), W, c->stream);
+    if (rc) return rc;
+    Out o[] = {{disp16, c->d16.p, (size_t)H * W * sizeof(int16_t)}};
+    return collect(c, o, 1);
 }
 
 // ---------------------------------------------------------------- profiling

@@ -6,7 +6,7 @@
 
 namespace sv {
 
-enum Cost { COST_SAD = 0, COST_SSD = 1, COST_HOG = 2 };
+enum Cost { COST_SAD = 0, COST_SSD = 1, COST_HOG = 2, COST_SGBM = 3 };
 
 // Disparity lanes: each wave is split into groups of LPG lanes (16/32/64); every lane of a
 // group owns DPL consecutive disparities of the same output pixel, so one group covers
@@ -107,6 +107,31 @@ struct AffineArgs {
     double ds, doff;          // AFF_F64: float(double(x) * ds + doff)
 };
 int launch_affine_f32(const AffineArgs& a, hipStream_t s);
+
+// SGBM-3WAY mode (sv_sgbm.hip).
+struct SgbmArgs {
+    const uint8_t* L;
+    const uint8_t* R;
+    int H, W, pitch;
+    int minD, D, r;            // r = blockSize / 2
+    int Dp;                    // per-pixel stride of the volumes: D rounded up to sgbm_dpl(D)
+    int X0, Wb;                // band [X0, X0 + Wb)
+    int cap, P1, P2, uniq, disp12;
+    uint16_t* hsum;            // [H][Wb][D] window-column sums of the pixel cost
+    uint16_t* C;               // [H][Wb][D] window sums
+    void* Llr;                 // [H][Wb][D] path costs, int16 (l32 = 0) or int32
+    void* Lrl;
+    int l32;
+    void* band;                // [H][Wb] {int16 x16 disparity after uniqueness + sub-pixel,
+                               //  int16 argmin index, int32 min cost (INT_MAX: not unique)}
+    int16_t* out;              // [H][opitch] final int16 x16 map
+    int opitch;
+};
+int sgbm_dpl(int D);                 // disparities per lane of the path kernels, -1 if D > 512
+size_t sgbm_hsum_lds(int W);
+int launch_sgbm(const SgbmArgs& a, hipStream_t s);
+int launch_speckles(int16_t* img, int H, int W, int pitch, int newv, int maxsize, int maxdiff, int* parent,
+                    int* size, hipStream_t s);
 
 // Post-processing modes for the median kernel.
 enum PostMode { POST_NONE = 0, POST_DEPTH = 1, POST_SCALED = 2 };

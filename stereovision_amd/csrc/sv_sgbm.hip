@@ -1,0 +1,546 @@
+// sv_sgbm.hip — SGBM-3WAY disparity mode on gfx950.
+//
+// The reference's disparity call is cv2.StereoSGBM(..., MODE_SGBM_3WAY).compute
+// (depth_map.py:894-909, fused_depth_map.py:988-1004).  Semantics: oracle/sv_sgbm_oracle.py
+// (OpenCV's published algorithm, one stripe, int32 aggregated costs; parity with OpenCV
+// itself unpinned).  Pipeline, one frame:
+//
+//  k_sgbm_hsum    per row: x-Sobel prefilter (clip to +-cap) + raw channel staged in LDS with
+//                 their Birchfield-Tomasi half-pixel intervals; pixel cost
+//                 BT(sobel) + BT(raw) >> 2 for every (x, d) of the band, summed over the
+//                 window columns (running sum, band-clamped) -> hsum u16 [H][Wb][D]
+//  k_sgbm_vsum    window rows (running sum down the column, row-clamped) -> C u16 [H][Wb][D]
+//  k_sgbm_hpath   left->right and right->left paths: one wave per (row, direction), lane l
+//                 owns DPL consecutive disparities; per step d+-1 come from wave_shr/shl DPP
+//                 and the path minimum from a row_ror butterfly + 4 readlanes; the next PF
+//                 steps' costs are in flight in a register ring -> L_lr, L_rl (int16 when
+//                 every value fits, else int32)
+//  k_sgbm_vpath   top->bottom path, one wave per band column walking down the rows with the
+//                 same prefetch ring, S = L_lr + L_rl + L_tb, argmin as a min over
+//                 ((S + 2^20) << 9 | d) keys, the uniqueness test as an OR reduction,
+//                 sub-pixel parabola by the owner lane, one 8-byte store per pixel
+//  k_sgbm_lrcheck per row: the right-view disparity by 64-bit LDS atomicMin over
+//                 (minS, rightmost x) keys, the +-disp12MaxDiff consistency test, band
+//                 borders -> int16 x16 output
+//  k_cc_*         filterSpeckles as GPU union-find over 4-connected |d1 - d2| <= maxDiff
+//                 edges (atomicMin linking), component sizes by atomics
+//
+// The DP kernels are latency-bound chains (W or H dependent steps); the sums are HBM-bound.
+#include "sv_internal.h"
+
+namespace sv {
+namespace {
+
+constexpr int kInf = 0x3FFFFFFF;
+
+__device__ __forceinline__ int dpp_shr1(int v, int old) {   // lane j <- lane j-1 (row of 16)
+    return __builtin_amdgcn_update_dpp(old, v, 0x111, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int dpp_shl1(int v, int old) {   // lane j <- lane j+1
+    return __builtin_amdgcn_update_dpp(old, v, 0x101, 0xF, 0xF, false);
+}
+template <int ROR>
+__device__ __forceinline__ int dpp_ror(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, 0x120 + ROR, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int row_min(int v) {             // min over the 16-lane row, all lanes
+    v = min(v, dpp_ror<8>(v));
+    v = min(v, dpp_ror<4>(v));
+    v = min(v, dpp_ror<2>(v));
+    v = min(v, dpp_ror<1>(v));
+    return v;
+}
+__device__ __forceinline__ uint32_t row_min_u(uint32_t v) {
+    v = min(v, (uint32_t)dpp_ror<8>((int)v));
+    v = min(v, (uint32_t)dpp_ror<4>((int)v));
+    v = min(v, (uint32_t)dpp_ror<2>((int)v));
+    v = min(v, (uint32_t)dpp_ror<1>((int)v));
+    return v;
+}
+__device__ __forceinline__ int row_max(int v) {
+    v = max(v, dpp_ror<8>(v));
+    v = max(v, dpp_ror<4>(v));
+    v = max(v, dpp_ror<2>(v));
+    v = max(v, dpp_ror<1>(v));
+    return v;
+}
+
+// -------------------------------------------------------------------------------------
+// pixel cost + horizontal window sums
+// -------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_sgbm_hsum(SgbmArgs a) {
+    extern __shared__ uint8_t lds[];
+    const int W = a.W, y = blockIdx.x, t = threadIdx.x;
+    // [image 0/1][channel 0 sobel / 1 raw][value, lo, hi][W]
+    uint8_t* buf = lds;
+    auto at = [&](int im, int ch, int f) { return buf + ((im * 2 + ch) * 3 + f) * W; };
+    const int ym = y > 0 ? y - 1 : y, yp = y < a.H - 1 ? y + 1 : y;
+    for (int im = 0; im < 2; ++im) {
+        const uint8_t* img = im == 0 ? a.L : a.R;
+        const uint8_t* r0 = img + (size_t)y * a.pitch;
+        const uint8_t* rm = img + (size_t)ym * a.pitch;
+        const uint8_t* rp = img + (size_t)yp * a.pitch;
+        for (int x = t; x < W; x += 256) {
+            int pf = a.cap, raw = a.cap;   // columns 0 and W-1: tab[0] in both channels
+            if (x > 0 && x < W - 1) {
+                const int s = (r0[x + 1] - r0[x - 1]) * 2 + rm[x + 1] - rm[x - 1] + rp[x + 1] - rp[x - 1];
+                pf = min(max(s, -a.cap), a.cap) + a.cap;
+                raw = r0[x];
+            }
+            at(im, 0, 0)[x] = (uint8_t)pf;
+            at(im, 1, 0)[x] = (uint8_t)raw;
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < 4 * W; i += 256) {
+        const int im = i / (2 * W), ch = (i / W) & 1, x = i % W;
+        const uint8_t* v = at(im, ch, 0);
+        const int c = v[x];
+        const int l = x > 0 ? (c + v[x - 1]) >> 1 : c;
+        const int r = x < W - 1 ? (c + v[x + 1]) >> 1 : c;
+        at(im, ch, 1)[x] = (uint8_t)min(min(l, r), c);
+        at(im, ch, 2)[x] = (uint8_t)max(max(l, r), c);
+    }
+    __syncthreads();
+    const int D = a.D, Wb = a.Wb, r = a.r;
+    const int nc = max(1, 256 / D);                  // column chunks per disparity
+    const int clen = (Wb + nc - 1) / nc;
+    const int Dp = a.Dp;
+    uint16_t* out = a.hsum + (size_t)y * Wb * Dp;
+    auto pix = [&](int xb, int d) -> int {
+        xb = min(max(xb, 0), Wb - 1);
+        const int x = a.X0 + xb, xr = x - a.minD - d;
+        int cost = 0;
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch) {
+            const int u = at(0, ch, 0)[x], u0 = at(0, ch, 1)[x], u1 = at(0, ch, 2)[x];
+            const int v = at(1, ch, 0)[xr], v0 = at(1, ch, 1)[xr], v1 = at(1, ch, 2)[xr];
+            const int c0 = max(max(0, u - v1), v0 - u);
+            const int c1 = max(max(0, v - u1), u0 - v);
+            cost += min(c0, c1) >> (ch * 2);
+        }
+        return cost;
+    };
+    for (int item = t; item < D * nc; item += 256) {
+        const int d = item % D, c = item / D;
+        const int xs = c * clen, xe = min(Wb, xs + clen);
+        if (xs >= xe) continue;
+        int hs = 0;
+        for (int i = -r; i <= r; ++i) hs += pix(xs + i, d);
+        out[(size_t)xs * Dp + d] = (uint16_t)hs;
+        for (int x = xs + 1; x < xe; ++x) {
+            hs += pix(x + r, d) - pix(x - r - 1, d);
+            out[(size_t)x * Dp + d] = (uint16_t)hs;
+        }
+    }
+}
+
+// window rows: C(y) = sum_{j=-r..r} hsum(clamp(y + j))
+__global__ __launch_bounds__(256) void k_sgbm_vsum(SgbmArgs a) {
+    const size_t plane = (size_t)a.Wb * a.Dp;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= plane) return;
+    const uint16_t* h = a.hsum + i;
+    uint16_t* c = a.C + i;
+    const int H = a.H, r = a.r;
+    int s = 0;
+    for (int j = -r; j <= r; ++j) s += h[(size_t)min(max(j, 0), H - 1) * plane];
+    c[0] = (uint16_t)s;
+    for (int y0 = 1; y0 < H; y0 += 8) {   // 16 independent loads in flight per step of 8 rows
+        int ad[8], sb[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int y = min(y0 + u, H - 1);
+            ad[u] = h[(size_t)min(y + r, H - 1) * plane];
+            sb[u] = h[(size_t)max(y - r - 1, 0) * plane];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (y0 + u >= H) break;
+            s += ad[u] - sb[u];
+            c[(size_t)(y0 + u) * plane] = (uint16_t)s;
+        }
+    }
+}
+
+// The path kernels give one wave the D disparities of one row (horizontal) or one column
+// (vertical): lane l owns d = l*DPL .. l*DPL+DPL-1.  A step is a dependent chain (the path
+// minimum of step s feeds step s+1), so the C / L inputs of the next PF steps are loaded
+// ahead into a register ring: the HBM latency of a load is covered by PF steps of compute.
+__device__ __forceinline__ int wave_shr1(int v, int old) {   // lane l <- lane l-1 (whole wave)
+    return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int wave_shl1(int v, int old) {   // lane l <- lane l+1
+    return __builtin_amdgcn_update_dpp(old, v, 0x130, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int wave_min(int v) {             // uniform (SGPR) result
+    v = row_min(v);
+    return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ uint32_t wave_min_u(uint32_t v) {
+    v = row_min_u(v);
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    return min(min(a, b), min(c, d));
+}
+__device__ __forceinline__ int wave_max(int v) {
+    v = row_max(v);
+    return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
+// DPL contiguous elements of type T as one vector load/store (DPL in {1, 2, 4, 8}).
+template <typename T, int DPL>
+struct alignas(sizeof(T) * DPL) Pack {
+    T v[DPL];
+};
+
+// One SGBM step for the DPL disparities of a lane: OpenCV's
+// L = C + min(prev[d], prev[d-1] + P1, prev[d+1] + P1, minprev + P2) - (minprev + P2).
+template <int DPL>
+__device__ __forceinline__ void path_step(int (&prev)[DPL], const int (&c)[DPL], int mn, int P1, int P2,
+                                          int dbase, int D) {
+    const int lo_in = wave_shr1(prev[DPL - 1], kInf);
+    const int hi_in = wave_shl1(prev[0], kInf);
+    int nxt[DPL];
+    const int mp = mn + P2;
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) {
+        const int lo = k > 0 ? prev[k - 1] : lo_in;
+        const int hi = k < DPL - 1 ? prev[k + 1] : hi_in;
+        const int m = min(min(prev[k], min(lo, hi) + P1), mp);
+        nxt[k] = dbase + k < D ? c[k] + m - mp : kInf;
+    }
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) prev[k] = nxt[k];
+}
+
+template <int DPL>
+__device__ __forceinline__ int lane_min(const int (&v)[DPL]) {
+    int m = v[0];
+#pragma unroll
+    for (int k = 1; k < DPL; ++k) m = min(m, v[k]);
+    return m;
+}
+
+// Horizontal paths: one wave per (row, direction); blockIdx.y = 0: left->right into Llr,
+// 1: right->left into Lrl.
+template <int DPL, typename LT, int PF>
+__global__ __launch_bounds__(64) void k_sgbm_hpath(SgbmArgs a) {
+    const int lane = threadIdx.x, y = blockIdx.x, dir = blockIdx.y;
+    const int D = a.D, Wb = a.Wb, dbase = lane * DPL;
+    const bool live = dbase < D;                      // lanes past D only pad
+    const int Dp = a.Dp;                             // row stride: D rounded up to DPL
+    LT* Lrow = static_cast<LT*>(dir == 0 ? a.Llr : a.Lrl) + (size_t)y * Wb * Dp + dbase;
+    const uint16_t* Crow = a.C + (size_t)y * Wb * Dp + dbase;
+    using CP = Pack<uint16_t, DPL>;
+    using LP = Pack<LT, DPL>;
+    auto xof = [&](int s) { return dir == 0 ? s : Wb - 1 - s; };
+    CP ring[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+        if (p < Wb && live) ring[p] = *reinterpret_cast<const CP*>(Crow + (size_t)xof(p) * Dp);
+    int prev[DPL];
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) prev[k] = dbase + k < D ? 0 : kInf;
+    int mn = 0;
+    for (int s0 = 0; s0 < Wb; s0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int s = s0 + u;
+            if (s < Wb) {
+            int c[DPL];
+#pragma unroll
+            for (int k = 0; k < DPL; ++k) c[k] = live ? (int)ring[u].v[k] : 0;
+            if (s + PF < Wb && live) ring[u] = *reinterpret_cast<const CP*>(Crow + (size_t)xof(s + PF) * Dp);
+            path_step<DPL>(prev, c, mn, a.P1, a.P2, dbase, D);
+            mn = wave_min(lane_min<DPL>(prev));
+            if (live) {
+                LP o;
+#pragma unroll
+                for (int k = 0; k < DPL; ++k) o.v[k] = (LT)prev[k];
+                *reinterpret_cast<LP*>(Lrow + (size_t)xof(s) * Dp) = o;
+            }
+            }
+        }
+    }
+}
+
+struct BandOut {      // one 8-byte store per band pixel
+    int16_t disp, best;
+    int32_t minS;
+};
+
+// Top->bottom path + winner-take-all: one wave per band column, walking down the rows.
+template <int DPL, typename LT, int PF>
+__global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
+    const int lane = threadIdx.x, xb = blockIdx.x;
+    const int D = a.D, Wb = a.Wb, dbase = lane * DPL;
+    const bool live = dbase < D;
+    const size_t plane = (size_t)Wb * a.Dp;
+    const size_t col = (size_t)xb * a.Dp + dbase;
+    const LT* Llr = static_cast<const LT*>(a.Llr) + col;
+    const LT* Lrl = static_cast<const LT*>(a.Lrl) + col;
+    const uint16_t* Cc = a.C + col;
+    using CP = Pack<uint16_t, DPL>;
+    using LP = Pack<LT, DPL>;
+    CP rc[PF];
+    LP rl[PF], rr[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+        if (p < a.H && live) {
+            rc[p] = *reinterpret_cast<const CP*>(Cc + (size_t)p * plane);
+            rl[p] = *reinterpret_cast<const LP*>(Llr + (size_t)p * plane);
+            rr[p] = *reinterpret_cast<const LP*>(Lrl + (size_t)p * plane);
+        }
+    int prev[DPL];
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) prev[k] = dbase + k < D ? 0 : kInf;
+    int mn = 0;
+    const int u100 = 100 - a.uniq;
+    BandOut* bo = reinterpret_cast<BandOut*>(a.band) + xb;
+    for (int y0 = 0; y0 < a.H; y0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int y = y0 + u;
+            if (y < a.H) {
+            int c[DPL], s[DPL];
+#pragma unroll
+            for (int k = 0; k < DPL; ++k) {
+                c[k] = live ? (int)rc[u].v[k] : 0;
+                s[k] = live ? (int)rl[u].v[k] + (int)rr[u].v[k] : 0;
+            }
+            if (y + PF < a.H && live) {
+                const size_t o = (size_t)(y + PF) * plane;
+                rc[u] = *reinterpret_cast<const CP*>(Cc + o);
+                rl[u] = *reinterpret_cast<const LP*>(Llr + o);
+                rr[u] = *reinterpret_cast<const LP*>(Lrl + o);
+            }
+            path_step<DPL>(prev, c, mn, a.P1, a.P2, dbase, D);
+            mn = wave_min(lane_min<DPL>(prev));
+            uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = 0; k < DPL; ++k) {
+                if (dbase + k < D) {
+                    s[k] += prev[k];
+                    key = min(key, ((uint32_t)(s[k] + (1 << 20)) << 9) | (uint32_t)(dbase + k));
+                }
+            }
+            key = wave_min_u(key);
+            const int b = (int)(key & 511u);
+            const int minS = (int)(key >> 9) - (1 << 20);
+            int viol = 0;
+#pragma unroll
+            for (int k = 0; k < DPL; ++k) {
+                const int d = dbase + k;
+                viol |= (d < D) && (s[k] * u100 < minS * 100) && (abs(d - b) > 1);
+            }
+            viol = wave_max(viol);
+            const int sl = wave_shr1(s[DPL - 1], 0), sr = wave_shl1(s[0], 0);
+            if (b >= dbase && b < dbase + DPL) {       // the lane that owns b writes
+                const int kb = b - dbase;
+                int sm = sl, sp = sr;
+#pragma unroll
+                for (int k = 0; k < DPL; ++k) {
+                    if (k == kb - 1) sm = s[k];
+                    if (k == kb + 1) sp = s[k];
+                }
+                int d16 = b * 16;
+                if (b > 0 && b < D - 1) {
+                    const int denom2 = max(sm + sp - 2 * minS, 1);
+                    d16 += ((sm - sp) * 16 + denom2) / (denom2 * 2);
+                }
+                BandOut o;
+                o.disp = (int16_t)(viol ? (a.minD - 1) * 16 : d16 + a.minD * 16);
+                o.best = (int16_t)b;
+                o.minS = viol ? 0x7FFFFFFF : minS;
+                bo[(size_t)y * Wb] = o;
+            }
+            }
+        }
+    }
+}
+
+// Left-right consistency (disp12MaxDiff) and band borders: one workgroup per row.
+__global__ __launch_bounds__(256) void k_sgbm_lrcheck(SgbmArgs a) {
+    extern __shared__ unsigned long long keys[];
+    const int y = blockIdx.x, t = threadIdx.x, W = a.W, Wb = a.Wb;
+    for (int x = t; x < W; x += 256) keys[x] = ~0ull;
+    __syncthreads();
+    const BandOut* band = reinterpret_cast<const BandOut*>(a.band) + (size_t)y * Wb;
+    for (int xb = t; xb < Wb; xb += 256) {
+        const int ms = band[xb].minS;
+        if (ms < 32767) {                                   // disp2cost starts at SHRT_MAX
+            const int x = a.X0 + xb;
+            const int x2 = x - (band[xb].best + a.minD);
+            const unsigned long long k = ((unsigned long long)(uint32_t)(ms + 0x40000000) << 32) |
+                                         (uint32_t)(0xFFFFFFFFu - (uint32_t)x);
+            atomicMin(&keys[x2], k);
+        }
+    }
+    __syncthreads();
+    const int inv = (a.minD - 1) * 16;
+    int16_t* orow = a.out + (size_t)y * a.opitch;
+    for (int x = t; x < W; x += 256) {
+        int v = inv;
+        const int xb = x - a.X0;
+        if (xb >= 0 && xb < Wb) {
+            v = band[xb].disp;
+            if (v != inv && a.disp12 >= 0) {
+                const int dd = (v >> 4), du = (v + 15) >> 4;
+                const int x1 = x - dd, x2 = x - du;
+                auto d2 = [&](int xx) -> int {
+                    const unsigned long long k = keys[xx];
+                    if (k == ~0ull) return a.minD - 1;
+                    const int xs = (int)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull));
+                    return xs - xx;
+                };
+                if (x1 >= 0 && x1 < W && x2 >= 0 && x2 < W) {
+                    const int a1 = d2(x1), a2 = d2(x2);
+                    if (a1 >= a.minD && abs(a1 - dd) > a.disp12 && a2 >= a.minD && abs(a2 - du) > a.disp12)
+                        v = inv;
+                }
+            }
+        }
+        orow[x] = (int16_t)v;
+    }
+}
+
+// ---- filterSpeckles: union-find connected components -----------------------------------
+// Find with path halving: a non-root's parent is only ever replaced by one of its
+// ancestors (roots are the only entries unite() hooks), so the plain stores keep every
+// node inside its tree while shortening the chains.
+__device__ __forceinline__ int uf_find(int* p, int x) {
+    int q = __atomic_load_n(&p[x], __ATOMIC_RELAXED);
+    while (q != x) {
+        const int r = __atomic_load_n(&p[q], __ATOMIC_RELAXED);
+        if (r != q) __atomic_store_n(&p[x], r, __ATOMIC_RELAXED);
+        x = q;
+        q = r;
+    }
+    return x;
+}
+
+__device__ __forceinline__ void uf_unite(int* p, int a, int b) {
+    while (true) {
+        a = uf_find(p, a);
+        b = uf_find(p, b);
+        if (a == b) return;
+        if (a < b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        const int old = atomicMin(&p[a], b);
+        if (old == a) return;
+        a = old;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_cc_init(const int16_t* img, int H, int W, int pitch, int newv, int* parent,
+                                                 int* size) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= H * W) return;
+    const int y = i / W, x = i % W;
+    parent[i] = img[(size_t)y * pitch + x] != newv ? i : -1;
+    size[i] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_cc_union(const int16_t* img, int H, int W, int pitch, int newv, int maxdiff,
+                                                  int* parent) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= H * W) return;
+    const int y = i / W, x = i % W;
+    const int v = img[(size_t)y * pitch + x];
+    if (v == newv) return;
+    if (x + 1 < W) {
+        const int w = img[(size_t)y * pitch + x + 1];
+        if (w != newv && abs(w - v) <= maxdiff) uf_unite(parent, i, i + 1);
+    }
+    if (y + 1 < H) {
+        const int w = img[(size_t)(y + 1) * pitch + x];
+        if (w != newv && abs(w - v) <= maxdiff) uf_unite(parent, i, i + W);
+    }
+}
+
+// Component sizes, counted only as far as the filter needs: a pixel skips its increment
+// once its root's count already exceeds maxsize, so the decision size <= maxsize stays
+// exact while a large component stops hammering one counter after maxsize+1 atomics.
+// Lanes of a wave that share a root add their population in one atomic.
+__global__ __launch_bounds__(256) void k_cc_count(int H, int W, int maxsize, int* parent, int* size) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const bool on = i < H * W && parent[i] >= 0;
+    const int root = on ? uf_find(parent, i) : -1;
+    const int r0 = __builtin_amdgcn_readfirstlane(root);
+    const unsigned long long same = __ballot(on && root == r0);
+    const unsigned long long act = __ballot(on);
+    if (same == act) {                                   // the whole wave shares one root
+        if ((threadIdx.x & 63) == (unsigned)__builtin_ctzll(act) &&
+            __atomic_load_n(&size[r0], __ATOMIC_RELAXED) <= maxsize)
+            atomicAdd(&size[r0], (int)__builtin_popcountll(act));
+        return;
+    }
+    if (on && __atomic_load_n(&size[root], __ATOMIC_RELAXED) <= maxsize) atomicAdd(&size[root], 1);
+}
+
+__global__ __launch_bounds__(256) void k_cc_apply(int16_t* img, int H, int W, int pitch, int newv, int maxsize,
+                                                  int* parent, const int* size) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= H * W || parent[i] < 0) return;
+    if (size[uf_find(parent, i)] <= maxsize) img[(size_t)(i / W) * pitch + i % W] = (int16_t)newv;
+}
+
+template <typename LT>
+int launch_paths_t(const SgbmArgs& a, int dpl, hipStream_t s) {
+    dim3 gh(a.H, 2), gv(a.Wb);
+#define SV_SGBM_DPL(N, PFH, PFV)                                                  \
+    case N:                                                                       \
+        hipLaunchKernelGGL((k_sgbm_hpath<N, LT, PFH>), gh, dim3(64), 0, s, a);   \
+        hipLaunchKernelGGL((k_sgbm_vpath<N, LT, PFV>), gv, dim3(64), 0, s, a);   \
+        break;
+    switch (dpl) {
+        SV_SGBM_DPL(1, 24, 12) SV_SGBM_DPL(2, 24, 12) SV_SGBM_DPL(4, 16, 8) SV_SGBM_DPL(8, 8, 4)
+        default: return (int)hipErrorInvalidValue;
+    }
+#undef SV_SGBM_DPL
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
+int sgbm_dpl(int D) {
+    const int need = (D + 63) / 64;
+    for (int o = 1; o <= 8; o *= 2)
+        if (o >= need) return o;
+    return -1;
+}
+
+size_t sgbm_hsum_lds(int W) { return (size_t)12 * W; }
+
+int launch_sgbm(const SgbmArgs& a, hipStream_t s) {
+    if (a.H <= 0 || a.W <= 0) return 0;
+    if (a.Wb > 0) {
+        hipLaunchKernelGGL(k_sgbm_hsum, dim3(a.H), dim3(256), sgbm_hsum_lds(a.W), s, a);
+        const size_t plane = (size_t)a.Wb * a.Dp;
+        hipLaunchKernelGGL(k_sgbm_vsum, dim3((unsigned)((plane + 255) / 256)), dim3(256), 0, s, a);
+        const int dpl = sgbm_dpl(a.D);
+        const int e = a.l32 ? launch_paths_t<int32_t>(a, dpl, s) : launch_paths_t<int16_t>(a, dpl, s);
+        if (e) return e;
+    }
+    hipLaunchKernelGGL(k_sgbm_lrcheck, dim3(a.H), dim3(256), (size_t)a.W * 8, s, a);
+    return (int)hipGetLastError();
+}
+
+int launch_speckles(int16_t* img, int H, int W, int pitch, int newv, int maxsize, int maxdiff, int* parent,
+                    int* size, hipStream_t s) {
+    if (H <= 0 || W <= 0 || maxsize <= 0) return 0;
+    const unsigned n = (unsigned)(((size_t)H * W + 255) / 256);
+    hipLaunchKernelGGL(k_cc_init, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, parent, size);
+    hipLaunchKernelGGL(k_cc_union, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, maxdiff, parent);
+    hipLaunchKernelGGL(k_cc_count, dim3(n), dim3(256), 0, s, H, W, maxsize, parent, size);
+    hipLaunchKernelGGL(k_cc_apply, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, maxsize, parent, size);
+    return (int)hipGetLastError();
+}
+
+}  // namespace sv

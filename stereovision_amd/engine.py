@@ -19,10 +19,11 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SV_LIB_PATH", os.path.join(_HERE, "lib", "libsvhip.so"))
 
-COSTS = {"sad": 0, "ssd": 1, "hog": 2}
+COSTS = {"sad": 0, "ssd": 1, "hog": 2, "sgbm": 3}
 POST_NONE, POST_DEPTH, POST_SCALED = 0, 1, 2
 KERNELS = {"gray": 0, "harris": 1, "hog": 2, "match": 3, "median": 4, "post": 5, "remap": 6,
-           "undistort": 7, "resize": 8, "stats": 9, "select": 10, "affine": 11}
+           "undistort": 7, "resize": 8, "stats": 9, "select": 10, "affine": 11, "sgbm": 12,
+           "speckle": 13}
 
 # Every symbol include/stereovision_amd.h declares (checked by tests/test_capi.py).
 EXPORTED = [
@@ -36,7 +37,7 @@ EXPORTED = [
     "sv_depth_map_batch_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
     "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
     "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
-    "sv_select_ranks", "sv_affine_f32_dev",
+    "sv_select_ranks", "sv_affine_f32_dev", "sv_sgbm", "sv_sgbm_dev",
 ]
 
 
@@ -180,6 +181,8 @@ def _declare(lib):
                             _c_int),
         "sv_affine_f32_dev": ([_vp, _vp, ctypes.c_int64, _c_int, _c_float, _c_float, _c_float, _c_float,
                                ctypes.c_double, ctypes.c_double, _vp, _vp], _c_int),
+        "sv_sgbm": ([_vp, _u8p, _u8p] + [_c_int] * 14 + [_i16p], _c_int),
+        "sv_sgbm_dev": ([_vp, _vp, _vp] + [_c_int] * 13 + [_vp, _c_int, _vp], _c_int),
         "sv_profile_enable": ([_vp, _c_int], _c_int),
         "sv_profile_read": ([_vp, _c_int, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_longlong)], _c_int),
@@ -333,6 +336,38 @@ class Engine:
                                                      int(min_disp), int(num_disp), int(win),
                                                      _cost(cost), d16, hr))
         return (d16, hr) if harris else d16
+
+    def sgbm(self, left, right, min_disp: int, num_disp: int, block_size: int, P1: int = None,
+             P2: int = None, disp12_max_diff: int = 1, pre_filter_cap: int = 63,
+             uniqueness_ratio: int = 10, speckle_window_size: int = 100,
+             speckle_range: int = 32) -> np.ndarray:
+        """cv2.StereoSGBM_create(..., mode=MODE_SGBM_3WAY).compute(left, right) -> int16 x16
+        (defaults: the reference's parameters, depth_map.py:894-906)."""
+        left, H, W, C = _image(left)
+        right, H2, W2, C2 = _image(right)
+        if (H, W, C) != (H2, W2, C2):
+            raise ValueError("left/right shapes differ")
+        P1 = 8 * 3 * block_size * block_size if P1 is None else P1
+        P2 = 32 * 3 * block_size * block_size if P2 is None else P2
+        d16 = np.empty((H, W), np.int16)
+        _check("sv_sgbm", self.lib.sv_sgbm(self._h, left, right, H, W, C, W * C, int(min_disp),
+                                           int(num_disp), int(block_size), int(P1), int(P2),
+                                           int(disp12_max_diff), int(pre_filter_cap),
+                                           int(uniqueness_ratio), int(speckle_window_size),
+                                           int(speckle_range), d16))
+        return d16
+
+    def sgbm_dev(self, d_left: int, d_right: int, H: int, W: int, pitch: int, min_disp: int,
+                 num_disp: int, block_size: int, d_out16: int, out_pitch: int, P1: int = None,
+                 P2: int = None, disp12_max_diff: int = 1, pre_filter_cap: int = 63,
+                 uniqueness_ratio: int = 10, speckle_window_size: int = 100,
+                 speckle_range: int = 32, stream: int = 0):
+        P1 = 8 * 3 * block_size * block_size if P1 is None else P1
+        P2 = 32 * 3 * block_size * block_size if P2 is None else P2
+        _check("sv_sgbm_dev", self.lib.sv_sgbm_dev(
+            self._h, d_left, d_right, H, W, pitch, int(min_disp), int(num_disp), int(block_size),
+            int(P1), int(P2), int(disp12_max_diff), int(pre_filter_cap), int(uniqueness_ratio),
+            int(speckle_window_size), int(speckle_range), d_out16, out_pitch, stream or None))
 
     def disparity_rows(self, left, right, min_disp: int, num_disp: int, win: int, row0: int,
                        row1: int, cost="sad", out: np.ndarray | None = None) -> np.ndarray:

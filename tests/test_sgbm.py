@@ -1,0 +1,123 @@
+"""SGBM-3WAY mode: the reference's own matcher
+(cv2.StereoSGBM, MODE_SGBM_3WAY, depth_map.py:894-909) restated.
+
+Oracle: oracle/sv_sgbm_oracle.py (OpenCV's published algorithm, one stripe; parity with
+OpenCV itself unpinned — cv2 is absent).  GPU bar: the int16 x16 map bit-exact against
+the oracle for every parameter path (int16/int32 path storage, uniqueness, sub-pixel,
+left-right check, speckle filter, band borders, negative/positive min_disp).
+"""
+import numpy as np
+import pytest
+
+import sv_sgbm_oracle as SG
+from stereovision_amd.synthetic import stereo_pair
+
+
+# ---------------------------------------------------------------------------- CPU: oracle
+def test_oracle_recovers_integer_shift():
+    rng = np.random.default_rng(0)
+    base = rng.integers(0, 256, (40, 200), dtype=np.uint8)
+    shift = 7
+    L = base[:, :150].copy()                             # L(x) = R(x - shift)
+    R = base[:, shift:shift + 150].copy()
+    d = SG.sgbm(L, R, 0, 32, 5)
+    inner = d[3:-3, 40:-3].astype(np.int32)
+    assert (np.abs(inner - shift * 16) <= 1).mean() > 0.99      # sub-pixel within 1/16
+    assert (inner == shift * 16).mean() > 0.9
+    assert (d[:, :32] == -16).all()                     # band [X0, X1) only
+
+
+def test_oracle_invalid_band_and_negative_min_disp():
+    L, R, _ = stereo_pair(24, 90, 16, seed=2)
+    d = SG.sgbm(L, R, -8, 16, 3)
+    X0, X1 = max(-8 + 16, 0), 90 - 8
+    assert (d[:, :X0] == -9 * 16).all() and (d[:, X1:] == -9 * 16).all()
+
+
+def test_filter_speckles_known_answer():
+    img = np.full((10, 12), 100, np.int16)
+    img[2:4, 2:4] = 900                                  # 4-pixel island, differs by 800
+    img[6:9, 5:11] = 80                                  # joins the background (|diff| 20)
+    out = SG.filter_speckles(img, -16, 5, 512)
+    assert (out[2:4, 2:4] == -16).all() and (out[6:9, 5:11] == 80).all() and out[0, 0] == 100
+    out = SG.filter_speckles(img, -16, 3, 512)
+    assert (out[2:4, 2:4] == 900).all()                  # 4 > maxSpeckleSize 3: kept
+
+
+def test_oracle_quality_on_synthetic_pair():
+    L, R, gt = stereo_pair(48, 200, 32, seed=3)
+    d = SG.sgbm(L, R, 0, 32, 5)
+    ok = d[:, 40:] >= 0
+    assert ok.mean() > 0.8
+
+
+# ---------------------------------------------------------------------------- GPU parity
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,win,min_disp", [(16, 3, 0), (32, 5, 0), (48, 7, 0), (64, 9, 0),
+                                            (96, 5, 0), (32, 11, -8), (16, 1, 5), (80, 7, 3)])
+def test_gpu_sgbm_matches_oracle(engine, D, win, min_disp):
+    L, R, _ = stereo_pair(53, 240, max(D, 16), seed=D + win, min_disp=max(0, min_disp))
+    got = engine.sgbm(L, R, min_disp, D, win)
+    exp = SG.sgbm(L, R, min_disp, D, win)
+    np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(disp12_max_diff=-1), dict(uniqueness_ratio=0),
+                                dict(speckle_window_size=0), dict(P2=40000),
+                                dict(P1=50, P2=10), dict(pre_filter_cap=31, speckle_range=2)])
+def test_gpu_sgbm_parameter_paths(engine, kw):
+    L, R, _ = stereo_pair(37, 200, 32, seed=11)
+    got = engine.sgbm(L, R, 0, 32, 5, **kw)
+    okw = {"disp12_max_diff": "disp12MaxDiff", "uniqueness_ratio": "uniquenessRatio",
+           "speckle_window_size": "speckleWindowSize", "pre_filter_cap": "preFilterCap",
+           "speckle_range": "speckleRange"}
+    exp = SG.sgbm(L, R, 0, 32, 5, **{okw.get(k, k): v for k, v in kw.items()})
+    np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.gpu
+def test_gpu_sgbm_int32_paths_window15(engine):
+    L, R, _ = stereo_pair(40, 180, 32, seed=5)
+    np.testing.assert_array_equal(engine.sgbm(L, R, 0, 32, 15), SG.sgbm(L, R, 0, 32, 15))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W", [(1, 40), (2, 33), (5, 17), (30, 20)])
+def test_gpu_sgbm_ragged(engine, H, W):
+    rng = np.random.default_rng(H * W)
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    np.testing.assert_array_equal(engine.sgbm(L, R, 0, 16, 3), SG.sgbm(L, R, 0, 16, 3))
+
+
+@pytest.mark.gpu
+def test_gpu_sgbm_through_generic_entry_points(engine):
+    """cost='sgbm' through sv_disparity / sv_depth_map: the reference's parameters."""
+    import sv_oracle as O
+    from stereovision_amd.synthetic import to_bgr
+    L, R, _ = stereo_pair(45, 210, 48, seed=8)
+    exp = SG.sgbm(L, R, 0, 48, 7)
+    np.testing.assert_array_equal(engine.disparity(L, R, 0, 48, 7, "sgbm"), exp)
+    depth, disp, norm = engine.depth_map(to_bgr(L), to_bgr(R), 0, 48, 7, 0.3, 2.0, cost="sgbm")
+    e_disp = O.disparity_f32(exp)                        # /16 + medianBlur(5)
+    np.testing.assert_array_equal(disp, e_disp)
+    e_depth, e_norm = O.depth_post(e_disp, 0.3, 2.0, 0)
+    np.testing.assert_array_equal(depth, e_depth)
+    np.testing.assert_array_equal(norm, e_norm)
+    with pytest.raises(Exception):
+        engine.disparity_rows(L, R, 0, 48, 7, 5, 20, "sgbm")   # row bands: frames only
+
+
+@pytest.mark.gpu
+def test_gpu_sgbm_1080p_properties(engine):
+    """Benchmark size: integer-shift scene recovered; invalid band exact."""
+    rng = np.random.default_rng(1)
+    base = rng.integers(0, 256, (1080, 1920 + 32), dtype=np.uint8).astype(np.int32)
+    base = ((base + np.roll(base, 1, 1) + np.roll(base, 1, 0)) // 3).astype(np.uint8)
+    L = np.ascontiguousarray(base[:, :1920])            # L(x) = R(x - 20)
+    R = np.ascontiguousarray(base[:, 20:20 + 1920])
+    d = engine.sgbm(L, R, 0, 128, 7)
+    assert (d[:, :128] == -16).all()
+    inner = d[10:-10, 140:-10].astype(np.int32)
+    assert (np.abs(inner - 20 * 16) <= 1).mean() > 0.99

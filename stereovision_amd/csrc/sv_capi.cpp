@@ -221,13 +221,14 @@ int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, in
     SV_HIP(c->sg_hsum.ensure(vol * 2 + 256));
     SV_HIP(c->sg_c.ensure(vol * 2 + 256));
     SV_HIP(c->sg_l.ensure(vol * (a.l32 ? 8 : 2) + 256));
-    SV_HIP(c->sg_band.ensure((size_t)H * a.Wb * 8 + 256));
+    SV_HIP(c->sg_band.ensure((size_t)H * a.Wb * 8 + 256 + 64 * 128));
     a.hsum = c->sg_hsum.as<uint16_t>();
     a.C = c->sg_c.as<uint16_t>();
     // int16 paths: L_lr reuses the hsum volume (dead after the window-row sums)
     a.Llr = a.l32 ? c->sg_l.p : c->sg_hsum.p;
     a.Lrl = a.l32 ? (void*)(c->sg_l.as<int32_t>() + vol) : c->sg_l.p;
     a.band = c->sg_band.p;
+    a.dummy = c->sg_band.as<uint8_t>() + ((size_t)H * a.Wb * 8 + 255) / 256 * 256;
     a.out = out;
     a.opitch = opitch;
     SV_LAUNCH(c, SV_K_SGBM, s, sv::launch_sgbm(a, s));

@@ -126,6 +126,7 @@ struct SgbmArgs {
                                //  int16 argmin index, int32 min cost (INT_MAX: not unique)}
     int16_t* out;              // [H][opitch] final int16 x16 map
     int opitch;
+    void* dummy;               // >= 64 x 128 bytes: store target of the padding lanes
 };
 int sgbm_dpl(int D);                 // disparities per lane of the path kernels, -1 if D > 512
 size_t sgbm_hsum_lds(int W);

@@ -22,8 +22,9 @@
 //  k_sgbm_lrcheck per row: the right-view disparity by 64-bit LDS atomicMin over
 //                 (minS, rightmost x) keys, the +-disp12MaxDiff consistency test, band
 //                 borders -> int16 x16 output
-//  k_cc_*         filterSpeckles as GPU union-find over 4-connected |d1 - d2| <= maxDiff
-//                 edges (atomicMin linking), component sizes by atomics
+//  k_cc_*         filterSpeckles as union-find over 4-connected |d1 - d2| <= maxDiff edges:
+//                 32x32 tiles in LDS first, then the tile-border edges in the global forest
+//                 (atomicMin linking); component sizes by wave-aggregated, capped atomics
 //
 // The DP kernels are latency-bound chains (W or H dependent steps); the sums are HBM-bound.
 #include "sv_internal.h"
@@ -32,6 +33,7 @@ namespace sv {
 namespace {
 
 constexpr int kInf = 0x3FFFFFFF;
+constexpr int kNegInf = -0x7FFFFFFF - 1;
 
 __device__ __forceinline__ int dpp_shr1(int v, int old) {   // lane j <- lane j-1 (row of 16)
     return __builtin_amdgcn_update_dpp(old, v, 0x111, 0xF, 0xF, false);
@@ -163,36 +165,20 @@ __global__ __launch_bounds__(256) void k_sgbm_vsum(SgbmArgs a) {
     }
 }
 
-// The path kernels give one wave the D disparities of one row (horizontal) or one column
-// (vertical): lane l owns d = l*DPL .. l*DPL+DPL-1.  A step is a dependent chain (the path
-// minimum of step s feeds step s+1), so the C / L inputs of the next PF steps are loaded
-// ahead into a register ring: the HBM latency of a load is covered by PF steps of compute.
-__device__ __forceinline__ int wave_shr1(int v, int old) {   // lane l <- lane l-1 (whole wave)
-    return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xF, 0xF, false);
-}
-__device__ __forceinline__ int wave_shl1(int v, int old) {   // lane l <- lane l+1
-    return __builtin_amdgcn_update_dpp(old, v, 0x130, 0xF, 0xF, false);
-}
-__device__ __forceinline__ int wave_min(int v) {             // uniform (SGPR) result
-    v = row_min(v);
-    return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
-               min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
-}
-__device__ __forceinline__ uint32_t wave_min_u(uint32_t v) {
-    v = row_min_u(v);
-    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
-    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
-    return min(min(a, b), min(c, d));
-}
-__device__ __forceinline__ int wave_max(int v) {
-    v = row_max(v);
-    return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
-               max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
-}
+// The path kernels run one line's DP (a chain of W or H dependent steps: the path minimum
+// of step s feeds step s+1) in a 16-lane row of a wave, so a wave advances 4 lines at once
+// and the loop-carried chain per step is ~11 VALU ops: the d+-1 neighbours by row_shr/shl
+// DPP, 4 ops per disparity, an in-lane min3 tree and a 4-step row_ror min butterfly (no
+// readlane, no SALU).  Lane j of a row owns d = j*DPL .. j*DPL+DPL-1.  The inputs of the
+// next PF steps are loaded ahead into a register ring; the loads are unconditional (a
+// branch between a prefetch and its use makes the compiler wait for it at once).
 
-// DPL contiguous elements of type T as one vector load/store (DPL in {1, 2, 4, 8}).
+// DPL contiguous elements of type T as one vector load/store.
+constexpr int pack_align(int bytes) {
+    return bytes % 16 == 0 ? 16 : bytes % 8 == 0 ? 8 : bytes % 4 == 0 ? 4 : bytes % 2 == 0 ? 2 : 1;
+}
 template <typename T, int DPL>
-struct alignas(sizeof(T) * DPL) Pack {
+struct alignas(pack_align(sizeof(T) * DPL)) Pack {
     T v[DPL];
 };
 
@@ -201,8 +187,8 @@ struct alignas(sizeof(T) * DPL) Pack {
 template <int DPL>
 __device__ __forceinline__ void path_step(int (&prev)[DPL], const int (&c)[DPL], int mn, int P1, int P2,
                                           int dbase, int D) {
-    const int lo_in = wave_shr1(prev[DPL - 1], kInf);
-    const int hi_in = wave_shl1(prev[0], kInf);
+    const int lo_in = dpp_shr1(prev[DPL - 1], kInf);
+    const int hi_in = dpp_shl1(prev[0], kInf);
     int nxt[DPL];
     const int mp = mn + P2;
 #pragma unroll
@@ -224,62 +210,73 @@ __device__ __forceinline__ int lane_min(const int (&v)[DPL]) {
     return m;
 }
 
-// Horizontal paths: one wave per (row, direction); blockIdx.y = 0: left->right into Llr,
-// 1: right->left into Lrl.
+// Horizontal paths: 4 rows per wave; blockIdx.y = 0: left->right into Llr, 1: right->left
+// into Lrl.
 template <int DPL, typename LT, int PF>
 __global__ __launch_bounds__(64) void k_sgbm_hpath(SgbmArgs a) {
-    const int lane = threadIdx.x, y = blockIdx.x, dir = blockIdx.y;
-    const int D = a.D, Wb = a.Wb, dbase = lane * DPL;
-    const bool live = dbase < D;                      // lanes past D only pad
-    const int Dp = a.Dp;                             // row stride: D rounded up to DPL
-    LT* Lrow = static_cast<LT*>(dir == 0 ? a.Llr : a.Lrl) + (size_t)y * Wb * Dp + dbase;
-    const uint16_t* Crow = a.C + (size_t)y * Wb * Dp + dbase;
+    const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+    const int y = blockIdx.x * 4 + g, dir = blockIdx.y;
+    const int D = a.D, Wb = a.Wb, Dp = a.Dp, dbase = j * DPL;
+    // rows past H and lanes past D re-read valid cells and store into a private dummy
+    // slot: no load or store sits under a branch
+    const bool live = y < a.H && dbase < D;
+    const int yc = min(y, a.H - 1);
+    LT* Lrow = live ? static_cast<LT*>(dir == 0 ? a.Llr : a.Lrl) + (size_t)yc * Wb * Dp + dbase
+                    : reinterpret_cast<LT*>(a.dummy) + lane * (128 / sizeof(LT));
+    const int xstride = live ? Dp : 0;
+    const uint16_t* Crow = a.C + (size_t)yc * Wb * Dp + (dbase < D ? dbase : 0);
     using CP = Pack<uint16_t, DPL>;
     using LP = Pack<LT, DPL>;
     auto xof = [&](int s) { return dir == 0 ? s : Wb - 1 - s; };
     CP ring[PF];
 #pragma unroll
-    for (int p = 0; p < PF; ++p)
-        if (p < Wb && live) ring[p] = *reinterpret_cast<const CP*>(Crow + (size_t)xof(p) * Dp);
+    for (int p = 0; p < PF; ++p) ring[p] = *reinterpret_cast<const CP*>(Crow + (size_t)xof(min(p, Wb - 1)) * Dp);
     int prev[DPL];
 #pragma unroll
     for (int k = 0; k < DPL; ++k) prev[k] = dbase + k < D ? 0 : kInf;
     int mn = 0;
-    for (int s0 = 0; s0 < Wb; s0 += PF) {
+    auto step = [&](int s, const CP& cp) {
+        int c[DPL];
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) c[k] = (int)cp.v[k];
+        path_step<DPL>(prev, c, mn, a.P1, a.P2, dbase, D);
+        mn = row_min(lane_min<DPL>(prev));
+        LP o;
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) o.v[k] = (LT)prev[k];
+        *reinterpret_cast<LP*>(Lrow + (size_t)xof(s) * xstride) = o;
+    };
+    int s0 = 0;
+    for (; s0 + PF <= Wb; s0 += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
-            const int s = s0 + u;
-            if (s < Wb) {
-            int c[DPL];
-#pragma unroll
-            for (int k = 0; k < DPL; ++k) c[k] = live ? (int)ring[u].v[k] : 0;
-            if (s + PF < Wb && live) ring[u] = *reinterpret_cast<const CP*>(Crow + (size_t)xof(s + PF) * Dp);
-            path_step<DPL>(prev, c, mn, a.P1, a.P2, dbase, D);
-            mn = wave_min(lane_min<DPL>(prev));
-            if (live) {
-                LP o;
-#pragma unroll
-                for (int k = 0; k < DPL; ++k) o.v[k] = (LT)prev[k];
-                *reinterpret_cast<LP*>(Lrow + (size_t)xof(s) * Dp) = o;
-            }
-            }
+            const CP cur = ring[u];
+            ring[u] = *reinterpret_cast<const CP*>(Crow + (size_t)xof(min(s0 + u + PF, Wb - 1)) * Dp);
+            step(s0 + u, cur);
         }
     }
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (s0 + u < Wb) step(s0 + u, ring[u]);
 }
 
-struct BandOut {      // one 8-byte store per band pixel
+struct BandOut {      // one 8-byte record per band pixel
     int16_t disp, best;
     int32_t minS;
 };
 
-// Top->bottom path + winner-take-all: one wave per band column, walking down the rows.
+// Top->bottom path + winner-take-all: 4 band columns per wave walking down the rows.  The
+// argmin / uniqueness / sub-pixel work of a row does not feed the next row, so it overlaps
+// the loop-carried path chain.
 template <int DPL, typename LT, int PF>
 __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
-    const int lane = threadIdx.x, xb = blockIdx.x;
-    const int D = a.D, Wb = a.Wb, dbase = lane * DPL;
-    const bool live = dbase < D;
+    const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+    const int xb = blockIdx.x * 4 + g;
+    const int D = a.D, Wb = a.Wb, dbase = j * DPL;
+    const bool colok = xb < Wb;
+    const bool live = colok && dbase < D;
     const size_t plane = (size_t)Wb * a.Dp;
-    const size_t col = (size_t)xb * a.Dp + dbase;
+    const size_t col = (size_t)min(xb, Wb - 1) * a.Dp + (dbase < D ? dbase : 0);
     const LT* Llr = static_cast<const LT*>(a.Llr) + col;
     const LT* Lrl = static_cast<const LT*>(a.Lrl) + col;
     const uint16_t* Cc = a.C + col;
@@ -287,79 +284,82 @@ __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
     using LP = Pack<LT, DPL>;
     CP rc[PF];
     LP rl[PF], rr[PF];
+    auto fetch = [&](int y, CP& c, LP& l, LP& r) {
+        const size_t o = (size_t)min(y, a.H - 1) * plane;
+        c = *reinterpret_cast<const CP*>(Cc + o);
+        l = *reinterpret_cast<const LP*>(Llr + o);
+        r = *reinterpret_cast<const LP*>(Lrl + o);
+    };
 #pragma unroll
-    for (int p = 0; p < PF; ++p)
-        if (p < a.H && live) {
-            rc[p] = *reinterpret_cast<const CP*>(Cc + (size_t)p * plane);
-            rl[p] = *reinterpret_cast<const LP*>(Llr + (size_t)p * plane);
-            rr[p] = *reinterpret_cast<const LP*>(Lrl + (size_t)p * plane);
-        }
+    for (int p = 0; p < PF; ++p) fetch(p, rc[p], rl[p], rr[p]);
     int prev[DPL];
 #pragma unroll
     for (int k = 0; k < DPL; ++k) prev[k] = dbase + k < D ? 0 : kInf;
     int mn = 0;
     const int u100 = 100 - a.uniq;
-    BandOut* bo = reinterpret_cast<BandOut*>(a.band) + xb;
-    for (int y0 = 0; y0 < a.H; y0 += PF) {
+    BandOut* bo = colok ? reinterpret_cast<BandOut*>(a.band) + xb : reinterpret_cast<BandOut*>(a.dummy) + lane;
+    const int ystride = colok ? Wb : 0;
+    auto row = [&](int y, const CP& cp, const LP& lp, const LP& rp) {
+        int c[DPL], s[DPL];
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) {
+            c[k] = (int)cp.v[k];
+            s[k] = (int)lp.v[k] + (int)rp.v[k];
+        }
+        path_step<DPL>(prev, c, mn, a.P1, a.P2, dbase, D);
+        mn = row_min(lane_min<DPL>(prev));
+        uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) {
+            s[k] += prev[k];
+            if (dbase + k < D) key = min(key, ((uint32_t)(s[k] + (1 << 20)) << 9) | (uint32_t)(dbase + k));
+        }
+        key = row_min_u(key);
+        const int b = (int)(key & 511u);
+        const int minS = (int)(key >> 9) - (1 << 20);
+        int viol = 0;
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) {
+            const int d = dbase + k;
+            viol |= (d < D) & (s[k] * u100 < minS * 100) & (abs(d - b) > 1);
+        }
+        viol = row_max(viol);
+        // S[b-1], S[b+1] from the lane that owns b, broadcast within the row
+        const int sl = dpp_shr1(s[DPL - 1], 0), sr = dpp_shl1(s[0], 0);
+        const int kb = b - dbase;
+        const bool own = kb >= 0 && kb < DPL;
+        int sm = sl, sp = sr;
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) {
+            if (k == kb - 1) sm = s[k];
+            if (k == kb + 1) sp = s[k];
+        }
+        sm = row_max(own ? sm : kNegInf);
+        sp = row_max(own ? sp : kNegInf);
+        int d16 = b * 16;
+        if (b > 0 && b < D - 1) {
+            const int denom2 = max(sm + sp - 2 * minS, 1);
+            d16 += ((sm - sp) * 16 + denom2) / (denom2 * 2);
+        }
+        BandOut o;
+        o.disp = (int16_t)(viol ? (a.minD - 1) * 16 : d16 + a.minD * 16);
+        o.best = (int16_t)b;
+        o.minS = viol ? 0x7FFFFFFF : minS;
+        bo[(size_t)y * ystride] = o;          // the 16 lanes of a row store the same record
+    };
+    int y0 = 0;
+    for (; y0 + PF <= a.H; y0 += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
-            const int y = y0 + u;
-            if (y < a.H) {
-            int c[DPL], s[DPL];
-#pragma unroll
-            for (int k = 0; k < DPL; ++k) {
-                c[k] = live ? (int)rc[u].v[k] : 0;
-                s[k] = live ? (int)rl[u].v[k] + (int)rr[u].v[k] : 0;
-            }
-            if (y + PF < a.H && live) {
-                const size_t o = (size_t)(y + PF) * plane;
-                rc[u] = *reinterpret_cast<const CP*>(Cc + o);
-                rl[u] = *reinterpret_cast<const LP*>(Llr + o);
-                rr[u] = *reinterpret_cast<const LP*>(Lrl + o);
-            }
-            path_step<DPL>(prev, c, mn, a.P1, a.P2, dbase, D);
-            mn = wave_min(lane_min<DPL>(prev));
-            uint32_t key = 0xFFFFFFFFu;
-#pragma unroll
-            for (int k = 0; k < DPL; ++k) {
-                if (dbase + k < D) {
-                    s[k] += prev[k];
-                    key = min(key, ((uint32_t)(s[k] + (1 << 20)) << 9) | (uint32_t)(dbase + k));
-                }
-            }
-            key = wave_min_u(key);
-            const int b = (int)(key & 511u);
-            const int minS = (int)(key >> 9) - (1 << 20);
-            int viol = 0;
-#pragma unroll
-            for (int k = 0; k < DPL; ++k) {
-                const int d = dbase + k;
-                viol |= (d < D) && (s[k] * u100 < minS * 100) && (abs(d - b) > 1);
-            }
-            viol = wave_max(viol);
-            const int sl = wave_shr1(s[DPL - 1], 0), sr = wave_shl1(s[0], 0);
-            if (b >= dbase && b < dbase + DPL) {       // the lane that owns b writes
-                const int kb = b - dbase;
-                int sm = sl, sp = sr;
-#pragma unroll
-                for (int k = 0; k < DPL; ++k) {
-                    if (k == kb - 1) sm = s[k];
-                    if (k == kb + 1) sp = s[k];
-                }
-                int d16 = b * 16;
-                if (b > 0 && b < D - 1) {
-                    const int denom2 = max(sm + sp - 2 * minS, 1);
-                    d16 += ((sm - sp) * 16 + denom2) / (denom2 * 2);
-                }
-                BandOut o;
-                o.disp = (int16_t)(viol ? (a.minD - 1) * 16 : d16 + a.minD * 16);
-                o.best = (int16_t)b;
-                o.minS = viol ? 0x7FFFFFFF : minS;
-                bo[(size_t)y * Wb] = o;
-            }
-            }
+            const CP c = rc[u];
+            const LP l = rl[u], r = rr[u];
+            fetch(y0 + u + PF, rc[u], rl[u], rr[u]);
+            row(y0 + u, c, l, r);
         }
     }
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (y0 + u < a.H) row(y0 + u, rc[u], rl[u], rr[u]);
 }
 
 // Left-right consistency (disp12MaxDiff) and band borders: one workgroup per row.
@@ -438,27 +438,67 @@ __device__ __forceinline__ void uf_unite(int* p, int a, int b) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_cc_init(const int16_t* img, int H, int W, int pitch, int newv, int* parent,
-                                                 int* size) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= H * W) return;
-    const int y = i / W, x = i % W;
-    parent[i] = img[(size_t)y * pitch + x] != newv ? i : -1;
-    size[i] = 0;
+// Phase 1: union-find inside a 32x32 tile in LDS (no global atomics).  A component's
+// local root is its smallest row-major tile index, whose global index is therefore also the
+// smallest of its members: parent[i] <= i holds globally, as uf_unite() requires.
+constexpr int kCT = 32;
+__global__ __launch_bounds__(256) void k_cc_local(const int16_t* img, int H, int W, int pitch, int newv,
+                                                  int maxdiff, int* parent, int* size) {
+    __shared__ int lp[kCT * kCT];
+    __shared__ int16_t lv[kCT * kCT];
+    const int x0 = blockIdx.x * kCT, y0 = blockIdx.y * kCT, t = threadIdx.x;
+    for (int l = t; l < kCT * kCT; l += 256) {
+        const int x = x0 + (l % kCT), y = y0 + l / kCT;
+        const bool in = x < W && y < H;
+        const int v = in ? img[(size_t)y * pitch + x] : newv;
+        lv[l] = (int16_t)v;
+        lp[l] = v != newv ? l : -1;
+    }
+    __syncthreads();
+    for (int l = t; l < kCT * kCT; l += 256) {
+        const int v = lv[l];
+        if (v == newv) continue;
+        const int lx = l % kCT;
+        if (lx + 1 < kCT) {
+            const int w = lv[l + 1];
+            if (w != newv && abs(w - v) <= maxdiff) uf_unite(lp, l, l + 1);
+        }
+        if (l + kCT < kCT * kCT) {
+            const int w = lv[l + kCT];
+            if (w != newv && abs(w - v) <= maxdiff) uf_unite(lp, l, l + kCT);
+        }
+    }
+    __syncthreads();
+    for (int l = t; l < kCT * kCT; l += 256) {
+        const int x = x0 + (l % kCT), y = y0 + l / kCT;
+        if (x >= W || y >= H) continue;
+        const size_t gi = (size_t)y * W + x;
+        size[gi] = 0;
+        if (lp[l] < 0) {
+            parent[gi] = -1;
+            continue;
+        }
+        const int r = uf_find(lp, l);
+        parent[gi] = (y0 + r / kCT) * W + x0 + (r % kCT);
+    }
 }
 
-__global__ __launch_bounds__(256) void k_cc_union(const int16_t* img, int H, int W, int pitch, int newv, int maxdiff,
-                                                  int* parent) {
+// Phase 2: the edges that cross tile borders, united in the global forest.
+__global__ __launch_bounds__(256) void k_cc_border(const int16_t* img, int H, int W, int pitch, int newv,
+                                                   int maxdiff, int* parent) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= H * W) return;
     const int y = i / W, x = i % W;
+    const bool right = (x % kCT) == kCT - 1 && x + 1 < W;
+    const bool down = (y % kCT) == kCT - 1 && y + 1 < H;
+    if (!right && !down) return;
     const int v = img[(size_t)y * pitch + x];
     if (v == newv) return;
-    if (x + 1 < W) {
+    if (right) {
         const int w = img[(size_t)y * pitch + x + 1];
         if (w != newv && abs(w - v) <= maxdiff) uf_unite(parent, i, i + 1);
     }
-    if (y + 1 < H) {
+    if (down) {
         const int w = img[(size_t)(y + 1) * pitch + x];
         if (w != newv && abs(w - v) <= maxdiff) uf_unite(parent, i, i + W);
     }
@@ -493,14 +533,16 @@ __global__ __launch_bounds__(256) void k_cc_apply(int16_t* img, int H, int W, in
 
 template <typename LT>
 int launch_paths_t(const SgbmArgs& a, int dpl, hipStream_t s) {
-    dim3 gh(a.H, 2), gv(a.Wb);
+    dim3 gh((a.H + 3) / 4, 2), gv((a.Wb + 3) / 4);
 #define SV_SGBM_DPL(N, PFH, PFV)                                                  \
     case N:                                                                       \
         hipLaunchKernelGGL((k_sgbm_hpath<N, LT, PFH>), gh, dim3(64), 0, s, a);   \
         hipLaunchKernelGGL((k_sgbm_vpath<N, LT, PFV>), gv, dim3(64), 0, s, a);   \
         break;
     switch (dpl) {
-        SV_SGBM_DPL(1, 24, 12) SV_SGBM_DPL(2, 24, 12) SV_SGBM_DPL(4, 16, 8) SV_SGBM_DPL(8, 8, 4)
+        SV_SGBM_DPL(1, 24, 16) SV_SGBM_DPL(2, 24, 16) SV_SGBM_DPL(4, 16, 12) SV_SGBM_DPL(8, 16, 8)
+        SV_SGBM_DPL(12, 10, 4) SV_SGBM_DPL(16, 8, 3) SV_SGBM_DPL(20, 6, 2) SV_SGBM_DPL(24, 6, 2)
+        SV_SGBM_DPL(32, 4, 1)
         default: return (int)hipErrorInvalidValue;
     }
 #undef SV_SGBM_DPL
@@ -510,8 +552,9 @@ int launch_paths_t(const SgbmArgs& a, int dpl, hipStream_t s) {
 }  // namespace
 
 int sgbm_dpl(int D) {
-    const int need = (D + 63) / 64;
-    for (int o = 1; o <= 8; o *= 2)
+    const int need = (D + 15) / 16;
+    const int opts[] = {1, 2, 4, 8, 12, 16, 20, 24, 32};
+    for (int o : opts)
         if (o >= need) return o;
     return -1;
 }
@@ -536,8 +579,9 @@ int launch_speckles(int16_t* img, int H, int W, int pitch, int newv, int maxsize
                     int* size, hipStream_t s) {
     if (H <= 0 || W <= 0 || maxsize <= 0) return 0;
     const unsigned n = (unsigned)(((size_t)H * W + 255) / 256);
-    hipLaunchKernelGGL(k_cc_init, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, parent, size);
-    hipLaunchKernelGGL(k_cc_union, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, maxdiff, parent);
+    dim3 tiles((W + kCT - 1) / kCT, (H + kCT - 1) / kCT);
+    hipLaunchKernelGGL(k_cc_local, tiles, dim3(256), 0, s, img, H, W, pitch, newv, maxdiff, parent, size);
+    hipLaunchKernelGGL(k_cc_border, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, maxdiff, parent);
     hipLaunchKernelGGL(k_cc_count, dim3(n), dim3(256), 0, s, H, W, maxsize, parent, size);
     hipLaunchKernelGGL(k_cc_apply, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, maxsize, parent, size);
     return (int)hipGetLastError();

@@ -121,3 +121,12 @@ def test_gpu_sgbm_1080p_properties(engine):
     assert (d[:, :128] == -16).all()
     inner = d[10:-10, 140:-10].astype(np.int32)
     assert (np.abs(inner - 20 * 16) <= 1).mean() > 0.99
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,win", [(160, 5), (256, 7), (320, 7), (384, 3), (512, 5)])
+def test_gpu_sgbm_wide_disparity_ranges(engine, D, win):
+    """Every lane plan of the path kernels (DPL 12..32), incl. the reference's default
+    NUM_DISP = 16*20 = 320 with WINDOW_SIZE = 7 (depth_map.py:31-33)."""
+    L, R, _ = stereo_pair(21, D + 90, D, seed=D)
+    np.testing.assert_array_equal(engine.sgbm(L, R, 0, D, win), SG.sgbm(L, R, 0, D, win))

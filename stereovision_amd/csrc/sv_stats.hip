@@ -28,26 +28,66 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-// One workgroup (256 threads) per 48x48 tile of one image (grid.z = image).
+// LDS histogram increment with wave aggregation: when every active lane of the wave adds
+// to the same bin (flat image regions, or the constant high digits of a radix pass: the
+// common case) one atomic adds the population; otherwise each lane adds 1.
+__device__ __forceinline__ void hist_add(uint32_t* h, uint32_t bin) {
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)bin);
+    const unsigned long long act = __ballot(1);
+    const unsigned long long same = __ballot(bin == b0);
+    if (same == act) {
+        if (__lane_id() == (unsigned)__builtin_ctzll(act)) atomicAdd(&h[b0], (uint32_t)__builtin_popcountll(act));
+    } else {
+        atomicAdd(&h[bin], 1u);
+    }
+}
+
+// One workgroup (256 threads) per 48x48 tile of one image (grid.z = image).  A thread owns
+// one (row, 4-pixel group) of the tile per iteration (48 rows x 12 groups), gray rows read
+// as dwords (48 is a multiple of 4: a group never straddles two tiles); one LDS histogram
+// copy per wave.
 __global__ __launch_bounds__(256) void k_frame_stats(FrameStatsArgs a) {
-    __shared__ uint32_t hist[256];
+    __shared__ uint32_t hist[4][256];
     __shared__ uint32_t part[2][4];
     const int z = blockIdx.z;
     const uint8_t* img = z == 0 ? a.img0 : a.img1;
-    const int tx = blockIdx.x, ty = blockIdx.y, t = threadIdx.x;
-    hist[t] = 0;
+    const int tx = blockIdx.x, ty = blockIdx.y, t = threadIdx.x, wv = t >> 6;
+    for (int i = t; i < 4 * 256; i += 256) (&hist[0][0])[i] = 0;
     __syncthreads();
     const int x0 = tx * kTile, y0 = ty * kTile;
     const int w = min(kTile, a.W - x0), h = min(kTile, a.H - y0);
+    const int groups = (w + 3) >> 2;
     uint32_t s = 0, q = 0;
-    for (int i = t; i < w * h; i += 256) {
-        const int y = y0 + i / w, x = x0 + i % w;
-        const uint8_t* p = img + (size_t)y * a.pitch + (size_t)x * a.cn;
-        const uint32_t v = a.cn == 3 ? (uint32_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14)
-                                     : (uint32_t)p[0];
-        s += v;
-        q += v * v;
-        atomicAdd(&hist[v], 1u);
+    for (int i = t; i < h * groups; i += 256) {
+        const int r = i / groups, g = i - r * groups;
+        const int x = x0 + 4 * g, n = min(4, w - 4 * g);
+        const uint8_t* p = img + (size_t)(y0 + r) * a.pitch + (size_t)x * a.cn;
+        uint32_t v4[4];
+        if (a.cn == 1 && n == 4 && (((uintptr_t)p & 3) == 0)) {
+            const uint32_t d = *reinterpret_cast<const uint32_t*>(p);
+            v4[0] = d & 0xff;
+            v4[1] = (d >> 8) & 0xff;
+            v4[2] = (d >> 16) & 0xff;
+            v4[3] = d >> 24;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint8_t* pk = p + k * a.cn;
+                v4[k] = k >= n ? 0u
+                        : a.cn == 3 ? (uint32_t)((pk[0] * 1868 + pk[1] * 9617 + pk[2] * 4899 + (1 << 13)) >> 14)
+                                    : (uint32_t)pk[0];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < n) {
+                s += v4[k];
+                q += v4[k] * v4[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < n) hist_add(hist[wv], v4[k]);
     }
     s = wave_sum(s);
     q = wave_sum(q);
@@ -61,7 +101,7 @@ __global__ __launch_bounds__(256) void k_frame_stats(FrameStatsArgs a) {
         a.block_sum[b] = part[0][0] + part[0][1] + part[0][2] + part[0][3];
         a.block_sq[b] = part[1][0] + part[1][1] + part[1][2] + part[1][3];
     }
-    const uint32_t c = hist[t];
+    const uint32_t c = hist[0][t] + hist[1][t] + hist[2][t] + hist[3][t];
     if (c) atomicAdd(&a.hist[z * 256 + t], c);
 }
 
@@ -97,7 +137,7 @@ __global__ __launch_bounds__(256) void k_select_hist(SelectArgs a) {
         const uint32_t d = (k >> a.shift) & (uint32_t)(nb - 1);
         const uint32_t hi = a.shift + a.bits >= 32 ? 0u : (k >> (a.shift + a.bits));
         for (int r = 0; r < a.nranks; ++r)
-            if (hi == a.prefix[r]) atomicAdd(&h[r][d], 1u);
+            if (hi == a.prefix[r]) hist_add(h[r], d);
     }
     __syncthreads();
     for (int r = 0; r < a.nranks; ++r)
@@ -141,8 +181,10 @@ int launch_frame_stats(const FrameStatsArgs& a, int nimg, hipStream_t s) {
 
 int launch_select_hist(const SelectArgs& a, hipStream_t s) {
     if (a.n == 0) return 0;
-    int blocks = (int)((a.n + 255) / 256);
-    if (blocks > 2048) blocks = 2048;
+    // ~16 elements per thread: each block zeroes and merges a 2048-bin histogram per rank
+    int blocks = (int)((a.n + 4095) / 4096);
+    if (blocks > 1024) blocks = 1024;
+    if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_select_hist, dim3(blocks), dim3(256), 0, s, a);
     return (int)hipGetLastError();
 }

@@ -57,6 +57,14 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
     }
+    // for self-cleaning accumulators (the kernels that read them zero them again)
+    hipError_t ensure_zeroed(size_t n) {
+        if (n <= cap) return hipSuccess;
+        hipError_t e = ensure(n);
+        if (e == hipSuccess) e = hipMemset(p, 0, cap);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        return e;
+    }
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
@@ -92,7 +100,7 @@ struct sv_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut, rmap1, rmap2, rdst[2], stats, sel,
-        sg_hsum, sg_c, sg_l, sg_band, cc_parent, cc_size;
+        sg_hsum, sg_c, sg_l, sg_band, cc_parent, cc_size, hist_copies;
     // cached post-processing table: key = (mode, params, range); `lut_ev` marks its build
     struct LutKey {
         int mode = -1, min_disp = 0, num_disp = 0, m0 = 0, n = 0;
@@ -549,7 +557,7 @@ void sv_destroy(sv_ctx* c) {
         DevBuf* bufs[] = {&c->img[0], &c->img[1], &c->gray[0], &c->gray[1], &c->d16, &c->fa, &c->fb,
                           &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->lut,
                           &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1], &c->stats, &c->sel,
-                          &c->sg_hsum, &c->sg_c, &c->sg_l, &c->sg_band, &c->cc_parent,
+                          &c->sg_hsum, &c->sg_c, &c->sg_l, &c->sg_band, &c->cc_parent, &c->hist_copies,
                           &c->cc_size};
         if (c->lut_ev) (void)hipEventDestroy(c->lut_ev);
         for (auto* b : bufs) b->release();
@@ -1135,8 +1143,9 @@ int sv_frame_stats_dev(sv_ctx* c, const uint8_t* d_img0, const uint8_t* d_img1, 
     if (pitch < W * channels) return fail(SV_EINVAL, "pitch smaller than a row");
     hipStream_t s = pick(c, stream);
     const int nimg = d_img1 ? 2 : 1;
-    SV_HIP(hipMemsetAsync(d_hist, 0, (size_t)nimg * 256 * sizeof(uint32_t), s));
+    SV_HIP(c->hist_copies.ensure_zeroed((size_t)sv::kHistCopies * 2 * 256 * sizeof(uint32_t)));
     sv::FrameStatsArgs a{};
+    a.hist_copies = c->hist_copies.as<uint32_t>();
     a.img0 = d_img0;
     a.img1 = d_img1;
     a.H = H;
@@ -1172,8 +1181,9 @@ int sv_frame_stats(sv_ctx* c, const uint8_t* img0, const uint8_t* img1, int H, i
     }
     SV_HIP(c->stats.ensure(nimg * (2 * nb + 256) * sizeof(uint32_t)));
     uint32_t* d = c->stats.as<uint32_t>();
-    SV_HIP(hipMemsetAsync(d + 2 * nimg * nb, 0, (size_t)nimg * 256 * sizeof(uint32_t), c->stream));
+    SV_HIP(c->hist_copies.ensure_zeroed((size_t)sv::kHistCopies * 2 * 256 * sizeof(uint32_t)));
     sv::FrameStatsArgs a{};
+    a.hist_copies = c->hist_copies.as<uint32_t>();
     a.img0 = c->img[0].as<uint8_t>();
     a.img1 = nimg == 2 ? c->img[1].as<uint8_t>() : nullptr;
     a.H = H;
@@ -1200,14 +1210,19 @@ static int check_select(const float* d_x, int64_t n, int mask_mode, const float*
 
 // One select pass over the context stream: ghist[nranks][2048] back on the host.
 static int select_pass(sv_ctx* c, sv::SelectArgs& a, uint32_t* hist_host, unsigned long long* counts_host) {
+    // device: [copies][kMaxRanks][2048] accumulators | count slots | folded hist | counts
     const size_t hb = (size_t)sv::kMaxRanks * 2048 * sizeof(uint32_t);
-    SV_HIP(c->sel.ensure(hb + 2 * sizeof(unsigned long long)));
-    a.ghist = c->sel.as<uint32_t>();
-    a.counts = counts_host ? reinterpret_cast<unsigned long long*>(c->sel.as<uint8_t>() + hb) : nullptr;
-    SV_HIP(hipMemsetAsync(c->sel.p, 0, hb + 2 * sizeof(unsigned long long), c->stream));
+    const size_t ab = sv::kHistCopies * hb;
+    const size_t cb = (size_t)sv::kCountSlots * 16 * sizeof(unsigned long long);
+    SV_HIP(c->sel.ensure_zeroed(ab + cb + hb + 16));
+    uint8_t* base = c->sel.as<uint8_t>();
+    a.ghist = reinterpret_cast<uint32_t*>(base);
+    a.counts = reinterpret_cast<unsigned long long*>(base + ab);
+    a.hist_out = reinterpret_cast<uint32_t*>(base + ab + cb);
+    a.counts_out = reinterpret_cast<unsigned long long*>(base + ab + cb + hb);
     SV_LAUNCH(c, SV_K_SELECT, c->stream, sv::launch_select_hist(a, c->stream));
     SV_HIP(c->hout.ensure(hb + 16));
-    SV_HIP(hipMemcpyAsync(c->hout.p, c->sel.p, hb + 16, hipMemcpyDeviceToHost, c->stream));
+    SV_HIP(hipMemcpyAsync(c->hout.p, a.hist_out, hb + 16, hipMemcpyDeviceToHost, c->stream));
     SV_HIP(hipStreamSynchronize(c->stream));
     std::memcpy(hist_host, c->hout.p, (size_t)a.nranks * 2048 * sizeof(uint32_t));
     if (counts_host) std::memcpy(counts_host, c->hout.as<uint8_t>() + hb, 16);

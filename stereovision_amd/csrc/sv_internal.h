@@ -77,8 +77,12 @@ struct FrameStatsArgs {
     int bh, bw;               // blocks of compute_block_homogeneity: max(1, H/48) x max(1, W/48)
     uint32_t* block_sum;      // [nimg][bh][bw]
     uint32_t* block_sq;
-    uint32_t* hist;           // [nimg][256], accumulated with atomics (zero it first)
+    uint32_t* hist;           // [nimg][256], written whole by the fold kernel
+    uint32_t* hist_copies;    // accumulators [kHistCopies][nimg][256], zero on entry and exit
 };
+// Global histograms are accumulated into kHistCopies copies (block b adds into copy
+// b % kHistCopies: hundreds of same-address atomics serialise at L2) and folded after.
+constexpr int kHistCopies = 8;
 int launch_frame_stats(const FrameStatsArgs& a, int nimg, hipStream_t s);
 
 enum SelectMask { SEL_ALL = 0, SEL_POSITIVE = 1, SEL_MASK_GT = 2 };
@@ -92,9 +96,12 @@ struct SelectArgs {
     int shift, bits;          // digit = (key >> shift) & ((1 << bits) - 1)
     int nranks;
     uint32_t prefix[kMaxRanks];   // key >> (shift + bits) of each rank's target
-    uint32_t* ghist;          // [nranks][2048]
-    unsigned long long* counts;   // pass 0: [selected, nan]
+    uint32_t* ghist;          // accumulators [kHistCopies][kMaxRanks][2048], zero on entry and exit
+    unsigned long long* counts;   // accumulators [kCountSlots][16] (slot = {selected, nan, pad})
+    uint32_t* hist_out;       // [nranks][2048], folded by the launcher's second kernel
+    unsigned long long* counts_out;   // [selected, nan]
 };
+constexpr int kCountSlots = 32;   // blocks add their counts into slot blockIdx % 32 (128 B apart)
 int launch_select_hist(const SelectArgs& a, hipStream_t s);
 
 enum AffineMode { AFF_F32 = 0, AFF_F64 = 1, AFF_FILL = 2 };

@@ -274,7 +274,6 @@ __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
     const int xb = blockIdx.x * 4 + g;
     const int D = a.D, Wb = a.Wb, dbase = j * DPL;
     const bool colok = xb < Wb;
-    const bool live = colok && dbase < D;
     const size_t plane = (size_t)Wb * a.Dp;
     const size_t col = (size_t)min(xb, Wb - 1) * a.Dp + (dbase < D ? dbase : 0);
     const LT* Llr = static_cast<const LT*>(a.Llr) + col;

@@ -28,81 +28,108 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-// LDS histogram increment with wave aggregation: when every active lane of the wave adds
-// to the same bin (flat image regions, or the constant high digits of a radix pass: the
-// common case) one atomic adds the population; otherwise each lane adds 1.
+// LDS histogram increment with wave aggregation: up to GROUPS distinct bins of the wave
+// (flat image regions; the few high digits of a radix pass) are added by a leader lane
+// with the bin's population, since same-address LDS atomics from many lanes serialise;
+// the remaining lanes add 1 each.
+template <int GROUPS>
 __device__ __forceinline__ void hist_add(uint32_t* h, uint32_t bin) {
-    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)bin);
-    const unsigned long long act = __ballot(1);
-    const unsigned long long same = __ballot(bin == b0);
-    if (same == act) {
-        if (__lane_id() == (unsigned)__builtin_ctzll(act)) atomicAdd(&h[b0], (uint32_t)__builtin_popcountll(act));
-    } else {
-        atomicAdd(&h[bin], 1u);
+    unsigned long long rem = __ballot(1);
+#pragma unroll
+    for (int it = 0; it < GROUPS; ++it) {
+        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)__builtin_ctzll(rem));
+        const unsigned long long grp = __ballot(bin == b0) & rem;
+        if (__lane_id() == (unsigned)__builtin_ctzll(grp)) atomicAdd(&h[b0], (uint32_t)__builtin_popcountll(grp));
+        if (bin == b0) return;
+        rem &= ~grp;
     }
+    atomicAdd(&h[bin], 1u);
 }
 
-// One workgroup (256 threads) per 48x48 tile of one image (grid.z = image).  A thread owns
-// one (row, 4-pixel group) of the tile per iteration (48 rows x 12 groups), gray rows read
-// as dwords (48 is a multiple of 4: a group never straddles two tiles); one LDS histogram
-// copy per wave.
+// One wave per 48x48 tile, four tiles side by side per workgroup (grid.z = image).  The
+// tile is 48 rows x 12 dword groups = 576 slots, 9 per lane, all loaded before any is
+// used (one memory latency per tile); the tile moments are a wave reduction.  One LDS
+// histogram copy per wave, merged into the image's global histogram at the end.
+constexpr int kSlots = (kTile * kTile / 4 + 63) / 64;   // 9
+
+__device__ __forceinline__ uint32_t gray_at(const uint8_t* p, int cn) {
+    return cn == 3 ? (uint32_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14) : (uint32_t)p[0];
+}
+
 __global__ __launch_bounds__(256) void k_frame_stats(FrameStatsArgs a) {
     __shared__ uint32_t hist[4][256];
-    __shared__ uint32_t part[2][4];
     const int z = blockIdx.z;
     const uint8_t* img = z == 0 ? a.img0 : a.img1;
-    const int tx = blockIdx.x, ty = blockIdx.y, t = threadIdx.x, wv = t >> 6;
+    const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
     for (int i = t; i < 4 * 256; i += 256) (&hist[0][0])[i] = 0;
     __syncthreads();
+    const int tx = blockIdx.x * 4 + wv, ty = blockIdx.y;
     const int x0 = tx * kTile, y0 = ty * kTile;
-    const int w = min(kTile, a.W - x0), h = min(kTile, a.H - y0);
-    const int groups = (w + 3) >> 2;
-    uint32_t s = 0, q = 0;
-    for (int i = t; i < h * groups; i += 256) {
-        const int r = i / groups, g = i - r * groups;
-        const int x = x0 + 4 * g, n = min(4, w - 4 * g);
-        const uint8_t* p = img + (size_t)(y0 + r) * a.pitch + (size_t)x * a.cn;
-        uint32_t v4[4];
-        if (a.cn == 1 && n == 4 && (((uintptr_t)p & 3) == 0)) {
-            const uint32_t d = *reinterpret_cast<const uint32_t*>(p);
-            v4[0] = d & 0xff;
-            v4[1] = (d >> 8) & 0xff;
-            v4[2] = (d >> 16) & 0xff;
-            v4[3] = d >> 24;
+    if (x0 < a.W) {
+        const int w = min(kTile, a.W - x0), h = min(kTile, a.H - y0);
+        const int groups = (w + 3) >> 2;
+        const bool fast = a.cn == 1 && w == kTile && ((a.pitch & 3) == 0) && ((((uintptr_t)img) & 3) == 0);
+        uint32_t s = 0, q = 0;
+        if (fast) {
+            uint32_t d[kSlots];
+#pragma unroll
+            for (int k = 0; k < kSlots; ++k) {
+                const int i = lane + 64 * k;
+                const int r = i / 12, g = i - r * 12;
+                d[k] = (i < 576 && r < h) ? *reinterpret_cast<const uint32_t*>(img + (size_t)(y0 + r) * a.pitch + x0 + 4 * g)
+                                          : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < kSlots; ++k) {
+                const int i = lane + 64 * k;
+                if (i < 576 && i / 12 < h) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t v = (d[k] >> (8 * j)) & 0xff;
+                        s += v;
+                        q += v * v;
+                        hist_add<1>(hist[wv], v);
+                    }
+                }
+            }
         } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint8_t* pk = p + k * a.cn;
-                v4[k] = k >= n ? 0u
-                        : a.cn == 3 ? (uint32_t)((pk[0] * 1868 + pk[1] * 9617 + pk[2] * 4899 + (1 << 13)) >> 14)
-                                    : (uint32_t)pk[0];
+            for (int i = lane; i < h * groups; i += 64) {
+                const int r = i / groups, g = i - r * groups;
+                const int n = min(4, w - 4 * g);
+                const uint8_t* p = img + (size_t)(y0 + r) * a.pitch + (size_t)(x0 + 4 * g) * a.cn;
+                for (int j = 0; j < n; ++j) {
+                    const uint32_t v = gray_at(p + j * a.cn, a.cn);
+                    s += v;
+                    q += v * v;
+                    hist_add<1>(hist[wv], v);
+                }
             }
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < n) {
-                s += v4[k];
-                q += v4[k] * v4[k];
-            }
+        s = wave_sum(s);
+        q = wave_sum(q);
+        if (lane == 0 && tx < a.bw && ty < a.bh) {   // a block of compute_block_homogeneity
+            const int b = z * a.bh * a.bw + ty * a.bw + tx;
+            a.block_sum[b] = s;
+            a.block_sq[b] = q;
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (k < n) hist_add(hist[wv], v4[k]);
-    }
-    s = wave_sum(s);
-    q = wave_sum(q);
-    if ((t & 63) == 0) {
-        part[0][t >> 6] = s;
-        part[1][t >> 6] = q;
     }
     __syncthreads();
-    if (t == 0 && tx < a.bw && ty < a.bh) {   // a block of compute_block_homogeneity
-        const int b = z * a.bh * a.bw + ty * a.bw + tx;
-        a.block_sum[b] = part[0][0] + part[0][1] + part[0][2] + part[0][3];
-        a.block_sq[b] = part[1][0] + part[1][1] + part[1][2] + part[1][3];
-    }
     const uint32_t c = hist[0][t] + hist[1][t] + hist[2][t] + hist[3][t];
-    if (c) atomicAdd(&a.hist[z * 256 + t], c);
+    const int copy = (blockIdx.y * gridDim.x + blockIdx.x) % kHistCopies;
+    if (c) atomicAdd(&a.hist_copies[((size_t)copy * gridDim.z + z) * 256 + t], c);
+}
+
+// dst[i] = sum over copies of acc[c * stride + i]; the accumulators are left zeroed for
+// the next call (no memset launch).
+__global__ __launch_bounds__(256) void k_fold_u32(uint32_t* acc, int copies, size_t stride, int n, uint32_t* dst) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t v = 0;
+    for (int k = 0; k < copies; ++k) {
+        v += acc[(size_t)k * stride + i];
+        acc[(size_t)k * stride + i] = 0;
+    }
+    dst[i] = v;
 }
 
 // Order-preserving map of float32 bits to uint32 (-0.0 folded onto +0.0, NaN excluded by
@@ -116,6 +143,28 @@ __device__ __forceinline__ uint32_t f32_key(float f) {
 // Pass `shift` of the select: histogram of digit (key >> shift) & (nbins-1) over the
 // selected elements whose key agrees with prefix[r] above the digit, for each rank r.
 // Pass 0 (shift = 21, all prefixes empty) also counts selected elements and NaNs.
+constexpr int kSelVec = 4;   // float4 loads per thread per iteration (16 elements)
+
+__device__ __forceinline__ void select_one(const SelectArgs& a, uint32_t (*h)[2048], int nb, float v, float m,
+                                           uint32_t& cnt, uint32_t& nan) {
+    if (a.mask_mode == SEL_MASK_GT && !(m > a.thr)) return;   // confidence > 0.7
+    if (v != v) {                                               // NaN in the selection -> nan
+        nan += a.mask_mode != SEL_POSITIVE;
+        return;
+    }
+    if (a.mask_mode == SEL_POSITIVE && !(v > 0.f)) return;     // disparity > 0
+    ++cnt;
+    const uint32_t k = f32_key(v);
+    const uint32_t d = (k >> a.shift) & (uint32_t)(nb - 1);
+    const uint32_t hi = a.shift + a.bits >= 32 ? 0u : (k >> (a.shift + a.bits));
+    for (int r = 0; r < a.nranks; ++r)
+        if (hi == a.prefix[r]) hist_add<4>(h[r], d);
+}
+
+// Pass `shift` of the select: histogram of digit (key >> shift) & (nbins-1) over the
+// selected elements whose key agrees with prefix[r] above the digit, for each rank r.
+// Pass 0 (shift = 21, all prefixes empty) also counts selected elements and NaNs.
+// Each thread loads kSelVec float4s (and mask float4s) before using any of them.
 __global__ __launch_bounds__(256) void k_select_hist(SelectArgs a) {
     __shared__ uint32_t h[kMaxRanks][2048];
     const int nb = 1 << a.bits;
@@ -123,33 +172,73 @@ __global__ __launch_bounds__(256) void k_select_hist(SelectArgs a) {
         for (int i = threadIdx.x; i < nb; i += 256) h[r][i] = 0;
     __syncthreads();
     uint32_t cnt = 0, nan = 0;
-    const size_t stride = (size_t)gridDim.x * 256;
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) {
-        if (a.mask_mode == SEL_MASK_GT && !(a.mask[i] > a.thr)) continue;   // confidence > 0.7
-        const float v = a.x[i];
-        if (v != v) {                        // NaN in the selection: np.percentile -> nan
-            nan += a.mask_mode != SEL_POSITIVE;
-            continue;
+    const bool vec = ((((uintptr_t)a.x) & 15) == 0) && (a.mask_mode != SEL_MASK_GT || ((((uintptr_t)a.mask) & 15) == 0));
+    const size_t n4 = vec ? a.n / 4 : 0;
+    const float4* x4 = reinterpret_cast<const float4*>(a.x);
+    const float4* m4 = reinterpret_cast<const float4*>(a.mask);
+    const bool use_mask = a.mask_mode == SEL_MASK_GT;
+    const size_t step = (size_t)gridDim.x * 256 * kSelVec;
+    for (size_t base = (size_t)blockIdx.x * 256 * kSelVec + threadIdx.x; base < n4; base += step) {
+        float4 v[kSelVec], m[kSelVec];
+#pragma unroll
+        for (int k = 0; k < kSelVec; ++k) {
+            const size_t j = base + (size_t)k * 256;
+            const size_t jj = j < n4 ? j : n4 - 1;
+            v[k] = x4[jj];
+            m[k] = use_mask ? m4[jj] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        if (a.mask_mode == SEL_POSITIVE && !(v > 0.f)) continue;            // disparity > 0
-        ++cnt;
-        const uint32_t k = f32_key(v);
-        const uint32_t d = (k >> a.shift) & (uint32_t)(nb - 1);
-        const uint32_t hi = a.shift + a.bits >= 32 ? 0u : (k >> (a.shift + a.bits));
-        for (int r = 0; r < a.nranks; ++r)
-            if (hi == a.prefix[r]) hist_add(h[r], d);
+#pragma unroll
+        for (int k = 0; k < kSelVec; ++k) {
+            if (base + (size_t)k * 256 < n4) {
+                select_one(a, h, nb, v[k].x, m[k].x, cnt, nan);
+                select_one(a, h, nb, v[k].y, m[k].y, cnt, nan);
+                select_one(a, h, nb, v[k].z, m[k].z, cnt, nan);
+                select_one(a, h, nb, v[k].w, m[k].w, cnt, nan);
+            }
+        }
     }
+    // scalar elements: the tail after the float4s, or everything when unaligned
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (size_t)gridDim.x * 256)
+        select_one(a, h, nb, a.x[i], use_mask ? a.mask[i] : 0.f, cnt, nan);
     __syncthreads();
     for (int r = 0; r < a.nranks; ++r)
         for (int i = threadIdx.x; i < nb; i += 256)
-            if (h[r][i]) atomicAdd(&a.ghist[r * 2048 + i], h[r][i]);
-    if (a.counts) {
+            if (h[r][i]) atomicAdd(&a.ghist[((blockIdx.x % kHistCopies) * kMaxRanks + r) * 2048 + i], h[r][i]);
+    {   // one add per block, striped over slots (same-address atomics serialise at L2)
+        __shared__ uint32_t part[2][4];
         cnt = wave_sum(cnt);
         nan = wave_sum(nan);
         if ((threadIdx.x & 63) == 0) {
-            atomicAdd(&a.counts[0], (unsigned long long)cnt);
-            atomicAdd(&a.counts[1], (unsigned long long)nan);
+            part[0][threadIdx.x >> 6] = cnt;
+            part[1][threadIdx.x >> 6] = nan;
         }
+        __syncthreads();
+        if (threadIdx.x < 2) {
+            const uint32_t* p = part[threadIdx.x];
+            atomicAdd(&a.counts[(blockIdx.x % kCountSlots) * 16 + threadIdx.x],
+                      (unsigned long long)p[0] + p[1] + p[2] + p[3]);
+        }
+    }
+}
+
+// hist_out = sum of the accumulator copies (nranks x 2048 bins, 8 blocks per rank), counts_out
+// = sum of the count slots; every accumulator read is zeroed for the next pass.
+__global__ __launch_bounds__(256) void k_select_fold(SelectArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;   // < nranks * 2048
+    uint32_t v = 0;
+    for (int k = 0; k < kHistCopies; ++k) {
+        uint32_t* p = a.ghist + (size_t)k * kMaxRanks * 2048 + i;
+        v += *p;
+        *p = 0;
+    }
+    a.hist_out[i] = v;
+    if (blockIdx.x == 0 && threadIdx.x < 2) {
+        unsigned long long c = 0;
+        for (int k = 0; k < kCountSlots; ++k) {
+            c += a.counts[k * 16 + threadIdx.x];
+            a.counts[k * 16 + threadIdx.x] = 0;
+        }
+        a.counts_out[threadIdx.x] = c;
     }
 }
 
@@ -174,18 +263,22 @@ __global__ __launch_bounds__(256) void k_affine_f32(AffineArgs a) {
 
 int launch_frame_stats(const FrameStatsArgs& a, int nimg, hipStream_t s) {
     if (a.H <= 0 || a.W <= 0 || nimg <= 0) return 0;
-    dim3 grid((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, nimg);
+    const int tiles_x = (a.W + kTile - 1) / kTile;
+    dim3 grid((tiles_x + 3) / 4, (a.H + kTile - 1) / kTile, nimg);
+    const size_t nh = (size_t)nimg * 256;
     hipLaunchKernelGGL(k_frame_stats, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_fold_u32, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, s, a.hist_copies,
+                       kHistCopies, nh, (int)nh, a.hist);
     return (int)hipGetLastError();
 }
 
 int launch_select_hist(const SelectArgs& a, hipStream_t s) {
-    if (a.n == 0) return 0;
-    // ~16 elements per thread: each block zeroes and merges a 2048-bin histogram per rank
-    int blocks = (int)((a.n + 4095) / 4096);
+    // 16 elements per thread: each block zeroes and merges a 2048-bin histogram per rank
+    int blocks = (int)((a.n + 256 * 4 * kSelVec - 1) / (256 * 4 * kSelVec));
     if (blocks > 1024) blocks = 1024;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_select_hist, dim3(blocks), dim3(256), 0, s, a);
+    if (a.n > 0) hipLaunchKernelGGL(k_select_hist, dim3(blocks), dim3(256), 0, s, a);
+    // the fold runs for n = 0 too: it writes the (empty) result
+    hipLaunchKernelGGL(k_select_fold, dim3(a.nranks * 8), dim3(256), 0, s, a);
     return (int)hipGetLastError();
 }
 

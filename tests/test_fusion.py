@@ -172,7 +172,7 @@ def test_gpu_detect_camera_occlusion(kinds):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 2, 3, 1000, 1 << 20])
+@pytest.mark.parametrize("n", [1, 2, 3, 1000, 1 << 20, 1000003])
 def test_gpu_select_ranks_exact(engine, n):
     rng = np.random.default_rng(n)
     x = (rng.normal(size=n) * 1e3).astype(np.float32)
@@ -190,6 +190,30 @@ def test_gpu_select_ranks_exact(engine, n):
     if sm.size:
         np.testing.assert_array_equal(engine.select_ranks(d, n, [0, sm.size - 1], 2, dc, 0.7),
                                       sm[[0, sm.size - 1]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("off", [1, 2, 3])
+def test_gpu_select_unaligned_and_nan(engine, off):
+    """Arrays not 16-byte aligned (the scalar path) and NaN counting, every mask mode."""
+    n = 300001
+    rng = np.random.default_rng(off)
+    x = (rng.random(n) * 100 - 10).astype(np.float32)
+    x[rng.integers(0, n, 50)] = np.nan
+    conf = rng.random(n).astype(np.float32)
+    d = engine.upload("t_x", x)
+    dc = engine.upload("t_c", conf)
+    xs, cs = x[off:], conf[off:]
+    m = n - off
+    assert engine.select_count(d + 4 * off, m) == ((~np.isnan(xs)).sum(), np.isnan(xs).sum())
+    assert engine.select_count(d + 4 * off, m, fusion.SEL_POSITIVE) == ((xs > 0).sum(), 0)
+    sel = cs > np.float32(0.7)
+    assert engine.select_count(d + 4 * off, m, 2, dc + 4 * off, 0.7) == \
+        ((sel & ~np.isnan(xs)).sum(), (sel & np.isnan(xs)).sum())
+    pos = np.sort(xs[xs > 0])
+    np.testing.assert_array_equal(engine.select_ranks(d + 4 * off, m, [0, pos.size // 2, pos.size - 1],
+                                                      fusion.SEL_POSITIVE),
+                                  pos[[0, pos.size // 2, pos.size - 1]])
 
 
 @pytest.mark.gpu

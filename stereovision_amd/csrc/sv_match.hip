@@ -84,6 +84,10 @@ template <int COST, int ND> struct PackCfg {
 };
 template <int NW> struct Pk { uint32_t w[NW]; };
 
+// 4-row kind with r <= 5 (win <= 11): argmin keys are (cost << 16) | idx, maintained with
+// v_sad_hi_u8 (cost max 30855: keys incl. the padding offset stay below 2^32).
+__host__ __device__ constexpr bool hi_keys(int cost, int r) { return cost == COST_SAD4 && r <= 5; }
+
 // Pointer to a column-pack slot (main array + the split common-word array).
 template <int COST, int ND, typename X, typename C> struct PackPtrT {
     X* x;
@@ -381,6 +385,7 @@ __device__ __forceinline__ void match_chunk(
     constexpr int NW = PackCfg<COST, ND>::NW;
     constexpr int ROWS = PackCfg<COST, ND>::ROWS;
     constexpr bool RUN = COST != COST_HOG;            // running horizontal window
+    constexpr bool HI = hi_keys(COST, ND);            // dbits == 16 (plan_match)
 #pragma unroll
     for (int u = 0; u < DPL; ++u) {
         // ring slot u receives this step's entering right column; its previous content
@@ -396,6 +401,26 @@ __device__ __forceinline__ void match_chunk(
 #pragma unroll
         for (int k = 0; k < DPL; ++k) {
             const int sk = (u - k + DPL) % DPL;
+            if constexpr (HI) {
+                // keys (cost << 16) | idx updated by v_sad_hi_u8, which adds (SAD << 16):
+                // m = (old row-q SAD + old common - new common) << 16, then
+                // h = h + (new row-q SAD << 16) - m: 2 v_sad + 1 v_sub per cell, 1 v_sub
+                // per 4 cells (instead of 2 v_sad + v_sub + v_mad per cell)
+                constexpr int NC = PackCfg<COST, ND>::NC;
+                uint32_t cn = 0u, co = 0u;
+#pragma unroll
+                for (int i = 0; i < NC; ++i) {
+                    cn = __builtin_amdgcn_sad_hi_u8(L.w[i], rn[sk].w[i], cn);
+                    co = __builtin_amdgcn_sad_hi_u8(LO.w[i], ro[sk].w[i], co);
+                }
+                const uint32_t nch = co - cn;
+#pragma unroll
+                for (int q = 0; q < ROWS; ++q) {
+                    const uint32_t m = __builtin_amdgcn_sad_hi_u8(LO.w[NC + q], ro[sk].w[NC + q], nch);
+                    h[k][q] = __builtin_amdgcn_sad_hi_u8(L.w[NC + q], rn[sk].w[NC + q], h[k][q]) - m;
+                }
+                continue;
+            }
             uint32_t vn[ROWS];
             ccol<COST, ND, NW>(L, rn[sk], vn);
             if constexpr (RUN) {
@@ -742,6 +767,7 @@ int plan_match(int num_disp, int win, int cost, MatchPlan* plan) {
     int n = plan->dpl * plan->lpg - 1, bits = 0;
     while (n > 0) { ++bits; n >>= 1; }
     plan->dbits = bits < 1 ? 1 : bits;
+    if (hi_keys(kind, win / 2)) plan->dbits = 16;
     const uint64_t cmax = max_cost(win, cost);
     if ((cmax << plan->dbits) >= (1ull << 32)) return -34;  // ERANGE: key would overflow
     // padding disparities (idx >= D) carry keys above (cmax + 1) << dbits

@@ -194,7 +194,7 @@ SgbmParams sgbm_reference_params(int win) {
 // Enqueue the whole SGBM-3WAY pipeline for one frame (buffers grown in the context).
 int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, int pitch, int min_disp,
                  int num_disp, int win, SgbmParams p, int16_t* out, int opitch, hipStream_t s) {
-    if (sv::sgbm_dpl(num_disp) < 0) return fail(SV_EINVAL, "num_disp must be in [1, 512]");
+    if (sv::sgbm_dp(num_disp) < 0) return fail(SV_EINVAL, "num_disp must be in [1, 512]");
     if (W > 16384) return fail(SV_EINVAL, "SGBM: width beyond 16384");
     if (p.P1 < 0 || p.P2 < 0) return fail(SV_EINVAL, "negative P1/P2");
     if (p.P2 <= p.P1) p.P2 = p.P1 + 1;                       // OpenCV: P2 = max(P2, P1 + 1)
@@ -223,8 +223,7 @@ int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, in
     const long long cmax = (long long)(2 * p.cap + 63) * win * win;   // max window cost
     if (cmax > 65535) return fail(SV_EINVAL, "SGBM: window cost beyond 16 bits (lower preFilterCap/blockSize)");
     a.l32 = (cmax > 32767 || p.P2 > 32768) ? 1 : 0;
-    const int dpl = sv::sgbm_dpl(num_disp);
-    a.Dp = (num_disp + dpl - 1) / dpl * dpl;
+    a.Dp = sv::sgbm_dp(num_disp);
     const size_t vol = (size_t)H * a.Wb * a.Dp;
     SV_HIP(c->sg_hsum.ensure(vol * 2 + 256));
     SV_HIP(c->sg_c.ensure(vol * 2 + 256));

@@ -121,7 +121,7 @@ struct SgbmArgs {
     const uint8_t* R;
     int H, W, pitch;
     int minD, D, r;            // r = blockSize / 2
-    int Dp;                    // per-pixel stride of the volumes: D rounded up to sgbm_dpl(D)
+    int Dp;                    // per-pixel stride of the volumes: sgbm_dp(D)
     int X0, Wb;                // band [X0, X0 + Wb)
     int cap, P1, P2, uniq, disp12;
     uint16_t* hsum;            // [H][Wb][D] window-column sums of the pixel cost
@@ -135,7 +135,7 @@ struct SgbmArgs {
     int opitch;
     void* dummy;               // >= 64 x 128 bytes: store target of the padding lanes
 };
-int sgbm_dpl(int D);                 // disparities per lane of the path kernels, -1 if D > 512
+int sgbm_dp(int D);                  // per-pixel volume stride for D disparities, -1 if D > 512
 size_t sgbm_hsum_lds(int W);
 int launch_sgbm(const SgbmArgs& a, hipStream_t s);
 int launch_speckles(int16_t* img, int H, int W, int pitch, int newv, int maxsize, int maxdiff, int* parent,

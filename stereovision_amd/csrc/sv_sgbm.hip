@@ -137,6 +137,118 @@ __global__ __launch_bounds__(256) void k_sgbm_hsum(SgbmArgs a) {
     }
 }
 
+// Tiled form of the same sums (r <= kHsumMaxR): one workgroup per (row, 256-column slab of
+// the band).  Per image column a 16-byte record {value, BT lo, BT hi} with the two channels
+// (x-Sobel, raw) as the u16 halves of each dword, so the pixel cost of a cell is 7 packed
+// u16 ops (saturating subtracts give the max(0, .) of Birchfield-Tomasi for free) + 2; the
+// window's leaving column comes from a register ring (one pixel cost per cell, not two).
+constexpr int kHX = 256;          // band columns per workgroup
+constexpr int kHsumMaxR = 8;
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us2, v); }
+__device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// {value, lo, hi} of image column x of row y, both channels (see k_sgbm_hsum)
+__device__ __forceinline__ uint4 bt_record(const SgbmArgs& a, const uint8_t* img, int y, int x) {
+    const int W = a.W;
+    const int ym = y > 0 ? y - 1 : y, yp = y < a.H - 1 ? y + 1 : y;
+    const uint8_t* r0 = img + (size_t)y * a.pitch;
+    const uint8_t* rm = img + (size_t)ym * a.pitch;
+    const uint8_t* rp = img + (size_t)yp * a.pitch;
+    int pf[3], raw[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {   // columns x-1, x, x+1
+        const int xx = x - 1 + k;
+        int p = a.cap, w = a.cap;
+        if (xx > 0 && xx < W - 1) {
+            const int s = (r0[xx + 1] - r0[xx - 1]) * 2 + rm[xx + 1] - rm[xx - 1] + rp[xx + 1] - rp[xx - 1];
+            p = min(max(s, -a.cap), a.cap) + a.cap;
+            w = r0[xx];
+        }
+        pf[k] = p;
+        raw[k] = w;
+    }
+    auto bt = [&](const int (&v)[3], int& lo, int& hi) {
+        const int c = v[1];
+        const int l = x > 0 ? (c + v[0]) >> 1 : c;
+        const int r = x < W - 1 ? (c + v[2]) >> 1 : c;
+        lo = min(min(l, r), c);
+        hi = max(max(l, r), c);
+    };
+    int plo, phi, rlo, rhi;
+    bt(pf, plo, phi);
+    bt(raw, rlo, rhi);
+    return make_uint4((uint32_t)pf[1] | ((uint32_t)raw[1] << 16), (uint32_t)plo | ((uint32_t)rlo << 16),
+                      (uint32_t)phi | ((uint32_t)rhi << 16), 0u);
+}
+
+__device__ __forceinline__ int bt_cost(const uint4 l, const uint4 r) {
+    const us2 U = as_us2(l.x), U0 = as_us2(l.y), U1 = as_us2(l.z);
+    const us2 V = as_us2(r.x), V0 = as_us2(r.y), V1 = as_us2(r.z);
+    const us2 c0 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(U, V1), __builtin_elementwise_sub_sat(V0, U));
+    const us2 c1 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(V, U1), __builtin_elementwise_sub_sat(U0, V));
+    const uint32_t m = as_u32(__builtin_elementwise_min(c0, c1));
+    return (int)(m & 0xFFFFu) + (int)(m >> 18);
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void k_sgbm_hsum_tiled(SgbmArgs a) {
+    extern __shared__ uint4 rec[];
+    constexpr int W2 = 2 * R + 1;
+    const int y = blockIdx.y, t = threadIdx.x;
+    const int D = a.D, Wb = a.Wb;
+    const int xb0 = blockIdx.x * kHX, xb1 = min(xb0 + kHX, Wb);   // output band columns
+    // left records: band columns xb0-R .. xb1+R-1 (clamped to the band); right records:
+    // image columns xr0 .. xr1 that those columns reach at d = D-1 .. 0
+    const int nL = xb1 - xb0 + 2 * R;
+    const int xr0 = a.X0 + max(xb0 - R, 0) - a.minD - (D - 1);
+    const int xr1 = a.X0 + min(xb1 + R - 1, Wb - 1) - a.minD;
+    const int nR = xr1 - xr0 + 1;
+    uint4* recL = rec;
+    uint4* recR = rec + nL;
+    for (int i = t; i < nL + nR; i += 256) {
+        if (i < nL) recL[i] = bt_record(a, a.L, y, a.X0 + min(max(xb0 - R + i, 0), Wb - 1));
+        else recR[i - nL] = bt_record(a, a.R, y, xr0 + (i - nL));
+    }
+    __syncthreads();
+    const int nc = max(1, kHX / D);                  // column chunks per disparity
+    const int clen = (kHX + nc - 1) / nc;
+    for (int item = t; item < D * nc; item += 256) {
+        const int d = item % D, c = item / D;
+        const int xs = xb0 + c * clen, xe = min(xb1, xs + clen);
+        if (xs >= xe) continue;
+        // cell (xb, d): left record xb - (xb0 - R), right record x(xb) - minD - d - xr0
+        const int roff = a.X0 - a.minD - d - xr0;
+        auto pc = [&](int xb) {
+            const int xc = min(max(xb, 0), Wb - 1);
+            return bt_cost(recL[xb - xb0 + R], recR[xc + roff]);
+        };
+        uint16_t* out = a.hsum + ((size_t)y * Wb + xs) * a.Dp + d;
+        int ring[W2];
+        int hs = 0;
+#pragma unroll
+        for (int k = 0; k < W2; ++k) {
+            ring[k] = pc(xs - R + k);
+            hs += ring[k];
+        }
+        out[0] = (uint16_t)hs;
+        // step j (output column xs + 1 + j) drops entry j (ring slot j mod W2)
+        for (int j0 = 0; xs + 1 + j0 < xe; j0 += W2) {
+#pragma unroll
+            for (int k = 0; k < W2; ++k) {
+                const int x = xs + 1 + j0 + k;
+                if (x < xe) {
+                    const int pn = pc(x + R);
+                    hs += pn - ring[k];
+                    ring[k] = pn;
+                    out[(size_t)(1 + j0 + k) * a.Dp] = (uint16_t)hs;
+                }
+            }
+        }
+    }
+}
+
 // window rows: C(y) = sum_{j=-r..r} hsum(clamp(y + j))
 __global__ __launch_bounds__(256) void k_sgbm_vsum(SgbmArgs a) {
     const size_t plane = (size_t)a.Wb * a.Dp;
@@ -182,13 +294,42 @@ struct alignas(pack_align(sizeof(T) * DPL)) Pack {
     T v[DPL];
 };
 
+// Lines of LPC lanes (16: one DPP row; 32: two rows, joined through ds_swizzle xor 16).
+__device__ __forceinline__ int swz16(int v) { return __builtin_amdgcn_ds_swizzle(v, 0x401F); }
+template <int LPC> __device__ __forceinline__ int line_min(int v) {
+    v = row_min(v);
+    if constexpr (LPC == 32) v = min(v, swz16(v));
+    return v;
+}
+template <int LPC> __device__ __forceinline__ uint32_t line_min_u(uint32_t v) {
+    v = row_min_u(v);
+    if constexpr (LPC == 32) v = min(v, (uint32_t)swz16((int)v));
+    return v;
+}
+template <int LPC> __device__ __forceinline__ int line_max(int v) {
+    v = row_max(v);
+    if constexpr (LPC == 32) v = max(v, swz16(v));
+    return v;
+}
+// value of lane j-1 / j+1 of the line (`edge` at the line's ends)
+template <int LPC> __device__ __forceinline__ int from_left(int v, int edge, int j) {
+    if constexpr (LPC == 16) return dpp_shr1(v, edge);
+    const int t = __builtin_amdgcn_update_dpp(edge, v, 0x138, 0xF, 0xF, false);   // wave_shr:1
+    return j == 0 ? edge : t;
+}
+template <int LPC> __device__ __forceinline__ int from_right(int v, int edge, int j) {
+    if constexpr (LPC == 16) return dpp_shl1(v, edge);
+    const int t = __builtin_amdgcn_update_dpp(edge, v, 0x130, 0xF, 0xF, false);   // wave_shl:1
+    return j == LPC - 1 ? edge : t;
+}
+
 // One SGBM step for the DPL disparities of a lane: OpenCV's
 // L = C + min(prev[d], prev[d-1] + P1, prev[d+1] + P1, minprev + P2) - (minprev + P2).
-template <int DPL>
+template <int DPL, int LPC>
 __device__ __forceinline__ void path_step(int (&prev)[DPL], const int (&c)[DPL], int mn, int P1, int P2,
-                                          int dbase, int D) {
-    const int lo_in = dpp_shr1(prev[DPL - 1], kInf);
-    const int hi_in = dpp_shl1(prev[0], kInf);
+                                          int dbase, int D, int j) {
+    const int lo_in = from_left<LPC>(prev[DPL - 1], kInf, j);
+    const int hi_in = from_right<LPC>(prev[0], kInf, j);
     int nxt[DPL];
     const int mp = mn + P2;
 #pragma unroll
@@ -210,12 +351,13 @@ __device__ __forceinline__ int lane_min(const int (&v)[DPL]) {
     return m;
 }
 
-// Horizontal paths: 4 rows per wave; blockIdx.y = 0: left->right into Llr, 1: right->left
-// into Lrl.
-template <int DPL, typename LT, int PF>
+// Horizontal paths: 64/LPC rows per wave; blockIdx.y = 0: left->right into Llr, 1:
+// right->left into Lrl.
+template <int DPL, int LPC, typename LT, int PF>
 __global__ __launch_bounds__(64) void k_sgbm_hpath(SgbmArgs a) {
-    const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
-    const int y = blockIdx.x * 4 + g, dir = blockIdx.y;
+    constexpr int NL = 64 / LPC;
+    const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
+    const int y = blockIdx.x * NL + g, dir = blockIdx.y;
     const int D = a.D, Wb = a.Wb, Dp = a.Dp, dbase = j * DPL;
     // rows past H and lanes past D re-read valid cells and store into a private dummy
     // slot: no load or store sits under a branch
@@ -239,8 +381,8 @@ __global__ __launch_bounds__(64) void k_sgbm_hpath(SgbmArgs a) {
         int c[DPL];
 #pragma unroll
         for (int k = 0; k < DPL; ++k) c[k] = (int)cp.v[k];
-        path_step<DPL>(prev, c, mn, a.P1, a.P2, dbase, D);
-        mn = row_min(lane_min<DPL>(prev));
+        path_step<DPL, LPC>(prev, c, mn, a.P1, a.P2, dbase, D, j);
+        mn = line_min<LPC>(lane_min<DPL>(prev));
         LP o;
 #pragma unroll
         for (int k = 0; k < DPL; ++k) o.v[k] = (LT)prev[k];
@@ -268,10 +410,11 @@ struct BandOut {      // one 8-byte record per band pixel
 // Top->bottom path + winner-take-all: 4 band columns per wave walking down the rows.  The
 // argmin / uniqueness / sub-pixel work of a row does not feed the next row, so it overlaps
 // the loop-carried path chain.
-template <int DPL, typename LT, int PF>
+template <int DPL, int LPC, typename LT, int PF>
 __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
-    const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
-    const int xb = blockIdx.x * 4 + g;
+    constexpr int NL = 64 / LPC;
+    const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
+    const int xb = blockIdx.x * NL + g;
     const int D = a.D, Wb = a.Wb, dbase = j * DPL;
     const bool colok = xb < Wb;
     const size_t plane = (size_t)Wb * a.Dp;
@@ -305,15 +448,15 @@ __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
             c[k] = (int)cp.v[k];
             s[k] = (int)lp.v[k] + (int)rp.v[k];
         }
-        path_step<DPL>(prev, c, mn, a.P1, a.P2, dbase, D);
-        mn = row_min(lane_min<DPL>(prev));
+        path_step<DPL, LPC>(prev, c, mn, a.P1, a.P2, dbase, D, j);
+        mn = line_min<LPC>(lane_min<DPL>(prev));
         uint32_t key = 0xFFFFFFFFu;
 #pragma unroll
         for (int k = 0; k < DPL; ++k) {
             s[k] += prev[k];
             if (dbase + k < D) key = min(key, ((uint32_t)(s[k] + (1 << 20)) << 9) | (uint32_t)(dbase + k));
         }
-        key = row_min_u(key);
+        key = line_min_u<LPC>(key);
         const int b = (int)(key & 511u);
         const int minS = (int)(key >> 9) - (1 << 20);
         int viol = 0;
@@ -322,9 +465,9 @@ __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
             const int d = dbase + k;
             viol |= (d < D) & (s[k] * u100 < minS * 100) & (abs(d - b) > 1);
         }
-        viol = row_max(viol);
-        // S[b-1], S[b+1] from the lane that owns b, broadcast within the row
-        const int sl = dpp_shr1(s[DPL - 1], 0), sr = dpp_shl1(s[0], 0);
+        viol = line_max<LPC>(viol);
+        // S[b-1], S[b+1] from the lane that owns b, broadcast within the line
+        const int sl = from_left<LPC>(s[DPL - 1], 0, j), sr = from_right<LPC>(s[0], 0, j);
         const int kb = b - dbase;
         const bool own = kb >= 0 && kb < DPL;
         int sm = sl, sp = sr;
@@ -333,8 +476,8 @@ __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
             if (k == kb - 1) sm = s[k];
             if (k == kb + 1) sp = s[k];
         }
-        sm = row_max(own ? sm : kNegInf);
-        sp = row_max(own ? sp : kNegInf);
+        sm = line_max<LPC>(own ? sm : kNegInf);
+        sp = line_max<LPC>(own ? sp : kNegInf);
         int d16 = b * 16;
         if (b > 0 && b < D - 1) {
             const int denom2 = max(sm + sp - 2 * minS, 1);
@@ -530,32 +673,72 @@ __global__ __launch_bounds__(256) void k_cc_apply(int16_t* img, int H, int W, in
     if (size[uf_find(parent, i)] <= maxsize) img[(size_t)(i / W) * pitch + i % W] = (int16_t)newv;
 }
 
+// Line plans: (lanes per line, disparities per lane).
+//  * horizontal paths: 16-lane lines.  Their cost is the loop-carried chain of W steps
+//    (path minimum -> next step); a 32-lane line adds a cross-row exchange to that chain
+//    and measured slower despite twice the waves.
+//  * vertical path + WTA: 32-lane lines for D > 32.  The per-row argmin / uniqueness /
+//    sub-pixel work is off the chain and issue-bound: 32-lane lines spread it over twice
+//    the waves (448 -> 896 at 1080p D=128: 872 -> 639 us).
+struct PathPlan {
+    int lpc, dpl;
+};
+PathPlan hpath_plan(int D) {
+    const int need = (D + 15) / 16;
+    const int opts[] = {1, 2, 4, 8, 12, 16, 20, 24, 32};
+    for (int o : opts)
+        if (o >= need) return {16, o};
+    return {0, -1};
+}
+PathPlan vpath_plan(int D) {
+    if (D <= 32) return hpath_plan(D);
+    const int need = (D + 31) / 32;
+    const int opts[] = {2, 4, 6, 8, 10, 12, 16};
+    for (int o : opts)
+        if (o >= need) return {32, o};
+    return {0, -1};
+}
+
 template <typename LT>
-int launch_paths_t(const SgbmArgs& a, int dpl, hipStream_t s) {
-    dim3 gh((a.H + 3) / 4, 2), gv((a.Wb + 3) / 4);
-#define SV_SGBM_DPL(N, PFH, PFV)                                                  \
-    case N:                                                                       \
-        hipLaunchKernelGGL((k_sgbm_hpath<N, LT, PFH>), gh, dim3(64), 0, s, a);   \
-        hipLaunchKernelGGL((k_sgbm_vpath<N, LT, PFV>), gv, dim3(64), 0, s, a);   \
-        break;
-    switch (dpl) {
-        SV_SGBM_DPL(1, 24, 16) SV_SGBM_DPL(2, 24, 16) SV_SGBM_DPL(4, 16, 12) SV_SGBM_DPL(8, 16, 8)
-        SV_SGBM_DPL(12, 10, 4) SV_SGBM_DPL(16, 8, 3) SV_SGBM_DPL(20, 6, 2) SV_SGBM_DPL(24, 6, 2)
-        SV_SGBM_DPL(32, 4, 1)
-        default: return (int)hipErrorInvalidValue;
+int launch_paths_t(const SgbmArgs& a, hipStream_t s) {
+    const PathPlan ph = hpath_plan(a.D), pv = vpath_plan(a.D);
+    const dim3 gh((a.H + 3) / 4, 2), gv((a.Wb + 64 / pv.lpc - 1) / (64 / pv.lpc));
+    bool h = false, v = false;
+#define SV_HPATH(N, PF)                                                              \
+    if (ph.dpl == N) {                                                               \
+        hipLaunchKernelGGL((k_sgbm_hpath<N, 16, LT, PF>), gh, dim3(64), 0, s, a);   \
+        h = true;                                                                    \
     }
-#undef SV_SGBM_DPL
+#define SV_VPATH(L, N, PF)                                                           \
+    if (!v && pv.lpc == L && pv.dpl == N) {                                          \
+        hipLaunchKernelGGL((k_sgbm_vpath<N, L, LT, PF>), gv, dim3(64), 0, s, a);    \
+        v = true;                                                                    \
+    }
+    SV_HPATH(1, 24) SV_HPATH(2, 24) SV_HPATH(4, 16) SV_HPATH(8, 16) SV_HPATH(12, 10) SV_HPATH(16, 8)
+    SV_HPATH(20, 6) SV_HPATH(24, 6) SV_HPATH(32, 4)
+    if (!h) return (int)hipErrorInvalidValue;
+    SV_VPATH(16, 1, 16) SV_VPATH(16, 2, 16)
+    SV_VPATH(32, 2, 16) SV_VPATH(32, 4, 12) SV_VPATH(32, 6, 10) SV_VPATH(32, 8, 8) SV_VPATH(32, 10, 6)
+    SV_VPATH(32, 12, 4) SV_VPATH(32, 16, 3)
+#undef SV_HPATH
+#undef SV_VPATH
+    if (!v) return (int)hipErrorInvalidValue;
     return (int)hipGetLastError();
 }
 
 }  // namespace
 
-int sgbm_dpl(int D) {
-    const int need = (D + 15) / 16;
-    const int opts[] = {1, 2, 4, 8, 12, 16, 20, 24, 32};
-    for (int o : opts)
-        if (o >= need) return o;
-    return -1;
+int sgbm_dp(int D) {
+    if (D < 1 || D > 512) return -1;
+    int x = hpath_plan(D).dpl, y = vpath_plan(D).dpl;   // Dp: a multiple of both lane widths
+    int g = x, r = y;
+    while (r) {
+        const int t = g % r;
+        g = r;
+        r = t;
+    }
+    const int l = x / g * y;
+    return (D + l - 1) / l * l;
 }
 
 size_t sgbm_hsum_lds(int W) { return (size_t)12 * W; }
@@ -563,11 +746,21 @@ size_t sgbm_hsum_lds(int W) { return (size_t)12 * W; }
 int launch_sgbm(const SgbmArgs& a, hipStream_t s) {
     if (a.H <= 0 || a.W <= 0) return 0;
     if (a.Wb > 0) {
-        hipLaunchKernelGGL(k_sgbm_hsum, dim3(a.H), dim3(256), sgbm_hsum_lds(a.W), s, a);
+        if (a.r <= kHsumMaxR) {
+            const dim3 grid((unsigned)((a.Wb + kHX - 1) / kHX), (unsigned)a.H);
+            const size_t lds = (size_t)(2 * kHX + 4 * a.r + a.D - 1) * sizeof(uint4);
+            switch (a.r) {
+#define SV_HSUM_R(R) case R: hipLaunchKernelGGL(k_sgbm_hsum_tiled<R>, grid, dim3(256), lds, s, a); break;
+                SV_HSUM_R(0) SV_HSUM_R(1) SV_HSUM_R(2) SV_HSUM_R(3) SV_HSUM_R(4) SV_HSUM_R(5) SV_HSUM_R(6)
+                SV_HSUM_R(7) SV_HSUM_R(8)
+#undef SV_HSUM_R
+            }
+        } else {
+            hipLaunchKernelGGL(k_sgbm_hsum, dim3(a.H), dim3(256), sgbm_hsum_lds(a.W), s, a);
+        }
         const size_t plane = (size_t)a.Wb * a.Dp;
         hipLaunchKernelGGL(k_sgbm_vsum, dim3((unsigned)((plane + 255) / 256)), dim3(256), 0, s, a);
-        const int dpl = sgbm_dpl(a.D);
-        const int e = a.l32 ? launch_paths_t<int32_t>(a, dpl, s) : launch_paths_t<int16_t>(a, dpl, s);
+        const int e = a.l32 ? launch_paths_t<int32_t>(a, s) : launch_paths_t<int16_t>(a, s);
         if (e) return e;
     }
     hipLaunchKernelGGL(k_sgbm_lrcheck, dim3(a.H), dim3(256), (size_t)a.W * 8, s, a);

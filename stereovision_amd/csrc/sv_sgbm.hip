@@ -33,7 +33,6 @@ namespace sv {
 namespace {
 
 constexpr int kInf = 0x3FFFFFFF;
-constexpr int kNegInf = -0x7FFFFFFF - 1;
 
 __device__ __forceinline__ int dpp_shr1(int v, int old) {   // lane j <- lane j-1 (row of 16)
     return __builtin_amdgcn_update_dpp(old, v, 0x111, 0xF, 0xF, false);
@@ -441,47 +440,50 @@ __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
     const int u100 = 100 - a.uniq;
     BandOut* bo = colok ? reinterpret_cast<BandOut*>(a.band) + xb : reinterpret_cast<BandOut*>(a.dummy) + lane;
     const int ystride = colok ? Wb : 0;
+    // S of the line, so the lanes can read S[b-1], S[b+1] (LDS ops of one wave are ordered)
+    __shared__ int lds_s[64 * DPL];
+    int* my_s = lds_s + lane * DPL;
+    const int* line_s = lds_s + g * LPC * DPL;
+    // argmin keys ((S + 2^20) << 9) | d = (S << 9) + dk[k]
+    uint32_t dk[DPL];
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) dk[k] = (uint32_t)(dbase + k) + (1u << 29);
     auto row = [&](int y, const CP& cp, const LP& lp, const LP& rp) {
         int c[DPL], s[DPL];
 #pragma unroll
-        for (int k = 0; k < DPL; ++k) {
-            c[k] = (int)cp.v[k];
-            s[k] = (int)lp.v[k] + (int)rp.v[k];
-        }
+        for (int k = 0; k < DPL; ++k) c[k] = (int)cp.v[k];
         path_step<DPL, LPC>(prev, c, mn, a.P1, a.P2, dbase, D, j);
         mn = line_min<LPC>(lane_min<DPL>(prev));
         uint32_t key = 0xFFFFFFFFu;
 #pragma unroll
         for (int k = 0; k < DPL; ++k) {
-            s[k] += prev[k];
-            if (dbase + k < D) key = min(key, ((uint32_t)(s[k] + (1 << 20)) << 9) | (uint32_t)(dbase + k));
+            s[k] = (int)lp.v[k] + (int)rp.v[k] + prev[k];
+            my_s[k] = s[k];
+            if (dbase + k < D) key = min(key, ((uint32_t)s[k] << 9) + dk[k]);
         }
         key = line_min_u<LPC>(key);
         const int b = (int)(key & 511u);
         const int minS = (int)(key >> 9) - (1 << 20);
-        int viol = 0;
+        // uniqueness: the smallest S with |d - b| > 1 against minS (|S| < 2^23: 24-bit products)
+        const int e = dbase - b + 1;
+        int m2 = 0x7FFFFFFF;
 #pragma unroll
-        for (int k = 0; k < DPL; ++k) {
-            const int d = dbase + k;
-            viol |= (d < D) & (s[k] * u100 < minS * 100) & (abs(d - b) > 1);
-        }
-        viol = line_max<LPC>(viol);
-        // S[b-1], S[b+1] from the lane that owns b, broadcast within the line
-        const int sl = from_left<LPC>(s[DPL - 1], 0, j), sr = from_right<LPC>(s[0], 0, j);
-        const int kb = b - dbase;
-        const bool own = kb >= 0 && kb < DPL;
-        int sm = sl, sp = sr;
-#pragma unroll
-        for (int k = 0; k < DPL; ++k) {
-            if (k == kb - 1) sm = s[k];
-            if (k == kb + 1) sp = s[k];
-        }
-        sm = line_max<LPC>(own ? sm : kNegInf);
-        sp = line_max<LPC>(own ? sp : kNegInf);
+        for (int k = 0; k < DPL; ++k)
+            if (dbase + k < D && (unsigned)(e + k) > 2u) m2 = min(m2, s[k]);
+        m2 = line_min<LPC>(m2);
+        const bool viol = m2 != 0x7FFFFFFF && __mul24(m2, u100) < __mul24(minS, 100);
         int d16 = b * 16;
         if (b > 0 && b < D - 1) {
+            const int sm = line_s[b - 1], sp = line_s[b + 1];
+            // sub-pixel parabola; |num| <= 17 * den / 2 (sm, sp >= minS): a float quotient
+            // and one correction give C's truncating division
             const int denom2 = max(sm + sp - 2 * minS, 1);
-            d16 += ((sm - sp) * 16 + denom2) / (denom2 * 2);
+            const int num = (sm - sp) * 16 + denom2, den = denom2 * 2;
+            const int an = abs(num);
+            int q = (int)((float)an * __builtin_amdgcn_rcpf((float)den));
+            const int r = an - (int)__umul24((unsigned)q, (unsigned)den);
+            q += (r >= den) - (r < 0);
+            d16 += num < 0 ? -q : q;
         }
         BandOut o;
         o.disp = (int16_t)(viol ? (a.minD - 1) * 16 : d16 + a.minD * 16);

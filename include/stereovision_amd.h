@@ -257,6 +257,14 @@ int sv_sgbm_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int 
                 int pre_filter_cap, int uniqueness_ratio, int speckle_window_size,
                 int speckle_range, int16_t* d_disp16, int out_pitch, void* stream);
 
+/* cv2.filterSpeckles(img, newVal, maxSpeckleSize, maxDiff) on an int16 map, in place: the
+ * speckle stage of StereoSGBM (OpenCV calib3d, called from stereo.compute at
+ * depth_map.py:909).  4-connected regions whose neighbours differ by <= max_diff and that
+ * hold <= max_speckle_size pixels are set to new_val; max_speckle_size <= 0 is a no-op. */
+int sv_filter_speckles(sv_ctx* ctx, int16_t* img, int H, int W, int new_val, int max_speckle_size, int max_diff);
+int sv_filter_speckles_dev(sv_ctx* ctx, int16_t* d_img, int H, int W, int pitch, int new_val,
+                           int max_speckle_size, int max_diff, void* stream);
+
 /* ---- reductions around the path ----------------------------
  * Image statistics of detect_camera_occlusion (fused_depth_map.py:131-301) for one image
  * or a pair (img1 nullable): per 48x48 block of compute_block_homogeneity

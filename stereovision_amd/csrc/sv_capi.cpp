@@ -192,6 +192,19 @@ SgbmParams sgbm_reference_params(int win) {
 }
 
 // Enqueue the whole SGBM-3WAY pipeline for one frame (buffers grown in the context).
+// cv2.filterSpeckles on an int16 device map (speckle stage of SGBM, sv_filter_speckles).
+int enqueue_speckles(sv_ctx* c, int16_t* d_img, int H, int W, int pitch, int new_val, int max_speckle_size,
+                            int max_diff, hipStream_t s) {
+    if (max_speckle_size <= 0) return 0;
+    const size_t n = (size_t)H * W;
+    SV_HIP(c->cc_parent.ensure(n * 4));
+    SV_HIP(c->cc_size.ensure(n * 4));
+    SV_LAUNCH(c, SV_K_SPECKLE, s,
+              sv::launch_speckles(d_img, H, W, pitch, new_val, max_speckle_size, max_diff, c->cc_parent.as<int>(),
+                                  c->cc_size.as<int>(), s));
+    return 0;
+}
+
 int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, int pitch, int min_disp,
                  int num_disp, int win, SgbmParams p, int16_t* out, int opitch, hipStream_t s) {
     if (sv::sgbm_dp(num_disp) < 0) return fail(SV_EINVAL, "num_disp must be in [1, 512]");
@@ -239,15 +252,7 @@ int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, in
     a.out = out;
     a.opitch = opitch;
     SV_LAUNCH(c, SV_K_SGBM, s, sv::launch_sgbm(a, s));
-    if (p.speckle_win > 0) {
-        const size_t n = (size_t)H * W;
-        SV_HIP(c->cc_parent.ensure(n * 4));
-        SV_HIP(c->cc_size.ensure(n * 4));
-        SV_LAUNCH(c, SV_K_SPECKLE, s,
-                  sv::launch_speckles(out, H, W, opitch, (min_disp - 1) * 16, p.speckle_win, 16 * p.speckle_range,
-                                      c->cc_parent.as<int>(), c->cc_size.as<int>(), s));
-    }
-    return 0;
+    return enqueue_speckles(c, out, H, W, opitch, (min_disp - 1) * 16, p.speckle_win, 16 * p.speckle_range, s);
 }
 
 // Enqueue disparity for rows [row0,row1) of gray device images.
@@ -1358,6 +1363,28 @@ int sv_sgbm(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, 
                       block_size, p, c->d16.as<int16_t>(), W, c->stream);
     if (rc) return rc;
     Out o[] = {{disp16, c->d16.p, (size_t)H * W * sizeof(int16_t)}};
+    return collect(c, o, 1);
+}
+
+// cv2.filterSpeckles(img, newVal, maxSpeckleSize, maxDiff) on an int16 map, in place.
+int sv_filter_speckles_dev(sv_ctx* c, int16_t* d_img, int H, int W, int pitch, int new_val, int max_speckle_size,
+                           int max_diff, void* stream) {
+    SV_ENTER(c);
+    if (!d_img || H <= 0 || W <= 0 || pitch < W) return fail(SV_EINVAL, "bad speckle-filter arguments");
+    return enqueue_speckles(c, d_img, H, W, pitch, new_val, max_speckle_size, max_diff, pick(c, stream));
+}
+
+int sv_filter_speckles(sv_ctx* c, int16_t* img, int H, int W, int new_val, int max_speckle_size, int max_diff) {
+    SV_ENTER(c);
+    if (!img || H <= 0 || W <= 0) return fail(SV_EINVAL, "bad speckle-filter arguments");
+    const size_t bytes = (size_t)H * W * sizeof(int16_t);
+    SV_HIP(c->d16.ensure(bytes));
+    SV_HIP(c->hin.ensure(bytes));
+    std::memcpy(c->hin.p, img, bytes);
+    SV_HIP(hipMemcpyAsync(c->d16.p, c->hin.p, bytes, hipMemcpyHostToDevice, c->stream));
+    const int rc = enqueue_speckles(c, c->d16.as<int16_t>(), H, W, W, new_val, max_speckle_size, max_diff, c->stream);
+    if (rc) return rc;
+    Out o[] = {{img, c->d16.p, bytes}};
     return collect(c, o, 1);
 }
 

@@ -584,11 +584,14 @@ __device__ __forceinline__ void uf_unite(int* p, int a, int b) {
 
 // Phase 1: union-find inside a 32x32 tile in LDS (no global atomics).  A component's
 // local root is its smallest row-major tile index, whose global index is therefore also the
-// smallest of its members: parent[i] <= i holds globally, as uf_unite() requires.
+// smallest of its members: parent[i] <= i holds globally, as uf_unite() requires.  The
+// local component sizes are counted in LDS and stored at the local roots (size[] is 0
+// everywhere else).
 constexpr int kCT = 32;
 __global__ __launch_bounds__(256) void k_cc_local(const int16_t* img, int H, int W, int pitch, int newv,
                                                   int maxdiff, int* parent, int* size) {
     __shared__ int lp[kCT * kCT];
+    __shared__ int lc[kCT * kCT];
     __shared__ int16_t lv[kCT * kCT];
     const int x0 = blockIdx.x * kCT, y0 = blockIdx.y * kCT, t = threadIdx.x;
     for (int l = t; l < kCT * kCT; l += 256) {
@@ -597,6 +600,7 @@ __global__ __launch_bounds__(256) void k_cc_local(const int16_t* img, int H, int
         const int v = in ? img[(size_t)y * pitch + x] : newv;
         lv[l] = (int16_t)v;
         lp[l] = v != newv ? l : -1;
+        lc[l] = 0;
     }
     __syncthreads();
     for (int l = t; l < kCT * kCT; l += 256) {
@@ -613,23 +617,33 @@ __global__ __launch_bounds__(256) void k_cc_local(const int16_t* img, int H, int
         }
     }
     __syncthreads();
-    for (int l = t; l < kCT * kCT; l += 256) {
+    int root[kCT * kCT / 256];
+#pragma unroll
+    for (int u = 0; u < kCT * kCT / 256; ++u) {
+        const int l = t + 256 * u;
+        root[u] = lp[l] < 0 ? -1 : uf_find(lp, l);
+        if (root[u] >= 0) atomicAdd(&lc[root[u]], 1);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kCT * kCT / 256; ++u) {
+        const int l = t + 256 * u;
         const int x = x0 + (l % kCT), y = y0 + l / kCT;
         if (x >= W || y >= H) continue;
         const size_t gi = (size_t)y * W + x;
-        size[gi] = 0;
-        if (lp[l] < 0) {
-            parent[gi] = -1;
-            continue;
-        }
-        const int r = uf_find(lp, l);
-        parent[gi] = (y0 + r / kCT) * W + x0 + (r % kCT);
+        const int r = root[u];
+        parent[gi] = r < 0 ? -1 : (y0 + r / kCT) * W + x0 + (r % kCT);
+        size[gi] = r == l ? lc[l] : 0;
     }
 }
 
-// Phase 2: the edges that cross tile borders, united in the global forest.
+// Phase 2: the edges that cross tile borders, united in the global forest.  An edge whose
+// two ends both already sit in a tree holding a local component larger than maxsize is
+// skipped: both ends end up in components that are not speckles whether or not they are
+// joined (parent[p] is always a local root of p's tree, whose size[] is a local size).
+// This drops the background's border edges, which otherwise all contend for one root.
 __global__ __launch_bounds__(256) void k_cc_border(const int16_t* img, int H, int W, int pitch, int newv,
-                                                   int maxdiff, int* parent) {
+                                                   int maxdiff, int maxsize, int* parent, const int* size) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= H * W) return;
     const int y = i / W, x = i % W;
@@ -638,34 +652,28 @@ __global__ __launch_bounds__(256) void k_cc_border(const int16_t* img, int H, in
     if (!right && !down) return;
     const int v = img[(size_t)y * pitch + x];
     if (v == newv) return;
+    auto big = [&](int p) { return size[__atomic_load_n(&parent[p], __ATOMIC_RELAXED)] > maxsize; };
+    const bool bi = big(i);
     if (right) {
         const int w = img[(size_t)y * pitch + x + 1];
-        if (w != newv && abs(w - v) <= maxdiff) uf_unite(parent, i, i + 1);
+        if (w != newv && abs(w - v) <= maxdiff && !(bi && big(i + 1))) uf_unite(parent, i, i + 1);
     }
     if (down) {
         const int w = img[(size_t)(y + 1) * pitch + x];
-        if (w != newv && abs(w - v) <= maxdiff) uf_unite(parent, i, i + W);
+        if (w != newv && abs(w - v) <= maxdiff && !(bi && big(i + W))) uf_unite(parent, i, i + W);
     }
 }
 
-// Component sizes, counted only as far as the filter needs: a pixel skips its increment
-// once its root's count already exceeds maxsize, so the decision size <= maxsize stays
-// exact while a large component stops hammering one counter after maxsize+1 atomics.
-// Lanes of a wave that share a root add their population in one atomic.
+// Component sizes: every local root adds its local size to its tree's root, unless that
+// count already exceeds maxsize (the decision size <= maxsize stays exact).  Non-roots
+// keep size 0 and the roots' own entries start at their local size.
 __global__ __launch_bounds__(256) void k_cc_count(int H, int W, int maxsize, int* parent, int* size) {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    const bool on = i < H * W && parent[i] >= 0;
-    const int root = on ? uf_find(parent, i) : -1;
-    const int r0 = __builtin_amdgcn_readfirstlane(root);
-    const unsigned long long same = __ballot(on && root == r0);
-    const unsigned long long act = __ballot(on);
-    if (same == act) {                                   // the whole wave shares one root
-        if ((threadIdx.x & 63) == (unsigned)__builtin_ctzll(act) &&
-            __atomic_load_n(&size[r0], __ATOMIC_RELAXED) <= maxsize)
-            atomicAdd(&size[r0], (int)__builtin_popcountll(act));
-        return;
-    }
-    if (on && __atomic_load_n(&size[root], __ATOMIC_RELAXED) <= maxsize) atomicAdd(&size[root], 1);
+    if (i >= H * W) return;
+    const int s = size[i];
+    if (s <= 0) return;
+    const int r = uf_find(parent, i);
+    if (r != i && __atomic_load_n(&size[r], __ATOMIC_RELAXED) <= maxsize) atomicAdd(&size[r], s);
 }
 
 __global__ __launch_bounds__(256) void k_cc_apply(int16_t* img, int H, int W, int pitch, int newv, int maxsize,
@@ -775,7 +783,8 @@ int launch_speckles(int16_t* img, int H, int W, int pitch, int newv, int maxsize
     const unsigned n = (unsigned)(((size_t)H * W + 255) / 256);
     dim3 tiles((W + kCT - 1) / kCT, (H + kCT - 1) / kCT);
     hipLaunchKernelGGL(k_cc_local, tiles, dim3(256), 0, s, img, H, W, pitch, newv, maxdiff, parent, size);
-    hipLaunchKernelGGL(k_cc_border, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, maxdiff, parent);
+    hipLaunchKernelGGL(k_cc_border, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, maxdiff, maxsize, parent,
+                       size);
     hipLaunchKernelGGL(k_cc_count, dim3(n), dim3(256), 0, s, H, W, maxsize, parent, size);
     hipLaunchKernelGGL(k_cc_apply, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, maxsize, parent, size);
     return (int)hipGetLastError();

@@ -37,7 +37,8 @@ EXPORTED = [
     "sv_depth_map_batch_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
     "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
     "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
-    "sv_select_ranks", "sv_affine_f32_dev", "sv_sgbm", "sv_sgbm_dev",
+    "sv_select_ranks", "sv_affine_f32_dev", "sv_sgbm", "sv_sgbm_dev", "sv_filter_speckles",
+    "sv_filter_speckles_dev",
 ]
 
 
@@ -183,6 +184,8 @@ def _declare(lib):
                                ctypes.c_double, ctypes.c_double, _vp, _vp], _c_int),
         "sv_sgbm": ([_vp, _u8p, _u8p] + [_c_int] * 14 + [_i16p], _c_int),
         "sv_sgbm_dev": ([_vp, _vp, _vp] + [_c_int] * 13 + [_vp, _c_int, _vp], _c_int),
+        "sv_filter_speckles": ([_vp, _i16p] + [_c_int] * 5, _c_int),
+        "sv_filter_speckles_dev": ([_vp, _vp] + [_c_int] * 6 + [_vp], _c_int),
         "sv_profile_enable": ([_vp, _c_int], _c_int),
         "sv_profile_read": ([_vp, _c_int, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_longlong)], _c_int),
@@ -368,6 +371,24 @@ class Engine:
             self._h, d_left, d_right, H, W, pitch, int(min_disp), int(num_disp), int(block_size),
             int(P1), int(P2), int(disp12_max_diff), int(pre_filter_cap), int(uniqueness_ratio),
             int(speckle_window_size), int(speckle_range), d_out16, out_pitch, stream or None))
+
+    def filter_speckles(self, img: np.ndarray, new_val: int, max_speckle_size: int,
+                        max_diff: int) -> np.ndarray:
+        """cv2.filterSpeckles(img, newVal, maxSpeckleSize, maxDiff) on an int16 map; returns
+        the filtered copy."""
+        img = np.ascontiguousarray(img, np.int16).copy()
+        if img.ndim != 2:
+            raise ValueError("filter_speckles expects an H x W int16 map")
+        H, W = img.shape
+        _check("sv_filter_speckles", self.lib.sv_filter_speckles(
+            self._h, img, H, W, int(new_val), int(max_speckle_size), int(max_diff)))
+        return img
+
+    def filter_speckles_dev(self, d_img: int, H: int, W: int, pitch: int, new_val: int,
+                            max_speckle_size: int, max_diff: int, stream: int = 0):
+        _check("sv_filter_speckles_dev", self.lib.sv_filter_speckles_dev(
+            self._h, d_img, H, W, pitch, int(new_val), int(max_speckle_size), int(max_diff),
+            stream or None))
 
     def disparity_rows(self, left, right, min_disp: int, num_disp: int, win: int, row0: int,
                        row1: int, cost="sad", out: np.ndarray | None = None) -> np.ndarray:

@@ -130,3 +130,55 @@ def test_gpu_sgbm_wide_disparity_ranges(engine, D, win):
     NUM_DISP = 16*20 = 320 with WINDOW_SIZE = 7 (depth_map.py:31-33)."""
     L, R, _ = stereo_pair(21, D + 90, D, seed=D)
     np.testing.assert_array_equal(engine.sgbm(L, R, 0, D, win), SG.sgbm(L, R, 0, D, win))
+
+
+def _speckle_scene(H, W, seed):
+    """Regions of every size, many crossing the 32x32 tiles: random blobs of constant
+    disparity on a smooth background, plus snakes and invalid pixels."""
+    rng = np.random.default_rng(seed)
+    img = (rng.integers(0, 3, (H, W)) + 40 * 16).astype(np.int16)          # background
+    for _ in range(H * W // 300):
+        y, x = int(rng.integers(0, H)), int(rng.integers(0, W))
+        h, w = int(rng.integers(1, 14)), int(rng.integers(1, 14))
+        img[y:y + h, x:x + w] = int(rng.integers(0, 128)) * 16
+    for _ in range(H * W // 4000):                                          # 1-pixel snakes
+        y, x = int(rng.integers(0, H)), int(rng.integers(0, W))
+        v = int(rng.integers(0, 128)) * 16
+        for _ in range(int(rng.integers(20, 200))):
+            img[y, x] = v
+            if rng.random() < 0.5:
+                x = min(max(x + int(rng.integers(-1, 2)), 0), W - 1)
+            else:
+                y = min(max(y + int(rng.integers(-1, 2)), 0), H - 1)
+    img[rng.random((H, W)) < 0.02] = -16                                    # invalid
+    return img
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,maxsize,maxdiff", [(67, 130, 100, 32), (200, 301, 100, 512),
+                                                 (96, 96, 5, 16), (150, 170, 1000, 64),
+                                                 (1, 50, 3, 0), (40, 1, 3, 0)])
+def test_gpu_filter_speckles_matches_oracle(engine, H, W, maxsize, maxdiff):
+    """cv2.filterSpeckles restated (SG.filter_speckles) vs the union-find kernels: regions
+    across tile borders, snakes, invalid pixels, tiny and huge size limits."""
+    img = _speckle_scene(H, W, H * 7 + W)
+    np.testing.assert_array_equal(engine.filter_speckles(img, -16, maxsize, maxdiff),
+                                  SG.filter_speckles(img, -16, maxsize, maxdiff))
+
+
+@pytest.mark.gpu
+def test_gpu_filter_speckles_1080p_property(engine):
+    """Benchmark size: a background that spans every tile stays, isolated small blocks on
+    it go, blocks of more than maxsize pixels stay (the border-skip path)."""
+    H, W = 1080, 1920
+    img = np.full((H, W), 50 * 16, np.int16)
+    exp = img.copy()
+    for i, y in enumerate(range(5, H - 20, 40)):
+        for j, x in enumerate(range(5, W - 20, 40)):
+            s = 7 if (i + j) % 2 else 12                      # 49 px (speckle) / 144 px (kept)
+            img[y + 20:y + 20 + s, x + 20:x + 20 + s] = (100 + (i * 7 + j) % 20) * 16
+            if s == 12:
+                exp[y + 20:y + 20 + s, x + 20:x + 20 + s] = img[y + 20, x + 20]
+            else:
+                exp[y + 20:y + 20 + s, x + 20:x + 20 + s] = -16
+    np.testing.assert_array_equal(engine.filter_speckles(img, -16, 100, 32), exp)

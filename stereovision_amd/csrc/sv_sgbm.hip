@@ -5,26 +5,31 @@
 // (OpenCV's published algorithm, one stripe, int32 aggregated costs; parity with OpenCV
 // itself unpinned).  Pipeline, one frame:
 //
-//  k_sgbm_hsum    per row: x-Sobel prefilter (clip to +-cap) + raw channel staged in LDS with
-//                 their Birchfield-Tomasi half-pixel intervals; pixel cost
-//                 BT(sobel) + BT(raw) >> 2 for every (x, d) of the band, summed over the
-//                 window columns (running sum, band-clamped) -> hsum u16 [H][Wb][D]
-//  k_sgbm_vsum    window rows (running sum down the column, row-clamped) -> C u16 [H][Wb][D]
-//  k_sgbm_hpath   left->right and right->left paths: one wave per (row, direction), lane l
-//                 owns DPL consecutive disparities; per step d+-1 come from wave_shr/shl DPP
-//                 and the path minimum from a row_ror butterfly + 4 readlanes; the next PF
-//                 steps' costs are in flight in a register ring -> L_lr, L_rl (int16 when
-//                 every value fits, else int32)
-//  k_sgbm_vpath   top->bottom path, one wave per band column walking down the rows with the
-//                 same prefetch ring, S = L_lr + L_rl + L_tb, argmin as a min over
-//                 ((S + 2^20) << 9 | d) keys, the uniqueness test as an OR reduction,
-//                 sub-pixel parabola by the owner lane, one 8-byte store per pixel
+//  k_sgbm_hsum_tiled  per (row, 256-column slab): x-Sobel prefilter (clip to +-cap) and raw
+//                 channel with their Birchfield-Tomasi half-pixel intervals as 16-byte LDS
+//                 records; pixel cost BT(sobel) + BT(raw) >> 2 in packed u16 ops for every
+//                 (x, d) of the band, summed over the window columns (running sum with a
+//                 register ring, band-clamped) -> hsum u16 [H][Wb][Dp]  (k_sgbm_hsum: the
+//                 untiled form for radii > 8)
+//  k_sgbm_vsum    window rows (running sum down the column, row-clamped) -> C u16 [H][Wb][Dp]
+//  k_sgbm_hpath   left->right and right->left paths: 16 lanes per row, 4 rows per wave; lane
+//                 j owns DPL consecutive disparities; per step d+-1 come from row_shr/shl DPP
+//                 and the path minimum from a row_ror butterfly; the next PF steps' costs
+//                 are in flight in a register ring -> L_lr, L_rl (int16 when every value
+//                 fits, else int32)
+//  k_sgbm_vpath   top->bottom path + WTA, 32 lanes per band column (two DPP rows joined by
+//                 v_permlane16_swap), walking down the rows with the same prefetch ring:
+//                 S = L_lr + L_rl + L_tb, argmin over ((S + 2^20) << 9 | d) keys, uniqueness
+//                 from the smallest non-neighbour S, S[b-1] / S[b+1] through LDS for the
+//                 sub-pixel parabola, one 8-byte record per pixel
 //  k_sgbm_lrcheck per row: the right-view disparity by 64-bit LDS atomicMin over
 //                 (minS, rightmost x) keys, the +-disp12MaxDiff consistency test, band
 //                 borders -> int16 x16 output
 //  k_cc_*         filterSpeckles as union-find over 4-connected |d1 - d2| <= maxDiff edges:
-//                 32x32 tiles in LDS first, then the tile-border edges in the global forest
-//                 (atomicMin linking); component sizes by wave-aggregated, capped atomics
+//                 32x32 tiles in LDS first (with local component sizes), then the
+//                 tile-border edges in the global forest (atomicMin linking; edges between
+//                 two trees that already hold a component > maxSpeckleSize are skipped), sizes
+//                 summed per local root
 //
 // The DP kernels are latency-bound chains (W or H dependent steps); the sums are HBM-bound.
 #include "sv_internal.h"
@@ -293,21 +298,37 @@ struct alignas(pack_align(sizeof(T) * DPL)) Pack {
     T v[DPL];
 };
 
-// Lines of LPC lanes (16: one DPP row; 32: two rows, joined through ds_swizzle xor 16).
-__device__ __forceinline__ int swz16(int v) { return __builtin_amdgcn_ds_swizzle(v, 0x401F); }
+// Lines of LPC lanes (16: one DPP row; 32: two rows, joined by v_permlane16_swap, which
+// hands each row of a pair the other's values in one VALU op).
+struct RowPair {
+    int even, odd;   // per lane: the value of the pair's even row / odd row
+};
+__device__ __forceinline__ RowPair row_pair(int v) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return {(int)r[0], (int)r[1]};
+}
 template <int LPC> __device__ __forceinline__ int line_min(int v) {
     v = row_min(v);
-    if constexpr (LPC == 32) v = min(v, swz16(v));
+    if constexpr (LPC == 32) {
+        const RowPair p = row_pair(v);
+        v = min(p.even, p.odd);
+    }
     return v;
 }
 template <int LPC> __device__ __forceinline__ uint32_t line_min_u(uint32_t v) {
     v = row_min_u(v);
-    if constexpr (LPC == 32) v = min(v, (uint32_t)swz16((int)v));
+    if constexpr (LPC == 32) {
+        const RowPair p = row_pair((int)v);
+        v = min((uint32_t)p.even, (uint32_t)p.odd);
+    }
     return v;
 }
 template <int LPC> __device__ __forceinline__ int line_max(int v) {
     v = row_max(v);
-    if constexpr (LPC == 32) v = max(v, swz16(v));
+    if constexpr (LPC == 32) {
+        const RowPair p = row_pair(v);
+        v = max(p.even, p.odd);
+    }
     return v;
 }
 // value of lane j-1 / j+1 of the line (`edge` at the line's ends)
@@ -684,16 +705,16 @@ __global__ __launch_bounds__(256) void k_cc_apply(int16_t* img, int H, int W, in
 }
 
 // Line plans: (lanes per line, disparities per lane).
-//  * horizontal paths: 16-lane lines.  Their cost is the loop-carried chain of W steps
-//    (path minimum -> next step); a 32-lane line adds a cross-row exchange to that chain
-//    and measured slower despite twice the waves.
+//  * horizontal paths: 16-lane lines.  One wave per SIMD issues the W-step chain; 32-lane
+//    lines (1080 waves at 1080p, some SIMDs holding two) measured 490 vs 471 us.
 //  * vertical path + WTA: 32-lane lines for D > 32.  The per-row argmin / uniqueness /
 //    sub-pixel work is off the chain and issue-bound: 32-lane lines spread it over twice
-//    the waves (448 -> 896 at 1080p D=128: 872 -> 639 us).
+//    the waves (448 -> 896 at 1080p D=128: 872 -> 639 us; 532 us after the WTA trims and
+//    with v_permlane16_swap instead of ds_swizzle joining the two rows of a line).
 struct PathPlan {
     int lpc, dpl;
 };
-PathPlan hpath_plan(int D) {
+PathPlan hpath16_plan(int D) {
     const int need = (D + 15) / 16;
     const int opts[] = {1, 2, 4, 8, 12, 16, 20, 24, 32};
     for (int o : opts)
@@ -701,7 +722,7 @@ PathPlan hpath_plan(int D) {
     return {0, -1};
 }
 PathPlan vpath_plan(int D) {
-    if (D <= 32) return hpath_plan(D);
+    if (D <= 32) return hpath16_plan(D);
     const int need = (D + 31) / 32;
     const int opts[] = {2, 4, 6, 8, 10, 12, 16};
     for (int o : opts)
@@ -709,14 +730,16 @@ PathPlan vpath_plan(int D) {
     return {0, -1};
 }
 
+PathPlan hpath_plan(int D) { return hpath16_plan(D); }
+
 template <typename LT>
 int launch_paths_t(const SgbmArgs& a, hipStream_t s) {
     const PathPlan ph = hpath_plan(a.D), pv = vpath_plan(a.D);
-    const dim3 gh((a.H + 3) / 4, 2), gv((a.Wb + 64 / pv.lpc - 1) / (64 / pv.lpc));
+    const dim3 gh((a.H + 64 / ph.lpc - 1) / (64 / ph.lpc), 2), gv((a.Wb + 64 / pv.lpc - 1) / (64 / pv.lpc));
     bool h = false, v = false;
-#define SV_HPATH(N, PF)                                                              \
-    if (ph.dpl == N) {                                                               \
-        hipLaunchKernelGGL((k_sgbm_hpath<N, 16, LT, PF>), gh, dim3(64), 0, s, a);   \
+#define SV_HPATH(L, N, PF)                                                           \
+    if (!h && ph.lpc == L && ph.dpl == N) {                                          \
+        hipLaunchKernelGGL((k_sgbm_hpath<N, L, LT, PF>), gh, dim3(64), 0, s, a);    \
         h = true;                                                                    \
     }
 #define SV_VPATH(L, N, PF)                                                           \
@@ -724,8 +747,8 @@ int launch_paths_t(const SgbmArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((k_sgbm_vpath<N, L, LT, PF>), gv, dim3(64), 0, s, a);    \
         v = true;                                                                    \
     }
-    SV_HPATH(1, 24) SV_HPATH(2, 24) SV_HPATH(4, 16) SV_HPATH(8, 16) SV_HPATH(12, 10) SV_HPATH(16, 8)
-    SV_HPATH(20, 6) SV_HPATH(24, 6) SV_HPATH(32, 4)
+    SV_HPATH(16, 1, 24) SV_HPATH(16, 2, 24) SV_HPATH(16, 4, 16) SV_HPATH(16, 8, 16) SV_HPATH(16, 12, 10)
+    SV_HPATH(16, 16, 8) SV_HPATH(16, 20, 6) SV_HPATH(16, 24, 6) SV_HPATH(16, 32, 4)
     if (!h) return (int)hipErrorInvalidValue;
     SV_VPATH(16, 1, 16) SV_VPATH(16, 2, 16)
     SV_VPATH(32, 2, 16) SV_VPATH(32, 4, 12) SV_VPATH(32, 6, 10) SV_VPATH(32, 8, 8) SV_VPATH(32, 10, 6)

@@ -136,7 +136,6 @@ struct SgbmArgs {
     void* dummy;               // >= 64 x 128 bytes: store target of the padding lanes
 };
 int sgbm_dp(int D);                  // per-pixel volume stride for D disparities, -1 if D > 512
-size_t sgbm_hsum_lds(int W);
 int launch_sgbm(const SgbmArgs& a, hipStream_t s);
 int launch_speckles(int16_t* img, int H, int W, int pitch, int newv, int maxsize, int maxdiff, int* parent,
                     int* size, hipStream_t s);

@@ -9,8 +9,7 @@
 //                 channel with their Birchfield-Tomasi half-pixel intervals as 16-byte LDS
 //                 records; pixel cost BT(sobel) + BT(raw) >> 2 in packed u16 ops for every
 //                 (x, d) of the band, summed over the window columns (running sum with a
-//                 register ring, band-clamped) -> hsum u16 [H][Wb][Dp]  (k_sgbm_hsum: the
-//                 untiled form for radii > 8)
+//                 register ring, band-clamped) -> hsum u16 [H][Wb][Dp]
 //  k_sgbm_vsum    window rows (running sum down the column, row-clamped) -> C u16 [H][Wb][Dp]
 //  k_sgbm_hpath   left->right and right->left paths: 16 lanes per row, 4 rows per wave; lane
 //                 j owns DPL consecutive disparities; per step d+-1 come from row_shr/shl DPP
@@ -74,86 +73,20 @@ __device__ __forceinline__ int row_max(int v) {
 // -------------------------------------------------------------------------------------
 // pixel cost + horizontal window sums
 // -------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_sgbm_hsum(SgbmArgs a) {
-    extern __shared__ uint8_t lds[];
-    const int W = a.W, y = blockIdx.x, t = threadIdx.x;
-    // [image 0/1][channel 0 sobel / 1 raw][value, lo, hi][W]
-    uint8_t* buf = lds;
-    auto at = [&](int im, int ch, int f) { return buf + ((im * 2 + ch) * 3 + f) * W; };
-    const int ym = y > 0 ? y - 1 : y, yp = y < a.H - 1 ? y + 1 : y;
-    for (int im = 0; im < 2; ++im) {
-        const uint8_t* img = im == 0 ? a.L : a.R;
-        const uint8_t* r0 = img + (size_t)y * a.pitch;
-        const uint8_t* rm = img + (size_t)ym * a.pitch;
-        const uint8_t* rp = img + (size_t)yp * a.pitch;
-        for (int x = t; x < W; x += 256) {
-            int pf = a.cap, raw = a.cap;   // columns 0 and W-1: tab[0] in both channels
-            if (x > 0 && x < W - 1) {
-                const int s = (r0[x + 1] - r0[x - 1]) * 2 + rm[x + 1] - rm[x - 1] + rp[x + 1] - rp[x - 1];
-                pf = min(max(s, -a.cap), a.cap) + a.cap;
-                raw = r0[x];
-            }
-            at(im, 0, 0)[x] = (uint8_t)pf;
-            at(im, 1, 0)[x] = (uint8_t)raw;
-        }
-    }
-    __syncthreads();
-    for (int i = t; i < 4 * W; i += 256) {
-        const int im = i / (2 * W), ch = (i / W) & 1, x = i % W;
-        const uint8_t* v = at(im, ch, 0);
-        const int c = v[x];
-        const int l = x > 0 ? (c + v[x - 1]) >> 1 : c;
-        const int r = x < W - 1 ? (c + v[x + 1]) >> 1 : c;
-        at(im, ch, 1)[x] = (uint8_t)min(min(l, r), c);
-        at(im, ch, 2)[x] = (uint8_t)max(max(l, r), c);
-    }
-    __syncthreads();
-    const int D = a.D, Wb = a.Wb, r = a.r;
-    const int nc = max(1, 256 / D);                  // column chunks per disparity
-    const int clen = (Wb + nc - 1) / nc;
-    const int Dp = a.Dp;
-    uint16_t* out = a.hsum + (size_t)y * Wb * Dp;
-    auto pix = [&](int xb, int d) -> int {
-        xb = min(max(xb, 0), Wb - 1);
-        const int x = a.X0 + xb, xr = x - a.minD - d;
-        int cost = 0;
-#pragma unroll
-        for (int ch = 0; ch < 2; ++ch) {
-            const int u = at(0, ch, 0)[x], u0 = at(0, ch, 1)[x], u1 = at(0, ch, 2)[x];
-            const int v = at(1, ch, 0)[xr], v0 = at(1, ch, 1)[xr], v1 = at(1, ch, 2)[xr];
-            const int c0 = max(max(0, u - v1), v0 - u);
-            const int c1 = max(max(0, v - u1), u0 - v);
-            cost += min(c0, c1) >> (ch * 2);
-        }
-        return cost;
-    };
-    for (int item = t; item < D * nc; item += 256) {
-        const int d = item % D, c = item / D;
-        const int xs = c * clen, xe = min(Wb, xs + clen);
-        if (xs >= xe) continue;
-        int hs = 0;
-        for (int i = -r; i <= r; ++i) hs += pix(xs + i, d);
-        out[(size_t)xs * Dp + d] = (uint16_t)hs;
-        for (int x = xs + 1; x < xe; ++x) {
-            hs += pix(x + r, d) - pix(x - r - 1, d);
-            out[(size_t)x * Dp + d] = (uint16_t)hs;
-        }
-    }
-}
-
-// Tiled form of the same sums (r <= kHsumMaxR): one workgroup per (row, 256-column slab of
-// the band).  Per image column a 16-byte record {value, BT lo, BT hi} with the two channels
+// Pixel cost + window columns: one workgroup per (row, 256-column slab of the band).  Per image column a 16-byte record {value, BT lo, BT hi} with the two channels
 // (x-Sobel, raw) as the u16 halves of each dword, so the pixel cost of a cell is 7 packed
 // u16 ops (saturating subtracts give the max(0, .) of Birchfield-Tomasi for free) + 2; the
 // window's leaving column comes from a register ring (one pixel cost per cell, not two).
 constexpr int kHX = 256;          // band columns per workgroup
-constexpr int kHsumMaxR = 8;
+constexpr int kMaxR = 7;          // blockSize <= 15 (check_match)
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us2, v); }
 __device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
 
-// {value, lo, hi} of image column x of row y, both channels (see k_sgbm_hsum)
+// {value, lo, hi} of image column x of row y, both channels: x-Sobel clipped to +-cap (+cap)
+// and the raw value, columns 0 and W-1 holding cap in both (OpenCV's tab[0]), with the
+// Birchfield-Tomasi half-pixel interval [min, max] of (c, (c+left)/2, (c+right)/2)
 __device__ __forceinline__ uint4 bt_record(const SgbmArgs& a, const uint8_t* img, int y, int x) {
     const int W = a.W;
     const int ym = y > 0 ? y - 1 : y, yp = y < a.H - 1 ? y + 1 : y;
@@ -774,22 +707,17 @@ int sgbm_dp(int D) {
     return (D + l - 1) / l * l;
 }
 
-size_t sgbm_hsum_lds(int W) { return (size_t)12 * W; }
-
 int launch_sgbm(const SgbmArgs& a, hipStream_t s) {
     if (a.H <= 0 || a.W <= 0) return 0;
     if (a.Wb > 0) {
-        if (a.r <= kHsumMaxR) {
-            const dim3 grid((unsigned)((a.Wb + kHX - 1) / kHX), (unsigned)a.H);
-            const size_t lds = (size_t)(2 * kHX + 4 * a.r + a.D - 1) * sizeof(uint4);
-            switch (a.r) {
+        if (a.r > kMaxR) return (int)hipErrorInvalidValue;
+        const dim3 grid((unsigned)((a.Wb + kHX - 1) / kHX), (unsigned)a.H);
+        const size_t lds = (size_t)(2 * kHX + 4 * a.r + a.D - 1) * sizeof(uint4);
+        switch (a.r) {
 #define SV_HSUM_R(R) case R: hipLaunchKernelGGL(k_sgbm_hsum_tiled<R>, grid, dim3(256), lds, s, a); break;
-                SV_HSUM_R(0) SV_HSUM_R(1) SV_HSUM_R(2) SV_HSUM_R(3) SV_HSUM_R(4) SV_HSUM_R(5) SV_HSUM_R(6)
-                SV_HSUM_R(7) SV_HSUM_R(8)
+            SV_HSUM_R(0) SV_HSUM_R(1) SV_HSUM_R(2) SV_HSUM_R(3) SV_HSUM_R(4) SV_HSUM_R(5) SV_HSUM_R(6)
+            SV_HSUM_R(7)
 #undef SV_HSUM_R
-            }
-        } else {
-            hipLaunchKernelGGL(k_sgbm_hsum, dim3(a.H), dim3(256), sgbm_hsum_lds(a.W), s, a);
         }
         const size_t plane = (size_t)a.Wb * a.Dp;
         hipLaunchKernelGGL(k_sgbm_vsum, dim3((unsigned)((plane + 255) / 256)), dim3(256), 0, s, a);

@@ -100,7 +100,10 @@ struct sv_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut, rmap1, rmap2, rdst[2], stats, sel,
-        sg_hsum, sg_c, sg_l, sg_band, cc_parent, cc_size, hist_copies;
+        sg_hsum, sg_c, sg_l, sg_lt, sg_band, cc_parent, cc_size, hist_copies;
+    // SGBM: second stream + fork/join events for the vertical path beside the horizontal ones
+    hipStream_t sg_aux = nullptr;
+    hipEvent_t sg_ev[2] = {nullptr, nullptr};
     // cached post-processing table: key = (mode, params, range); `lut_ev` marks its build
     struct LutKey {
         int mode = -1, min_disp = 0, num_disp = 0, m0 = 0, n = 0;
@@ -241,17 +244,24 @@ int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, in
     SV_HIP(c->sg_hsum.ensure(vol * 2 + 256));
     SV_HIP(c->sg_c.ensure(vol * 2 + 256));
     SV_HIP(c->sg_l.ensure(vol * (a.l32 ? 8 : 2) + 256));
+    SV_HIP(c->sg_lt.ensure(vol * (a.l32 ? 4 : 2) + 256));
+    if (!c->sg_aux) {
+        SV_HIP(hipStreamCreateWithFlags(&c->sg_aux, hipStreamNonBlocking));
+        SV_HIP(hipEventCreateWithFlags(&c->sg_ev[0], hipEventDisableTiming));
+        SV_HIP(hipEventCreateWithFlags(&c->sg_ev[1], hipEventDisableTiming));
+    }
     SV_HIP(c->sg_band.ensure((size_t)H * a.Wb * 8 + 256 + 64 * 128));
     a.hsum = c->sg_hsum.as<uint16_t>();
     a.C = c->sg_c.as<uint16_t>();
     // int16 paths: L_lr reuses the hsum volume (dead after the window-row sums)
     a.Llr = a.l32 ? c->sg_l.p : c->sg_hsum.p;
     a.Lrl = a.l32 ? (void*)(c->sg_l.as<int32_t>() + vol) : c->sg_l.p;
+    a.Ltb = c->sg_lt.p;
     a.band = c->sg_band.p;
     a.dummy = c->sg_band.as<uint8_t>() + ((size_t)H * a.Wb * 8 + 255) / 256 * 256;
     a.out = out;
     a.opitch = opitch;
-    SV_LAUNCH(c, SV_K_SGBM, s, sv::launch_sgbm(a, s));
+    SV_LAUNCH(c, SV_K_SGBM, s, sv::launch_sgbm(a, s, c->sg_aux, c->sg_ev[0], c->sg_ev[1]));
     return enqueue_speckles(c, out, H, W, opitch, (min_disp - 1) * 16, p.speckle_win, 16 * p.speckle_range, s);
 }
 
@@ -561,9 +571,16 @@ void sv_destroy(sv_ctx* c) {
         DevBuf* bufs[] = {&c->img[0], &c->img[1], &c->gray[0], &c->gray[1], &c->d16, &c->fa, &c->fb,
                           &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->lut,
                           &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1], &c->stats, &c->sel,
-                          &c->sg_hsum, &c->sg_c, &c->sg_l, &c->sg_band, &c->cc_parent, &c->hist_copies,
+                          &c->sg_hsum, &c->sg_c, &c->sg_l, &c->sg_lt, &c->sg_band, &c->cc_parent,
+                          &c->hist_copies,
                           &c->cc_size};
         if (c->lut_ev) (void)hipEventDestroy(c->lut_ev);
+        if (c->sg_aux) {
+            (void)hipStreamSynchronize(c->sg_aux);
+            (void)hipStreamDestroy(c->sg_aux);
+        }
+        for (auto e : c->sg_ev)
+            if (e) (void)hipEventDestroy(e);
         for (auto* b : bufs) b->release();
         c->hin.release();
         c->hout.release();

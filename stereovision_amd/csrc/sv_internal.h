@@ -128,6 +128,7 @@ struct SgbmArgs {
     uint16_t* C;               // [H][Wb][D] window sums
     void* Llr;                 // [H][Wb][D] path costs, int16 (l32 = 0) or int32
     void* Lrl;
+    void* Ltb;                 // [H][Wb][Dp] top->bottom path costs (same type as Llr)
     int l32;
     void* band;                // [H][Wb] {int16 x16 disparity after uniqueness + sub-pixel,
                                //  int16 argmin index, int32 min cost (INT_MAX: not unique)}
@@ -136,7 +137,9 @@ struct SgbmArgs {
     void* dummy;               // >= 64 x 128 bytes: store target of the padding lanes
 };
 int sgbm_dp(int D);                  // per-pixel volume stride for D disparities, -1 if D > 512
-int launch_sgbm(const SgbmArgs& a, hipStream_t s);
+// aux / fork / join: a second stream and two events for the concurrent vertical path (aux =
+// nullptr: everything on s)
+int launch_sgbm(const SgbmArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
 int launch_speckles(int16_t* img, int H, int W, int pitch, int newv, int maxsize, int maxdiff, int* parent,
                     int* size, hipStream_t s);
 

@@ -16,11 +16,12 @@
 //                 and the path minimum from a row_ror butterfly; the next PF steps' costs
 //                 are in flight in a register ring -> L_lr, L_rl (int16 when every value
 //                 fits, else int32)
-//  k_sgbm_vpath   top->bottom path + WTA, 32 lanes per band column (two DPP rows joined by
-//                 v_permlane16_swap), walking down the rows with the same prefetch ring:
-//                 S = L_lr + L_rl + L_tb, argmin over ((S + 2^20) << 9 | d) keys, uniqueness
-//                 from the smallest non-neighbour S, S[b-1] / S[b+1] through LDS for the
-//                 sub-pixel parabola, one 8-byte record per pixel
+//  k_sgbm_vpath   top->bottom path, 32 lanes per band column (two DPP rows joined by
+//                 v_permlane16_swap) walking down the rows with the same prefetch ring ->
+//                 L_tb; on a second stream, concurrent with k_sgbm_hpath
+//  k_sgbm_wta     S = L_lr + L_rl + L_tb per pixel, argmin over ((S + 2^20) << 9 | d) keys,
+//                 uniqueness from the smallest non-neighbour S, S[b-1] / S[b+1] through LDS
+//                 for the sub-pixel parabola, one 8-byte record per pixel (full occupancy)
 //  k_sgbm_lrcheck per row: the right-view disparity by 64-bit LDS atomicMin over
 //                 (minS, rightmost x) keys, the +-disp12MaxDiff consistency test, band
 //                 borders -> int16 x16 output
@@ -32,6 +33,8 @@
 //
 // The DP kernels are latency-bound chains (W or H dependent steps); the sums are HBM-bound.
 #include "sv_internal.h"
+
+#include <cstdlib>
 
 namespace sv {
 namespace {
@@ -278,22 +281,30 @@ template <int LPC> __device__ __forceinline__ int from_right(int v, int edge, in
 
 // One SGBM step for the DPL disparities of a lane: OpenCV's
 // L = C + min(prev[d], prev[d-1] + P1, prev[d+1] + P1, minprev + P2) - (minprev + P2).
+// pad[k] = INT_MIN for d < D, kInf for the padding disparities (which stay at kInf: a max
+// instead of a per-disparity branch).
 template <int DPL, int LPC>
 __device__ __forceinline__ void path_step(int (&prev)[DPL], const int (&c)[DPL], int mn, int P1, int P2,
-                                          int dbase, int D, int j) {
+                                          const int (&pad)[DPL], int j) {
     const int lo_in = from_left<LPC>(prev[DPL - 1], kInf, j);
     const int hi_in = from_right<LPC>(prev[0], kInf, j);
     int nxt[DPL];
-    const int mp = mn + P2;
+    const int mp = mn + P2, nmp = -mp;
 #pragma unroll
     for (int k = 0; k < DPL; ++k) {
         const int lo = k > 0 ? prev[k - 1] : lo_in;
         const int hi = k < DPL - 1 ? prev[k + 1] : hi_in;
         const int m = min(min(prev[k], min(lo, hi) + P1), mp);
-        nxt[k] = dbase + k < D ? c[k] + m - mp : kInf;
+        nxt[k] = max(c[k] + m + nmp, pad[k]);
     }
 #pragma unroll
     for (int k = 0; k < DPL; ++k) prev[k] = nxt[k];
+}
+
+template <int DPL>
+__device__ __forceinline__ void pad_init(int (&pad)[DPL], int dbase, int D) {
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) pad[k] = dbase + k < D ? (int)0x80000000 : kInf;
 }
 
 template <int DPL>
@@ -316,43 +327,50 @@ __global__ __launch_bounds__(64) void k_sgbm_hpath(SgbmArgs a) {
     // slot: no load or store sits under a branch
     const bool live = y < a.H && dbase < D;
     const int yc = min(y, a.H - 1);
-    LT* Lrow = live ? static_cast<LT*>(dir == 0 ? a.Llr : a.Lrl) + (size_t)yc * Wb * Dp + dbase
-                    : reinterpret_cast<LT*>(a.dummy) + lane * (128 / sizeof(LT));
-    const int xstride = live ? Dp : 0;
-    const uint16_t* Crow = a.C + (size_t)yc * Wb * Dp + (dbase < D ? dbase : 0);
+    // x walks 0 .. Wb-1 (dir 0) or Wb-1 .. 0 (dir 1): pointers step by +-Dp per x
+    const ptrdiff_t xstep = dir == 0 ? Dp : -(ptrdiff_t)Dp;
+    const size_t x0 = dir == 0 ? 0 : (size_t)(Wb - 1) * Dp;
+    LT* Lp = live ? static_cast<LT*>(dir == 0 ? a.Llr : a.Lrl) + (size_t)yc * Wb * Dp + dbase + x0
+                  : reinterpret_cast<LT*>(a.dummy) + lane * (128 / sizeof(LT));
+    const ptrdiff_t lstep = live ? xstep : 0;
+    const uint16_t* Crow = a.C + (size_t)yc * Wb * Dp + (dbase < D ? dbase : 0) + x0;
     using CP = Pack<uint16_t, DPL>;
     using LP = Pack<LT, DPL>;
-    auto xof = [&](int s) { return dir == 0 ? s : Wb - 1 - s; };
     CP ring[PF];
 #pragma unroll
-    for (int p = 0; p < PF; ++p) ring[p] = *reinterpret_cast<const CP*>(Crow + (size_t)xof(min(p, Wb - 1)) * Dp);
-    int prev[DPL];
+    for (int p = 0; p < PF; ++p) ring[p] = *reinterpret_cast<const CP*>(Crow + (ptrdiff_t)min(p, Wb - 1) * xstep);
+    // next load: x index PF, clamped to Wb-1 (the pointer stops there)
+    const uint16_t* Cn = Crow + (ptrdiff_t)min(PF, Wb - 1) * xstep;
+    int prev[DPL], pad[DPL];
+    pad_init<DPL>(pad, dbase, D);
 #pragma unroll
     for (int k = 0; k < DPL; ++k) prev[k] = dbase + k < D ? 0 : kInf;
     int mn = 0;
-    auto step = [&](int s, const CP& cp) {
+    auto step = [&](const CP& cp) {
         int c[DPL];
 #pragma unroll
         for (int k = 0; k < DPL; ++k) c[k] = (int)cp.v[k];
-        path_step<DPL, LPC>(prev, c, mn, a.P1, a.P2, dbase, D, j);
+        path_step<DPL, LPC>(prev, c, mn, a.P1, a.P2, pad, j);
         mn = line_min<LPC>(lane_min<DPL>(prev));
         LP o;
 #pragma unroll
         for (int k = 0; k < DPL; ++k) o.v[k] = (LT)prev[k];
-        *reinterpret_cast<LP*>(Lrow + (size_t)xof(s) * xstride) = o;
+        *reinterpret_cast<LP*>(Lp) = o;
+        Lp += lstep;
     };
     int s0 = 0;
     for (; s0 + PF <= Wb; s0 += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
             const CP cur = ring[u];
-            ring[u] = *reinterpret_cast<const CP*>(Crow + (size_t)xof(min(s0 + u + PF, Wb - 1)) * Dp);
-            step(s0 + u, cur);
+            ring[u] = *reinterpret_cast<const CP*>(Cn);
+            Cn += s0 + u + PF < Wb - 1 ? xstep : 0;
+            step(cur);
         }
     }
 #pragma unroll
     for (int u = 0; u < PF; ++u)
-        if (s0 + u < Wb) step(s0 + u, ring[u]);
+        if (s0 + u < Wb) step(ring[u]);
 }
 
 struct BandOut {      // one 8-byte record per band pixel
@@ -360,104 +378,122 @@ struct BandOut {      // one 8-byte record per band pixel
     int32_t minS;
 };
 
-// Top->bottom path + winner-take-all: 4 band columns per wave walking down the rows.  The
-// argmin / uniqueness / sub-pixel work of a row does not feed the next row, so it overlaps
-// the loop-carried path chain.
+// Winner-take-all of one pixel on a line of LPC lanes (lane j holds S[dbase .. dbase+DPL)):
+// argmin over keys (S << 9) + (d + 2^29) = ((S + 2^20) << 9) | d (first minimum), the
+// uniqueness test from the smallest S with |d - b| > 1 (24-bit products: |S| < 2^23), S[b-1]
+// and S[b+1] through the line's LDS slice (LDS ops of one wave are ordered), the sub-pixel
+// parabola with a float-reciprocal quotient plus one correction (C's truncating division;
+// |num| <= 17 * den / 2 because S[b+-1] >= minS).
+template <int DPL, int LPC>
+__device__ __forceinline__ BandOut wta_line(const SgbmArgs& a, const int (&s)[DPL], int dbase, int* my_s,
+                                            const int* line_s) {
+    const int D = a.D;
+    uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) {
+        my_s[k] = s[k];
+        if (dbase + k < D) key = min(key, ((uint32_t)s[k] << 9) + ((uint32_t)(dbase + k) + (1u << 29)));
+    }
+    key = line_min_u<LPC>(key);
+    const int b = (int)(key & 511u);
+    const int minS = (int)(key >> 9) - (1 << 20);
+    const int e = dbase - b + 1;
+    int m2 = 0x7FFFFFFF;
+#pragma unroll
+    for (int k = 0; k < DPL; ++k)
+        if (dbase + k < D && (unsigned)(e + k) > 2u) m2 = min(m2, s[k]);
+    m2 = line_min<LPC>(m2);
+    const bool viol = m2 != 0x7FFFFFFF && __mul24(m2, 100 - a.uniq) < __mul24(minS, 100);
+    int d16 = b * 16;
+    if (b > 0 && b < D - 1) {
+        const int sm = line_s[b - 1], sp = line_s[b + 1];
+        const int denom2 = max(sm + sp - 2 * minS, 1);
+        const int num = (sm - sp) * 16 + denom2, den = denom2 * 2;
+        const int an = abs(num);
+        int q = (int)((float)an * __builtin_amdgcn_rcpf((float)den));
+        const int r = an - (int)__umul24((unsigned)q, (unsigned)den);
+        q += (r >= den) - (r < 0);
+        d16 += num < 0 ? -q : q;
+    }
+    BandOut o;
+    o.disp = (int16_t)(viol ? (a.minD - 1) * 16 : d16 + a.minD * 16);
+    o.best = (int16_t)b;
+    o.minS = viol ? 0x7FFFFFFF : minS;
+    return o;
+}
+
+// Top->bottom path: one band column per line of LPC lanes walking down the rows -> L_tb.  It
+// depends on C only, so it runs on a second stream beside the horizontal paths (both are
+// chains of dependent steps that leave most of a SIMD idle).
 template <int DPL, int LPC, typename LT, int PF>
 __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
     constexpr int NL = 64 / LPC;
     const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
     const int xb = blockIdx.x * NL + g;
     const int D = a.D, Wb = a.Wb, dbase = j * DPL;
-    const bool colok = xb < Wb;
+    const bool live = xb < Wb && dbase < D;
     const size_t plane = (size_t)Wb * a.Dp;
     const size_t col = (size_t)min(xb, Wb - 1) * a.Dp + (dbase < D ? dbase : 0);
-    const LT* Llr = static_cast<const LT*>(a.Llr) + col;
-    const LT* Lrl = static_cast<const LT*>(a.Lrl) + col;
     const uint16_t* Cc = a.C + col;
+    LT* Lt = live ? static_cast<LT*>(a.Ltb) + col : reinterpret_cast<LT*>(a.dummy) + lane * (128 / sizeof(LT));
+    const size_t ystride = live ? plane : 0;
     using CP = Pack<uint16_t, DPL>;
     using LP = Pack<LT, DPL>;
     CP rc[PF];
-    LP rl[PF], rr[PF];
-    auto fetch = [&](int y, CP& c, LP& l, LP& r) {
-        const size_t o = (size_t)min(y, a.H - 1) * plane;
-        c = *reinterpret_cast<const CP*>(Cc + o);
-        l = *reinterpret_cast<const LP*>(Llr + o);
-        r = *reinterpret_cast<const LP*>(Lrl + o);
-    };
 #pragma unroll
-    for (int p = 0; p < PF; ++p) fetch(p, rc[p], rl[p], rr[p]);
-    int prev[DPL];
+    for (int p = 0; p < PF; ++p) rc[p] = *reinterpret_cast<const CP*>(Cc + (size_t)min(p, a.H - 1) * plane);
+    int prev[DPL], pad[DPL];
+    pad_init<DPL>(pad, dbase, D);
 #pragma unroll
     for (int k = 0; k < DPL; ++k) prev[k] = dbase + k < D ? 0 : kInf;
     int mn = 0;
-    const int u100 = 100 - a.uniq;
-    BandOut* bo = colok ? reinterpret_cast<BandOut*>(a.band) + xb : reinterpret_cast<BandOut*>(a.dummy) + lane;
-    const int ystride = colok ? Wb : 0;
-    // S of the line, so the lanes can read S[b-1], S[b+1] (LDS ops of one wave are ordered)
-    __shared__ int lds_s[64 * DPL];
-    int* my_s = lds_s + lane * DPL;
-    const int* line_s = lds_s + g * LPC * DPL;
-    // argmin keys ((S + 2^20) << 9) | d = (S << 9) + dk[k]
-    uint32_t dk[DPL];
-#pragma unroll
-    for (int k = 0; k < DPL; ++k) dk[k] = (uint32_t)(dbase + k) + (1u << 29);
-    auto row = [&](int y, const CP& cp, const LP& lp, const LP& rp) {
-        int c[DPL], s[DPL];
+    auto row = [&](int y, const CP& cp) {
+        int c[DPL];
 #pragma unroll
         for (int k = 0; k < DPL; ++k) c[k] = (int)cp.v[k];
-        path_step<DPL, LPC>(prev, c, mn, a.P1, a.P2, dbase, D, j);
+        path_step<DPL, LPC>(prev, c, mn, a.P1, a.P2, pad, j);
         mn = line_min<LPC>(lane_min<DPL>(prev));
-        uint32_t key = 0xFFFFFFFFu;
+        LP o;
 #pragma unroll
-        for (int k = 0; k < DPL; ++k) {
-            s[k] = (int)lp.v[k] + (int)rp.v[k] + prev[k];
-            my_s[k] = s[k];
-            if (dbase + k < D) key = min(key, ((uint32_t)s[k] << 9) + dk[k]);
-        }
-        key = line_min_u<LPC>(key);
-        const int b = (int)(key & 511u);
-        const int minS = (int)(key >> 9) - (1 << 20);
-        // uniqueness: the smallest S with |d - b| > 1 against minS (|S| < 2^23: 24-bit products)
-        const int e = dbase - b + 1;
-        int m2 = 0x7FFFFFFF;
-#pragma unroll
-        for (int k = 0; k < DPL; ++k)
-            if (dbase + k < D && (unsigned)(e + k) > 2u) m2 = min(m2, s[k]);
-        m2 = line_min<LPC>(m2);
-        const bool viol = m2 != 0x7FFFFFFF && __mul24(m2, u100) < __mul24(minS, 100);
-        int d16 = b * 16;
-        if (b > 0 && b < D - 1) {
-            const int sm = line_s[b - 1], sp = line_s[b + 1];
-            // sub-pixel parabola; |num| <= 17 * den / 2 (sm, sp >= minS): a float quotient
-            // and one correction give C's truncating division
-            const int denom2 = max(sm + sp - 2 * minS, 1);
-            const int num = (sm - sp) * 16 + denom2, den = denom2 * 2;
-            const int an = abs(num);
-            int q = (int)((float)an * __builtin_amdgcn_rcpf((float)den));
-            const int r = an - (int)__umul24((unsigned)q, (unsigned)den);
-            q += (r >= den) - (r < 0);
-            d16 += num < 0 ? -q : q;
-        }
-        BandOut o;
-        o.disp = (int16_t)(viol ? (a.minD - 1) * 16 : d16 + a.minD * 16);
-        o.best = (int16_t)b;
-        o.minS = viol ? 0x7FFFFFFF : minS;
-        bo[(size_t)y * ystride] = o;          // the 16 lanes of a row store the same record
+        for (int k = 0; k < DPL; ++k) o.v[k] = (LT)prev[k];
+        *reinterpret_cast<LP*>(Lt + (size_t)y * ystride) = o;
     };
     int y0 = 0;
     for (; y0 + PF <= a.H; y0 += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
             const CP c = rc[u];
-            const LP l = rl[u], r = rr[u];
-            fetch(y0 + u + PF, rc[u], rl[u], rr[u]);
-            row(y0 + u, c, l, r);
+            rc[u] = *reinterpret_cast<const CP*>(Cc + (size_t)min(y0 + u + PF, a.H - 1) * plane);
+            row(y0 + u, c);
         }
     }
 #pragma unroll
     for (int u = 0; u < PF; ++u)
-        if (y0 + u < a.H) row(y0 + u, rc[u], rl[u], rr[u]);
+        if (y0 + u < a.H) row(y0 + u, rc[u]);
+}
+
+// S = L_lr + L_rl + L_tb and the winner-take-all, one pixel per line of LPC lanes: every
+// pixel is independent, so this runs with full occupancy (it was the issue-bound half of a
+// fused vertical-path kernel on ~900 waves).
+template <int DPL, int LPC, typename LT>
+__global__ __launch_bounds__(64) void k_sgbm_wta(SgbmArgs a) {
+    constexpr int NL = 64 / LPC;
+    const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
+    const size_t npx = (size_t)a.H * a.Wb;
+    const size_t p = (size_t)blockIdx.x * NL + g;
+    const int dbase = j * DPL;
+    const size_t pc = p < npx ? p : npx - 1;
+    const size_t off = pc * a.Dp + (dbase < a.D ? dbase : 0);
+    using LP = Pack<LT, DPL>;
+    const LP l = *reinterpret_cast<const LP*>(static_cast<const LT*>(a.Llr) + off);
+    const LP r = *reinterpret_cast<const LP*>(static_cast<const LT*>(a.Lrl) + off);
+    const LP t = *reinterpret_cast<const LP*>(static_cast<const LT*>(a.Ltb) + off);
+    __shared__ int lds_s[64 * DPL];
+    int s[DPL];
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) s[k] = (int)l.v[k] + (int)r.v[k] + (int)t.v[k];
+    const BandOut o = wta_line<DPL, LPC>(a, s, dbase, lds_s + lane * DPL, lds_s + g * LPC * DPL);
+    if (p < npx && j == 0) reinterpret_cast<BandOut*>(a.band)[p] = o;
 }
 
 // Left-right consistency (disp12MaxDiff) and band borders: one workgroup per row.
@@ -640,10 +676,9 @@ __global__ __launch_bounds__(256) void k_cc_apply(int16_t* img, int H, int W, in
 // Line plans: (lanes per line, disparities per lane).
 //  * horizontal paths: 16-lane lines.  One wave per SIMD issues the W-step chain; 32-lane
 //    lines (1080 waves at 1080p, some SIMDs holding two) measured 490 vs 471 us.
-//  * vertical path + WTA: 32-lane lines for D > 32.  The per-row argmin / uniqueness /
-//    sub-pixel work is off the chain and issue-bound: 32-lane lines spread it over twice
-//    the waves (448 -> 896 at 1080p D=128: 872 -> 639 us; 532 us after the WTA trims and
-//    with v_permlane16_swap instead of ds_swizzle joining the two rows of a line).
+//  * vertical path and WTA: 32-lane lines for D > 32 (two DPP rows joined by
+//    v_permlane16_swap).  The vertical path runs beside the horizontal ones on a second
+//    stream; 16-lane lines there measured the same (536 vs 528 us, concurrent).
 struct PathPlan {
     int lpc, dpl;
 };
@@ -666,29 +701,46 @@ PathPlan vpath_plan(int D) {
 PathPlan hpath_plan(int D) { return hpath16_plan(D); }
 
 template <typename LT>
-int launch_paths_t(const SgbmArgs& a, hipStream_t s) {
-    const PathPlan ph = hpath_plan(a.D), pv = vpath_plan(a.D);
-    const dim3 gh((a.H + 64 / ph.lpc - 1) / (64 / ph.lpc), 2), gv((a.Wb + 64 / pv.lpc - 1) / (64 / pv.lpc));
-    bool h = false, v = false;
+int launch_paths_t(const SgbmArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
+    const PathPlan ph = hpath_plan(a.D), pv = vpath_plan(a.D), pw = pv;
+    const dim3 gh((a.H + 3) / 4, 2), gv((a.Wb + 64 / pv.lpc - 1) / (64 / pv.lpc));
+    const size_t npx = (size_t)a.H * a.Wb;
+    const dim3 gw((unsigned)((npx + 64 / pw.lpc - 1) / (64 / pw.lpc)));
+    // vertical path on the second stream, beside the horizontal paths
+    hipStream_t sv = aux ? aux : s;
+    if (aux) {
+        if (hipEventRecord(fork, s) != hipSuccess || hipStreamWaitEvent(aux, fork, 0) != hipSuccess)
+            return (int)hipErrorLaunchFailure;
+    }
+    bool v = false, h = false, w = false;
+#define SV_VPATH(L, N, PF)                                                           \
+    if (!v && pv.lpc == L && pv.dpl == N) {                                          \
+        hipLaunchKernelGGL((k_sgbm_vpath<N, L, LT, PF>), gv, dim3(64), 0, sv, a);   \
+        v = true;                                                                    \
+    }
+    SV_VPATH(16, 1, 16) SV_VPATH(16, 2, 16)
+    SV_VPATH(32, 2, 16) SV_VPATH(32, 4, 12) SV_VPATH(32, 6, 10) SV_VPATH(32, 8, 8) SV_VPATH(32, 10, 6)
+    SV_VPATH(32, 12, 4) SV_VPATH(32, 16, 3)
+#undef SV_VPATH
+    if (aux && hipEventRecord(join, aux) != hipSuccess) return (int)hipErrorLaunchFailure;
 #define SV_HPATH(L, N, PF)                                                           \
     if (!h && ph.lpc == L && ph.dpl == N) {                                          \
         hipLaunchKernelGGL((k_sgbm_hpath<N, L, LT, PF>), gh, dim3(64), 0, s, a);    \
         h = true;                                                                    \
     }
-#define SV_VPATH(L, N, PF)                                                           \
-    if (!v && pv.lpc == L && pv.dpl == N) {                                          \
-        hipLaunchKernelGGL((k_sgbm_vpath<N, L, LT, PF>), gv, dim3(64), 0, s, a);    \
-        v = true;                                                                    \
-    }
     SV_HPATH(16, 1, 24) SV_HPATH(16, 2, 24) SV_HPATH(16, 4, 16) SV_HPATH(16, 8, 16) SV_HPATH(16, 12, 10)
     SV_HPATH(16, 16, 8) SV_HPATH(16, 20, 6) SV_HPATH(16, 24, 6) SV_HPATH(16, 32, 4)
-    if (!h) return (int)hipErrorInvalidValue;
-    SV_VPATH(16, 1, 16) SV_VPATH(16, 2, 16)
-    SV_VPATH(32, 2, 16) SV_VPATH(32, 4, 12) SV_VPATH(32, 6, 10) SV_VPATH(32, 8, 8) SV_VPATH(32, 10, 6)
-    SV_VPATH(32, 12, 4) SV_VPATH(32, 16, 3)
 #undef SV_HPATH
-#undef SV_VPATH
-    if (!v) return (int)hipErrorInvalidValue;
+    if (aux && hipStreamWaitEvent(s, join, 0) != hipSuccess) return (int)hipErrorLaunchFailure;
+#define SV_WTA(L, N)                                                                 \
+    if (!w && pw.lpc == L && pw.dpl == N) {                                          \
+        hipLaunchKernelGGL((k_sgbm_wta<N, L, LT>), gw, dim3(64), 0, s, a);           \
+        w = true;                                                                    \
+    }
+    SV_WTA(16, 1) SV_WTA(16, 2) SV_WTA(32, 2) SV_WTA(32, 4) SV_WTA(32, 6) SV_WTA(32, 8) SV_WTA(32, 10)
+    SV_WTA(32, 12) SV_WTA(32, 16)
+#undef SV_WTA
+    if (!v || !h || !w) return (int)hipErrorInvalidValue;
     return (int)hipGetLastError();
 }
 
@@ -707,7 +759,7 @@ int sgbm_dp(int D) {
     return (D + l - 1) / l * l;
 }
 
-int launch_sgbm(const SgbmArgs& a, hipStream_t s) {
+int launch_sgbm(const SgbmArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
     if (a.H <= 0 || a.W <= 0) return 0;
     if (a.Wb > 0) {
         if (a.r > kMaxR) return (int)hipErrorInvalidValue;
@@ -721,7 +773,8 @@ int launch_sgbm(const SgbmArgs& a, hipStream_t s) {
         }
         const size_t plane = (size_t)a.Wb * a.Dp;
         hipLaunchKernelGGL(k_sgbm_vsum, dim3((unsigned)((plane + 255) / 256)), dim3(256), 0, s, a);
-        const int e = a.l32 ? launch_paths_t<int32_t>(a, s) : launch_paths_t<int16_t>(a, s);
+        const int e = a.l32 ? launch_paths_t<int32_t>(a, s, aux, fork, join)
+                            : launch_paths_t<int16_t>(a, s, aux, fork, join);
         if (e) return e;
     }
     hipLaunchKernelGGL(k_sgbm_lrcheck, dim3(a.H), dim3(256), (size_t)a.W * 8, s, a);

@@ -229,12 +229,18 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
         if (pp.out_b) pp.out_b += o;
     }
     const int x0 = blockIdx.x * MQ_W, y0 = row0 + blockIdx.y * MQ_H;
-    for (int i = threadIdx.x; i < (MQ_H + 2) * (MQ_W + 4); i += 256) {
-        const int r = i / (MQ_W + 4), c = i % (MQ_W + 4);
-        const size_t xc = (size_t)clampi(x0 - 2 + c, 0, W - 1);
-        const uint16_t a = (uint16_t)in[(size_t)clampi(y0 - 2 + r, 0, H - 1) * W + xc];
-        const uint16_t b = (uint16_t)in[(size_t)clampi(y0 + r, 0, H - 1) * W + xc];
-        t2[r][c] = (uint32_t)a | ((uint32_t)b << 16);
+    {   // thread -> one tile column (clamped once), rows g, g+3, ...: 204 of 256 threads load
+        constexpr int TC = MQ_W + 4, TR = MQ_H + 2, G = 256 / TC;   // 68 columns, 3 row groups
+        const int c = threadIdx.x % TC, g = threadIdx.x / TC;
+        if (g < G) {
+            const int16_t* col = in + clampi(x0 - 2 + c, 0, W - 1);
+#pragma unroll
+            for (int r = g; r < TR; r += G) {
+                const uint16_t a = (uint16_t)col[(size_t)clampi(y0 - 2 + r, 0, H - 1) * W];
+                const uint16_t b = (uint16_t)col[(size_t)clampi(y0 + r, 0, H - 1) * W];
+                t2[r][c] = (uint32_t)a | ((uint32_t)b << 16);
+            }
+        }
     }
     __syncthreads();
     const int tx = threadIdx.x % MQ_W, tb = 4 * (threadIdx.x / MQ_W);

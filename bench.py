@@ -204,8 +204,8 @@ def main():
     ap.add_argument("--win", type=int, default=9)
     ap.add_argument("--cost", default="sad", choices=["sad", "ssd", "hog", "sgbm"],
                     help="sad/ssd/hog: the north_star WTA engine; sgbm: the SGBM-3WAY mode")
-    ap.add_argument("--frames", type=int, default=8, help="distinct resident frames per rank")
-    ap.add_argument("--batch", type=int, default=8,
+    ap.add_argument("--frames", type=int, default=16, help="distinct resident frames per rank")
+    ap.add_argument("--batch", type=int, default=16,
                     help="frames mode: frames per step, one launch per kernel over the batch "
                          "(sv_depth_map_batch_dev); 1 = one frame per call (latency mode)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)

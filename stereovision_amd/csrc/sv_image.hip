@@ -10,6 +10,7 @@
 //  * k_post        the post-processing alone on an f32 disparity
 // All are HBM-bound stencils: LDS tiles with halos, one read and one write per pixel.
 // Built with -ffp-contract=off so every f32 operation rounds exactly like NumPy's.
+#include <type_traits>
 #include "sv_internal.h"
 #include "sv_median_net.h"
 
@@ -159,7 +160,10 @@ __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g,
 
 // ---------------------------------------------------------------------------------------
 // Post-processing of one f32 disparity value (shared by the median kernels and k_post).
-__device__ __forceinline__ void post_one(const PostParams& pp, size_t i, float d) {
+struct PostVals { float a, b; uint8_t u; };
+
+__device__ __forceinline__ PostVals post_vals(const PostParams& pp, float d) {
+    PostVals o{0.0f, 0.0f, 0};
     if (pp.mode == POST_DEPTH) {
         // depth_map.py:925-936 — NumPy-2 keeps float32 throughout
         const float fxb = (float)(700 * 0.08);
@@ -168,11 +172,11 @@ __device__ __forceinline__ void post_one(const PostParams& pp, size_t i, float d
         float dc = depth < pp.minf ? pp.minf : depth;
         dc = dc > pp.maxf ? pp.maxf : dc;
         const bool valid = (d > pp.min_disp_global) && (dc >= pp.minf) && (dc <= pp.maxf);
-        pp.out_a[i] = valid ? dc : 0.0f;
+        o.a = valid ? dc : 0.0f;
         float t = dc - pp.minf;
         t = t / pp.rangef;
         t = t * 255.0f;
-        pp.out_u8[i] = (uint8_t)(int)t;
+        o.u = (uint8_t)(int)t;
     } else if (pp.mode == POST_SCALED) {
         // fused_depth_map.py:1010-1024
         const float lo = (float)pp.min_disp, hi = (float)(pp.min_disp + pp.num_disp - 1);
@@ -181,11 +185,20 @@ __device__ __forceinline__ void post_one(const PostParams& pp, size_t i, float d
         float t = c - lo;
         t = t / (float)pp.num_disp;
         t = t * 255.0f;
-        const uint8_t u = (uint8_t)(int)t;
-        pp.out_u8[i] = u;
-        pp.out_a[i] = (float)u;
-        pp.out_b[i] = (d > (float)(pp.min_disp + 1) && d < hi) ? 1.0f : 0.0f;
+        o.u = (uint8_t)(int)t;
+        o.a = (float)o.u;
+        o.b = (d > (float)(pp.min_disp + 1) && d < hi) ? 1.0f : 0.0f;
     }
+    return o;
+}
+
+// Post-processing of one f32 disparity value (shared by the median kernels and k_post).
+__device__ __forceinline__ void post_one(const PostParams& pp, size_t i, float d) {
+    if (pp.mode == POST_NONE) return;
+    const PostVals o = post_vals(pp, d);
+    pp.out_a[i] = o.a;
+    pp.out_u8[i] = o.u;
+    if (pp.mode == POST_SCALED) pp.out_b[i] = o.b;
 }
 
 // Median-of-25 for the int16 map, 4 output rows per lane.
@@ -202,17 +215,25 @@ constexpr int MQ_W = 64, MQ_H = 16;       // k_median_i16: 64 columns x 16 rows 
 
 __device__ __forceinline__ s2 as_s2(uint32_t u) { return __builtin_bit_cast(s2, u); }
 
-__device__ __forceinline__ void emit_median(const PostParams& pp, float* disp, size_t i, int mv) {
-    const float d = (float)mv / 16.0f;
-    disp[i] = d;
-    const int li = mv - pp.lut_m0;
-    if (pp.mode != POST_NONE && li >= 0 && li < pp.lut_n) {   // table lookup (exact)
-        pp.out_a[i] = pp.lut_a[li];
-        pp.out_u8[i] = pp.lut_u8[li];
-        if (pp.mode == POST_SCALED) pp.out_b[i] = pp.lut_b[li];
-    } else {
-        post_one(pp, i, d);
+// Element i of a frame-based array through a 32-bit byte offset from a uniform base, so
+// loads and stores take the saddr + 32-bit voffset form (no 64-bit address arithmetic per
+// access; launch_median_i16 bounds a frame to < 2^30 elements).
+template <typename T>
+__device__ __forceinline__ T& at(T* base, uint32_t i) {
+    using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+    return *reinterpret_cast<T*>(reinterpret_cast<B*>(base) + (uint32_t)(i * (uint32_t)sizeof(T)));
+}
+
+__device__ __forceinline__ PostVals post_median(const PostParams& pp, int mv) {
+    const uint32_t li = (uint32_t)(mv - pp.lut_m0);
+    if (li < (uint32_t)pp.lut_n) {   // table lookup (exact)
+        PostVals o;
+        o.a = at(pp.lut_a, li);
+        o.u = at(pp.lut_u8, li);
+        o.b = pp.mode == POST_SCALED ? at(pp.lut_b, li) : 0.0f;
+        return o;
     }
+    return post_vals(pp, (float)mv / 16.0f);
 }
 
 __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ in, int H, int W,
@@ -233,19 +254,19 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
         constexpr int TC = MQ_W + 4, TR = MQ_H + 2, G = 256 / TC;   // 68 columns, 3 row groups
         const int c = threadIdx.x % TC, g = threadIdx.x / TC;
         if (g < G) {
-            const int16_t* col = in + clampi(x0 - 2 + c, 0, W - 1);
+            const uint32_t cx = (uint32_t)clampi(x0 - 2 + c, 0, W - 1);
 #pragma unroll
             for (int r = g; r < TR; r += G) {
-                const uint16_t a = (uint16_t)col[(size_t)clampi(y0 - 2 + r, 0, H - 1) * W];
-                const uint16_t b = (uint16_t)col[(size_t)clampi(y0 + r, 0, H - 1) * W];
+                const uint16_t a = (uint16_t)at(in, (uint32_t)clampi(y0 - 2 + r, 0, H - 1) * W + cx);
+                const uint16_t b = (uint16_t)at(in, (uint32_t)clampi(y0 + r, 0, H - 1) * W + cx);
                 t2[r][c] = (uint32_t)a | ((uint32_t)b << 16);
             }
         }
     }
     __syncthreads();
+    // every thread computes (the tile is clamped, so columns/rows past the edge read valid
+    // data); only in-range pixels are written, after the LDS transpose below
     const int tx = threadIdx.x % MQ_W, tb = 4 * (threadIdx.x / MQ_W);
-    const int x = x0 + tx, y = y0 + tb;
-    if (x >= W || y >= row1) return;
 
     s2 v[20];
 #pragma unroll
@@ -279,11 +300,49 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
             r = __builtin_elementwise_min(r, __builtin_elementwise_max(v[SV_SEL20_OUT[i]], u[4 - i]));
         m[h] = r;
     }
-    // m[0] = (row y, row y+2), m[1] = (row y+1, row y+3)
-    const int mv[4] = {m[0].x, m[1].x, m[0].y, m[1].y};
+    // m[0] = (row y, row y+2), m[1] = (row y+1, row y+3): park the four medians in LDS, then
+    // re-read them as 4 consecutive columns of one row per thread so the outputs leave as
+    // 16-byte (f32) and 4-byte (u8) stores instead of 4-byte / 1-byte ones
+    __shared__ int16_t med[MQ_H][MQ_W];
+    med[tb][tx] = m[0].x;
+    med[tb + 1][tx] = m[1].x;
+    med[tb + 2][tx] = m[0].y;
+    med[tb + 3][tx] = m[1].y;
+    __syncthreads();
+    const int r = threadIdx.x >> 4, c4 = (threadIdx.x & 15) * 4;
+    const int y = y0 + r, x = x0 + c4;
+    if (y >= row1 || x >= W) return;
+    const uint2 raw = *reinterpret_cast<const uint2*>(&med[r][c4]);
+    const int mv[4] = {(int)(int16_t)(raw.x & 0xFFFF), (int)(int16_t)(raw.x >> 16),
+                       (int)(int16_t)(raw.y & 0xFFFF), (int)(int16_t)(raw.y >> 16)};
+    const uint32_t i = (uint32_t)y * W + x;
+    const bool vec = x + 3 < W && (W & 3) == 0 &&
+                     (((uintptr_t)disp | (uintptr_t)pp.out_a | (uintptr_t)pp.out_b) & 15) == 0 &&
+                     ((uintptr_t)pp.out_u8 & 3) == 0;
+    if (vec) {
+        at(reinterpret_cast<float4*>(disp), i >> 2) =
+            make_float4((float)mv[0] / 16.0f, (float)mv[1] / 16.0f, (float)mv[2] / 16.0f, (float)mv[3] / 16.0f);
+        if (pp.mode == POST_NONE) return;
+        PostVals o[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-        if (y + q < row1) emit_median(pp, disp, (size_t)(y + q) * W + x, mv[q]);
+        for (int q = 0; q < 4; ++q) o[q] = post_median(pp, mv[q]);
+        at(reinterpret_cast<float4*>(pp.out_a), i >> 2) = make_float4(o[0].a, o[1].a, o[2].a, o[3].a);
+        at(reinterpret_cast<uint32_t*>(pp.out_u8), i >> 2) =
+            (uint32_t)o[0].u | ((uint32_t)o[1].u << 8) | ((uint32_t)o[2].u << 16) | ((uint32_t)o[3].u << 24);
+        if (pp.mode == POST_SCALED)
+            at(reinterpret_cast<float4*>(pp.out_b), i >> 2) = make_float4(o[0].b, o[1].b, o[2].b, o[3].b);
+        return;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (x + q >= W) break;
+        at(disp, i + q) = (float)mv[q] / 16.0f;
+        if (pp.mode == POST_NONE) continue;
+        const PostVals o = post_median(pp, mv[q]);
+        at(pp.out_a, i + q) = o.a;
+        at(pp.out_u8, i + q) = o.u;
+        if (pp.mode == POST_SCALED) at(pp.out_b, i + q) = o.b;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_median_f32(const float* __restrict__ in, int H, int W,
@@ -353,6 +412,7 @@ int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0
 int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float* disp,
                       const PostParams& pp, hipStream_t s, int nf, long long fs_in, long long fs_out) {
     if (row1 <= row0 || nf <= 0) return 0;
+    if ((long long)H * W >= (1LL << 30)) return (int)hipErrorInvalidValue;   // 32-bit offsets
     hipLaunchKernelGGL(k_median_i16, dim3((W + MQ_W - 1) / MQ_W, (row1 - row0 + MQ_H - 1) / MQ_H, nf),
                        dim3(256), 0, s, in, H, W, row0, row1, disp, pp, fs_in, fs_out);
     return (int)hipGetLastError();

@@ -182,3 +182,12 @@ def test_gpu_filter_speckles_1080p_property(engine):
             else:
                 exp[y + 20:y + 20 + s, x + 20:x + 20 + s] = -16
     np.testing.assert_array_equal(engine.filter_speckles(img, -16, 100, 32), exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,D,win", [(300, 120, 32, 9), (257, 96, 16, 3), (130, 72, 48, 15)])
+def test_gpu_sgbm_tall_frames_row_bands(engine, H, W, D, win):
+    """Tall frames: the window-row sums run in row bands of >= 64 rows (k_sgbm_vsum8), each
+    band re-summing its first window; band seams must be invisible."""
+    L, R, _ = stereo_pair(H, W, D, seed=H + W)
+    np.testing.assert_array_equal(engine.sgbm(L, R, 0, D, win), SG.sgbm(L, R, 0, D, win))

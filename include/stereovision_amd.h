@@ -30,6 +30,8 @@
  *   sv_select_count/ranks            order statistics of np.percentile in
  *                                    calibrate_midas_to_stereo / normalize_to_stereo_range
  *                                    (fused_depth_map.py:1169-1257, 1503-1554)
+ *   sv_multi_gpu_batch               the per-frame create_depth_map loop, frame-sharded over
+ *                                    several devices from one process
  *   sv_rectify_pair                  the two remap calls of apply_stereo_rectification
  *                                    (depth_map.py:779-834, fused_depth_map.py:444-500) with
  *                                    the maps resident on the device
@@ -194,6 +196,18 @@ int sv_depth_map_batch_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_
                            float max_depth, float depth_range, float min_disp_global,
                            float* d_depth, float* d_disparity, uint8_t* d_norm, void* stream);
 
+/* Frame-sharded batch over several devices from ONE host process:
+ * replaces the reference's per-frame loop over create_depth_map (depth_map.py:837-946,
+ * called once per captured frame; fused_depth_map.py:2591-2598 submits frames to a worker
+ * pool).  Host frames f of left/right at + f*H*W*channels (channels 1 = gray, 3 = BGR);
+ * outputs dense per frame (+ f*H*W).  Frames are split into ndev contiguous shards; context
+ * k (its own device and stream) stages, computes and returns shard k on its own host
+ * thread, concurrently with the others.  Every context must be distinct; the post-
+ * processing is create_depth_map's (depth_final, disparity, depth_normalized). */
+int sv_multi_gpu_batch(sv_ctx* const* ctxs, int ndev, const uint8_t* left, const uint8_t* right, int n_frames,
+                       int H, int W, int channels, int min_disp, int num_disp, int win, int cost, float min_depth,
+                       float max_depth, float depth_range, float min_disp_global, float* depth_final,
+                       float* disparity, uint8_t* depth_normalized);
 int sv_harris_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, float* d_out,
                   void* stream);
 int sv_hog_hist_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, int win,

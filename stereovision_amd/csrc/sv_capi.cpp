@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <new>
 #include <string>
 #include <vector>
@@ -726,6 +727,93 @@ int sv_depth_map_batch_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_ri
     if (rc) return rc;
     SV_LAUNCH(c, SV_K_MEDIAN, s,
               sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, d_disparity, pp, s, n_frames, fs, fs));
+    return 0;
+}
+
+// One shard of sv_multi_gpu_batch: frames [f0, f1) on context c (host buffers in and out).
+namespace {
+int depth_map_shard(sv_ctx* c, const uint8_t* left, const uint8_t* right, int f0, int f1, int H, int W,
+                    int channels, int min_disp, int num_disp, int win, int cost, float min_depth,
+                    float max_depth, float depth_range, float min_disp_global, float* depth_final,
+                    float* disparity, uint8_t* depth_normalized) {
+    SV_ENTER(c);
+    const int nf = f1 - f0;
+    if (nf <= 0) return 0;
+    const size_t n = (size_t)H * W, fin = n * channels;
+    // host frames -> pinned staging -> device (one copy per camera for the whole shard)
+    SV_HIP(c->hin.ensure(2 * nf * fin));
+    SV_HIP(c->gray[0].ensure(nf * n));
+    SV_HIP(c->gray[1].ensure(nf * n));
+    const uint8_t* src[2] = {left, right};
+    for (int k = 0; k < 2; ++k) {
+        uint8_t* stage = c->hin.as<uint8_t>() + k * nf * fin;
+        std::memcpy(stage, src[k] + (size_t)f0 * fin, nf * fin);
+        if (channels == 1) {
+            SV_HIP(hipMemcpyAsync(c->gray[k].p, stage, nf * fin, hipMemcpyHostToDevice, c->stream));
+        } else {
+            SV_HIP(c->img[k].ensure(nf * fin));
+            SV_HIP(hipMemcpyAsync(c->img[k].p, stage, nf * fin, hipMemcpyHostToDevice, c->stream));
+            for (int f = 0; f < nf; ++f)
+                SV_LAUNCH(c, SV_K_GRAY, c->stream,
+                          sv::launch_gray(c->img[k].as<uint8_t>() + f * fin, H, W, W * channels,
+                                          c->gray[k].as<uint8_t>() + f * n, c->stream));
+        }
+    }
+    SV_HIP(c->d16.ensure(nf * n * sizeof(int16_t)));
+    SV_HIP(c->fa.ensure(nf * n * sizeof(float)));
+    SV_HIP(c->fb.ensure(nf * n * sizeof(float)));
+    SV_HIP(c->u8.ensure(nf * n));
+    int rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
+                               win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream, nf, (long long)n, (long long)n);
+    if (rc) return rc;
+    sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                                  num_disp, c->fb.as<float>(), c->u8.as<uint8_t>(), nullptr);
+    rc = attach_lut(c, pp, c->stream);
+    if (rc) return rc;
+    SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
+              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fa.as<float>(), pp, c->stream, nf,
+                                    (long long)n, (long long)n));
+    Out o[] = {{depth_final + (size_t)f0 * n, c->fb.p, nf * n * sizeof(float)},
+               {disparity + (size_t)f0 * n, c->fa.p, nf * n * sizeof(float)},
+               {depth_normalized + (size_t)f0 * n, c->u8.p, nf * n}};
+    return collect(c, o, 3);
+}
+}  // namespace
+
+int sv_multi_gpu_batch(sv_ctx* const* ctxs, int ndev, const uint8_t* left, const uint8_t* right, int n_frames,
+                       int H, int W, int channels, int min_disp, int num_disp, int win, int cost, float min_depth,
+                       float max_depth, float depth_range, float min_disp_global, float* depth_final,
+                       float* disparity, uint8_t* depth_normalized) {
+    if (!ctxs || ndev < 1) return fail(SV_EINVAL, "no contexts");
+    for (int k = 0; k < ndev; ++k) {
+        if (!ctxs[k]) return fail(SV_EINVAL, "null context");
+        for (int j = 0; j < k; ++j)
+            if (ctxs[j] == ctxs[k]) return fail(SV_EINVAL, "a context appears twice");
+    }
+    if (n_frames < 0) return fail(SV_EINVAL, "negative frame count");
+    if (n_frames == 0) return 0;
+    if (!left || !right || !depth_final || !disparity || !depth_normalized) return fail(SV_EINVAL, "null buffers");
+    if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
+    sv::MatchPlan plan;
+    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    // contiguous shards, one host thread per context: each stages, computes and collects
+    // its frames on its own device/stream concurrently with the others
+    std::vector<int> rcs(ndev, 0);
+    std::vector<std::string> errs(ndev);
+    std::vector<std::thread> th;
+    for (int k = 0; k < ndev; ++k) {
+        const int f0 = (int)((long long)n_frames * k / ndev), f1 = (int)((long long)n_frames * (k + 1) / ndev);
+        th.emplace_back([&, k, f0, f1] {
+            rcs[k] = depth_map_shard(ctxs[k], left, right, f0, f1, H, W, channels, min_disp, num_disp, win, cost,
+                                     min_depth, max_depth, depth_range, min_disp_global, depth_final, disparity,
+                                     depth_normalized);
+            if (rcs[k]) errs[k] = g_err;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int k = 0; k < ndev; ++k)
+        if (rcs[k]) return fail(rcs[k], "device shard " + std::to_string(k) + ": " + errs[k]);
     return 0;
 }
 

@@ -38,7 +38,7 @@ EXPORTED = [
     "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
     "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
     "sv_select_ranks", "sv_affine_f32_dev", "sv_sgbm", "sv_sgbm_dev", "sv_filter_speckles",
-    "sv_filter_speckles_dev",
+    "sv_filter_speckles_dev", "sv_multi_gpu_batch",
 ]
 
 
@@ -123,6 +123,9 @@ def _declare(lib):
         "sv_depth_map": ([_vp, _u8p, _u8p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                           _c_int, _c_int, _c_float, _c_float, _c_float, _c_float, _f32p, _f32p,
                           _u8p], _c_int),
+        "sv_multi_gpu_batch": ([ctypes.POINTER(_vp), _c_int, _u8p, _u8p, _c_int, _c_int, _c_int,
+                                _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float,
+                                _c_float, _c_float, _f32p, _f32p, _u8p], _c_int),
         "sv_stereo_scaled": ([_vp, _u8p, _u8p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                               _c_int, _c_int, _f32p, _f32p, _u8p, _f32p], _c_int),
         "sv_harris": ([_vp, _u8p, _c_int, _c_int, _c_int, _f32p], _c_int),
@@ -728,6 +731,34 @@ class Engine:
         _check("sv_profile_read", self.lib.sv_profile_read(self._h, k, ctypes.byref(ms),
                                                            ctypes.byref(n)))
         return ms.value, n.value
+
+
+def multi_gpu_batch(engines, left, right, min_disp: int, num_disp: int, win: int,
+                    min_depth: float, max_depth: float, min_disp_global=None, cost="sad"):
+    """create_depth_map over a stack of frames (depth_map.py:837-946, once per frame),
+    frame-sharded over the devices of `engines` from this one process (sv_multi_gpu_batch:
+    one host thread + stream per device, contiguous shards).  left/right: F x H x W gray or
+    F x H x W x 3 BGR uint8.  Returns (depth_final, disparity, depth_normalized), F x H x W."""
+    engines = list(engines)
+    if not engines:
+        raise ValueError("no engines")
+    left = np.ascontiguousarray(left, dtype=np.uint8)
+    right = np.ascontiguousarray(right, dtype=np.uint8)
+    if left.shape != right.shape or left.ndim not in (3, 4) or (left.ndim == 4 and left.shape[3] != 3):
+        raise ValueError(f"expected matching F x H x W (x 3) stacks, got {left.shape} / {right.shape}")
+    F, H, W = left.shape[:3]
+    C = 3 if left.ndim == 4 else 1
+    mdg = min_disp if min_disp_global is None else min_disp_global
+    depth = np.empty((F, H, W), np.float32)
+    disp = np.empty((F, H, W), np.float32)
+    norm = np.empty((F, H, W), np.uint8)
+    hs = (_vp * len(engines))(*[e._h for e in engines])
+    lib = engines[0].lib
+    _check("sv_multi_gpu_batch", lib.sv_multi_gpu_batch(
+        hs, len(engines), left, right, F, H, W, C, int(min_disp), int(num_disp), int(win),
+        _cost(cost), np.float32(min_depth), np.float32(max_depth),
+        np.float32(float(max_depth) - float(min_depth)), np.float32(mdg), depth, disp, norm))
+    return depth, disp, norm
 
 
 _engines: dict[int, Engine] = {}

@@ -67,8 +67,9 @@ def cpu_baseline_sgbm(H, W, D, win, seconds):
                       f"in {dt:.1f} s, scaled by {rows}/{H} rows to frames/s; single process"}
 
 
-def cpu_baseline(H, W, D, win, cost, seconds):
-    """C oracle (the port) timed on this host: whole app-1 path per frame."""
+def cpu_baseline(H, W, D, win, cost, seconds, harris=False):
+    """C oracle (the port) timed on this host: whole app-1 path per frame (+ the Harris
+    response of the left frame for C2)."""
     if cost == "sgbm":
         return cpu_baseline_sgbm(H, W, D, win, seconds)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -89,6 +90,8 @@ def cpu_baseline(H, W, D, win, cost, seconds):
         lib.svo_depth_map(np.ascontiguousarray(L[i % 2]), np.ascontiguousarray(R[i % 2]), H, W,
                           0, D, win, costi, np.float32(0.3), np.float32(2.0),
                           np.float32(2.0 - 0.3), depth, disp, norm, threads)
+        if harris:
+            C.harris(np.ascontiguousarray(L[i % 2]))
 
     import ctypes
     f32 = ctypes.c_float
@@ -106,7 +109,8 @@ def cpu_baseline(H, W, D, win, cost, seconds):
     return {
         "value": round(n / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
         "sample": f"{n} full {W}x{H} frames (D={D}, win={win}, {cost}: disparity + median5 + "
-                  f"depth post) of the C oracle, OpenMP {threads} threads, {dt:.1f} s",
+                  f"depth post{' + Harris (1 thread)' if harris else ''}) of the C oracle, "
+                  f"OpenMP {threads} threads, {dt:.1f} s",
     }
 
 
@@ -223,6 +227,8 @@ def main():
                     help="camera pipeline: raw BGR frames resident in HBM -> rectify+gray "
                          "(k_remap, calibrated CV_16SC2 maps) -> disparity -> median/post")
     ap.add_argument("--no-aux", action="store_true", help="skip the aux-kernel rooflines")
+    ap.add_argument("--harris", action="store_true",
+                    help="C2: also compute the Harris response of every left frame (k_harris)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo rehearses N>1 with several ranks on one GPU")
     args = ap.parse_args()
@@ -275,6 +281,10 @@ def main():
         tile = RowTiledDepthMap(H, W, D, win, cost=args.cost, device=dev,
                                 rank=rank, world=world)
 
+    harris = args.harris and not rowtile
+    if harris:
+        hmap = torch.empty((B, H, W), dtype=torch.float32, device=f"cuda:{dev}")
+
     def gather(t):
         if world == 1:
             return
@@ -306,6 +316,9 @@ def main():
             eng.depth_map_batch_dev(pL[f], pR[f], B, H, W, W, H * W, 0, D, win, 0.3, 2.0,
                                     depth.data_ptr(), disp.data_ptr(), norm.data_ptr(),
                                     cost=args.cost, stream=stream)
+        if harris:      # one launch over the batch's left frames
+            eng.harris_batch_dev(gL.data_ptr() if rectify else pL[f], B, H, W, W, H * W,
+                                 hmap.data_ptr(), stream=stream)
         if args.gather:
             gather(disp)
 
@@ -335,6 +348,7 @@ def main():
     match_ms, match_n = eng.profile_read("sgbm" if args.cost == "sgbm" else "match")
     med_ms, med_n = eng.profile_read("median")
     remap_ms, remap_n = eng.profile_read("remap")
+    harris_ms, harris_n = eng.profile_read("harris")
     k_name = "sgbm pipeline (k_sgbm_*)" if args.cost == "sgbm" else "k_match"
 
     if world > 1:
@@ -351,6 +365,8 @@ def main():
     k_avg_s = (match_ms / match_n) * 1e-3 if match_n else None
     k_bytes = 4 * npx                          # 2 u8 images read + int16 map written
     frame_bytes = 11 * H * W                   # 2 u8 in; depth f32 + disparity f32 + u8 out
+    if harris:
+        frame_bytes += 4 * H * W               # + the f32 Harris response
     if rectify:
         frame_bytes = 11 * H * W + 2 * 10 * H * W   # + per camera: map 6 B, BGR 3 B, gray 1 B
     roofline = None
@@ -387,7 +403,10 @@ def main():
                                 "raw BGR frames resident in HBM -> rectify+gray (k_remap) -> "
                                 "disparity -> median5 + depth post" if rectify else
                                 f"{W}x{H} D={D} win={win} {args.cost.upper()} depth_map path "
-                                "(disparity + median5 + depth post), gray inputs resident in HBM"),
+                                "(disparity + median5 + depth post" + (" + Harris response"
+                                                                        if harris else "") +
+                                "), gray inputs resident in HBM"),
+                   "harris": harris,
                    "height": H, "width": W, "num_disp": D, "win": win, "cost": args.cost,
                    "frames_resident_per_rank": 1 if rowtile else F,
                    "frames_per_step": 1 if rowtile else B,
@@ -415,9 +434,14 @@ def main():
             result["aux_kernels"] = aux_kernels(eng, dev, H, W, B, stream, med_ms, med_n)
         except Exception as e:  # reported, never required
             log(f"aux kernels failed: {e}")
+    if harris and harris_n:     # 1 B/px gray read + 4 B/px f32 response written
+        result["aux_kernels"] = dict(result["aux_kernels"] or {})
+        result["aux_kernels"]["k_harris"] = hbm_entry("k_harris_lds", 5 * H * W * B, harris_ms,
+                                                       harris_n)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(H, W, D, win, args.cost, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(H, W, D, win, args.cost, args.cpu_seconds,
+                                                  harris=harris)
         except Exception as e:  # the baseline is reported, never required
             log(f"cpu baseline failed: {e}")
     if rank == 0:

@@ -210,6 +210,11 @@ int sv_multi_gpu_batch(sv_ctx* const* ctxs, int ndev, const uint8_t* left, const
                        float* disparity, uint8_t* depth_normalized);
 int sv_harris_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, float* d_out,
                   void* stream);
+/* Harris response of n_frames gray frames (frame z at d_gray + z*frame_stride bytes, output
+ * dense at d_out + z*H*W floats), one launch for the batch (C2: Harris beside the disparity
+ * of a frame stream). */
+int sv_harris_batch_dev(sv_ctx* ctx, const uint8_t* d_gray, int n_frames, int H, int W, int pitch,
+                        int64_t frame_stride, float* d_out, void* stream);
 int sv_hog_hist_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, int win,
                     int row0, int row1, uint16_t* d_out, void* stream);
 

@@ -825,6 +825,20 @@ int sv_harris_dev(sv_ctx* c, const uint8_t* d_gray, int H, int W, int pitch, flo
     return 0;
 }
 
+int sv_harris_batch_dev(sv_ctx* c, const uint8_t* d_gray, int n_frames, int H, int W, int pitch,
+                        int64_t frame_stride, float* d_out, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_gray, H, W) || !d_out || n_frames < 0) return fail(SV_EINVAL, "bad harris arguments");
+    if (pitch < W) return fail(SV_EINVAL, "pitch smaller than width");
+    if (n_frames > 1 && frame_stride < (int64_t)pitch * H) return fail(SV_EINVAL, "frame stride smaller than a frame");
+    if (n_frames == 0) return 0;
+    hipStream_t s = pick(c, stream);
+    SV_LAUNCH(c, SV_K_HARRIS, s,
+              sv::launch_harris(d_gray, H, W, pitch, d_out, s, n_frames, (long long)frame_stride,
+                                (long long)H * W));
+    return 0;
+}
+
 int sv_hog_hist_dev(sv_ctx* c, const uint8_t* d_gray, int H, int W, int pitch, int win, int row0, int row1,
                     uint16_t* d_out, void* stream) {
     SV_ENTER(c);

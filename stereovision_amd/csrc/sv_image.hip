@@ -1,7 +1,7 @@
 // sv_image.hip — the stencil kernels around the disparity engine (gfx950).
 //
 //  * k_gray        cv2.cvtColor(BGR2GRAY), 14-bit fixed point   (depth_map.py:871-880)
-//  * k_harris      Harris response, cornerHarris(3, 3, 0.04) convention (north_star)
+//  * k_harris_lds  Harris response, cornerHarris(3, 3, 0.04) convention (north_star)
 //  * k_hog_hist    per-pixel 9-bin gradient orientation + window histograms (north_star)
 //  * k_median_i16  medianBlur(disparity, 5) on the int16 x16 map, fused with the
 //                  reference's post-processing (depth_map.py:909-937 or
@@ -46,42 +46,62 @@ __device__ __forceinline__ void sobel(const uint8_t* g, int H, int W, int pitch,
 }
 
 // ---------------------------------------------------------------------------------------
-// Harris: 16x16 output tile; gradient products for the 18x18 reflected neighbourhood.
-constexpr int HT = 16;
-__global__ __launch_bounds__(256) void k_harris(const uint8_t* __restrict__ g, int H, int W,
-                                                int pitch, float* __restrict__ out) {
-    __shared__ int pxx[HT + 2][HT + 2], pxy[HT + 2][HT + 2], pyy[HT + 2][HT + 2];
-    const int x0 = blockIdx.x * HT, y0 = blockIdx.y * HT;
-    for (int i = threadIdx.x; i < (HT + 2) * (HT + 2); i += 256) {
-        const int ty = i / (HT + 2), tx = i % (HT + 2);
-        const int yy = refl101(clampi(y0 - 1 + ty, -1, H), H);
-        const int xx = refl101(clampi(x0 - 1 + tx, -1, W), W);
-        int gx, gy;
-        sobel(g, H, W, pitch, xx, yy, gx, gy);
-        pxx[ty][tx] = gx * gx;
-        pxy[ty][tx] = gx * gy;
-        pyy[ty][tx] = gy * gy;
+// Harris as one LDS stencil pass (north_star: Sobel + structure tensor fused): a block
+// stages the (64+4) x (16+4) image bytes of its 64 x 16 output tile once, forms the
+// gradient products of the (64+2) x (16+2) in-image positions around it from LDS, and box-
+// sums them per output (4 rows per thread).  Reflect-101 borders index the staged rows/cols
+// directly (every reflected index used lies inside the staged window), so the response is
+// identical to cv2.cornerHarris's convention.  grid.z = frame of a batch.
+constexpr int HX2 = 64, HY2 = 16;
+__global__ __launch_bounds__(256) void k_harris_lds(const uint8_t* __restrict__ g, int H, int W, int pitch,
+                                                    float* __restrict__ out, long long fs_in, long long fs_out) {
+    __shared__ uint8_t img[HY2 + 4][HX2 + 4];
+    __shared__ int pxx[HY2 + 2][HX2 + 2], pxy[HY2 + 2][HX2 + 2], pyy[HY2 + 2][HX2 + 2];
+    g += blockIdx.z * fs_in;
+    out += blockIdx.z * fs_out;
+    const int x0 = blockIdx.x * HX2, y0 = blockIdx.y * HY2;
+    for (int i = threadIdx.x; i < (HY2 + 4) * (HX2 + 4); i += 256) {
+        const int r = i / (HX2 + 4), c = i - r * (HX2 + 4);
+        img[r][c] = g[(size_t)clampi(y0 - 2 + r, 0, H - 1) * pitch + clampi(x0 - 2 + c, 0, W - 1)];
     }
     __syncthreads();
-    const int tx = threadIdx.x % HT, ty = threadIdx.x / HT;
-    const int x = x0 + tx, y = y0 + ty;
-    if (x >= W || y >= H) return;
-    // box over the reflected neighbours: position (x+i) maps to tile column of refl(x+i)
-    int sxx = 0, sxy = 0, syy = 0;
-    for (int j = -1; j <= 1; ++j)
-        for (int i = -1; i <= 1; ++i) {
-            const int ry = refl101(y + j, H) - (y0 - 1);
-            const int rx = refl101(x + i, W) - (x0 - 1);
-            sxx += pxx[ry][rx];
-            sxy += pxy[ry][rx];
-            syy += pyy[ry][rx];
-        }
+    for (int i = threadIdx.x; i < (HY2 + 2) * (HX2 + 2); i += 256) {
+        const int r = i / (HX2 + 2), c = i - r * (HX2 + 2);
+        const int y = y0 - 1 + r, x = x0 - 1 + c;
+        if (y < 0 || y >= H || x < 0 || x >= W) continue;   // never read (box sums reflect)
+        const int ym = refl101(y - 1, H) - (y0 - 2), yp = refl101(y + 1, H) - (y0 - 2), yc = y - (y0 - 2);
+        const int xm = refl101(x - 1, W) - (x0 - 2), xp = refl101(x + 1, W) - (x0 - 2), xc = x - (x0 - 2);
+        const int gx = (img[ym][xp] + 2 * img[yc][xp] + img[yp][xp]) - (img[ym][xm] + 2 * img[yc][xm] + img[yp][xm]);
+        const int gy = (img[yp][xm] + 2 * img[yp][xc] + img[yp][xp]) - (img[ym][xm] + 2 * img[ym][xc] + img[ym][xp]);
+        pxx[r][c] = gx * gx;
+        pxy[r][c] = gx * gy;
+        pyy[r][c] = gy * gy;
+    }
+    __syncthreads();
+    const int tx = threadIdx.x % HX2, tq = 4 * (threadIdx.x / HX2);
+    const int x = x0 + tx;
+    if (x >= W) return;
+    const int cm = refl101(x - 1, W) - (x0 - 1), cc = x - (x0 - 1), cp = refl101(x + 1, W) - (x0 - 1);
     const float s2 = (float)((1.0 / (4.0 * 3.0 * 255.0)) * (1.0 / (4.0 * 3.0 * 255.0)));
-    const float a = (float)sxx * s2, b = (float)sxy * s2, c = (float)syy * s2;
-    const float t1 = a * c, t2 = b * b, t3 = a + c, t4 = t3 * t3;
-    const float rr = t1 - t2;
-    const float kt = 0.04f * t4;
-    out[(size_t)y * W + x] = rr - kt;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int y = y0 + tq + q;
+        if (y >= H) break;
+        const int rows[3] = {refl101(y - 1, H) - (y0 - 1), y - (y0 - 1), refl101(y + 1, H) - (y0 - 1)};
+        int sxx = 0, sxy = 0, syy = 0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int rr = rows[j];
+            sxx += pxx[rr][cm] + pxx[rr][cc] + pxx[rr][cp];
+            sxy += pxy[rr][cm] + pxy[rr][cc] + pxy[rr][cp];
+            syy += pyy[rr][cm] + pyy[rr][cc] + pyy[rr][cp];
+        }
+        const float a = (float)sxx * s2, b = (float)sxy * s2, c = (float)syy * s2;
+        const float t1 = a * c, t2 = b * b, t3 = a + c, t4 = t3 * t3;
+        const float rr = t1 - t2;
+        const float kt = 0.04f * t4;
+        out[(size_t)y * W + x] = rr - kt;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -391,9 +411,11 @@ int launch_gray(const uint8_t* bgr, int H, int W, int pitch, uint8_t* gray, hipS
     return (int)hipGetLastError();
 }
 
-int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_harris, dim3((W + HT - 1) / HT, (H + HT - 1) / HT), dim3(256), 0, s, g, H,
-                       W, pitch, out);
+int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStream_t s, int nf,
+                  long long fs_in, long long fs_out) {
+    if (nf <= 0) return 0;
+    hipLaunchKernelGGL(k_harris_lds, dim3((W + HX2 - 1) / HX2, (H + HY2 - 1) / HY2, nf), dim3(256), 0, s, g,
+                       H, W, pitch, out, fs_in, fs_out);
     return (int)hipGetLastError();
 }
 

@@ -48,7 +48,9 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
 int launch_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v, hipStream_t s);
 
 int launch_gray(const uint8_t* bgr, int H, int W, int pitch, uint8_t* gray, hipStream_t s);
-int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStream_t s);
+// nf frames (grid.z): frame z reads g + z*fs_in bytes and writes out + z*fs_out floats.
+int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStream_t s, int nf = 1,
+                  long long fs_in = 0, long long fs_out = 0);
 int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0, int row1,
                     uint16_t* hist, hipStream_t s);
 

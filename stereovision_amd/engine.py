@@ -38,7 +38,7 @@ EXPORTED = [
     "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
     "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
     "sv_select_ranks", "sv_affine_f32_dev", "sv_sgbm", "sv_sgbm_dev", "sv_filter_speckles",
-    "sv_filter_speckles_dev", "sv_multi_gpu_batch",
+    "sv_filter_speckles_dev", "sv_multi_gpu_batch", "sv_harris_batch_dev",
 ]
 
 
@@ -123,6 +123,8 @@ def _declare(lib):
         "sv_depth_map": ([_vp, _u8p, _u8p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                           _c_int, _c_int, _c_float, _c_float, _c_float, _c_float, _f32p, _f32p,
                           _u8p], _c_int),
+        "sv_harris_batch_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, ctypes.c_int64, _vp,
+                                 _vp], _c_int),
         "sv_multi_gpu_batch": ([ctypes.POINTER(_vp), _c_int, _u8p, _u8p, _c_int, _c_int, _c_int,
                                 _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float,
                                 _c_float, _c_float, _f32p, _f32p, _u8p], _c_int),
@@ -564,6 +566,11 @@ class Engine:
             int(min_disp), int(num_disp), int(win), _cost(cost), np.float32(min_depth),
             np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
             np.float32(mdg), d_depth, d_disp, d_norm, stream or None))
+
+    def harris_batch_dev(self, d_gray: int, n_frames: int, H: int, W: int, pitch: int,
+                         frame_stride: int, d_out: int, stream: int = 0):
+        _check("sv_harris_batch_dev", self.lib.sv_harris_batch_dev(
+            self._h, d_gray, int(n_frames), H, W, pitch, int(frame_stride), d_out, stream or None))
 
     def harris_dev(self, d_gray: int, H: int, W: int, pitch: int, d_out: int, stream: int = 0):
         _check("sv_harris_dev", self.lib.sv_harris_dev(self._h, d_gray, H, W, pitch, d_out,

@@ -444,3 +444,25 @@ def test_torch_first_runtime_and_row_tiled_module():
     """ % (root, os.path.join(root, "oracle")))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("H,W", [(45, 150), (16, 64), (33, 130), (2, 70), (17, 3)])
+def test_harris_batch_dev_per_frame(engine, H, W):
+    """sv_harris_batch_dev (one launch over grid.z, LDS-staged tiles) == the oracle's Harris
+    frame by frame, with a row pitch wider than the frame (tile edges, reflect-101 borders)."""
+    nf, pitch = 3, W + 5
+    rng = np.random.default_rng(H * W)
+    frames = rng.integers(0, 256, (nf, H, pitch), dtype=np.uint8)
+    n = nf * H * pitch
+    dg, dout = engine.dev_alloc(n), engine.dev_alloc(nf * H * W * 4)
+    try:
+        engine.to_device(dg, frames)
+        engine.harris_batch_dev(dg, nf, H, W, pitch, H * pitch, dout)
+        got = engine.to_host(dout, (nf, H, W), np.float32)
+        for z in range(nf):
+            g = np.ascontiguousarray(frames[z, :, :W])
+            assert np.abs(got[z] - O.harris(g)).max() <= HARRIS_TOL, f"frame {z}"
+            np.testing.assert_array_equal(got[z], O.harris(g))     # observed bit-exact
+    finally:
+        engine.dev_free(dg)
+        engine.dev_free(dout)

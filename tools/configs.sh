@@ -17,7 +17,8 @@ for line in open(sys.argv[2]):
               f"median {r.get('median_post_avg_us')} us  batch {d['config'].get('frames_per_step')}")
 PY
 }
-run c1c2_640x480_d64_w9 --height 480 --width 640 --num-disp 64 --win 9
+run c1_640x480_d64_w9 --height 480 --width 640 --num-disp 64 --win 9
+run c2_640x480_d64_w9_harris --height 480 --width 640 --num-disp 64 --win 9 --harris
 run c3_1080p_d128_w11 --win 11
 run metric_1080p_d128_w9
 run metric_batch1 --batch 1

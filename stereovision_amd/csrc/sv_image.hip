@@ -111,70 +111,100 @@ constexpr int GX_MAX = GT_W + 2 * GR_MAX, GY_MAX = GT_H + 2 * GR_MAX;
 __constant__ int c_hog_cos[8] = {15396, 12551, 8192, 2845, -2845, -8192, -12551, -15396};
 __constant__ int c_hog_sin[8] = {5604, 10531, 14189, 16135, 16135, 14189, 10531, 5604};
 
+template <int r>   // window radius: compile-time, so the tile loops index by constants
 __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g, int H, int W,
-                                                  int pitch, int r, int row0, int row1,
+                                                  int pitch, int row0, int row1,
                                                   uint16_t* __restrict__ hist) {
-    __shared__ uint8_t sbin[GY_MAX][GX_MAX];
-    __shared__ uint8_t smag[GY_MAX][GX_MAX];
-    __shared__ uint16_t vsum[GT_H][GX_MAX][9];
-    __shared__ __attribute__((aligned(16))) uint16_t otile[GT_H][GT_W][10];
+    __shared__ uint8_t simg[GY_MAX + 2][GX_MAX + 2];
+    __shared__ uint16_t sbm[GY_MAX][GX_MAX];             // (bin << 8) | magnitude
+    // window-sum records: bins 2k, 2k+1 as the u16 halves of dword k (dword 4's high half
+    // is the zero pad bin 9).  Sums stay below 2^16 (<= 15*15*255), so packed adds and
+    // subtracts never carry or borrow between halves.
+    __shared__ uint32_t vrec[GT_H][GX_MAX][5];
     const int x0 = blockIdx.x * GT_W, y0 = row0 + blockIdx.y * GT_H;
-    const int nx = GT_W + 2 * r, ny = GT_H + 2 * r;
+    constexpr int nx = GT_W + 2 * r, ny = GT_H + 2 * r;
+    // stage the image bytes once (all loads independent): rows y0-r-1 .. y0+GT_H+r and
+    // columns x0-r-1 .. x0+GT_W+r, clamped; every pixel the gradients below read (the
+    // replicate-clamped window positions and their reflect-101 neighbours) lies inside
+    const int sy0 = y0 - r - 1, sx0 = x0 - r - 1;
+    for (int i = threadIdx.x; i < (ny + 2) * (nx + 2); i += 256) {
+        const int ty = i / (nx + 2), tx = i - ty * (nx + 2);
+        simg[ty][tx] = g[(size_t)clampi(sy0 + ty, 0, H - 1) * pitch + clampi(sx0 + tx, 0, W - 1)];
+    }
+    __syncthreads();
     for (int i = threadIdx.x; i < nx * ny; i += 256) {
         const int ty = i / nx, tx = i % nx;
         const int yy = clampi(y0 - r + ty, 0, H - 1);
         const int xx = clampi(x0 - r + tx, 0, W - 1);
-        int gx, gy;
-        sobel(g, H, W, pitch, xx, yy, gx, gy);
+        const int ym = refl101(yy - 1, H) - sy0, yc = yy - sy0, yp = refl101(yy + 1, H) - sy0;
+        const int xm = refl101(xx - 1, W) - sx0, xc = xx - sx0, xp = refl101(xx + 1, W) - sx0;
+        int gx = (simg[ym][xp] + 2 * simg[yc][xp] + simg[yp][xp]) - (simg[ym][xm] + 2 * simg[yc][xm] + simg[yp][xm]);
+        int gy = (simg[yp][xm] + 2 * simg[yp][xc] + simg[yp][xp]) - (simg[ym][xm] + 2 * simg[ym][xc] + simg[ym][xp]);
         const int m = (abs(gx) + abs(gy)) >> 3;
         if (gy < 0 || (gy == 0 && gx < 0)) { gx = -gx; gy = -gy; }
         int b = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) b += (c_hog_cos[k] * gy - c_hog_sin[k] * gx >= 0);
-        sbin[ty][tx] = (uint8_t)b;
-        smag[ty][tx] = (uint8_t)m;
+        sbm[ty][tx] = (uint16_t)((b << 8) | m);
     }
     __syncthreads();
-    // vertical window sums: task = (column, bin)
-    for (int task = threadIdx.x; task < nx * 9; task += 256) {
-        const int tx = task / 9, b = task % 9;
-        uint32_t s = 0;
-        for (int j = 0; j < 2 * r + 1; ++j) s += sbin[j][tx] == b ? smag[j][tx] : 0u;
-        vsum[0][tx][b] = (uint16_t)s;
-        for (int oy = 1; oy < GT_H; ++oy) {
-            const int ja = oy + 2 * r, jd = oy - 1;
-            s += (sbin[ja][tx] == b ? smag[ja][tx] : 0u);
-            s -= (sbin[jd][tx] == b ? smag[jd][tx] : 0u);
-            vsum[oy][tx][b] = (uint16_t)s;
+    // vertical window sums: task = (column, half of the tile's rows), one packed record
+    auto acc = [](uint32_t (&v)[5], uint32_t code, bool add) {
+        const int k = (int)(code >> 9);                                  // bin / 2
+        const uint32_t val = (code & 0xFFu) << ((code & 0x100u) ? 16 : 0);
+#pragma unroll
+        for (int kk = 0; kk < 5; ++kk) {
+            const uint32_t t = kk == k ? val : 0u;
+            v[kk] = add ? v[kk] + t : v[kk] - t;
+        }
+    };
+    for (int task = threadIdx.x; task < nx * 2; task += 256) {
+        const int tx = task >> 1, oy0 = (task & 1) * (GT_H / 2);
+        uint32_t v[5] = {0u, 0u, 0u, 0u, 0u};
+        for (int j = 0; j <= 2 * r; ++j) acc(v, sbm[oy0 + j][tx], true);
+#pragma unroll
+        for (int kk = 0; kk < 5; ++kk) vrec[oy0][tx][kk] = v[kk];
+        for (int oy = oy0 + 1; oy < oy0 + GT_H / 2; ++oy) {
+            acc(v, sbm[oy + 2 * r][tx], true);
+            acc(v, sbm[oy - 1][tx], false);
+#pragma unroll
+            for (int kk = 0; kk < 5; ++kk) vrec[oy][tx][kk] = v[kk];
         }
     }
     __syncthreads();
-    // horizontal window sums: task = (row, bin)
-    for (int task = threadIdx.x; task < GT_H * 10; task += 256) {
-        const int oy = task / 10, b = task % 10;
-        if (b == 9) {
-            for (int ox = 0; ox < GT_W; ++ox) otile[oy][ox][9] = 0;
-            continue;
+    // horizontal window sums: task = (row, run of 4 columns): 256 running sums of 4 steps,
+    // each thread storing its 4 records (80 contiguous bytes) straight to HBM
+    {
+        const int oy = threadIdx.x >> 4, c0 = (threadIdx.x & 15) * 4;
+        const int y = y0 + oy, x = x0 + c0;
+        uint32_t o[4][5];
+        uint32_t v[5] = {0u, 0u, 0u, 0u, 0u};
+        for (int i = 0; i <= 2 * r; ++i)
+#pragma unroll
+            for (int kk = 0; kk < 5; ++kk) v[kk] += vrec[oy][c0 + i][kk];
+#pragma unroll
+        for (int kk = 0; kk < 5; ++kk) o[0][kk] = v[kk];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+#pragma unroll
+            for (int kk = 0; kk < 5; ++kk) {
+                v[kk] += vrec[oy][c0 + q + 2 * r][kk] - vrec[oy][c0 + q - 1][kk];
+                o[q][kk] = v[kk];
+            }
         }
-        uint32_t s = 0;
-        for (int i = 0; i < 2 * r + 1; ++i) s += vsum[oy][i][b];
-        otile[oy][0][b] = (uint16_t)s;
-        for (int ox = 1; ox < GT_W; ++ox) {
-            s += vsum[oy][ox + 2 * r][b];
-            s -= vsum[oy][ox - 1][b];
-            otile[oy][ox][b] = (uint16_t)s;
+        if (y < row1 && x < W) {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(hist + ((size_t)y * W + x) * 10);
+            if (x + 3 < W && ((uintptr_t)dst & 15) == 0) {
+                const uint32_t* f = &o[0][0];
+                uint4* d4 = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+                for (int k = 0; k < 5; ++k) d4[k] = make_uint4(f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
+            } else {
+                for (int q = 0; q < 4 && x + q < W; ++q)
+#pragma unroll
+                    for (int kk = 0; kk < 5; ++kk) dst[q * 5 + kk] = o[q][kk];
+            }
         }
-    }
-    __syncthreads();
-    // coalesced copy-out: each tile row is 64 px * 20 B = 320 dwords, contiguous in HBM
-    const int wv = min(GT_W, W - x0);
-    for (int i = threadIdx.x; i < GT_H * GT_W * 5; i += 256) {
-        const int oy = i / (GT_W * 5), rem = i % (GT_W * 5);
-        const int y = y0 + oy;
-        if (y >= row1 || rem >= wv * 5) continue;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(&otile[oy][0][0]);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(hist + ((size_t)y * W + x0) * 10);
-        dst[rem] = src[rem];
     }
 }
 
@@ -426,8 +456,12 @@ int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0
     if (row0 < 0) row0 = 0;
     if (row1 > H) row1 = H;
     if (row1 <= row0) return 0;
-    hipLaunchKernelGGL(k_hog_hist, dim3((W + GT_W - 1) / GT_W, (row1 - row0 + GT_H - 1) / GT_H),
-                       dim3(256), 0, s, g, H, W, pitch, r, row0, row1, hist);
+    const dim3 grid((W + GT_W - 1) / GT_W, (row1 - row0 + GT_H - 1) / GT_H);
+    switch (r) {
+#define SV_HOG_R(R) case R: hipLaunchKernelGGL(k_hog_hist<R>, grid, dim3(256), 0, s, g, H, W, pitch, row0, row1, hist); break;
+        SV_HOG_R(0) SV_HOG_R(1) SV_HOG_R(2) SV_HOG_R(3) SV_HOG_R(4) SV_HOG_R(5) SV_HOG_R(6) SV_HOG_R(7)
+#undef SV_HOG_R
+    }
     return (int)hipGetLastError();
 }
 

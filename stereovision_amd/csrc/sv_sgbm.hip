@@ -234,31 +234,37 @@ __device__ __forceinline__ uint4 add4(uint4 s, uint4 a, uint4 b) {
     return o;
 }
 
+template <int R>   // window radius: the 2R+1 rows of the window stay in a register ring
 __global__ __launch_bounds__(256) void k_sgbm_vsum8(SgbmArgs a, int vb) {
+    constexpr int W2 = 2 * R + 1;
     const size_t p8 = (size_t)a.Wb * a.Dp / 8;        // uint4 per row plane
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= p8) return;
     const uint4* h = reinterpret_cast<const uint4*>(a.hsum) + i;
     uint4* c = reinterpret_cast<uint4*>(a.C) + i;
-    const int H = a.H, r = a.r;
-    const int y0 = blockIdx.y * vb, y1 = min(H, y0 + vb);
+    const int H = a.H;
+    const int y0 = blockIdx.y * vb, n = min(H, y0 + vb) - y0;
     const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    // ring[k] = row clamp(y0 - R + k): the window of output row y0
+    uint4 ring[W2];
     uint4 s = z;
-    for (int j = -r; j <= r; ++j) s = add4(s, h[(size_t)min(max(y0 + j, 0), H - 1) * p8], z);
+#pragma unroll
+    for (int k = 0; k < W2; ++k) {
+        ring[k] = h[(size_t)min(max(y0 - R + k, 0), H - 1) * p8];
+        s = add4(s, ring[k], z);
+    }
     c[(size_t)y0 * p8] = s;
-    for (int yb = y0 + 1; yb < y1; yb += 4) {   // 8 independent 16-B loads in flight
-        uint4 ad[4], sb[4];
+    // output row y0 + t adds row clamp(y0 + t + R) and drops ring slot (t - 1) mod W2, which
+    // holds row clamp(y0 + t - R - 1); loads past the band stay in the image (clamped)
+    for (int t0 = 1; t0 < n; t0 += W2) {
+        uint4 in[W2];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int y = min(yb + u, H - 1);
-            ad[u] = h[(size_t)min(y + r, H - 1) * p8];
-            sb[u] = h[(size_t)max(y - r - 1, 0) * p8];
-        }
+        for (int u = 0; u < W2; ++u) in[u] = h[(size_t)min(y0 + t0 + u + R, H - 1) * p8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (yb + u >= y1) break;
-            s = add4(s, ad[u], sb[u]);
-            c[(size_t)(yb + u) * p8] = s;
+        for (int u = 0; u < W2; ++u) {
+            s = add4(s, in[u], ring[u]);
+            ring[u] = in[u];
+            if (t0 + u < n) c[(size_t)(y0 + t0 + u) * p8] = s;
         }
     }
 }
@@ -824,8 +830,13 @@ int launch_sgbm(const SgbmArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fo
             const size_t blocks = (plane / 8 + 255) / 256;
             const int nb = (int)std::max<size_t>(1, std::min<size_t>((size_t)a.H / 64, (1024 + blocks - 1) / blocks));
             const int vb = (a.H + nb - 1) / nb;
-            hipLaunchKernelGGL(k_sgbm_vsum8, dim3((unsigned)blocks, (unsigned)((a.H + vb - 1) / vb)), dim3(256), 0, s,
-                               a, vb);
+            const dim3 grid8((unsigned)blocks, (unsigned)((a.H + vb - 1) / vb));
+            switch (a.r) {
+#define SV_VSUM_R(R) case R: hipLaunchKernelGGL(k_sgbm_vsum8<R>, grid8, dim3(256), 0, s, a, vb); break;
+                SV_VSUM_R(0) SV_VSUM_R(1) SV_VSUM_R(2) SV_VSUM_R(3) SV_VSUM_R(4) SV_VSUM_R(5) SV_VSUM_R(6)
+                SV_VSUM_R(7)
+#undef SV_VSUM_R
+            }
         } else {
             hipLaunchKernelGGL(k_sgbm_vsum, dim3((unsigned)((plane + 255) / 256)), dim3(256), 0, s, a);
         }

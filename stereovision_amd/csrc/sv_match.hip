@@ -77,8 +77,10 @@ template <int COST, int ND> struct PackCfg {
     // SPLIT (4-row kind with <= 2 common words): the common words live in a separate
     // 8-byte-per-slot array, the 4 per-row words in the 16-byte array: 24 B per pack
     // instead of a 32-byte slot, so a 4-LPG segment still fits 2 waves per SIMD in LDS
-    static constexpr int NC = COST == COST_SAD4 ? NW - 4 : 0;
-    static constexpr bool SPLIT = COST == COST_SAD4 && NC <= 2;
+    // HOG (5 words) splits too: word 0 in the 8-byte array, words 1-4 in a 16-byte slot, so
+    // a group's 16 lanes (slots DPL+1 apart) read disjoint banks (32-byte slots: 2-way)
+    static constexpr int NC = COST == COST_SAD4 ? NW - 4 : COST == COST_HOG ? 1 : 0;
+    static constexpr bool SPLIT = (COST == COST_SAD4 && NC <= 2) || COST == COST_HOG;
     static constexpr int QX = SPLIT ? 1 : Q;          // uint4 per slot in the main array
     static constexpr int SLOT_BYTES = 16 * QX + (SPLIT ? 8 : 0);
 };
@@ -781,7 +783,7 @@ size_t match_lds_bytes(const MatchPlan& p, int r, int cost) {
     const int nw = kind == COST_SAD ? p.ndw : kind == COST_SSD ? p.ndw + 1 : kind == COST_SAD2 ? p.ndw + 2
                  : kind == COST_SAD4 ? (2 * p.ndw - 2 + 3) / 4 + 4 : 5;
     const int wpb = kind == COST_SAD4 ? 1 : 4;
-    const bool split = kind == COST_SAD4 && nw - 4 <= 2;
+    const bool split = (kind == COST_SAD4 && nw - 4 <= 2) || kind == COST_HOG;
     const int Q = (nw + 3) / 4;
     const int c0 = (p.dpl - (4 * r + 1) % p.dpl) % p.dpl;
     const int wc = wave_cols(p.lpg, p.dpl, seg_mult(kind, r));

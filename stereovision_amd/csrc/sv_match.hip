@@ -33,6 +33,7 @@
 #include "sv_internal.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace sv {
 namespace {
@@ -80,9 +81,12 @@ template <int COST, int ND> struct PackCfg {
     // HOG (5 words) splits too: word 0 in the 8-byte array, words 1-4 in a 16-byte slot, so
     // a group's 16 lanes (slots DPL+1 apart) read disjoint banks (32-byte slots: 2-way)
     static constexpr int NC = COST == COST_SAD4 ? NW - 4 : COST == COST_HOG ? 1 : 0;
-    static constexpr bool SPLIT = (COST == COST_SAD4 && NC <= 2) || COST == COST_HOG;
+    // (r 6..7: 3 common words in a 16-byte slot of their own)
+    static constexpr bool SPLIT = (COST == COST_SAD4 && NC <= 3) || COST == COST_HOG;
+    static constexpr int CW = NC <= 2 ? 2 : 4;        // words per slot of the common array
+    using CT = typename std::conditional<CW == 2, uint2, uint4>::type;
     static constexpr int QX = SPLIT ? 1 : Q;          // uint4 per slot in the main array
-    static constexpr int SLOT_BYTES = 16 * QX + (SPLIT ? 8 : 0);
+    static constexpr int SLOT_BYTES = 16 * QX + (SPLIT ? 4 * CW : 0);
 };
 template <int NW> struct Pk { uint32_t w[NW]; };
 
@@ -98,17 +102,19 @@ template <int COST, int ND, typename X, typename C> struct PackPtrT {
         return {x + s * PackCfg<COST, ND>::QX, PackCfg<COST, ND>::SPLIT ? c + s : c};
     }
 };
-template <int COST, int ND> using PackPtr = PackPtrT<COST, ND, const uint4, const uint2>;
-template <int COST, int ND> using PackOut = PackPtrT<COST, ND, uint4, uint2>;
+template <int COST, int ND>
+using PackPtr = PackPtrT<COST, ND, const uint4, const typename PackCfg<COST, ND>::CT>;
+template <int COST, int ND> using PackOut = PackPtrT<COST, ND, uint4, typename PackCfg<COST, ND>::CT>;
 
 template <int COST, int ND>
 __device__ __forceinline__ Pk<PackCfg<COST, ND>::NW> ld(PackPtr<COST, ND> p) {
     using P = PackCfg<COST, ND>;
     Pk<P::NW> v;
     if constexpr (P::SPLIT) {
-        const uint2 c = *p.c;
+        const typename P::CT c = *p.c;
         v.w[0] = c.x;
         if constexpr (P::NC > 1) v.w[1] = c.y;
+        if constexpr (P::NC > 2) v.w[2] = c.z;
         const uint32_t* q = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(p.x, 16));
 #pragma unroll
         for (int i = 0; i < 4; ++i) v.w[P::NC + i] = q[i];
@@ -125,7 +131,8 @@ template <int COST, int ND>
 __device__ __forceinline__ void put(PackOut<COST, ND> p, const uint32_t (&w)[8]) {
     using P = PackCfg<COST, ND>;
     if constexpr (P::SPLIT) {
-        *p.c = make_uint2(w[0], P::NC > 1 ? w[1] : 0u);
+        if constexpr (P::CW == 2) *p.c = make_uint2(w[0], P::NC > 1 ? w[1] : 0u);
+        else *p.c = make_uint4(w[0], w[1], w[2], 0u);
         p.x[0] = make_uint4(w[P::NC], w[P::NC + 1], w[P::NC + 2], w[P::NC + 3]);
     } else {
         p.x[0] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -530,7 +537,7 @@ __global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) 
     // per-wave LDS region: [L main | R main | L common | R common] (common arrays: SPLIT)
     using P = PackCfg<COST, ND>;
     uint4* wbase = reinterpret_cast<uint4*>(reinterpret_cast<char*>(smem) + (size_t)wid * (NL + NRphys) * P::SLOT_BYTES);
-    uint2* cbase = reinterpret_cast<uint2*>(wbase + (size_t)(NL + NRphys) * P::QX);
+    typename P::CT* cbase = reinterpret_cast<typename P::CT*>(wbase + (size_t)(NL + NRphys) * P::QX);
     const PackOut<COST, ND> Lw{wbase, cbase};
     const PackOut<COST, ND> Rw{wbase + (size_t)NL * P::QX, cbase + NL};
     const PackPtr<COST, ND> Lp{Lw.x, Lw.c};
@@ -783,14 +790,15 @@ size_t match_lds_bytes(const MatchPlan& p, int r, int cost) {
     const int nw = kind == COST_SAD ? p.ndw : kind == COST_SSD ? p.ndw + 1 : kind == COST_SAD2 ? p.ndw + 2
                  : kind == COST_SAD4 ? (2 * p.ndw - 2 + 3) / 4 + 4 : 5;
     const int wpb = kind == COST_SAD4 ? 1 : 4;
-    const bool split = (kind == COST_SAD4 && nw - 4 <= 2) || kind == COST_HOG;
+    const bool split = (kind == COST_SAD4 && nw - 4 <= 3) || kind == COST_HOG;
+    const int cw = kind == COST_SAD4 && nw - 4 == 3 ? 4 : 2;
     const int Q = (nw + 3) / 4;
     const int c0 = (p.dpl - (4 * r + 1) % p.dpl) % p.dpl;
     const int wc = wave_cols(p.lpg, p.dpl, seg_mult(kind, r));
     const int NL = wc + 4 * r + p.dpl + 1;
     const int NRlog = wc + 4 * r + p.lpg * p.dpl + p.dpl;
     const int NRphys = NRlog + (NRlog + c0) / p.dpl + 1;
-    return (size_t)wpb * (NL + NRphys) * (split ? 24 : Q * 16);
+    return (size_t)wpb * (NL + NRphys) * (split ? 16 + 4 * cw : Q * 16);
 }
 
 int launch_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v, hipStream_t s) {

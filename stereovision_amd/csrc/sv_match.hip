@@ -80,9 +80,10 @@ template <int COST, int ND> struct PackCfg {
     // instead of a 32-byte slot, so a 4-LPG segment still fits 2 waves per SIMD in LDS
     // HOG (5 words) splits too: word 0 in the 8-byte array, words 1-4 in a 16-byte slot, so
     // a group's 16 lanes (slots DPL+1 apart) read disjoint banks (32-byte slots: 2-way)
-    static constexpr int NC = COST == COST_SAD4 ? NW - 4 : COST == COST_HOG ? 1 : 0;
+    static constexpr int NC = COST == COST_SAD4 ? NW - 4 : (COST == COST_HOG || (COST == COST_SSD && NW == 5)) ? 1 : 0;
     // (r 6..7: 3 common words in a 16-byte slot of their own)
-    static constexpr bool SPLIT = (COST == COST_SAD4 && NC <= 3) || COST == COST_HOG;
+    static constexpr bool SPLIT = (COST == COST_SAD4 && NC <= 3) || COST == COST_HOG ||
+                                  (COST == COST_SSD && NW == 5);
     static constexpr int CW = NC <= 2 ? 2 : 4;        // words per slot of the common array
     using CT = typename std::conditional<CW == 2, uint2, uint4>::type;
     static constexpr int QX = SPLIT ? 1 : Q;          // uint4 per slot in the main array
@@ -790,7 +791,7 @@ size_t match_lds_bytes(const MatchPlan& p, int r, int cost) {
     const int nw = kind == COST_SAD ? p.ndw : kind == COST_SSD ? p.ndw + 1 : kind == COST_SAD2 ? p.ndw + 2
                  : kind == COST_SAD4 ? (2 * p.ndw - 2 + 3) / 4 + 4 : 5;
     const int wpb = kind == COST_SAD4 ? 1 : 4;
-    const bool split = (kind == COST_SAD4 && nw - 4 <= 3) || kind == COST_HOG;
+    const bool split = (kind == COST_SAD4 && nw - 4 <= 3) || kind == COST_HOG || (kind == COST_SSD && nw == 5);
     const int cw = kind == COST_SAD4 && nw - 4 == 3 ? 4 : 2;
     const int Q = (nw + 3) / 4;
     const int c0 = (p.dpl - (4 * r + 1) % p.dpl) % p.dpl;

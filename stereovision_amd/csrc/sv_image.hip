@@ -303,13 +303,27 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
     {   // thread -> one tile column (clamped once), rows g, g+3, ...: 204 of 256 threads load
         constexpr int TC = MQ_W + 4, TR = MQ_H + 2, G = 256 / TC;   // 68 columns, 3 row groups
         const int c = threadIdx.x % TC, g = threadIdx.x / TC;
+        static_assert(TR % G == 0, "row groups must tile the pair rows");
         if (g < G) {
             const uint32_t cx = (uint32_t)clampi(x0 - 2 + c, 0, W - 1);
+            if (y0 >= 2 && y0 + TR - 1 <= H - 1) {   // interior rows (uniform): no row clamps
+                uint32_t off = (uint32_t)(y0 - 2 + g) * W + cx;
+                const uint32_t two = 2u * (uint32_t)W, step = (uint32_t)G * W;
 #pragma unroll
-            for (int r = g; r < TR; r += G) {
-                const uint16_t a = (uint16_t)at(in, (uint32_t)clampi(y0 - 2 + r, 0, H - 1) * W + cx);
-                const uint16_t b = (uint16_t)at(in, (uint32_t)clampi(y0 + r, 0, H - 1) * W + cx);
-                t2[r][c] = (uint32_t)a | ((uint32_t)b << 16);
+                for (int k = 0; k < TR / G; ++k) {
+                    const uint16_t a = (uint16_t)at(in, off);
+                    const uint16_t b = (uint16_t)at(in, off + two);
+                    t2[g + G * k][c] = (uint32_t)a | ((uint32_t)b << 16);
+                    off += step;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < TR / G; ++k) {
+                    const int r = g + G * k;
+                    const uint16_t a = (uint16_t)at(in, (uint32_t)clampi(y0 - 2 + r, 0, H - 1) * W + cx);
+                    const uint16_t b = (uint16_t)at(in, (uint32_t)clampi(y0 + r, 0, H - 1) * W + cx);
+                    t2[r][c] = (uint32_t)a | ((uint32_t)b << 16);
+                }
             }
         }
     }

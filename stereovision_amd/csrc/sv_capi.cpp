@@ -799,19 +799,27 @@ int sv_multi_gpu_batch(sv_ctx* const* ctxs, int ndev, const uint8_t* left, const
     if (rc) return rc;
     // contiguous shards, one host thread per context: each stages, computes and collects
     // its frames on its own device/stream concurrently with the others
+    // (no C++ exception may cross the ABI: thread creation failures become SV_ENOMEM)
     std::vector<int> rcs(ndev, 0);
     std::vector<std::string> errs(ndev);
     std::vector<std::thread> th;
-    for (int k = 0; k < ndev; ++k) {
-        const int f0 = (int)((long long)n_frames * k / ndev), f1 = (int)((long long)n_frames * (k + 1) / ndev);
-        th.emplace_back([&, k, f0, f1] {
-            rcs[k] = depth_map_shard(ctxs[k], left, right, f0, f1, H, W, channels, min_disp, num_disp, win, cost,
-                                     min_depth, max_depth, depth_range, min_disp_global, depth_final, disparity,
-                                     depth_normalized);
-            if (rcs[k]) errs[k] = g_err;
-        });
+    int spawn_rc = 0;
+    try {
+        th.reserve(ndev);
+        for (int k = 0; k < ndev; ++k) {
+            const int f0 = (int)((long long)n_frames * k / ndev), f1 = (int)((long long)n_frames * (k + 1) / ndev);
+            th.emplace_back([&, k, f0, f1] {
+                rcs[k] = depth_map_shard(ctxs[k], left, right, f0, f1, H, W, channels, min_disp, num_disp, win,
+                                         cost, min_depth, max_depth, depth_range, min_disp_global, depth_final,
+                                         disparity, depth_normalized);
+                if (rcs[k]) errs[k] = g_err;
+            });
+        }
+    } catch (...) {
+        spawn_rc = SV_ENOMEM;
     }
     for (auto& t : th) t.join();
+    if (spawn_rc) return fail(spawn_rc, "could not start the per-device host threads");
     for (int k = 0; k < ndev; ++k)
         if (rcs[k]) return fail(rcs[k], "device shard " + std::to_string(k) + ": " + errs[k]);
     return 0;

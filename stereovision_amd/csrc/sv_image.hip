@@ -108,8 +108,11 @@ __global__ __launch_bounds__(256) void k_harris_lds(const uint8_t* __restrict__ 
 // HOG window histograms: 64x16 output tile, window radius r <= 7.
 constexpr int GT_W = 64, GT_H = 16, GR_MAX = 7;
 constexpr int GX_MAX = GT_W + 2 * GR_MAX, GY_MAX = GT_H + 2 * GR_MAX;
-__constant__ int c_hog_cos[8] = {15396, 12551, 8192, 2845, -2845, -8192, -12551, -15396};
-__constant__ int c_hog_sin[8] = {5604, 10531, 14189, 16135, 16135, 14189, 10531, 5604};
+// bin boundaries at 20°·(k+1): round(16384·cos), round(16384·sin); cos[7-k] = -cos[k] and
+// sin[7-k] = sin[k], so the 8 tests need only 4 products pairs: boundary k is
+// cos·gy >= sin·gx, boundary 7-k is -cos·gy >= sin·gx.
+constexpr int kHogCos[4] = {15396, 12551, 8192, 2845};
+constexpr int kHogSin[4] = {5604, 10531, 14189, 16135};
 
 template <int r>   // window radius: compile-time, so the tile loops index by constants
 __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g, int H, int W,
@@ -144,7 +147,10 @@ __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g,
         if (gy < 0 || (gy == 0 && gx < 0)) { gx = -gx; gy = -gy; }
         int b = 0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) b += (c_hog_cos[k] * gy - c_hog_sin[k] * gx >= 0);
+        for (int k = 0; k < 4; ++k) {
+            const int cy = kHogCos[k] * gy, sx = kHogSin[k] * gx;   // |products| < 2^24
+            b += (cy >= sx) + (-cy >= sx);
+        }
         sbm[ty][tx] = (uint16_t)((b << 8) | m);
     }
     __syncthreads();

@@ -1,42 +1,56 @@
 #!/usr/bin/env python3
-"""bench.py — disparity frames/s of the MI355X engine (BASELINE.json metric).
+"""bench.py — disparity frames/s of the MI355X engine (BASELINE.json metric).  No PyTorch.
 
 Workload (BASELINE.json metric): 1920x1080 rectified synthetic pairs, D=128, 9x9 SAD
 window, the whole device path of depth_map.create_depth_map per frame:
     disparity (k_match) -> medianBlur 5 + depth post (k_median_i16, fused)
-Inputs are gray u8 pairs already resident in HBM (8 distinct frames per rank, cycled);
+Inputs are gray u8 pairs already resident in HBM (16 distinct frames per GPU, cycled);
 outputs are depth f32, disparity f32 and depth u8 per frame.  One step = one batch of
---batch frame pairs (default 8) through sv_depth_map_batch_dev: one k_match and one
-k_median_i16 launch over the whole batch (grid.z = frame), which keeps all 256 CUs busy
-instead of leaving a partial last wave of blocks per frame.  --batch 1 = one call per frame.
+--batch frame pairs (default 16) through sv_depth_map_batch_dev: one k_match and one
+k_median_i16 launch over the batch (grid.z = frame).  --batch 1 = one call per frame.
 
-Multi-GPU: one process per GPU (torch.distributed.run), frames sharded across ranks with
-no collective in the data path (weak scaling); value = frames of all ranks / max time.
+Multi-GPU (frames mode = C4, weak scaling; rowtile mode = C5, strong scaling):
+  * under `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N` (the
+    driver's launch; only the launcher is torch's): one process per GPU, RANK/WORLD_SIZE/
+    LOCAL_RANK from the environment, barrier + max-over-ranks through RCCL
+    (stereovision_amd.distributed: file rendezvous + sv_comm_* of libsvhip);
+  * `python bench.py --gpus N` without a launcher: ONE process drives N devices
+    (sv_multi_gpu_depth_map_dev / sv_depth_map_rows_multi when gathering).
+value = frames of all GPUs / max wall time of the timed region.
 
-Extra JSON fields: `roofline` for the dominant kernel (k_match; HIP-event durations
-measured inside the timed region) with the VALU-tap figure beside the HBM one, and
-`cpu_baseline` = the C oracle (oracle/sv_oracle.c, OpenMP) on this host's cores.
-
-torch is imported BEFORE the engine library so libsvhip binds to torch's HIP runtime
-(both ship libamdhip64.so.7; see DESIGN.md "One HIP runtime per process").
+Extra JSON fields:
+  roofline      k_match against the HBM roofline with SURVEY.md §8(d)'s algorithmic bytes
+                (6 B/px: 2 u8 images read + the f32 disparity map); launch times from HIP
+                events inside the timed region; `traffic` and `valu` from rocprofv3 PMC passes
+                run live by this script on this box (separate --pmc passes, a child process
+                each; --no-live-pmc skips them)
+  host_path     the drop-in create_depth_map (BGR NumPy in -> NumPy out, one frame per call,
+                PCIe-inclusive) and its pipelined form (several frames in flight)
+  cpu_baseline  the C oracle (oracle/sv_oracle.c, OpenMP over every core of this process's
+                affinity) on full frames
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import signal
+import subprocess
 import sys
+import tempfile
 import time
 
-import torch  # noqa: E402  (must precede the engine library load)
-import torch.distributed as dist
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from stereovision_amd.engine import get_engine  # noqa: E402
-from stereovision_amd.synthetic import stereo_batch, synthetic_calibration  # noqa: E402
+from stereovision_amd.engine import (Communicator, device_count, depth_map_rows_multi,  # noqa: E402
+                                     get_engine, multi_gpu_depth_map_dev)
+from stereovision_amd.synthetic import stereo_batch, stereo_pair, synthetic_calibration, to_bgr  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2   # 256 CU x 4 SIMD, one wave64 VALU instr per 2 cycles
@@ -46,6 +60,23 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_cores():
+    """(cores this process may run on, os.cpu_count()): the affinity set, capped by a cgroup
+    CPU quota when one is set (a GPU box's per-GPU CPU share)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            aff = max(1, min(aff, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return aff, os.cpu_count() or aff
+
+
+# ---- CPU baseline (the oracle: test infrastructure, timed only here) ------------------------
 def cpu_baseline_sgbm(H, W, D, win, seconds):
     """SGBM mode: the NumPy SGBM-3WAY oracle (single process) on horizontal strips of the
     frame (full width, the whole disparity range), scaled to frames/s by the strip share."""
@@ -68,50 +99,82 @@ def cpu_baseline_sgbm(H, W, D, win, seconds):
 
 
 def cpu_baseline(H, W, D, win, cost, seconds, harris=False):
-    """C oracle (the port) timed on this host: whole app-1 path per frame (+ the Harris
-    response of the left frame for C2)."""
+    """The C oracle (the port of the engine's semantics; the reference's own CPU path is
+    OpenCV StereoSGBM, not importable on this image) timed on this host: the whole app-1
+    path per frame (+ the Harris response of the left frame for C2), OpenMP over all cores of
+    the process's affinity; plus the single-thread rate of the same port."""
     if cost == "sgbm":
         return cpu_baseline_sgbm(H, W, D, win, seconds)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes
     import sv_oracle_c as C  # test infrastructure, used here only as the CPU baseline
     lib = C.lib()
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, 16))
+    aff, ncpu = host_cores()
     L, R = stereo_batch(2, H, W, D, seed=4242)
     depth = np.empty((H, W), np.float32)
     disp = np.empty((H, W), np.float32)
     norm = np.empty((H, W), np.uint8)
     costi = {"sad": 0, "ssd": 1, "hog": 2}[cost]
+    f32 = ctypes.c_float
+    lib.svo_depth_map.argtypes = [C._u8p, C._u8p, C._i, C._i, C._i, C._i, C._i, C._i, f32, f32,
+                                  f32, C._f32p, C._f32p, C._u8p, C._i]
+    lib.svo_depth_map.restype = C._i
 
-    def one(i):
+    def one(i, threads):
         lib.svo_depth_map(np.ascontiguousarray(L[i % 2]), np.ascontiguousarray(R[i % 2]), H, W,
                           0, D, win, costi, np.float32(0.3), np.float32(2.0),
                           np.float32(2.0 - 0.3), depth, disp, norm, threads)
         if harris:
             C.harris(np.ascontiguousarray(L[i % 2]))
 
-    import ctypes
-    f32 = ctypes.c_float
-    lib.svo_depth_map.argtypes = [C._u8p, C._u8p, C._i, C._i, C._i, C._i, C._i, C._i, f32, f32,
-                                  f32, C._f32p, C._f32p, C._u8p, C._i]
-    lib.svo_depth_map.restype = C._i
-    one(0)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        one(n)
-        n += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds or n >= 200:
-            break
+    def rate(threads, budget, cap):
+        one(0, threads)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            one(n, threads)
+            n += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget or n >= cap:
+                return n, dt
+
+    n, dt = rate(aff, seconds, 400)
+    n1, dt1 = rate(1, max(1.0, seconds / 4), 20)
     return {
-        "value": round(n / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+        "value": round(n / dt, 3), "unit": "frames/s", "cores": aff, "kind": "port",
+        "cpu_count": ncpu, "affinity_cores": aff,
+        "single_thread_value": round(n1 / dt1, 4),
         "sample": f"{n} full {W}x{H} frames (D={D}, win={win}, {cost}: disparity + median5 + "
-                  f"depth post{' + Harris (1 thread)' if harris else ''}) of the C oracle, "
-                  f"OpenMP {threads} threads, {dt:.1f} s",
+                  f"depth post{' + Harris (1 thread)' if harris else ''}) of the C oracle "
+                  f"(oracle/sv_oracle.c, the engine's semantics; the reference's cv2.StereoSGBM "
+                  f"is not installed), OpenMP {aff} threads = every core this process may use "
+                  f"(affinity set, capped by the cgroup CPU quota; os.cpu_count() {ncpu}), "
+                  f"{dt:.1f} s; single thread: {n1} frames "
+                  f"in {dt1:.1f} s",
     }
+
+
+# ---- helpers -------------------------------------------------------------------------------
+class DevArena:
+    """Device buffers of one engine, freed together."""
+
+    def __init__(self, eng):
+        self.eng, self.ptrs = eng, []
+
+    def alloc(self, nbytes):
+        p = self.eng.dev_alloc(max(256, int(nbytes)))
+        self.ptrs.append(p)
+        return p
+
+    def upload(self, a):
+        a = np.ascontiguousarray(a)
+        p = self.alloc(a.nbytes)
+        self.eng.to_device(p, a)
+        return p
+
+    def free(self):
+        for p in self.ptrs:
+            self.eng.dev_free(p)
+        self.ptrs = []
 
 
 def make_rectifier(eng, W, H):
@@ -135,68 +198,157 @@ def hbm_entry(name, bytes_per_launch, ms, n):
             "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4), "launches": n}
 
 
-def aux_kernels(eng, dev, H, W, B, stream, med_ms, med_n, reps=20):
+def aux_kernels(eng, H, W, B, med_ms, med_n, reps=20):
     """HBM rooflines of the memory-bound kernels around k_match, measured after the timed
-    region (not part of `value`): k_median_i16 from the timed steps, and k_remap (the
-    rectify+gray stage in front of the path) over a batch of B raw 1080p BGR frames."""
+    region (not part of `value`): k_median_i16 from the timed steps, k_remap (the
+    rectify+gray stage in front of the path) over a batch of B raw BGR frames, the occlusion
+    statistics of a pair and one radix-select pass."""
     out = {"k_median_i16": hbm_entry("k_median_i16", 11 * H * W * B, med_ms, med_n)}
-    rect = make_rectifier(eng, W, H)
-    src = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=f"cuda:{dev}")
-    dst = torch.empty((B, H, W), dtype=torch.uint8, device=f"cuda:{dev}")
-    m1, m2 = rect.device_maps[0], rect.device_maps[1]
-    for _ in range(3):
-        eng.remap_dev(src.data_ptr(), H, W, 3, 3 * W, m1, m2, H, W, dst.data_ptr(), W,
-                      gray_out=True, n_frames=B, src_frame_stride=3 * H * W,
-                      dst_frame_stride=H * W, stream=stream)
-    torch.cuda.synchronize()
-    eng.profile_reset()
-    eng.profile(True)
-    for _ in range(reps):
-        eng.remap_dev(src.data_ptr(), H, W, 3, 3 * W, m1, m2, H, W, dst.data_ptr(), W,
-                      gray_out=True, n_frames=B, src_frame_stride=3 * H * W,
-                      dst_frame_stride=H * W, stream=stream)
-    torch.cuda.synchronize()
-    eng.profile(False)
-    ms, n = eng.profile_read("remap")
-    # algorithmic bytes per output pixel: 6 (map1 + map2) + 3 (BGR source) + 1 (gray out)
-    out["k_remap_bgr2gray"] = hbm_entry("k_remap<3,gray>", 10 * H * W * B, ms, n)
-    rect.close()
-    # occlusion statistics of a rectified gray pair (1 B/px per image read once)
-    nb = max(1, H // 48) * max(1, W // 48)
-    st = torch.zeros(2 * (2 * nb + 256), dtype=torch.int32, device=f"cuda:{dev}")
-    p0 = dst[0].data_ptr()
-    p1 = dst[1].data_ptr()
-    sp = st.data_ptr()
-    eng.profile_reset()
-    eng.profile(True)
-    for _ in range(reps):
-        eng.frame_stats_dev(p0, p1, H, W, 1, W, sp, sp + 8 * nb, sp + 16 * nb, stream=stream)
-    torch.cuda.synchronize()
-    eng.profile(False)
-    ms, n = eng.profile_read("stats")
-    out["k_frame_stats"] = hbm_entry("k_frame_stats", 2 * H * W, ms, n)
-    # one radix-select pass over a float32 disparity map (4 B/px)
-    d = torch.rand((H, W), dtype=torch.float32, device=f"cuda:{dev}")
-    eng.profile_reset()
-    eng.profile(True)
-    for _ in range(reps):
-        eng.select_count(d.data_ptr(), H * W, 1)
-    eng.profile(False)
-    ms, n = eng.profile_read("select")
-    out["k_select_hist"] = hbm_entry("k_select_hist", 4 * H * W, ms, n)
+    arena = DevArena(eng)
+    try:
+        Bs = max(2, B)
+        rect = make_rectifier(eng, W, H)
+        rng = np.random.default_rng(7)
+        src = arena.upload(rng.integers(0, 256, (B, H, W, 3), dtype=np.uint8))
+        dst = arena.alloc(Bs * H * W)
+        m1, m2 = rect.device_maps[0], rect.device_maps[1]
+
+        def remap():
+            eng.remap_dev(src, H, W, 3, 3 * W, m1, m2, H, W, dst, W, gray_out=True, n_frames=B,
+                          src_frame_stride=3 * H * W, dst_frame_stride=H * W)
+        for _ in range(3):
+            remap()
+        eng.synchronize()
+        eng.profile_reset()
+        eng.profile(True)
+        for _ in range(reps):
+            remap()
+        eng.synchronize()
+        eng.profile(False)
+        ms, n = eng.profile_read("remap")
+        # algorithmic bytes per output pixel: 6 (map1 + map2) + 3 (BGR source) + 1 (gray out)
+        out["k_remap_bgr2gray"] = hbm_entry("k_remap<3,gray>", 10 * H * W * B, ms, n)
+        rect.close()
+        # occlusion statistics of a rectified gray pair (1 B/px per image read once)
+        nb = max(1, H // 48) * max(1, W // 48)
+        st = arena.alloc(4 * 2 * (2 * nb + 256))
+        eng.profile_reset()
+        eng.profile(True)
+        for _ in range(reps):
+            eng.frame_stats_dev(dst, dst + H * W, H, W, 1, W, st, st + 8 * nb, st + 16 * nb)
+        eng.synchronize()
+        eng.profile(False)
+        ms, n = eng.profile_read("stats")
+        out["k_frame_stats"] = hbm_entry("k_frame_stats", 2 * H * W, ms, n)
+        # one radix-select pass over a float32 disparity map (4 B/px)
+        d = arena.upload(rng.random((H, W), dtype=np.float32))
+        eng.profile_reset()
+        eng.profile(True)
+        for _ in range(reps):
+            eng.select_count(d, H * W, 1)
+        eng.profile(False)
+        ms, n = eng.profile_read("select")
+        out["k_select_hist"] = hbm_entry("k_select_hist", 4 * H * W, ms, n)
+    finally:
+        arena.free()
     return out
 
 
-def pmc_entry(workload_key):
-    """k_match PMC figures per launch from the committed rocprofv3 summary, if any."""
-    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def host_path(H, W, D, win, seconds=3.0):
+    """PCIe-inclusive rate of the drop-in path the reference actually calls (depth_map.py:
+    1181-1183): BGR NumPy frames -> depth_map.create_depth_map -> (depth, disparity,
+    colormap) NumPy arrays, one frame per call; and the pipelined form of the same calls
+    (stereovision_amd.pipeline: several frames in flight, as fused_depth_map.py:2591-2598
+    submits frames to a worker pool)."""
+    from stereovision_amd import depth_map as DM
+    frames = []
+    for s in range(4):
+        L, R, _ = stereo_pair(H, W, D, seed=900 + s)
+        frames.append((to_bgr(L), to_bgr(R)))
+    DM.NUM_DISP, DM.WINDOW_SIZE, DM.MIN_DISP = D, win, 0
+    for i in range(3):
+        DM.create_depth_map(*frames[i % 4])
+    n, t0 = 0, time.perf_counter()
+    while True:
+        DM.create_depth_map(*frames[n % 4])
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds or n >= 2000:
+            break
+    out = {"unit": "frames/s", "frames": n, "value": round(n / dt, 1),
+           "ms_per_call": round(dt * 1e3 / n, 3),
+           "path": "BGR uint8 NumPy pair -> depth_map.create_depth_map -> (depth f32, disparity "
+                   "f32, colormap u8x3) NumPy, one synchronous call per frame",
+           "bytes_h2d_per_frame": 6 * H * W}
     try:
-        with open(p) as f:
-            return json.load(f).get(workload_key, {})
-    except (OSError, ValueError):
-        return {}
+        from stereovision_amd.pipeline import DepthMapPipeline
+    except ImportError:
+        return out
+    pipe = DepthMapPipeline(D, win)
+    try:
+        for i in range(4):
+            pipe.submit(*frames[i % 4]).result()
+        futs, n, t0 = [], 0, time.perf_counter()
+        while True:
+            futs.append(pipe.submit(*frames[n % 4]))
+            n += 1
+            if len(futs) > pipe.depth:
+                futs.pop(0).result()
+            dt = time.perf_counter() - t0
+            if dt >= seconds or n >= 4000:
+                break
+        for f in futs:
+            f.result()
+        dt = time.perf_counter() - t0
+        out["pipelined"] = {"value": round(n / dt, 1), "frames": n, "in_flight": pipe.depth,
+                            "path": "the same calls through DepthMapPipeline.submit (futures)"}
+    finally:
+        pipe.close()
+    return out
 
 
+# ---- live PMC (rocprofv3 passes over a short child run of this script) -----------------------
+PMC_PASSES = [("sq", ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT"]),
+              ("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE"])]
+
+
+def live_pmc(args, kernel_tag="k_match", timeout=150):
+    rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(rocprof):
+        return {"error": "rocprofv3 not found"}
+    tmp = tempfile.mkdtemp(prefix="sv_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "6", "--warmup", "2",
+             "--height", str(args.height), "--width", str(args.width), "--num-disp", str(args.num_disp),
+             "--win", str(args.win), "--cost", args.cost, "--batch", str(args.batch),
+             "--frames", str(args.frames)]
+    agg = {}
+    try:
+        for name, counters in PMC_PASSES:
+            cmd = [rocprof, "--pmc", *counters, "--output-format", "csv", "-d",
+                   os.path.join(tmp, name), "-o", name, "--", *child]
+            p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=tmp,
+                                 start_new_session=True, env=dict(os.environ, TMPDIR=tmp))
+            try:
+                _, err = p.communicate(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                return {"error": f"rocprofv3 pass {name} timed out"}
+            if p.returncode != 0:
+                return {"error": f"rocprofv3 pass {name} rc={p.returncode}: "
+                                 f"{err.decode(errors='replace')[-300:]}"}
+            for f in glob.glob(os.path.join(tmp, name, "**", "*counter_collection.csv"), recursive=True):
+                for r in csv.DictReader(open(f)):
+                    if kernel_tag in r["Kernel_Name"]:
+                        agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    res = {k: sum(v) / len(v) for k, v in agg.items()}
+    res["dispatches"] = max((len(v) for v in agg.values()), default=0)
+    return res
+
+
+# ---- main ----------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -208,10 +360,10 @@ def main():
     ap.add_argument("--win", type=int, default=9)
     ap.add_argument("--cost", default="sad", choices=["sad", "ssd", "hog", "sgbm"],
                     help="sad/ssd/hog: the north_star WTA engine; sgbm: the SGBM-3WAY mode")
-    ap.add_argument("--frames", type=int, default=16, help="distinct resident frames per rank")
+    ap.add_argument("--frames", type=int, default=16, help="distinct resident frames per GPU")
     ap.add_argument("--batch", type=int, default=16,
-                    help="frames mode: frames per step, one launch per kernel over the batch "
-                         "(sv_depth_map_batch_dev); 1 = one frame per call (latency mode)")
+                    help="frames mode: frames per step and GPU, one launch per kernel over the "
+                         "batch (sv_depth_map_batch_dev); 1 = one frame per call (latency mode)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed loop")
@@ -219,119 +371,145 @@ def main():
                     help="bracket the kernels of every N-th timed step with HIP events (each "
                          "event record costs a few us of queue time; 1 = every step)")
     ap.add_argument("--mode", default="frames", choices=["frames", "rowtile"],
-                    help="frames: independent frames per rank (C4, weak scaling); rowtile: "
-                         "one frame row-tiled across ranks + RCCL row gather (C5, strong)")
+                    help="frames: independent frames per GPU (C4, weak scaling); rowtile: one "
+                         "frame row-tiled across GPUs + RCCL band gather (C5, strong scaling)")
     ap.add_argument("--gather", action="store_true",
-                    help="frames mode: gather every step's disparity maps to rank 0 (RCCL)")
+                    help="frames mode: gather every step's output maps to GPU 0 over xGMI")
     ap.add_argument("--rectify", action="store_true",
                     help="camera pipeline: raw BGR frames resident in HBM -> rectify+gray "
                          "(k_remap, calibrated CV_16SC2 maps) -> disparity -> median/post")
     ap.add_argument("--no-aux", action="store_true", help="skip the aux-kernel rooflines")
     ap.add_argument("--harris", action="store_true",
                     help="C2: also compute the Harris response of every left frame (k_harris)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo rehearses N>1 with several ranks on one GPU")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "rccl", "host"],
+                    help="one-process-per-GPU launch: RCCL (auto falls back to the file store "
+                         "when ranks share a GPU)")
+    ap.add_argument("--no-live-pmc", action="store_true", help="skip the rocprofv3 PMC passes")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the host_path measurement")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.pmc_child:
+        args.no_cpu_baseline = args.no_aux = args.no_live_pmc = args.no_host_path = True
+        args.no_profile = True
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = torch.cuda.device_count()
-    dev = local % max(1, ndev) if world > 1 else 0
-    torch.cuda.set_device(dev)
-    gloo = args.dist_backend == "gloo"
-    if world > 1:
-        if gloo:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-    comm_dev = "cpu" if gloo else f"cuda:{dev}"
+    launched = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    pg = None
+    if launched:
+        from stereovision_amd.distributed import init_process_group
+        pg = init_process_group(backend=args.dist_backend)
+        rank, world = pg.rank, pg.world
+        devices = [pg.device]
+    else:
+        rank, world = 0, 1
+        n = max(1, args.gpus)
+        nd = device_count()
+        if n > nd:
+            raise SystemExit(f"--gpus {n} but only {nd} device(s) are visible")
+        devices = list(range(n))
+    ngpu = world * len(devices)
+    engines = [get_engine(d) for d in devices]
+    eng = engines[0]
 
     H, W, D, win = args.height, args.width, args.num_disp, args.win
     F = max(1, args.frames)
     B = max(1, min(args.batch, F))
     F = (F // B) * B
-    L, R = stereo_batch(F, H, W, D, seed=1000 * rank)
-    dL = torch.from_numpy(L).to(f"cuda:{dev}")
-    dR = torch.from_numpy(R).to(f"cuda:{dev}")
-    depth = torch.empty((B, H, W), dtype=torch.float32, device=f"cuda:{dev}")
-    disp = torch.empty((B, H, W), dtype=torch.float32, device=f"cuda:{dev}")
-    norm = torch.empty((B, H, W), dtype=torch.uint8, device=f"cuda:{dev}")
-    torch.cuda.synchronize()
-
-    eng = get_engine(dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    pL = [dL[i].data_ptr() for i in range(F)]
-    pR = [dR[i].data_ptr() for i in range(F)]
     rowtile = args.mode == "rowtile"
     rectify = args.rectify and not rowtile
-    if rectify:      # raw camera frames: BGR, unrectified; gray intermediates per batch
-        rect = make_rectifier(eng, W, H)
-        bL = torch.from_numpy(np.repeat(L[..., None], 3, axis=3)).to(f"cuda:{dev}")
-        bR = torch.from_numpy(np.repeat(R[..., None], 3, axis=3)).to(f"cuda:{dev}")
-        gL = torch.empty((B, H, W), dtype=torch.uint8, device=f"cuda:{dev}")
-        gR = torch.empty((B, H, W), dtype=torch.uint8, device=f"cuda:{dev}")
-        m1l, m2l, m1r, m2r, _, _ = rect.device_maps
-        torch.cuda.synchronize()
-    if rowtile:
-        from stereovision_amd.distributed import RowTiledDepthMap, gather_rows
-        L0, R0 = stereo_batch(1, H, W, D, seed=4242)      # the SAME frame on every rank
-        dL = torch.from_numpy(L0).to(f"cuda:{dev}")
-        dR = torch.from_numpy(R0).to(f"cuda:{dev}")
-        tile = RowTiledDepthMap(H, W, D, win, cost=args.cost, device=dev,
-                                rank=rank, world=world)
-
+    if rectify and len(devices) > 1:
+        raise SystemExit("--rectify runs one GPU per process (use the torch.distributed.run launch)")
     harris = args.harris and not rowtile
-    if harris:
-        hmap = torch.empty((B, H, W), dtype=torch.float32, device=f"cuda:{dev}")
+    n_px = H * W
+    arenas = [DevArena(e) for e in engines]
 
-    def gather(t):
-        if world == 1:
-            return
-        src = t.to(comm_dev) if gloo else t
+    # resident inputs: F distinct frames per GPU (rowtile: the SAME frame on every GPU)
+    dL, dR = [], []
+    for k, (e, a) in enumerate(zip(engines, arenas)):
         if rowtile:
-            gather_rows(src, H)
+            L, R = stereo_batch(1, H, W, D, seed=4242)
         else:
-            out = torch.empty((world,) + tuple(src.shape), dtype=src.dtype, device=src.device)
-            dist.all_gather_into_tensor(out, src.unsqueeze(0).contiguous())
+            L, R = stereo_batch(F, H, W, D, seed=1000 * (rank * len(devices) + k))
+        if rectify:
+            L, R = np.repeat(L[..., None], 3, axis=3), np.repeat(R[..., None], 3, axis=3)
+        dL.append(a.upload(L))
+        dR.append(a.upload(R))
+    nb_out = B if not rowtile else 1
+    gather_all = args.gather and not rowtile and len(engines) > 1
+    out_frames = nb_out * (len(engines) if gather_all else 1)
+    depth = [a.alloc(4 * n_px * out_frames) for a in arenas]
+    disp = [a.alloc(4 * n_px * out_frames) for a in arenas]
+    norm = [a.alloc(n_px * out_frames) for a in arenas]
+    if rectify:
+        rect = make_rectifier(eng, W, H)
+        gL, gR = arenas[0].alloc(B * n_px), arenas[0].alloc(B * n_px)
+        m1l, m2l, m1r, m2r, _, _ = rect.device_maps
+    if harris:
+        hmaps = [a.alloc(4 * n_px * B) for a in arenas]
+    tile = None
+    if rowtile and launched:
+        from stereovision_amd.distributed import RowTiledDepthMap
+        tile = RowTiledDepthMap(H, W, D, win, cost=args.cost, device=devices[0], rank=rank,
+                                world=world, engine=eng)
+    comms = None
+    if not launched and len(engines) > 1 and (args.gather or rowtile):
+        try:
+            comms = Communicator.init_all(devices)
+        except Exception as ex:  # peer copies instead
+            log(f"RCCL group unavailable ({ex}); gathering with peer copies")
+    gather_frames_d = None
+    if launched and args.gather and not rowtile and world > 1 and rank == 0:
+        gather_frames_d = arenas[0].alloc(4 * n_px * B * world)
 
     def step(i):
-        if rowtile:
-            band_disp, _, _, _ = tile.compute(dL[0], dR[0])
-            gather(band_disp)
-            return
         f = (i * B) % F
-        if rectify:
-            for src, m1, m2, g in ((bL, m1l, m2l, gL), (bR, m1r, m2r, gR)):
-                eng.remap_dev(src[f].data_ptr(), H, W, 3, 3 * W, m1, m2, H, W, g.data_ptr(), W,
-                              gray_out=True, n_frames=B, src_frame_stride=3 * H * W,
-                              dst_frame_stride=H * W, stream=stream)
-            eng.depth_map_batch_dev(gL.data_ptr(), gR.data_ptr(), B, H, W, W, H * W, 0, D, win,
-                                    0.3, 2.0, depth.data_ptr(), disp.data_ptr(), norm.data_ptr(),
-                                    cost=args.cost, stream=stream)
-        elif B == 1:
-            eng.depth_map_dev(pL[f], pR[f], H, W, W, 0, D, win, 0.3, 2.0, depth.data_ptr(),
-                              disp.data_ptr(), norm.data_ptr(), cost=args.cost, stream=stream)
-        else:
-            eng.depth_map_batch_dev(pL[f], pR[f], B, H, W, W, H * W, 0, D, win, 0.3, 2.0,
-                                    depth.data_ptr(), disp.data_ptr(), norm.data_ptr(),
-                                    cost=args.cost, stream=stream)
-        if harris:      # one launch over the batch's left frames
-            eng.harris_batch_dev(gL.data_ptr() if rectify else pL[f], B, H, W, W, H * W,
-                                 hmap.data_ptr(), stream=stream)
-        if args.gather:
-            gather(disp)
+        if rowtile:
+            if launched:
+                tile.compute(dL[0], dR[0])
+                if world > 1:
+                    tile.gather(pg, stream=eng.stream)
+            else:
+                depth_map_rows_multi(engines, comms, dL, dR, H, W, W, 0, D, win, 0.3, 2.0,
+                                     depth[0], disp[0], norm[0], cost=args.cost)
+            return
+        if gather_all:     # one process, N devices, maps gathered on device 0
+            multi_gpu_depth_map_dev(engines, comms, [p + f * n_px for p in dL],
+                                    [p + f * n_px for p in dR], [B] * len(engines), H, W, W, n_px,
+                                    0, D, win, 0.3, 2.0, depth[0], disp[0], norm[0], cost=args.cost)
+            return
+        for k, e in enumerate(engines):
+            if rectify:
+                for src, m1, m2, g in ((dL[k], m1l, m2l, gL), (dR[k], m1r, m2r, gR)):
+                    e.remap_dev(src + f * 3 * n_px, H, W, 3, 3 * W, m1, m2, H, W, g, W,
+                                gray_out=True, n_frames=B, src_frame_stride=3 * n_px,
+                                dst_frame_stride=n_px)
+                e.depth_map_batch_dev(gL, gR, B, H, W, W, n_px, 0, D, win, 0.3, 2.0, depth[k],
+                                      disp[k], norm[k], cost=args.cost)
+            elif B == 1:
+                e.depth_map_dev(dL[k] + f * n_px, dR[k] + f * n_px, H, W, W, 0, D, win, 0.3, 2.0,
+                                depth[k], disp[k], norm[k], cost=args.cost)
+            else:
+                e.depth_map_batch_dev(dL[k] + f * n_px, dR[k] + f * n_px, B, H, W, W, n_px, 0, D, win,
+                                      0.3, 2.0, depth[k], disp[k], norm[k], cost=args.cost)
+            if harris:      # one launch over the batch's left frames
+                e.harris_batch_dev(gL if rectify else dL[k] + f * n_px, B, H, W, W, n_px, hmaps[k])
+        if launched and args.gather and world > 1:
+            from stereovision_amd.distributed import gather_frames
+            gather_frames(pg, disp[0], B, gather_frames_d or 0, 4 * n_px, stream=eng.stream)
+
+    def sync_all():
+        for e in engines:
+            e.synchronize()
 
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize()
+    sync_all()
     eng.profile(False)
     eng.profile_reset()
     every = max(1, args.profile_every)
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    if pg is not None:
+        pg.barrier()
+    sync_all()
     t0 = time.perf_counter()
     for i in range(args.steps):
         if not args.no_profile and every > 1:
@@ -339,9 +517,9 @@ def main():
         elif i == 0:
             eng.profile(not args.no_profile)
         step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync_all()
+    if pg is not None:
+        pg.barrier()
     elapsed = time.perf_counter() - t0
 
     eng.profile(False)
@@ -350,55 +528,82 @@ def main():
     remap_ms, remap_n = eng.profile_read("remap")
     harris_ms, harris_n = eng.profile_read("harris")
     k_name = "sgbm pipeline (k_sgbm_*)" if args.cost == "sgbm" else "k_match"
+    if pg is not None:
+        elapsed = pg.allreduce_max(elapsed)
 
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=comm_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    frames = args.steps if rowtile else world * args.steps * B
+    frames = args.steps if rowtile else ngpu * args.steps * B
     value = frames / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
-    npx = H * W * (1 if rowtile else B)
-    if rowtile:       # per-launch work is one band (+ median halo rows) of the frame
-        npx = (tile.h1 - tile.h0) * W
+    if args.pmc_child:
+        print(json.dumps({"pmc_child": True, "value": value}), flush=True)
+        return
+    # pixels of one k_match launch: the batch (frames) or this GPU's band + median halo
+    npx = n_px * B
+    if rowtile:
+        from stereovision_amd.distributed import band_rows, median_halo
+        r0, r1 = band_rows(H, 0, ngpu)
+        h0, h1 = median_halo(r0, r1, H)
+        npx = (h1 - h0) * W
     k_avg_s = (match_ms / match_n) * 1e-3 if match_n else None
-    k_bytes = 4 * npx                          # 2 u8 images read + int16 map written
-    frame_bytes = 11 * H * W                   # 2 u8 in; depth f32 + disparity f32 + u8 out
+    k_bytes = 6 * npx         # 2 u8 images read + the f32 disparity map
+    k_bytes_kernel = 4 * npx  # what k_match itself moves: 2 u8 images in, int16 map out
+    frame_bytes = 11 * n_px   # 2 u8 in; depth f32 + disparity f32 + u8 out
     if harris:
-        frame_bytes += 4 * H * W               # + the f32 Harris response
+        frame_bytes += 4 * n_px
     if rectify:
-        frame_bytes = 11 * H * W + 2 * 10 * H * W   # + per camera: map 6 B, BGR 3 B, gray 1 B
+        frame_bytes = 11 * n_px + 2 * 10 * n_px   # + per camera: map 6 B, BGR 3 B, gray 1 B
     roofline = None
+    pmc = {}
     if k_avg_s:
+        if rank == 0 and not args.no_live_pmc and not launched and len(engines) == 1 and not rowtile:
+            t_p = time.perf_counter()
+            pmc = live_pmc(args, "sgbm" if args.cost == "sgbm" else "k_match")
+            pmc["seconds"] = round(time.perf_counter() - t_p, 1)
         achieved = k_bytes / k_avg_s / 1e9
-        pmc = pmc_entry(f"{W}x{H}_D{D}_w{win}_{args.cost}" + (f"_b{B}" if B > 1 and not rowtile else ""))
-        insts = pmc.get("valu_insts_per_launch")
+        insts = pmc.get("SQ_INSTS_VALU")
+        fetch = pmc.get("FETCH_SIZE")
+        write = pmc.get("WRITE_SIZE")
+        traffic = round((fetch + write) * 1024) if fetch is not None and write is not None else None
         roofline = {
             "kernel": k_name, "bound": "hbm", "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": pmc.get("hbm_bytes_per_launch"),
-            "bytes_per_launch": k_bytes, "avg_launch_us": round(k_avg_s * 1e6, 2),
-            "launches": match_n,
+            "traffic": traffic,
+            "bytes_per_launch": k_bytes,
+            "bytes_rule": "SURVEY.md §8(d): 6 B/px (2 u8 images + f32 disparity) x pixels per launch",
+            "kernel_bytes_per_launch": k_bytes_kernel,
+            "frac_kernel_bytes": round(k_bytes_kernel / k_avg_s / 1e9 / HBM_PEAK_GBS, 5),
+            "avg_launch_us": round(k_avg_s * 1e6, 2), "launches": match_n,
+            "limiter": "valu",
             # what actually bounds k_match: VALU issue.  SQ_INSTS_VALU per
-            # launch (rocprofv3 PMC, profiles/) over the live launch time, against the
+            # launch from the live rocprofv3 pass over the live launch time, against the
             # full-rate issue peak (1 wave64 instruction / 2 cycles / SIMD); v_sad_u8 and the
             # other VOP3 integer ops issue at half that rate (profiles/r01_valu_rate.txt).
-            "valu": {"unit": "wave-instr/s",
+            "valu": {"bound": "valu", "unit": "wave-instr/s",
                      "achieved": round(insts / k_avg_s) if insts else None,
                      "peak": VALU_ISSUE_PEAK,
                      "frac": round(insts / k_avg_s / VALU_ISSUE_PEAK, 4) if insts else None,
-                     "insts_per_launch": insts,
+                     "insts_per_launch": round(insts) if insts else None,
+                     "insts_per_wave_cell": (round(insts / (npx * D / 64), 3) if insts else None),
                      "cells_per_s": round(npx * D / k_avg_s)},
+            "pmc": {"source": "rocprofv3 --pmc, 3 separate passes over a 6-step child run of this "
+                              "script on this box (mean per k_match dispatch)",
+                    "traffic_note": "FETCH_SIZE + WRITE_SIZE (KiB x 1024), uncorrected: the gfx950 "
+                                    "x2 FETCH correction applies to 16-B/lane streaming reads; "
+                                    "k_match reads dwords",
+                    **{k: (round(v, 1) if isinstance(v, float) else v) for k, v in pmc.items()}},
             "median_post_avg_us": round(med_ms / med_n * 1e3, 2) if med_n else None,
         }
 
+    parallelism = (f"row-tiled x{ngpu} + band gather" if rowtile else
+                   f"frame-sharded x{ngpu}" + (" + gather" if args.gather else ""))
+    if ngpu > 1:
+        parallelism += (f" ({'one process per GPU, ' + pg.backend if launched else 'one process, ' + ('RCCL group' if comms else 'peer copies')})")
     result = {
         "metric": "disparity frames/sec + HBM GB/s, 1920x1080 D=128 win=9, 1/2/4/8 GPU",
-        "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "value": round(value, 2), "unit": "frames/s", "n_gpus": ngpu, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong" if rowtile else "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic rectified pairs (stereovision_amd.synthetic, seeds per rank)",
+        "data": "synthetic rectified pairs (stereovision_amd.synthetic, distinct seeds per GPU)",
         "config": {"workload": (f"{W}x{H} D={D} win={win} {args.cost.upper()} camera pipeline: "
                                 "raw BGR frames resident in HBM -> rectify+gray (k_remap) -> "
                                 "disparity -> median5 + depth post" if rectify else
@@ -408,37 +613,42 @@ def main():
                                 "), gray inputs resident in HBM"),
                    "harris": harris,
                    "height": H, "width": W, "num_disp": D, "win": win, "cost": args.cost,
-                   "frames_resident_per_rank": 1 if rowtile else F,
-                   "frames_per_step": 1 if rowtile else B,
-                   "parallelism": (f"row-tiled x{world} + RCCL row gather" if rowtile else
-                                   f"frame-sharded x{world}" + (" + RCCL gather" if args.gather else "")),
-                   "dist_backend": args.dist_backend if world > 1 else None},
+                   "frames_resident_per_gpu": 1 if rowtile else F,
+                   "frames_per_step_per_gpu": 1 if rowtile else B,
+                   "parallelism": parallelism},
         "hbm_gbs_frame_path": round(frame_bytes * value / 1e9, 2),
         # BASELINE.md's fixed roofline formulas, per GPU: 6*H*W algorithmic bytes and
         # H*W*D*win^2 SAD taps per frame against 8.0e12 B/s and 157.3e12 taps/s.  The
         # taps fraction exceeds 1 because running window sums do O(1) work per tap column.
         "baseline_roofline": {
-            "fps_per_gpu": round(value / world, 2),
-            "achieved_hbm_frac": round(6 * H * W * value / world / 8.0e12, 5),
-            "achieved_valu_frac": round(H * W * D * win * win * value / world / 157.3e12, 4)},
+            "fps_per_gpu": round(value / ngpu, 2),
+            "achieved_hbm_frac": round(6 * n_px * value / ngpu / 8.0e12, 5),
+            "achieved_valu_frac": round(n_px * D * win * win * value / ngpu / 157.3e12, 4)},
         "roofline": roofline,
         "aux_kernels": None,
+        "host_path": None,
         "cpu_baseline": None,
     }
+    solo = rank == 0 and ngpu == 1
     if rectify and remap_n:
         result["aux_kernels"] = {
-            "k_remap_bgr2gray": hbm_entry("k_remap<3,gray>", 10 * H * W * B, remap_ms, remap_n)}
+            "k_remap_bgr2gray": hbm_entry("k_remap<3,gray>", 10 * n_px * B, remap_ms, remap_n)}
         rect.close()
-    elif rank == 0 and world == 1 and not rowtile and not args.no_aux:
+    elif solo and not rowtile and not args.no_aux:
         try:
-            result["aux_kernels"] = aux_kernels(eng, dev, H, W, B, stream, med_ms, med_n)
+            result["aux_kernels"] = aux_kernels(eng, H, W, B, med_ms, med_n)
         except Exception as e:  # reported, never required
             log(f"aux kernels failed: {e}")
     if harris and harris_n:     # 1 B/px gray read + 4 B/px f32 response written
         result["aux_kernels"] = dict(result["aux_kernels"] or {})
-        result["aux_kernels"]["k_harris"] = hbm_entry("k_harris_lds", 5 * H * W * B, harris_ms,
+        result["aux_kernels"]["k_harris"] = hbm_entry("k_harris_lds", 5 * n_px * B, harris_ms,
                                                        harris_n)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if solo and not args.no_host_path and args.cost != "sgbm" and not rectify:
+        try:
+            result["host_path"] = host_path(H, W, D, win)
+        except Exception as e:  # reported, never required
+            log(f"host path failed: {e}")
+    if solo and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(H, W, D, win, args.cost, args.cpu_seconds,
                                                   harris=harris)
@@ -446,8 +656,15 @@ def main():
             log(f"cpu baseline failed: {e}")
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if tile is not None:
+        tile.close()
+    for a in arenas:
+        a.free()
+    if comms:
+        for c in comms:
+            c.close()
+    if pg is not None:
+        pg.close()
 
 
 if __name__ == "__main__":

@@ -135,6 +135,22 @@ int sv_stereo_scaled(sv_ctx* ctx, const uint8_t* left, const uint8_t* right, int
                      float* disparity_normalized, float* disparity, uint8_t* normalized_u8,
                      float* confidence);
 
+/* The same two entry points with the display colormap of the drop-ins fused into the
+ * median/post kernel (cv2.applyColorMap(depth_normalized, COLORMAP_TURBO) at depth_map.py:937;
+ * COLORMAP_JET of the normalised disparity at fused_depth_map.py:1013): cmap_bgr is the
+ * 256 x 3 BGR table (the drop-ins pass cv2's own table, read back from cv2.applyColorMap, when
+ * cv2 is importable), depth_colormap the H x W x 3 BGR output.  depth_normalized /
+ * normalized_u8 are nullable here. */
+int sv_depth_map_color(sv_ctx* ctx, const uint8_t* left, const uint8_t* right, int H, int W,
+                       int channels, int stride, int min_disp, int num_disp, int win, int cost,
+                       float min_depth, float max_depth, float depth_range, float min_disp_global,
+                       const uint8_t* cmap_bgr, float* depth_final, float* disparity,
+                       uint8_t* depth_normalized, uint8_t* depth_colormap);
+int sv_stereo_scaled_color(sv_ctx* ctx, const uint8_t* left, const uint8_t* right, int H, int W,
+                           int channels, int stride, int min_disp, int num_disp, int win, int cost,
+                           const uint8_t* cmap_bgr, float* disparity_normalized, float* disparity,
+                           uint8_t* normalized_u8, float* confidence, uint8_t* depth_colormap);
+
 int sv_harris(sv_ctx* ctx, const uint8_t* gray, int H, int W, int stride, float* out);
 
 /* Row band [row0, row1) of the disparity map (halo rows read from the full frame, so the
@@ -208,6 +224,63 @@ int sv_multi_gpu_batch(sv_ctx* const* ctxs, int ndev, const uint8_t* left, const
                        int H, int W, int channels, int min_disp, int num_disp, int win, int cost, float min_depth,
                        float max_depth, float depth_range, float min_disp_global, float* depth_final,
                        float* disparity, uint8_t* depth_normalized);
+/* ---- multi-GPU: RCCL communicators + device-side gathers --------
+ * The reference has no distributed code; its unit of work is one frame pair per call
+ * (fused_depth_map.py:2591-2598 submits frames to a worker pool, depth_map.py:1181-1183
+ * calls create_depth_map once per frame).  The MI355X build shards frames (C4) or the row
+ * bands of one frame (C5) over GPUs and gathers the finished maps to one device over xGMI.
+ * RCCL (librccl.so.1) is loaded with dlopen on first use.
+ *   sv_comm_init_rank   one process per GPU (ncclCommInitRank; the id comes from one rank's
+ *                       sv_comm_unique_id, shared out of band)
+ *   sv_comm_init_all    one process, ndev distinct devices (ncclCommInitAll); comms[k] has
+ *                       rank k
+ *   sv_comm_barrier / sv_comm_allreduce_max_f64   blocking, one communicator per process
+ *   sv_comm_gatherv     rank k's send_bytes land at d_recv + recv_offsets[k] on `root`
+ *                       (ncclSend/ncclRecv in one group; the root's own block is a device
+ *                       copy unless it is already in place); enqueued on `stream` (NULL =
+ *                       the communicator's stream) */
+typedef struct sv_comm sv_comm;
+#define SV_COMM_ID_BYTES 128
+int sv_comm_available(void);
+int sv_comm_unique_id(uint8_t* id);
+int sv_comm_init_rank(int device, int nranks, int rank, const uint8_t* id, sv_comm** out);
+int sv_comm_init_all(int ndev, const int* devices, sv_comm** comms);
+void sv_comm_destroy(sv_comm* comm);
+int sv_comm_rank(sv_comm* comm, int* rank, int* nranks, int* device);
+int sv_comm_barrier(sv_comm* comm);
+int sv_comm_allreduce_max_f64(sv_comm* comm, double* value);
+int sv_comm_gatherv(sv_comm* comm, const void* d_send, uint64_t send_bytes, void* d_recv,
+                    const uint64_t* recv_offsets, const uint64_t* recv_bytes, int root, void* stream);
+int sv_comm_synchronize(sv_comm* comm);
+
+/* C4 on device-resident frames, one process driving ndev contexts: context k computes
+ * create_depth_map (disparity -> median -> depth post, one launch per kernel over its
+ * frames) for n_frames[k] gray pairs at d_left[k]/d_right[k] (+ z*frame_stride bytes, on
+ * its own device), and the three outputs of every frame are gathered into d_depth /
+ * d_disparity / d_norm on ctxs[0]'s device, dense, in context order (frame z of context k
+ * at index sum(n_frames[:k]) + z).  comms (nullable; else comms[k] must be on ctxs[k]'s
+ * device with rank k): the gather runs as RCCL send/recv over xGMI; NULL: hipMemcpyPeerAsync
+ * (a plain device copy when two contexts share a device).  Returns after enqueueing: the
+ * outputs are complete once ctxs[0]'s stream is (sv_synchronize(ctxs[0])). */
+int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
+                               const uint8_t* const* d_left, const uint8_t* const* d_right,
+                               const int* n_frames, int H, int W, int pitch, int64_t frame_stride,
+                               int min_disp, int num_disp, int win, int cost, float min_depth,
+                               float max_depth, float depth_range, float min_disp_global,
+                               float* d_depth, float* d_disparity, uint8_t* d_norm);
+
+/* C5: ONE frame row-tiled over ndev contexts.  Every context holds the full gray frame
+ * (d_left[k]/d_right[k] on its device; the window and median halos are read locally, so the
+ * bands reassemble bit-exactly); context k computes output rows [H*k/ndev, H*(k+1)/ndev)
+ * of create_depth_map and the bands are gathered into the full H x W d_depth / d_disparity
+ * / d_norm on ctxs[0]'s device.  comms / completion as sv_multi_gpu_depth_map_dev. */
+int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
+                            const uint8_t* const* d_left, const uint8_t* const* d_right, int H,
+                            int W, int pitch, int min_disp, int num_disp, int win, int cost,
+                            float min_depth, float max_depth, float depth_range,
+                            float min_disp_global, float* d_depth, float* d_disparity,
+                            uint8_t* d_norm);
+
 int sv_harris_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, float* d_out,
                   void* stream);
 /* Harris response of n_frames gray frames (frame z at d_gray + z*frame_stride bytes, output

@@ -35,6 +35,23 @@ def _jet_lut() -> np.ndarray:
 
 
 _LUTS = {"turbo": _turbo_lut(), "jet": _jet_lut()}
+_TABLES: dict = {}
+
+
+def table(name: str) -> np.ndarray:
+    """The 256 x 3 BGR table of colormap `name` that the GPU epilogue applies: cv2's own
+    (read back through cv2.applyColorMap on the 256 gray levels, byte-exact with the
+    reference) when cv2 is importable, the built-in LUT otherwise."""
+    t = _TABLES.get(name)
+    if t is None:
+        if cv2 is not None:
+            code = cv2.COLORMAP_TURBO if name == "turbo" else cv2.COLORMAP_JET
+            t = np.ascontiguousarray(cv2.applyColorMap(np.arange(256, dtype=np.uint8).reshape(256, 1),
+                                                       code).reshape(256, 3))
+        else:
+            t = _LUTS[name]
+        _TABLES[name] = t
+    return t
 
 
 def apply(u8: np.ndarray, name: str) -> np.ndarray:

@@ -4,6 +4,7 @@
 // Host entry points stage into pinned memory, run the whole chain on the context stream
 // and copy results back; device entry points only enqueue.  No exception crosses the ABI.
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -22,6 +23,12 @@ int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+
+}  // namespace
+
+int sv::set_error(int code, const std::string& msg) { return fail(code, msg); }
+
+namespace {
 
 int hipfail(int e, const char* what) {
     return fail(SV_EHIP, std::string(what) + ": " + hipGetErrorString((hipError_t)e));
@@ -101,7 +108,9 @@ struct sv_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut, rmap1, rmap2, rdst[2], stats, sel,
-        sg_hsum, sg_c, sg_l, sg_lt, sg_band, cc_parent, cc_size, hist_copies;
+        sg_hsum, sg_c, sg_l, sg_lt, sg_band, cc_parent, cc_size, hist_copies, cmap, bgr;
+    uint8_t cmap_host[768] = {};   // BGR table currently in `cmap`
+    bool cmap_valid = false;
     // SGBM: second stream + fork/join events for the vertical path beside the horizontal ones
     hipStream_t sg_aux = nullptr;
     hipEvent_t sg_ev[2] = {nullptr, nullptr};
@@ -120,6 +129,13 @@ struct sv_ctx {
     hipEvent_t lut_ev = nullptr;
     hipStream_t lut_stream = nullptr;   // stream the table was built on
     HostBuf hin, hout;
+    // Cross-stream ordering of the context's scratch (d16, the post table, HOG histograms,
+    // SGBM volumes, reduction accumulators): `*_dev` calls may pass any stream, so a call on
+    // stream s first waits for the event recorded after the previous scratch user when that
+    // ran on another stream, and records a new one after enqueueing (ScratchUse below).
+    hipStream_t scr_stream = nullptr;
+    hipEvent_t scr_ev = nullptr;
+    hipEvent_t xev = nullptr;   // multi-device entry points: this context's part is enqueued
     bool prof = false;
     std::vector<EvPair> pending;
     std::vector<hipEvent_t> pool;
@@ -373,6 +389,27 @@ int attach_lut(sv_ctx* c, sv::PostParams& pp, hipStream_t s) {
     return 0;
 }
 
+// Device copy of a 256-entry BGR colormap table (re-uploaded only when it changes).
+int attach_cmap(sv_ctx* c, sv::PostParams& pp, const uint8_t* table, uint8_t* d_bgr, hipStream_t s) {
+    pp.out_bgr = nullptr;
+    pp.cmap = nullptr;
+    if (!d_bgr) return 0;
+    if (!table) return fail(SV_EINVAL, "colormap output without a table");
+    SV_HIP(c->cmap.ensure(256 * sizeof(uint32_t)));
+    if (!c->cmap_valid || std::memcmp(c->cmap_host, table, 768) != 0) {
+        uint32_t packed[256];
+        for (int i = 0; i < 256; ++i)
+            packed[i] = (uint32_t)table[3 * i] | ((uint32_t)table[3 * i + 1] << 8) | ((uint32_t)table[3 * i + 2] << 16);
+        SV_HIP(hipMemcpyAsync(c->cmap.p, packed, sizeof(packed), hipMemcpyHostToDevice, s));
+        SV_HIP(hipStreamSynchronize(s));   // `packed` lives on this stack frame
+        std::memcpy(c->cmap_host, table, 768);
+        c->cmap_valid = true;
+    }
+    pp.out_bgr = d_bgr;
+    pp.cmap = c->cmap.as<uint32_t>();
+    return 0;
+}
+
 sv::PostParams make_post(int mode, float minf, float maxf, float rangef, float mdg, int min_disp,
                          int num_disp, float* a, uint8_t* u8, float* b) {
     sv::PostParams pp{};
@@ -451,6 +488,31 @@ int collect(sv_ctx* c, const Out* outs, int n) {
     }
     return 0;
 }
+
+// RAII: wait for the previous user of the context scratch if it ran on another stream;
+// on scope exit (after this call's enqueues) record the event the next user waits for.
+struct ScratchUse {
+    sv_ctx* c;
+    hipStream_t s;
+    int rc = 0;
+    ScratchUse(sv_ctx* ctx, hipStream_t stream) : c(ctx), s(stream) {
+        if (c->scr_stream && c->scr_stream != s && c->scr_ev) {
+            hipError_t e = hipStreamWaitEvent(s, c->scr_ev, 0);
+            if (e != hipSuccess) rc = hipfail((int)e, "hipStreamWaitEvent (context scratch)");
+        }
+    }
+    ~ScratchUse() {
+        if (!c->scr_ev && hipEventCreateWithFlags(&c->scr_ev, hipEventDisableTiming) != hipSuccess) {
+            c->scr_ev = nullptr;
+            return;
+        }
+        if (hipEventRecord(c->scr_ev, s) == hipSuccess) c->scr_stream = s;
+    }
+};
+
+#define SV_SCRATCH(ctx, stream)                                             \
+    ScratchUse scratch_(ctx, stream);                                       \
+    if (scratch_.rc) return scratch_.rc
 
 struct Guard {
     sv_ctx* c;
@@ -573,9 +635,11 @@ void sv_destroy(sv_ctx* c) {
                           &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->lut,
                           &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1], &c->stats, &c->sel,
                           &c->sg_hsum, &c->sg_c, &c->sg_l, &c->sg_lt, &c->sg_band, &c->cc_parent,
-                          &c->hist_copies,
+                          &c->hist_copies, &c->cmap, &c->bgr,
                           &c->cc_size};
         if (c->lut_ev) (void)hipEventDestroy(c->lut_ev);
+        if (c->scr_ev) (void)hipEventDestroy(c->scr_ev);
+        if (c->xev) (void)hipEventDestroy(c->xev);
         if (c->sg_aux) {
             (void)hipStreamSynchronize(c->sg_aux);
             (void)hipStreamDestroy(c->sg_aux);
@@ -625,8 +689,10 @@ int sv_disparity_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, i
     if (check_image(d_left, H, W) || check_image(d_right, H, W) || !d_disp16)
         return fail(SV_EINVAL, "bad disparity arguments");
     if (pitch < W || out_pitch < W) return fail(SV_EINVAL, "pitch smaller than width");
+    hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
     return enqueue_disparity(c, d_left, d_right, H, W, pitch, min_disp, num_disp, win, cost, row0, row1,
-                             d_disp16, out_pitch, pick(c, stream));
+                             d_disp16, out_pitch, s);
 }
 
 int sv_median_post_dev(sv_ctx* c, const int16_t* d_disp16, int H, int W, int row0, int row1, int mode,
@@ -641,6 +707,7 @@ int sv_median_post_dev(sv_ctx* c, const int16_t* d_disp16, int H, int W, int row
     if (row0 < 0) row0 = 0;
     if (row1 > H) row1 = H;
     hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
     sv::PostParams pp = make_post(mode, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
                                   d_out_a, d_out_u8, d_out_b);
     int lrc = attach_lut(c, pp, s);
@@ -657,6 +724,7 @@ int sv_depth_map_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, i
     if (check_image(d_left, H, W) || check_image(d_right, H, W) || !d_depth || !d_disparity || !d_norm)
         return fail(SV_EINVAL, "bad depth-map arguments");
     hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
     SV_HIP(c->d16.ensure((size_t)H * W * sizeof(int16_t)));
     int rc = enqueue_disparity(c, d_left, d_right, H, W, pitch, min_disp, num_disp, win, cost, 0, H,
                                c->d16.as<int16_t>(), W, s);
@@ -680,8 +748,10 @@ int sv_disparity_batch_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_ri
     if (n_frames > 1 && (frame_stride < (int64_t)pitch * H || out_frame_stride < (int64_t)out_pitch * H))
         return fail(SV_EINVAL, "frame stride smaller than a frame");
     if (n_frames == 0) return 0;
+    hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
     return enqueue_disparity(c, d_left, d_right, H, W, pitch, min_disp, num_disp, win, cost, 0, H, d_disp16,
-                             out_pitch, pick(c, stream), n_frames, frame_stride, out_frame_stride);
+                             out_pitch, s, n_frames, frame_stride, out_frame_stride);
 }
 
 int sv_median_post_batch_dev(sv_ctx* c, const int16_t* d_disp16, int n_frames, int H, int W, int mode,
@@ -695,6 +765,7 @@ int sv_median_post_batch_dev(sv_ctx* c, const int16_t* d_disp16, int n_frames, i
         return fail(SV_EINVAL, "scaled post outputs missing");
     if (n_frames == 0) return 0;
     hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
     sv::PostParams pp = make_post(mode, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
                                   d_out_a, d_out_u8, d_out_b);
     int rc = attach_lut(c, pp, s);
@@ -716,6 +787,7 @@ int sv_depth_map_batch_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_ri
     if (n_frames > 1 && frame_stride < (int64_t)pitch * H) return fail(SV_EINVAL, "frame stride smaller than a frame");
     if (n_frames == 0) return 0;
     hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
     const long long fs = (long long)H * W;
     SV_HIP(c->d16.ensure((size_t)n_frames * fs * sizeof(int16_t)));
     int rc = enqueue_disparity(c, d_left, d_right, H, W, pitch, min_disp, num_disp, win, cost, 0, H,
@@ -732,11 +804,22 @@ int sv_depth_map_batch_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_ri
 
 // One shard of sv_multi_gpu_batch: frames [f0, f1) on context c (host buffers in and out).
 namespace {
+int check_contexts(sv_ctx* const* ctxs, int ndev) {
+    if (!ctxs || ndev < 1) return fail(SV_EINVAL, "no contexts");
+    for (int k = 0; k < ndev; ++k) {
+        if (!ctxs[k]) return fail(SV_EINVAL, "null context");
+        for (int j = 0; j < k; ++j)
+            if (ctxs[j] == ctxs[k]) return fail(SV_EINVAL, "a context appears twice");
+    }
+    return 0;
+}
+
 int depth_map_shard(sv_ctx* c, const uint8_t* left, const uint8_t* right, int f0, int f1, int H, int W,
                     int channels, int min_disp, int num_disp, int win, int cost, float min_depth,
                     float max_depth, float depth_range, float min_disp_global, float* depth_final,
                     float* disparity, uint8_t* depth_normalized) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     const int nf = f1 - f0;
     if (nf <= 0) return 0;
     const size_t n = (size_t)H * W, fin = n * channels;
@@ -753,10 +836,10 @@ int depth_map_shard(sv_ctx* c, const uint8_t* left, const uint8_t* right, int f0
         } else {
             SV_HIP(c->img[k].ensure(nf * fin));
             SV_HIP(hipMemcpyAsync(c->img[k].p, stage, nf * fin, hipMemcpyHostToDevice, c->stream));
-            for (int f = 0; f < nf; ++f)
-                SV_LAUNCH(c, SV_K_GRAY, c->stream,
-                          sv::launch_gray(c->img[k].as<uint8_t>() + f * fin, H, W, W * channels,
-                                          c->gray[k].as<uint8_t>() + f * n, c->stream));
+            // contiguous frames: the shard's BGR stack is one (nf*H) x W image, one launch
+            SV_LAUNCH(c, SV_K_GRAY, c->stream,
+                      sv::launch_gray(c->img[k].as<uint8_t>(), nf * H, W, W * channels, c->gray[k].as<uint8_t>(),
+                                      c->stream));
         }
     }
     SV_HIP(c->d16.ensure(nf * n * sizeof(int16_t)));
@@ -784,35 +867,38 @@ int sv_multi_gpu_batch(sv_ctx* const* ctxs, int ndev, const uint8_t* left, const
                        int H, int W, int channels, int min_disp, int num_disp, int win, int cost, float min_depth,
                        float max_depth, float depth_range, float min_disp_global, float* depth_final,
                        float* disparity, uint8_t* depth_normalized) {
-    if (!ctxs || ndev < 1) return fail(SV_EINVAL, "no contexts");
-    for (int k = 0; k < ndev; ++k) {
-        if (!ctxs[k]) return fail(SV_EINVAL, "null context");
-        for (int j = 0; j < k; ++j)
-            if (ctxs[j] == ctxs[k]) return fail(SV_EINVAL, "a context appears twice");
-    }
+    int rc = check_contexts(ctxs, ndev);
+    if (rc) return rc;
     if (n_frames < 0) return fail(SV_EINVAL, "negative frame count");
     if (n_frames == 0) return 0;
     if (!left || !right || !depth_final || !disparity || !depth_normalized) return fail(SV_EINVAL, "null buffers");
     if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
     sv::MatchPlan plan;
-    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
     if (rc) return rc;
     // contiguous shards, one host thread per context: each stages, computes and collects
-    // its frames on its own device/stream concurrently with the others
-    // (no C++ exception may cross the ABI: thread creation failures become SV_ENOMEM)
-    std::vector<int> rcs(ndev, 0);
-    std::vector<std::string> errs(ndev);
-    std::vector<std::thread> th;
+    // its frames on its own device/stream concurrently with the others (every device
+    // returns its shard over its own PCIe link).  No C++ exception may cross the ABI: any
+    // allocation or thread-start failure becomes SV_ENOMEM.
     int spawn_rc = 0;
+    std::vector<int> rcs;
+    std::vector<std::string> errs;
+    std::vector<std::thread> th;
     try {
+        rcs.assign(ndev, 0);
+        errs.resize(ndev);
         th.reserve(ndev);
         for (int k = 0; k < ndev; ++k) {
             const int f0 = (int)((long long)n_frames * k / ndev), f1 = (int)((long long)n_frames * (k + 1) / ndev);
-            th.emplace_back([&, k, f0, f1] {
-                rcs[k] = depth_map_shard(ctxs[k], left, right, f0, f1, H, W, channels, min_disp, num_disp, win,
-                                         cost, min_depth, max_depth, depth_range, min_disp_global, depth_final,
-                                         disparity, depth_normalized);
-                if (rcs[k]) errs[k] = g_err;
+            th.emplace_back([&, k, f0, f1]() noexcept {
+                try {
+                    rcs[k] = depth_map_shard(ctxs[k], left, right, f0, f1, H, W, channels, min_disp, num_disp, win,
+                                             cost, min_depth, max_depth, depth_range, min_disp_global, depth_final,
+                                             disparity, depth_normalized);
+                    if (rcs[k]) errs[k] = g_err;
+                } catch (...) {
+                    rcs[k] = SV_ENOMEM;
+                }
             });
         }
     } catch (...) {
@@ -823,6 +909,265 @@ int sv_multi_gpu_batch(sv_ctx* const* ctxs, int ndev, const uint8_t* left, const
     for (int k = 0; k < ndev; ++k)
         if (rcs[k]) return fail(rcs[k], "device shard " + std::to_string(k) + ": " + errs[k]);
     return 0;
+}
+
+namespace {
+
+// Locks every context of a multi-device call (in address order: no lock-order inversion
+// between concurrent calls over overlapping context sets).
+struct MultiLock {
+    std::vector<std::unique_lock<std::mutex>> locks;
+    bool ok = true;
+    MultiLock(sv_ctx* const* ctxs, int n) {
+        try {
+            std::vector<sv_ctx*> v(ctxs, ctxs + n);
+            std::sort(v.begin(), v.end());
+            for (sv_ctx* c : v) locks.emplace_back(c->mu);
+        } catch (...) {
+            ok = false;
+        }
+    }
+};
+
+// Scratch hazard (ScratchUse) for an explicit device/stream, and the join event.
+int scratch_wait(sv_ctx* c, hipStream_t s) {
+    if (c->scr_stream && c->scr_stream != s && c->scr_ev) SV_HIP(hipStreamWaitEvent(s, c->scr_ev, 0));
+    return 0;
+}
+int scratch_mark(sv_ctx* c, hipStream_t s) {
+    if (!c->scr_ev) SV_HIP(hipEventCreateWithFlags(&c->scr_ev, hipEventDisableTiming));
+    SV_HIP(hipEventRecord(c->scr_ev, s));
+    c->scr_stream = s;
+    return 0;
+}
+int join_event(sv_ctx* c, hipStream_t s) {
+    if (!c->xev) SV_HIP(hipEventCreateWithFlags(&c->xev, hipEventDisableTiming));
+    SV_HIP(hipEventRecord(c->xev, s));
+    return 0;
+}
+
+int check_comms(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev) {
+    if (!comms) return 0;
+    for (int k = 0; k < ndev; ++k) {
+        if (!comms[k]) return fail(SV_EINVAL, "comms[k] is null");
+        if (sv::comm_device(comms[k]) != ctxs[k]->device || sv::comm_rank(comms[k]) != k ||
+            sv::comm_size(comms[k]) != ndev)
+            return fail(SV_EINVAL, "comms[k] must be rank k of an ndev-rank communicator on ctxs[k]'s device");
+    }
+    return 0;
+}
+
+// One block (device bytes) of context k -> the root's buffer, by peer copy on k's stream.
+int peer_copy(sv_ctx* root, sv_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) return 0;
+    if (c->device == root->device) {
+        SV_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+    } else {
+        SV_HIP(hipMemcpyPeerAsync(dst, root->device, src, c->device, bytes, s));
+    }
+    return 0;
+}
+
+int enable_peer(int from, int to) {
+    if (from == to) return 0;
+    int can = 0;
+    SV_HIP(hipDeviceCanAccessPeer(&can, from, to));
+    if (!can) return 0;   // hipMemcpyPeerAsync still works (staged by the runtime)
+    SV_HIP(hipSetDevice(from));
+    hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return hipfail((int)e, "hipDeviceEnablePeerAccess");
+    (void)hipGetLastError();   // clear the sticky "already enabled"
+    return 0;
+}
+
+struct Block {
+    void* dst;        // on the root device
+    const void* src;  // on context k's device
+    size_t bytes;
+};
+
+// Gather the blocks of contexts 1..ndev-1 into the root's buffers: RCCL send/recv in one
+// group (comms) or peer copies; the root stream then waits for every part.
+int gather_blocks(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const std::vector<std::vector<Block>>& blocks) {
+    sv_ctx* root = ctxs[0];
+    if (comms && ndev > 1) {
+        int rc = sv::comm_group_start();
+        if (rc) return rc;
+        int erc = 0;
+        for (int k = 1; k < ndev && !erc; ++k)
+            for (const Block& b : blocks[k]) {
+                if (!b.bytes) continue;
+                erc = sv::comm_send(comms[k], b.src, b.bytes, 0, ctxs[k]->stream);
+                if (!erc) erc = sv::comm_recv(comms[0], b.dst, b.bytes, k, root->stream);
+                if (erc) break;
+            }
+        rc = sv::comm_group_end();
+        if (erc) return erc;
+        if (rc) return rc;
+        return 0;
+    }
+    for (int k = 1; k < ndev; ++k) {
+        sv_ctx* c = ctxs[k];
+        SV_HIP(hipSetDevice(c->device));
+        for (const Block& b : blocks[k]) {
+            int rc = peer_copy(root, c, b.dst, b.src, b.bytes, c->stream);
+            if (rc) return rc;
+        }
+        int rc = join_event(c, c->stream);
+        if (rc) return rc;
+    }
+    SV_HIP(hipSetDevice(root->device));
+    for (int k = 1; k < ndev; ++k) SV_HIP(hipStreamWaitEvent(root->stream, ctxs[k]->xev, 0));
+    return 0;
+}
+
+int multi_prologue(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev) {
+    int rc = check_contexts(ctxs, ndev);
+    if (rc) return rc;
+    rc = check_comms(ctxs, comms, ndev);
+    if (rc) return rc;
+    if (!comms)
+        for (int k = 1; k < ndev; ++k) {
+            rc = enable_peer(ctxs[k]->device, ctxs[0]->device);
+            if (rc) return rc;
+        }
+    return 0;
+}
+
+}  // namespace
+
+int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
+                               const uint8_t* const* d_right, const int* n_frames, int H, int W, int pitch,
+                               int64_t frame_stride, int min_disp, int num_disp, int win, int cost, float min_depth,
+                               float max_depth, float depth_range, float min_disp_global, float* d_depth,
+                               float* d_disparity, uint8_t* d_norm) {
+    if (!d_left || !d_right || !n_frames || !d_depth || !d_disparity || !d_norm) return fail(SV_EINVAL, "null arguments");
+    int rc = multi_prologue(ctxs, comms, ndev);
+    if (rc) return rc;
+    sv::MatchPlan plan;
+    rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    if (pitch < W) return fail(SV_EINVAL, "pitch smaller than width");
+    for (int k = 0; k < ndev; ++k) {
+        if (n_frames[k] < 0) return fail(SV_EINVAL, "negative frame count");
+        if (n_frames[k] > 0 && (check_image(d_left[k], H, W) || check_image(d_right[k], H, W)))
+            return fail(SV_EINVAL, "null frames");
+        if (n_frames[k] > 1 && frame_stride < (int64_t)pitch * H) return fail(SV_EINVAL, "frame stride smaller than a frame");
+    }
+    MultiLock lock(ctxs, ndev);
+    if (!lock.ok) return fail(SV_ENOMEM, "lock allocation failed");
+    const size_t n = (size_t)H * W;
+    std::vector<std::vector<Block>> blocks;
+    try {
+        blocks.resize(ndev);
+    } catch (...) {
+        return fail(SV_ENOMEM, "allocation failed");
+    }
+    size_t f_off = 0;
+    for (int k = 0; k < ndev; ++k) {
+        sv_ctx* c = ctxs[k];
+        const int nf = n_frames[k];
+        const size_t off = f_off;
+        f_off += (size_t)nf;
+        if (nf == 0) continue;
+        SV_HIP(hipSetDevice(c->device));
+        hipStream_t s = c->stream;
+        rc = scratch_wait(c, s);
+        if (rc) return rc;
+        SV_HIP(c->d16.ensure((size_t)nf * n * sizeof(int16_t)));
+        float* o_depth = d_depth + off * n;
+        float* o_disp = d_disparity + off * n;
+        uint8_t* o_norm = d_norm + off * n;
+        if (k > 0) {   // results stay in this context's scratch until gathered
+            SV_HIP(c->fa.ensure((size_t)nf * n * sizeof(float)));
+            SV_HIP(c->fb.ensure((size_t)nf * n * sizeof(float)));
+            SV_HIP(c->u8.ensure((size_t)nf * n));
+            o_depth = c->fb.as<float>();
+            o_disp = c->fa.as<float>();
+            o_norm = c->u8.as<uint8_t>();
+        }
+        rc = enqueue_disparity(c, d_left[k], d_right[k], H, W, pitch, min_disp, num_disp, win, cost, 0, H,
+                               c->d16.as<int16_t>(), W, s, nf, frame_stride, (long long)n);
+        if (rc) return rc;
+        sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                                      num_disp, o_depth, o_norm, nullptr);
+        rc = attach_lut(c, pp, s);
+        if (rc) return rc;
+        SV_LAUNCH(c, SV_K_MEDIAN, s,
+                  sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, o_disp, pp, s, nf, (long long)n,
+                                        (long long)n));
+        rc = scratch_mark(c, s);
+        if (rc) return rc;
+        if (k > 0)
+            blocks[k] = {{d_depth + off * n, o_depth, (size_t)nf * n * sizeof(float)},
+                         {d_disparity + off * n, o_disp, (size_t)nf * n * sizeof(float)},
+                         {d_norm + off * n, o_norm, (size_t)nf * n}};
+    }
+    return gather_blocks(ctxs, comms, ndev, blocks);
+}
+
+int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
+                            const uint8_t* const* d_right, int H, int W, int pitch, int min_disp, int num_disp,
+                            int win, int cost, float min_depth, float max_depth, float depth_range,
+                            float min_disp_global, float* d_depth, float* d_disparity, uint8_t* d_norm) {
+    if (!d_left || !d_right || !d_depth || !d_disparity || !d_norm) return fail(SV_EINVAL, "null arguments");
+    int rc = multi_prologue(ctxs, comms, ndev);
+    if (rc) return rc;
+    sv::MatchPlan plan;
+    rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    if (cost == SV_COST_SGBM && ndev > 1) return fail(SV_EINVAL, "SGBM cannot be row-tiled (top-down path)");
+    if (pitch < W) return fail(SV_EINVAL, "pitch smaller than width");
+    for (int k = 0; k < ndev; ++k)
+        if (check_image(d_left[k], H, W) || check_image(d_right[k], H, W)) return fail(SV_EINVAL, "null frames");
+    MultiLock lock(ctxs, ndev);
+    if (!lock.ok) return fail(SV_ENOMEM, "lock allocation failed");
+    const size_t n = (size_t)H * W;
+    std::vector<std::vector<Block>> blocks;
+    try {
+        blocks.resize(ndev);
+    } catch (...) {
+        return fail(SV_ENOMEM, "allocation failed");
+    }
+    for (int k = 0; k < ndev; ++k) {
+        sv_ctx* c = ctxs[k];
+        const int r0 = (int)((long long)H * k / ndev), r1 = (int)((long long)H * (k + 1) / ndev);
+        if (r1 <= r0) continue;
+        const int h0 = r0 - 2 > 0 ? r0 - 2 : 0, h1 = r1 + 2 < H ? r1 + 2 : H;   // 5x5 median halo
+        SV_HIP(hipSetDevice(c->device));
+        hipStream_t s = c->stream;
+        rc = scratch_wait(c, s);
+        if (rc) return rc;
+        SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
+        float* o_depth = d_depth;
+        float* o_disp = d_disparity;
+        uint8_t* o_norm = d_norm;
+        if (k > 0) {
+            SV_HIP(c->fa.ensure(n * sizeof(float)));
+            SV_HIP(c->fb.ensure(n * sizeof(float)));
+            SV_HIP(c->u8.ensure(n));
+            o_depth = c->fb.as<float>();
+            o_disp = c->fa.as<float>();
+            o_norm = c->u8.as<uint8_t>();
+        }
+        rc = enqueue_disparity(c, d_left[k], d_right[k], H, W, pitch, min_disp, num_disp, win, cost, h0, h1,
+                               c->d16.as<int16_t>(), W, s);
+        if (rc) return rc;
+        sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                                      num_disp, o_depth, o_norm, nullptr);
+        rc = attach_lut(c, pp, s);
+        if (rc) return rc;
+        SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(c->d16.as<int16_t>(), H, W, r0, r1, o_disp, pp, s));
+        rc = scratch_mark(c, s);
+        if (rc) return rc;
+        if (k > 0) {
+            const size_t o = (size_t)r0 * W, m = (size_t)(r1 - r0) * W;
+            blocks[k] = {{d_depth + o, o_depth + o, m * sizeof(float)},
+                         {d_disparity + o, o_disp + o, m * sizeof(float)},
+                         {d_norm + o, o_norm + o, m}};
+        }
+    }
+    return gather_blocks(ctxs, comms, ndev, blocks);
 }
 
 int sv_harris_dev(sv_ctx* c, const uint8_t* d_gray, int H, int W, int pitch, float* d_out, void* stream) {
@@ -860,6 +1205,7 @@ int sv_hog_hist_dev(sv_ctx* c, const uint8_t* d_gray, int H, int W, int pitch, i
 // ---------------------------------------------------------------- host entry points
 int sv_gray(sv_ctx* c, const uint8_t* bgr, int H, int W, int stride, uint8_t* gray) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (check_image(bgr, H, W) || !gray) return fail(SV_EINVAL, "bad gray arguments");
     const size_t row = (size_t)W * 3, n = row * H;
     if (stride < (int)row) return fail(SV_EINVAL, "stride smaller than a row");
@@ -877,6 +1223,7 @@ int sv_gray(sv_ctx* c, const uint8_t* bgr, int H, int W, int stride, uint8_t* gr
 int sv_disparity(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels, int stride,
                  int min_disp, int num_disp, int win, int cost, int16_t* disp16, float* harris) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (!disp16) return fail(SV_EINVAL, "null disparity output");
     sv::MatchPlan plan;
     int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
@@ -901,6 +1248,7 @@ int sv_disparity_rows(sv_ctx* c, const uint8_t* left, const uint8_t* right, int 
                       int stride, int min_disp, int num_disp, int win, int cost, int row0, int row1,
                       int16_t* disp16) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (!disp16) return fail(SV_EINVAL, "null disparity output");
     if (row0 < 0) row0 = 0;
     if (row1 > H) row1 = H;
@@ -952,6 +1300,7 @@ int sv_copy_to_host(sv_ctx* c, void* dst, const void* src, uint64_t bytes) {
 
 int sv_median5_f32(sv_ctx* c, const float* in, int H, int W, float* out) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (check_image(in, H, W) || !out) return fail(SV_EINVAL, "bad median arguments");
     const size_t n = (size_t)H * W * sizeof(float);
     SV_HIP(c->hin.ensure(n));
@@ -987,6 +1336,7 @@ static int post_common(sv_ctx* c, const float* disparity, int n, const sv::PostP
 int sv_depth_post(sv_ctx* c, const float* disparity, int n, float min_depth, float max_depth, float depth_range,
                   float min_disp_global, float* depth_final, uint8_t* depth_normalized) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (!depth_final || !depth_normalized) return fail(SV_EINVAL, "null outputs");
     sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, 0, 0,
                                   nullptr, nullptr, nullptr);
@@ -996,6 +1346,7 @@ int sv_depth_post(sv_ctx* c, const float* disparity, int n, float min_depth, flo
 int sv_scaled_post(sv_ctx* c, const float* disparity, int n, int min_disp, int num_disp,
                    float* disparity_normalized, uint8_t* normalized_u8, float* confidence) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (!disparity_normalized || !normalized_u8 || !confidence || num_disp <= 0)
         return fail(SV_EINVAL, "bad scaled post arguments");
     sv::PostParams pp = make_post(SV_POST_SCALED, 0.f, 0.f, 0.f, 0.f, min_disp, num_disp, nullptr, nullptr,
@@ -1008,6 +1359,7 @@ int sv_depth_map(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, in
                  float depth_range, float min_disp_global, float* depth_final, float* disparity,
                  uint8_t* depth_normalized) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (!depth_final || !disparity || !depth_normalized) return fail(SV_EINVAL, "null outputs");
     sv::MatchPlan plan;
     int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
@@ -1038,6 +1390,7 @@ int sv_stereo_scaled(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H
                      int stride, int min_disp, int num_disp, int win, int cost, float* disparity_normalized,
                      float* disparity, uint8_t* normalized_u8, float* confidence) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (!disparity_normalized || !disparity || !normalized_u8 || !confidence)
         return fail(SV_EINVAL, "null outputs");
     sv::MatchPlan plan;
@@ -1067,8 +1420,82 @@ int sv_stereo_scaled(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H
     return collect(c, o, 4);
 }
 
+int sv_depth_map_color(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels,
+                       int stride, int min_disp, int num_disp, int win, int cost, float min_depth, float max_depth,
+                       float depth_range, float min_disp_global, const uint8_t* cmap_bgr, float* depth_final,
+                       float* disparity, uint8_t* depth_normalized, uint8_t* depth_colormap) {
+    SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
+    if (!depth_final || !disparity || !depth_colormap || !cmap_bgr) return fail(SV_EINVAL, "null outputs");
+    sv::MatchPlan plan;
+    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    rc = stage_pair(c, left, right, H, W, channels, stride);
+    if (rc) return rc;
+    const size_t n = (size_t)H * W;
+    SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
+    SV_HIP(c->fa.ensure(n * sizeof(float)));
+    SV_HIP(c->fb.ensure(n * sizeof(float)));
+    SV_HIP(c->u8.ensure(n));
+    SV_HIP(c->bgr.ensure(3 * n));
+    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
+                           win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
+    if (rc) return rc;
+    sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                                  num_disp, c->fb.as<float>(), c->u8.as<uint8_t>(), nullptr);
+    rc = attach_lut(c, pp, c->stream);
+    if (!rc) rc = attach_cmap(c, pp, cmap_bgr, c->bgr.as<uint8_t>(), c->stream);
+    if (rc) return rc;
+    SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
+              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fa.as<float>(), pp, c->stream));
+    Out o[] = {{depth_final, c->fb.p, n * sizeof(float)},
+               {disparity, c->fa.p, n * sizeof(float)},
+               {depth_colormap, c->bgr.p, 3 * n},
+               {depth_normalized, c->u8.p, n}};
+    return collect(c, o, 4);
+}
+
+int sv_stereo_scaled_color(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels,
+                           int stride, int min_disp, int num_disp, int win, int cost, const uint8_t* cmap_bgr,
+                           float* disparity_normalized, float* disparity, uint8_t* normalized_u8,
+                           float* confidence, uint8_t* depth_colormap) {
+    SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
+    if (!disparity_normalized || !disparity || !confidence || !depth_colormap || !cmap_bgr)
+        return fail(SV_EINVAL, "null outputs");
+    sv::MatchPlan plan;
+    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    rc = stage_pair(c, left, right, H, W, channels, stride);
+    if (rc) return rc;
+    const size_t n = (size_t)H * W;
+    SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
+    SV_HIP(c->fa.ensure(n * sizeof(float)));
+    SV_HIP(c->fb.ensure(n * sizeof(float)));
+    SV_HIP(c->fc.ensure(n * sizeof(float)));
+    SV_HIP(c->u8.ensure(n));
+    SV_HIP(c->bgr.ensure(3 * n));
+    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
+                           win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
+    if (rc) return rc;
+    sv::PostParams pp = make_post(SV_POST_SCALED, 0.f, 0.f, 0.f, 0.f, min_disp, num_disp, c->fb.as<float>(),
+                                  c->u8.as<uint8_t>(), c->fc.as<float>());
+    rc = attach_lut(c, pp, c->stream);
+    if (!rc) rc = attach_cmap(c, pp, cmap_bgr, c->bgr.as<uint8_t>(), c->stream);
+    if (rc) return rc;
+    SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
+              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fa.as<float>(), pp, c->stream));
+    Out o[] = {{disparity_normalized, c->fb.p, n * sizeof(float)},
+               {disparity, c->fa.p, n * sizeof(float)},
+               {depth_colormap, c->bgr.p, 3 * n},
+               {confidence, c->fc.p, n * sizeof(float)},
+               {normalized_u8, c->u8.p, n}};
+    return collect(c, o, 5);
+}
+
 int sv_harris(sv_ctx* c, const uint8_t* gray, int H, int W, int stride, float* out) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (check_image(gray, H, W) || !out || stride < W) return fail(SV_EINVAL, "bad harris arguments");
     const size_t n = (size_t)H * W;
     SV_HIP(c->hin.ensure(n));
@@ -1084,6 +1511,7 @@ int sv_harris(sv_ctx* c, const uint8_t* gray, int H, int W, int stride, float* o
 
 int sv_hog_hist(sv_ctx* c, const uint8_t* gray, int H, int W, int stride, int win, uint16_t* out) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (check_image(gray, H, W) || !out || stride < W) return fail(SV_EINVAL, "bad hog arguments");
     if (win < 1 || win > 15 || (win & 1) == 0) return fail(SV_EINVAL, "win must be odd in [1, 15]");
     const size_t n = (size_t)H * W;
@@ -1115,6 +1543,7 @@ int sv_init_undistort_rectify_map_dev(sv_ctx* c, const double* K, const double* 
 int sv_init_undistort_rectify_map(sv_ctx* c, const double* K, const double* dist, int ndist, const double* R,
                                   const double* P, int p_cols, int H, int W, int16_t* map1, uint16_t* map2) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (!map1 || !map2) return fail(SV_EINVAL, "null map outputs");
     sv::UndistortParams up;
     int rc = make_undistort(K, dist, ndist, R, P, p_cols, H, W, &up);
@@ -1181,6 +1610,7 @@ static int remap_host_common(sv_ctx* c, const uint8_t* const* srcs, int nimg, in
 int sv_remap(sv_ctx* c, const uint8_t* src, int sH, int sW, int channels, int stride, const int16_t* map1,
              const uint16_t* map2, int H, int W, uint8_t* dst) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     int rc = check_remap(src, sH, sW, channels, stride, map1, H, W, dst);
     if (rc) return rc;
     const size_t n = (size_t)H * W;
@@ -1200,6 +1630,7 @@ int sv_rectify_pair(sv_ctx* c, const int16_t* d_map1_left, const uint16_t* d_map
                     const uint8_t* right, int sH, int sW, int channels, int stride, uint8_t* out_left,
                     uint8_t* out_right) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     int rc = check_remap(left, sH, sW, channels, stride, d_map1_left, H, W, out_left);
     if (!rc) rc = check_remap(right, sH, sW, channels, stride, d_map1_right, H, W, out_right);
     if (rc) return rc;
@@ -1242,6 +1673,7 @@ int sv_resize_linear_f32_dev(sv_ctx* c, const float* d_src, int sH, int sW, int 
 int sv_resize_linear(sv_ctx* c, const uint8_t* src, int sH, int sW, int channels, int stride, uint8_t* dst,
                      int dH, int dW) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (!src || !dst || sH <= 0 || sW <= 0 || dH <= 0 || dW <= 0) return fail(SV_EINVAL, "bad resize arguments");
     if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
     const size_t row = (size_t)sW * channels, n = row * sH;
@@ -1273,6 +1705,7 @@ int sv_frame_stats_dev(sv_ctx* c, const uint8_t* d_img0, const uint8_t* d_img1, 
     if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
     if (pitch < W * channels) return fail(SV_EINVAL, "pitch smaller than a row");
     hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
     const int nimg = d_img1 ? 2 : 1;
     SV_HIP(c->hist_copies.ensure_zeroed((size_t)sv::kHistCopies * 2 * 256 * sizeof(uint32_t)));
     sv::FrameStatsArgs a{};
@@ -1294,6 +1727,7 @@ int sv_frame_stats_dev(sv_ctx* c, const uint8_t* d_img0, const uint8_t* d_img1, 
 int sv_frame_stats(sv_ctx* c, const uint8_t* img0, const uint8_t* img1, int H, int W, int channels, int stride,
                    uint32_t* block_sum, uint32_t* block_sq, uint32_t* hist) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (check_image(img0, H, W) || !block_sum || !block_sq || !hist) return fail(SV_EINVAL, "bad frame-stats arguments");
     if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
     const size_t row = (size_t)W * channels, n = row * H;
@@ -1363,6 +1797,7 @@ static int select_pass(sv_ctx* c, sv::SelectArgs& a, uint32_t* hist_host, unsign
 int sv_select_count(sv_ctx* c, const float* d_x, int64_t n, int mask_mode, const float* d_mask, float thr,
                     int64_t* selected, int64_t* nans) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     int rc = check_select(d_x, n, mask_mode, d_mask);
     if (rc) return rc;
     sv::SelectArgs a{};
@@ -1388,6 +1823,7 @@ int sv_select_count(sv_ctx* c, const float* d_x, int64_t n, int mask_mode, const
 int sv_select_ranks(sv_ctx* c, const float* d_x, int64_t n, int mask_mode, const float* d_mask, float thr,
                     const int64_t* ranks, int nranks, float* values) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     int rc = check_select(d_x, n, mask_mode, d_mask);
     if (rc) return rc;
     if (!ranks || !values || nranks < 1 || nranks > sv::kMaxRanks) return fail(SV_EINVAL, "1..4 ranks");
@@ -1470,14 +1906,17 @@ int sv_sgbm_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, int H,
     if (check_image(d_left, H, W) || check_image(d_right, H, W) || !d_disp16 || pitch < W || out_pitch < W)
         return fail(SV_EINVAL, "bad SGBM arguments");
     SgbmParams p{P1, P2, disp12_max_diff, pre_filter_cap, uniqueness_ratio, speckle_window_size, speckle_range};
+    hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
     return enqueue_sgbm(c, d_left, d_right, H, W, pitch, min_disp, num_disp, block_size, p, d_disp16, out_pitch,
-                        pick(c, stream));
+                        s);
 }
 
 int sv_sgbm(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels, int stride,
             int min_disp, int num_disp, int block_size, int P1, int P2, int disp12_max_diff, int pre_filter_cap,
             int uniqueness_ratio, int speckle_window_size, int speckle_range, int16_t* disp16) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (!disp16) return fail(SV_EINVAL, "null disparity output");
     sv::MatchPlan plan;
     int rc = check_match(H, W, min_disp, num_disp, block_size, SV_COST_SGBM, &plan);
@@ -1498,11 +1937,14 @@ int sv_filter_speckles_dev(sv_ctx* c, int16_t* d_img, int H, int W, int pitch, i
                            int max_diff, void* stream) {
     SV_ENTER(c);
     if (!d_img || H <= 0 || W <= 0 || pitch < W) return fail(SV_EINVAL, "bad speckle-filter arguments");
-    return enqueue_speckles(c, d_img, H, W, pitch, new_val, max_speckle_size, max_diff, pick(c, stream));
+    hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
+    return enqueue_speckles(c, d_img, H, W, pitch, new_val, max_speckle_size, max_diff, s);
 }
 
 int sv_filter_speckles(sv_ctx* c, int16_t* img, int H, int W, int new_val, int max_speckle_size, int max_diff) {
     SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
     if (!img || H <= 0 || W <= 0) return fail(SV_EINVAL, "bad speckle-filter arguments");
     const size_t bytes = (size_t)H * W * sizeof(int16_t);
     SV_HIP(c->d16.ensure(bytes));

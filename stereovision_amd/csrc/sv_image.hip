@@ -304,6 +304,7 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
         if (pp.out_a) pp.out_a += o;
         if (pp.out_u8) pp.out_u8 += o;
         if (pp.out_b) pp.out_b += o;
+        if (pp.out_bgr) pp.out_bgr += 3 * o;
     }
     const int x0 = blockIdx.x * MQ_W, y0 = row0 + blockIdx.y * MQ_H;
     {   // thread -> one tile column (clamped once), rows g, g+3, ...: 204 of 256 threads load
@@ -388,7 +389,7 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
     const uint32_t i = (uint32_t)y * W + x;
     const bool vec = x + 3 < W && (W & 3) == 0 &&
                      (((uintptr_t)disp | (uintptr_t)pp.out_a | (uintptr_t)pp.out_b) & 15) == 0 &&
-                     ((uintptr_t)pp.out_u8 & 3) == 0;
+                     (((uintptr_t)pp.out_u8 | (uintptr_t)pp.out_bgr) & 3) == 0;
     if (vec) {
         at(reinterpret_cast<float4*>(disp), i >> 2) =
             make_float4((float)mv[0] / 16.0f, (float)mv[1] / 16.0f, (float)mv[2] / 16.0f, (float)mv[3] / 16.0f);
@@ -401,6 +402,14 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
             (uint32_t)o[0].u | ((uint32_t)o[1].u << 8) | ((uint32_t)o[2].u << 16) | ((uint32_t)o[3].u << 24);
         if (pp.mode == POST_SCALED)
             at(reinterpret_cast<float4*>(pp.out_b), i >> 2) = make_float4(o[0].b, o[1].b, o[2].b, o[3].b);
+        if (pp.out_bgr) {   // 4 pixels = 12 bytes = 3 dwords (byte offset 3i, i % 4 == 0)
+            const uint32_t c0 = pp.cmap[o[0].u], c1 = pp.cmap[o[1].u], c2 = pp.cmap[o[2].u],
+                           c3 = pp.cmap[o[3].u];
+            uint32_t* d = &at(reinterpret_cast<uint32_t*>(pp.out_bgr), 3 * (i >> 2));
+            d[0] = c0 | (c1 << 24);
+            d[1] = (c1 >> 8) | (c2 << 16);
+            d[2] = (c2 >> 16) | (c3 << 8);
+        }
         return;
     }
 #pragma unroll
@@ -412,6 +421,13 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
         at(pp.out_a, i + q) = o.a;
         at(pp.out_u8, i + q) = o.u;
         if (pp.mode == POST_SCALED) at(pp.out_b, i + q) = o.b;
+        if (pp.out_bgr) {
+            const uint32_t c = pp.cmap[o.u];
+            uint8_t* d = &at(pp.out_bgr, 3 * (i + q));
+            d[0] = (uint8_t)c;
+            d[1] = (uint8_t)(c >> 8);
+            d[2] = (uint8_t)(c >> 16);
+        }
     }
 }
 
@@ -507,6 +523,7 @@ int launch_post_lut(const PostParams& pp, int m0, int n, float* lut_a, uint8_t* 
     q.out_a = lut_a;
     q.out_u8 = lut_u8;
     q.out_b = lut_b;
+    q.out_bgr = nullptr;
     q.lut_n = 0;
     hipLaunchKernelGGL(k_post_lut, dim3((n + 255) / 256), dim3(256), 0, s, q, m0, n);
     return (int)hipGetLastError();

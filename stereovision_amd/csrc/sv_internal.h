@@ -4,7 +4,23 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
+struct sv_comm;
+
 namespace sv {
+
+// Sets the calling thread's sv_last_error() message; returns `code`.
+int set_error(int code, const std::string& msg);
+
+// RCCL transfers of the multi-device entry points (sv_comm.cpp; librccl loaded on first use).
+int comm_group_start();
+int comm_group_end();
+int comm_send(sv_comm* c, const void* buf, size_t bytes, int peer, hipStream_t s);
+int comm_recv(sv_comm* c, void* buf, size_t bytes, int peer, hipStream_t s);
+int comm_rank(const sv_comm* c);
+int comm_size(const sv_comm* c);
+int comm_device(const sv_comm* c);
 
 enum Cost { COST_SAD = 0, COST_SSD = 1, COST_HOG = 2, COST_SGBM = 3 };
 
@@ -154,6 +170,11 @@ struct PostParams {
     float* out_a;      // DEPTH: depth_final        SCALED: disparity_normalized (f32)
     uint8_t* out_u8;   // DEPTH: depth_normalized   SCALED: disparity_normalized (u8)
     float* out_b;      // SCALED: confidence
+    // Optional display colormap of out_u8 (cv2.applyColorMap: TURBO at depth_map.py:937, JET
+    // at fused_depth_map.py:1013), fused into the median kernel's epilogue: out_bgr[3i..3i+2]
+    // = the B, G, R bytes of cmap[out_u8[i]] (cmap: 256 entries B | G << 8 | R << 16).
+    uint8_t* out_bgr;
+    const uint32_t* cmap;
     // Optional lookup table of the post-processing as a function of the int16 x16 median
     // value m in [lut_m0, lut_m0 + lut_n), built by launch_post_lut with the same f32 ops
     // (bit-identical to evaluating post_one per pixel; replaces two IEEE divisions).

@@ -82,10 +82,10 @@ def create_depth_map(left_img, right_img, stereo_calib=None, min_depth=0.3, max_
             print(f"ERROR: shapes differ after conversion: {gl.shape} vs {gr.shape}")
             gl, gr = _ensure_same_size(gl, gr)
             h, w = gl.shape[:2]
-        depth_final, disparity, depth_normalized = engine.depth_map(
+        # applyColorMap(depth_normalized, TURBO) (:937) runs in the same GPU epilogue
+        depth_final, disparity, depth_colormap = engine.depth_map_color(
             gl, gr, MIN_DISP, NUM_DISP, WINDOW_SIZE, float(min_depth), float(max_depth),
-            min_disp_global=MIN_DISP, cost=COST)
-        depth_colormap = colormap.apply(depth_normalized, "turbo")
+            colormap.table("turbo"), min_disp_global=MIN_DISP, cost=COST)
         return depth_final, disparity, depth_colormap
     except Exception as e:  # the reference's per-frame error convention (:941-946)
         print(f"Error creating depth map: {e}")

@@ -1,30 +1,44 @@
-"""Multi-GPU sharding of the disparity path: one process per GPU, torch.distributed.
+"""Multi-GPU sharding of the disparity path — no PyTorch.
 
-The reference has no distributed code; its work sharding is the build's
-own:
+The reference has no distributed code; its unit of work is one frame pair
+per call (depth_map.py:1181-1183; fused_depth_map.py:2591-2598 submits one frame at a time
+to a worker pool).  The build's sharding:
 
 * **frame sharding** (config C4): independent frames, frame i -> rank i % world.  No
-  collective in the data path; the finished maps may be gathered to rank 0 over RCCL/xGMI
-  (:func:`gather_frames`) when a consumer on one device needs them.
+  collective in the data path; finished maps may be gathered to rank 0 over RCCL/xGMI.
 * **row tiling** (config C5): one large frame, rank k computes output rows
   [H*k/world, H*(k+1)/world).  Every rank holds the full input frame, so the matching
-  window's halo rows (and the 5x5 median's 2-row halo, via :func:`median_halo`) are read
-  locally: bands reassemble bit-exactly (the border policy is applied only at the true
-  image border).  :func:`gather_rows` concatenates the bands on rank 0 with one
-  all_gather of equal-sized, padded bands (RCCL over xGMI with the "nccl" backend, or gloo
-  on CPU for tests).
+  window's halo rows (and the 5x5 median's 2-row halo, :func:`median_halo`) are read
+  locally: bands reassemble bit-exactly (the border policy applies only at the true image
+  border).  :func:`gather_rows` moves every band into rank 0's full-frame buffer with one
+  RCCL send/recv group (unequal bands, no padding).
 
-torch is imported before the engine library so libsvhip binds to torch's HIP runtime
-(one HIP runtime per process).
+Two ways to run N GPUs:
+
+* one process per GPU (``python -m torch.distributed.run ... bench.py``; only the launcher
+  is torch's, the workers never import torch): :func:`init_process_group` reads
+  RANK / WORLD_SIZE / LOCAL_RANK, rendezvouses through a directory on the node's local file
+  system (:class:`FileStore`; rank 0 publishes the RCCL unique id there) and returns a
+  :class:`ProcessGroup` over an RCCL communicator of libsvhip (``sv_comm_*``).  When RCCL
+  cannot run (ranks sharing one GPU, library missing) it falls back to the file store for
+  barriers and max-reductions and to host staging for gathers.
+* one process driving several GPUs: ``engine.multi_gpu_depth_map_dev`` /
+  ``engine.depth_map_rows_multi`` (sv_multi_gpu_depth_map_dev / sv_depth_map_rows_multi),
+  whose gathers run as one RCCL group (``Communicator.init_all``) or peer copies.
 """
 from __future__ import annotations
 
-import torch  # noqa: F401  (must precede the engine library load)
-import torch.distributed as dist
+import os
+import struct
+import sys
+import time
 
-from .engine import POST_DEPTH, POST_SCALED, get_engine
+import numpy as np
+
+from .engine import POST_DEPTH, POST_SCALED, Communicator, get_engine
 
 
+# ---- partition arithmetic -----------------------------------------------------------------
 def band_rows(H: int, rank: int, world: int) -> tuple[int, int]:
     """Output rows owned by `rank` in a `world`-way row tiling (balanced, contiguous)."""
     return H * rank // world, H * (rank + 1) // world
@@ -44,86 +58,286 @@ def max_band(H: int, world: int) -> int:
     return max(band_rows(H, k, world)[1] - band_rows(H, k, world)[0] for k in range(world))
 
 
-def gather_rows(band: torch.Tensor, H: int, group=None) -> torch.Tensor | None:
-    """Concatenate the row bands of all ranks on rank 0 (None on other ranks).
-
-    `band` is this rank's [r1 - r0, ...] tensor (on the rank's GPU for RCCL, CPU for gloo).
-    Bands are padded to the largest band so one all_gather_into_tensor moves them.
-    """
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    mb = max_band(H, world)
-    pad = torch.zeros((mb,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
-    pad[: band.shape[0]] = band
-    out = torch.empty((world * mb,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
-    dist.all_gather_into_tensor(out, pad, group=group)
-    if rank != 0:
-        return None
-    parts = []
+def rows_layout(H: int, world: int, row_nbytes: int) -> tuple[list[int], list[int]]:
+    """Byte offsets and sizes of every rank's band inside a full-frame buffer."""
+    offs, sizes = [], []
     for k in range(world):
         r0, r1 = band_rows(H, k, world)
-        parts.append(out[k * mb: k * mb + (r1 - r0)])
-    return torch.cat(parts, 0)
+        offs.append(r0 * row_nbytes)
+        sizes.append((r1 - r0) * row_nbytes)
+    return offs, sizes
 
 
-def gather_frames(frames: torch.Tensor, group=None) -> torch.Tensor | None:
-    """Stack equal-shaped per-rank results [n_local, ...] on rank 0 (rank-major order)."""
-    world = dist.get_world_size(group)
-    out = torch.empty((world * frames.shape[0],) + tuple(frames.shape[1:]), dtype=frames.dtype,
-                      device=frames.device)
-    dist.all_gather_into_tensor(out, frames.contiguous(), group=group)
-    return out if dist.get_rank(group) == 0 else None
+def frames_layout(counts, frame_nbytes: int) -> tuple[list[int], list[int]]:
+    """Byte offsets and sizes of every rank's frames in a rank-major stack."""
+    offs, sizes, acc = [], [], 0
+    for n in counts:
+        offs.append(acc * frame_nbytes)
+        sizes.append(n * frame_nbytes)
+        acc += n
+    return offs, sizes
+
+
+def gather_rows(comm, d_full: int, H: int, row_nbytes: int, root: int = 0, stream: int = 0):
+    """Row-tiled gather in place: every rank's band already sits at its row offset of its own
+    full-frame buffer `d_full`; afterwards the root's buffer holds every band."""
+    offs, sizes = rows_layout(H, comm.world, row_nbytes)
+    me = comm.rank
+    comm.gatherv(d_full + offs[me], sizes[me], d_full, offs, sizes, root=root, stream=stream)
+
+
+def gather_frames(comm, d_send: int, n_local: int, d_recv: int, frame_nbytes: int, counts=None,
+                  root: int = 0, stream: int = 0):
+    """Frame-sharded gather: rank k's n_local frames land after the frames of ranks < k."""
+    counts = [n_local] * comm.world if counts is None else list(counts)
+    offs, sizes = frames_layout(counts, frame_nbytes)
+    comm.gatherv(d_send, sizes[comm.rank], d_recv, offs, sizes, root=root, stream=stream)
+
+
+# ---- rendezvous ----------------------------------------------------------------------------
+class FileStore:
+    """Key/value store in a directory of the node's local file system: the rendezvous of
+    the one-process-per-GPU mode (all ranks run on one node).  Values are written to a
+    temporary name and renamed, so a reader never sees a partial value."""
+
+    def __init__(self, path: str, rank: int, world: int, timeout: float = 300.0):
+        self.path, self.rank, self.world, self.timeout = path, rank, world, timeout
+        os.makedirs(path, exist_ok=True)
+        self._n = 0
+
+    def set(self, key: str, value: bytes):
+        tmp = os.path.join(self.path, f".{key}.{self.rank}.tmp")
+        with open(tmp, "wb") as f:
+            f.write(value)
+        os.replace(tmp, os.path.join(self.path, key))
+
+    def get(self, key: str, timeout: float | None = None) -> bytes:
+        p = os.path.join(self.path, key)
+        t_end = time.monotonic() + (self.timeout if timeout is None else timeout)
+        delay = 0.0005
+        while True:
+            try:
+                with open(p, "rb") as f:
+                    return f.read()
+            except FileNotFoundError:
+                if time.monotonic() > t_end:
+                    raise TimeoutError(f"rendezvous: no key {key!r} in {self.path} after "
+                                       f"{self.timeout:.0f} s (a rank died or never started?)")
+                time.sleep(delay)
+                delay = min(delay * 2, 0.01)
+
+    def _tag(self, name: str) -> str:
+        self._n += 1
+        return f"{name}.{self._n}"
+
+    def barrier(self):
+        t = self._tag("barrier")
+        self.set(f"{t}.{self.rank}", b"1")
+        for k in range(self.world):
+            self.get(f"{t}.{k}")
+
+    def allgather(self, value: bytes) -> list[bytes]:
+        t = self._tag("allgather")
+        self.set(f"{t}.{self.rank}", value)
+        return [self.get(f"{t}.{k}") for k in range(self.world)]
+
+    def allreduce_max(self, value: float) -> float:
+        vals = self.allgather(struct.pack("<d", float(value)))
+        return max(struct.unpack("<d", v)[0] for v in vals)
+
+    def broadcast(self, value: bytes | None, root: int = 0) -> bytes:
+        t = self._tag("bcast")
+        if self.rank == root:
+            self.set(t, value)
+            return value
+        return self.get(t)
+
+    def close(self):
+        """Last barrier; every rank then marks that it has left it, and rank 0 removes the
+        directory once all have (a rank still reading the barrier's keys is never cut off)."""
+        try:
+            self.barrier()
+            self.set(f"exit.{self.rank}", b"1")
+            if self.rank == 0:
+                for k in range(self.world):
+                    self.get(f"exit.{k}")
+        finally:
+            if self.rank == 0:
+                for name in os.listdir(self.path):
+                    try:
+                        os.remove(os.path.join(self.path, name))
+                    except OSError:
+                        pass
+                try:
+                    os.rmdir(self.path)
+                except OSError:
+                    pass
+
+
+def default_store_path() -> str:
+    """Directory shared by the ranks of one launch: MASTER_PORT plus the launcher's pid
+    (torch.distributed.run's agent is every local worker's parent, and a new launch has a
+    new pid, so a stale directory of an earlier run is never reused)."""
+    if os.environ.get("SV_RDZV_DIR"):
+        return os.environ["SV_RDZV_DIR"]
+    port = os.environ.get("MASTER_PORT", "0")
+    run = os.environ.get("TORCHELASTIC_RUN_ID", "")
+    restart = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+    base = os.environ.get("TMPDIR", "/tmp")
+    return os.path.join(base, f"sv_rdzv_{port}_{os.getppid()}_{run}_{restart}")
+
+
+# ---- process groups --------------------------------------------------------------------------
+class ProcessGroup:
+    """rank/world of this process plus barrier, max-allreduce and gatherv over device
+    buffers: RCCL (`backend == "rccl"`) or the file store with host staging ("host")."""
+
+    def __init__(self, rank: int, world: int, device: int, store: FileStore | None,
+                 comm: Communicator | None, engine=None):
+        self.rank, self.world, self.device = rank, world, device
+        self.store, self.comm, self.engine = store, comm, engine
+        self.backend = "rccl" if comm is not None else ("host" if world > 1 else "local")
+
+    def barrier(self):
+        if self.comm is not None:
+            self.comm.barrier()
+        elif self.store is not None:
+            self.store.barrier()
+
+    def allreduce_max(self, value: float) -> float:
+        if self.comm is not None:
+            return self.comm.allreduce_max(value)
+        if self.store is not None:
+            return self.store.allreduce_max(value)
+        return float(value)
+
+    def gatherv(self, d_send: int, send_bytes: int, d_recv: int, offsets, sizes, root: int = 0,
+                stream: int = 0):
+        if self.comm is not None:
+            self.comm.gatherv(d_send, send_bytes, d_recv, offsets, sizes, root=root, stream=stream)
+            return
+        eng = self.engine or get_engine(self.device)
+        if self.world == 1 or self.store is None:
+            if d_send != d_recv + offsets[self.rank] and send_bytes:
+                eng.synchronize()
+                host = eng.to_host(d_send, (send_bytes,), np.uint8)
+                eng.to_device(d_recv + offsets[self.rank], host)
+            return
+        # host staging through the store (fallback when RCCL cannot run)
+        eng.synchronize()
+        t = self.store._tag("gatherv")
+        if self.rank != root:
+            host = eng.to_host(d_send, (send_bytes,), np.uint8) if send_bytes else np.empty(0, np.uint8)
+            self.store.set(f"{t}.{self.rank}", host.tobytes())
+            self.store.get(f"{t}.done")
+            return
+        for k in range(self.world):
+            if k == root:
+                if send_bytes and d_send != d_recv + offsets[k]:
+                    eng.to_device(d_recv + offsets[k], eng.to_host(d_send, (send_bytes,), np.uint8))
+                continue
+            data = np.frombuffer(self.store.get(f"{t}.{k}"), np.uint8)
+            if data.size != sizes[k]:
+                raise RuntimeError(f"gatherv: rank {k} sent {data.size} bytes, expected {sizes[k]}")
+            if data.size:
+                eng.to_device(d_recv + offsets[k], data)
+        self.store.set(f"{t}.done", b"1")
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None
+        if self.store is not None:
+            self.store.close()
+            self.store = None
+
+
+def _log(msg: str):
+    print(f"[stereovision_amd.distributed] {msg}", file=sys.stderr, flush=True)
+
+
+def init_process_group(device: int | None = None, backend: str = "auto",
+                       timeout: float = 300.0, engine=None) -> ProcessGroup:
+    """Process group of a torch.distributed.run-style launch, from RANK / WORLD_SIZE /
+    LOCAL_RANK (world 1 when unset).  backend: "auto" (RCCL unless it cannot run: ranks
+    sharing a GPU, library missing), "rccl" (required), "host" (file store only)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device is None:
+        from .engine import device_count
+        nd = max(1, device_count())
+        device = local % nd
+    if world == 1:
+        return ProcessGroup(0, 1, device, None, None, engine)
+    store = FileStore(default_store_path(), rank, world, timeout)
+    # collective decision (a rank must never be left alone inside ncclCommInitRank)
+    ok = backend != "host" and Communicator.available()
+    info = store.allgather(struct.pack("<ii", device, int(ok)))
+    devs = [struct.unpack("<ii", v)[0] for v in info]
+    all_ok = all(struct.unpack("<ii", v)[1] for v in info)
+    dup = len(set(devs)) < len(devs)
+    use_rccl = all_ok and not dup
+    if backend == "rccl" and not use_rccl:
+        raise RuntimeError(f"RCCL backend requested but unusable (devices {devs}, "
+                           f"library on every rank: {all_ok})")
+    comm = None
+    if use_rccl:
+        if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")   # single-node bootstrap
+        uid = store.broadcast(Communicator.unique_id() if rank == 0 else None)
+        comm = Communicator.init_rank(device, world, rank, uid)
+    elif rank == 0:
+        _log(f"RCCL not used (devices {devs}, RCCL loadable on every rank: {all_ok}); "
+             "barriers/reductions through the file store, gathers through host staging")
+    return ProcessGroup(rank, world, device, store, comm, engine)
 
 
 class RowTiledDepthMap:
     """Row-tiled app-1 / app-2 device path for one frame across the ranks of a group.
 
-    Each rank owns full-frame gray inputs in HBM (torch uint8 tensors on its GPU) and
-    computes its band: disparity for the band plus the median halo (sv_disparity_dev),
-    then median + post for the band (sv_median_post_dev), then the bands are gathered.
+    Each rank owns full-frame gray inputs in HBM (device pointers) and computes its band:
+    disparity for the band plus the median halo (sv_disparity_dev), then median + post for
+    the band (sv_median_post_dev); :meth:`gather` moves the bands into rank 0's buffers.
     """
 
     def __init__(self, H: int, W: int, num_disp: int, win: int, min_disp: int = 0,
-                 cost: str = "sad", device: int | None = None, group=None,
-                 rank: int | None = None, world: int | None = None):
+                 cost: str = "sad", device: int = 0, rank: int = 0, world: int = 1, engine=None):
         self.H, self.W = H, W
         self.num_disp, self.win, self.min_disp, self.cost = num_disp, win, min_disp, cost
-        self.group = group
-        inited = dist.is_available() and dist.is_initialized()
-        self.rank = rank if rank is not None else (dist.get_rank(group) if inited else 0)
-        self.world = world if world is not None else (dist.get_world_size(group) if inited else 1)
-        self.device = torch.cuda.current_device() if device is None else device
-        self.engine = get_engine(self.device)
-        self.r0, self.r1 = band_rows(H, self.rank, self.world)
+        self.rank, self.world = rank, world
+        self.engine = engine or get_engine(device)
+        self.r0, self.r1 = band_rows(H, rank, world)
         self.h0, self.h1 = median_halo(self.r0, self.r1, H)
-        dev = f"cuda:{self.device}"
-        n = self.r1 - self.r0
-        self.d16 = torch.empty((H, W), dtype=torch.int16, device=dev)
-        self.disp = torch.empty((H, W), dtype=torch.float32, device=dev)
-        self.out_a = torch.empty((H, W), dtype=torch.float32, device=dev)
-        self.out_b = torch.empty((H, W), dtype=torch.float32, device=dev)
-        self.out_u8 = torch.empty((H, W), dtype=torch.uint8, device=dev)
-        self.rows = n
+        e, n = self.engine, H * W
+        self.d16 = e.dev_alloc(2 * n)
+        self.disp = e.dev_alloc(4 * n)
+        self.out_a = e.dev_alloc(4 * n)
+        self.out_b = e.dev_alloc(4 * n)
+        self.out_u8 = e.dev_alloc(n)
+        self.rows = self.r1 - self.r0
 
-    def compute(self, d_left: torch.Tensor, d_right: torch.Tensor, mode: int = POST_DEPTH,
-                min_depth: float = 0.3, max_depth: float = 2.0, min_disp_global=None):
-        """Enqueue this rank's band on the current torch stream; returns band views
-        (disparity f32, out_a f32, out_u8, out_b f32)."""
+    def compute(self, d_left: int, d_right: int, mode: int = POST_DEPTH, min_depth: float = 0.3,
+                max_depth: float = 2.0, min_disp_global=None, stream: int = 0):
+        """Enqueue this rank's band; outputs at their full-frame row offsets of self.disp /
+        self.out_a / self.out_u8 (/ self.out_b for POST_SCALED)."""
         e, H, W = self.engine, self.H, self.W
-        stream = torch.cuda.current_stream(self.device).cuda_stream
-        e.disparity_dev(d_left.data_ptr(), d_right.data_ptr(), H, W, W, self.min_disp,
-                        self.num_disp, self.win, self.cost, self.h0, self.h1,
-                        self.d16.data_ptr(), W, stream=stream)
+        e.disparity_dev(d_left, d_right, H, W, W, self.min_disp, self.num_disp, self.win, self.cost,
+                        self.h0, self.h1, self.d16, W, stream=stream)
         mdg = self.min_disp if min_disp_global is None else min_disp_global
-        e.median_post_dev(self.d16.data_ptr(), H, W, self.r0, self.r1, mode,
-                          self.disp.data_ptr(), self.out_a.data_ptr(), self.out_u8.data_ptr(),
-                          self.out_b.data_ptr() if mode == POST_SCALED else 0,
+        e.median_post_dev(self.d16, H, W, self.r0, self.r1, mode, self.disp, self.out_a,
+                          self.out_u8, self.out_b if mode == POST_SCALED else 0,
                           min_depth=min_depth, max_depth=max_depth, min_disp_global=mdg,
                           min_disp=self.min_disp, num_disp=self.num_disp, stream=stream)
-        sl = slice(self.r0, self.r1)
-        return self.disp[sl], self.out_a[sl], self.out_u8[sl], self.out_b[sl]
 
-    def gather(self, band: torch.Tensor) -> torch.Tensor | None:
-        if self.world == 1:
-            return band
-        return gather_rows(band, self.H, self.group)
+    def gather(self, pg: ProcessGroup, root: int = 0, stream: int = 0, outputs=("disp", "out_a", "out_u8")):
+        """Bands of every rank into the root's full-frame buffers (in place)."""
+        for name in outputs:
+            elem = 1 if name == "out_u8" else 4
+            gather_rows(pg, getattr(self, name), self.H, self.W * elem, root=root, stream=stream)
+
+    def close(self):
+        for p in (self.d16, self.disp, self.out_a, self.out_b, self.out_u8):
+            if p:
+                self.engine.dev_free(p)
+        self.d16 = self.disp = self.out_a = self.out_b = self.out_u8 = 0

@@ -39,7 +39,12 @@ EXPORTED = [
     "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
     "sv_select_ranks", "sv_affine_f32_dev", "sv_sgbm", "sv_sgbm_dev", "sv_filter_speckles",
     "sv_filter_speckles_dev", "sv_multi_gpu_batch", "sv_harris_batch_dev",
+    "sv_comm_available", "sv_comm_unique_id", "sv_comm_init_rank", "sv_comm_init_all",
+    "sv_comm_destroy", "sv_comm_rank", "sv_comm_barrier", "sv_comm_allreduce_max_f64",
+    "sv_comm_gatherv", "sv_comm_synchronize", "sv_multi_gpu_depth_map_dev",
+    "sv_depth_map_rows_multi", "sv_depth_map_color", "sv_stereo_scaled_color",
 ]
+COMM_ID_BYTES = 128
 
 
 class SVError(RuntimeError):
@@ -86,6 +91,14 @@ class _NullableU16:
         if obj is None:
             return None
         return _u16p.from_param(obj)
+
+
+class _NullableU8:
+    @classmethod
+    def from_param(cls, obj):
+        if obj is None:
+            return None
+        return _u8p.from_param(obj)
 
 
 class _NullableF32:
@@ -191,6 +204,31 @@ def _declare(lib):
         "sv_sgbm_dev": ([_vp, _vp, _vp] + [_c_int] * 13 + [_vp, _c_int, _vp], _c_int),
         "sv_filter_speckles": ([_vp, _i16p] + [_c_int] * 5, _c_int),
         "sv_filter_speckles_dev": ([_vp, _vp] + [_c_int] * 6 + [_vp], _c_int),
+        "sv_comm_available": ([], _c_int),
+        "sv_comm_unique_id": ([ctypes.c_char_p], _c_int),
+        "sv_comm_init_rank": ([_c_int, _c_int, _c_int, ctypes.c_char_p, ctypes.POINTER(_vp)], _c_int),
+        "sv_comm_init_all": ([_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_vp)], _c_int),
+        "sv_comm_destroy": ([_vp], None),
+        "sv_comm_rank": ([_vp, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)],
+                         _c_int),
+        "sv_comm_barrier": ([_vp], _c_int),
+        "sv_comm_allreduce_max_f64": ([_vp, ctypes.POINTER(ctypes.c_double)], _c_int),
+        "sv_comm_gatherv": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.POINTER(ctypes.c_uint64),
+                             ctypes.POINTER(ctypes.c_uint64), _c_int, _vp], _c_int),
+        "sv_comm_synchronize": ([_vp], _c_int),
+        "sv_multi_gpu_depth_map_dev": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
+                                        ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                        ctypes.POINTER(_c_int), _c_int, _c_int, _c_int,
+                                        ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                        _c_float, _c_float, _c_float, _vp, _vp, _vp], _c_int),
+        "sv_depth_map_rows_multi": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
+                                     ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int, _c_int, _c_int,
+                                     _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float,
+                                     _c_float, _vp, _vp, _vp], _c_int),
+        "sv_depth_map_color": ([_vp, _u8p, _u8p] + [_c_int] * 8 + [_c_float] * 4 +
+                               [_u8p, _f32p, _f32p, _NullableU8, _u8p], _c_int),
+        "sv_stereo_scaled_color": ([_vp, _u8p, _u8p] + [_c_int] * 8 +
+                                   [_u8p, _f32p, _f32p, _NullableU8, _f32p, _u8p], _c_int),
         "sv_profile_enable": ([_vp, _c_int], _c_int),
         "sv_profile_read": ([_vp, _c_int, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_longlong)], _c_int),
@@ -485,6 +523,47 @@ class Engine:
             _cost(cost), dn, disp, du, cf))
         return dn, disp, du, cf
 
+    def depth_map_color(self, left, right, min_disp: int, num_disp: int, win: int,
+                        min_depth: float, max_depth: float, cmap_bgr: np.ndarray,
+                        min_disp_global=None, cost="sad", with_normalized: bool = False):
+        """create_depth_map's outputs with the colormap computed on the GPU:
+        (depth_final, disparity, depth_colormap HxWx3 BGR[, depth_normalized])."""
+        left, H, W, C = _image(left)
+        right, H2, W2, C2 = _image(right)
+        if (H, W, C) != (H2, W2, C2):
+            raise ValueError("left/right shapes differ")
+        lut = np.ascontiguousarray(cmap_bgr, np.uint8).reshape(256, 3)
+        mdg = min_disp if min_disp_global is None else min_disp_global
+        depth = np.empty((H, W), np.float32)
+        disp = np.empty((H, W), np.float32)
+        cmap = np.empty((H, W, 3), np.uint8)
+        norm = np.empty((H, W), np.uint8) if with_normalized else None
+        _check("sv_depth_map_color", self.lib.sv_depth_map_color(
+            self._h, left, right, H, W, C, W * C, int(min_disp), int(num_disp), int(win),
+            _cost(cost), np.float32(min_depth), np.float32(max_depth),
+            np.float32(float(max_depth) - float(min_depth)), np.float32(mdg), lut, depth, disp,
+            norm, cmap))
+        return (depth, disp, cmap, norm) if with_normalized else (depth, disp, cmap)
+
+    def stereo_scaled_color(self, left, right, min_disp: int, num_disp: int, win: int,
+                            cmap_bgr: np.ndarray, cost="sad", with_normalized: bool = False):
+        """create_depth_map_stereo_scaled's outputs with the colormap on the GPU:
+        (disparity_normalized, disparity, colormap HxWx3 BGR, confidence[, normalized u8])."""
+        left, H, W, C = _image(left)
+        right, H2, W2, C2 = _image(right)
+        if (H, W, C) != (H2, W2, C2):
+            raise ValueError("left/right shapes differ")
+        lut = np.ascontiguousarray(cmap_bgr, np.uint8).reshape(256, 3)
+        dn = np.empty((H, W), np.float32)
+        disp = np.empty((H, W), np.float32)
+        cf = np.empty((H, W), np.float32)
+        cmap = np.empty((H, W, 3), np.uint8)
+        du = np.empty((H, W), np.uint8) if with_normalized else None
+        _check("sv_stereo_scaled_color", self.lib.sv_stereo_scaled_color(
+            self._h, left, right, H, W, C, W * C, int(min_disp), int(num_disp), int(win),
+            _cost(cost), lut, dn, disp, du, cf, cmap))
+        return (dn, disp, cmap, cf, du) if with_normalized else (dn, disp, cmap, cf)
+
     def harris(self, gray: np.ndarray) -> np.ndarray:
         gray, H, W, C = _image(gray)
         if C != 1:
@@ -766,6 +845,130 @@ def multi_gpu_batch(engines, left, right, min_disp: int, num_disp: int, win: int
         _cost(cost), np.float32(min_depth), np.float32(max_depth),
         np.float32(float(max_depth) - float(min_depth)), np.float32(mdg), depth, disp, norm))
     return depth, disp, norm
+
+
+def _handles(items):
+    items = list(items)
+    return (_vp * len(items))(*[getattr(x, "_h", x) for x in items])
+
+
+def _ptrs(values):
+    values = [int(v) for v in values]
+    return (_vp * len(values))(*values)
+
+
+def _depth_args(min_depth, max_depth, min_disp, min_disp_global):
+    mdg = min_disp if min_disp_global is None else min_disp_global
+    return (np.float32(min_depth), np.float32(max_depth),
+            np.float32(float(max_depth) - float(min_depth)), np.float32(mdg))
+
+
+def multi_gpu_depth_map_dev(engines, comms, d_left, d_right, n_frames, H: int, W: int, pitch: int,
+                            frame_stride: int, min_disp: int, num_disp: int, win: int,
+                            min_depth: float, max_depth: float, d_depth: int, d_disp: int,
+                            d_norm: int, cost="sad", min_disp_global=None):
+    """C4 on device-resident frames from ONE process (sv_multi_gpu_depth_map_dev): engine k
+    runs create_depth_map over its n_frames[k] frames (its own device), and every output
+    frame is gathered to engines[0]'s device (d_depth/d_disp/d_norm, context order) over
+    RCCL (`comms`: Communicator list, rank k on engines[k]'s device) or peer copies (None).
+    Enqueue only: synchronize engines[0] before reading the outputs."""
+    engines = list(engines)
+    nd = len(engines)
+    lib = engines[0].lib
+    ch = None if comms is None else _handles([c.handle for c in comms])
+    nf = (_c_int * nd)(*[int(v) for v in n_frames])
+    _check("sv_multi_gpu_depth_map_dev", lib.sv_multi_gpu_depth_map_dev(
+        _handles(engines), ch, nd, _ptrs(d_left), _ptrs(d_right), nf, H, W, pitch,
+        int(frame_stride), int(min_disp), int(num_disp), int(win), _cost(cost),
+        *_depth_args(min_depth, max_depth, min_disp, min_disp_global), d_depth, d_disp, d_norm))
+
+
+def depth_map_rows_multi(engines, comms, d_left, d_right, H: int, W: int, pitch: int, min_disp: int,
+                         num_disp: int, win: int, min_depth: float, max_depth: float, d_depth: int,
+                         d_disp: int, d_norm: int, cost="sad", min_disp_global=None):
+    """C5 from ONE process (sv_depth_map_rows_multi): one frame row-tiled over the engines
+    (each holds the full gray frame on its device), bands gathered to engines[0]'s device
+    into the full-frame outputs.  Enqueue only."""
+    engines = list(engines)
+    lib = engines[0].lib
+    ch = None if comms is None else _handles([c.handle for c in comms])
+    _check("sv_depth_map_rows_multi", lib.sv_depth_map_rows_multi(
+        _handles(engines), ch, len(engines), _ptrs(d_left), _ptrs(d_right), H, W, pitch,
+        int(min_disp), int(num_disp), int(win), _cost(cost),
+        *_depth_args(min_depth, max_depth, min_disp, min_disp_global), d_depth, d_disp, d_norm))
+
+
+class Communicator:
+    """An RCCL communicator of libsvhip (sv_comm_*): rank `rank` of `nranks` on `device`."""
+
+    def __init__(self, handle, lib):
+        self._h = handle
+        self.lib = lib
+        r, n, d = _c_int(), _c_int(), _c_int()
+        _check("sv_comm_rank", lib.sv_comm_rank(handle, ctypes.byref(r), ctypes.byref(n), ctypes.byref(d)))
+        self.rank, self.nranks, self.device = r.value, n.value, d.value
+
+    @staticmethod
+    def available() -> bool:
+        return bool(load_library().sv_comm_available())
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        _check("sv_comm_unique_id", load_library().sv_comm_unique_id(buf))
+        return buf.raw
+
+    @classmethod
+    def init_rank(cls, device: int, nranks: int, rank: int, uid: bytes) -> "Communicator":
+        lib = load_library()
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError("unique id must be 128 bytes")
+        h = _vp()
+        _check("sv_comm_init_rank", lib.sv_comm_init_rank(device, nranks, rank, uid, ctypes.byref(h)))
+        return cls(h, lib)
+
+    @classmethod
+    def init_all(cls, devices) -> list["Communicator"]:
+        lib = load_library()
+        devices = [int(d) for d in devices]
+        hs = (_vp * len(devices))()
+        _check("sv_comm_init_all", lib.sv_comm_init_all(len(devices), (_c_int * len(devices))(*devices), hs))
+        return [cls(_vp(h), lib) for h in hs]
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.sv_comm_destroy(self._h)
+            self._h = None
+
+    def barrier(self):
+        _check("sv_comm_barrier", self.lib.sv_comm_barrier(self._h))
+
+    def allreduce_max(self, value: float) -> float:
+        v = ctypes.c_double(float(value))
+        _check("sv_comm_allreduce_max_f64", self.lib.sv_comm_allreduce_max_f64(self._h, ctypes.byref(v)))
+        return v.value
+
+    def gatherv(self, d_send: int, send_bytes: int, d_recv: int, offsets, sizes, root: int = 0,
+                stream: int = 0):
+        n = self.nranks
+        off = (ctypes.c_uint64 * n)(*[int(v) for v in offsets])
+        sz = (ctypes.c_uint64 * n)(*[int(v) for v in sizes])
+        _check("sv_comm_gatherv", self.lib.sv_comm_gatherv(self._h, d_send or None, int(send_bytes),
+                                                          d_recv or None, off, sz, int(root),
+                                                          stream or None))
+
+    def synchronize(self):
+        _check("sv_comm_synchronize", self.lib.sv_comm_synchronize(self._h))
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 _engines: dict[int, Engine] = {}

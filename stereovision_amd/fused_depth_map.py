@@ -73,9 +73,9 @@ def create_depth_map_stereo_scaled(left_img, right_img, min_disp, num_disp, wind
         gl = engine.gray(gl) if gl.ndim == 3 else gl
         gr = engine.gray(gr) if gr.ndim == 3 else gr
     try:
-        dn, disparity, dn_u8, confidence = engine.stereo_scaled(
-            gl, gr, int(min_disp), int(num_disp), int(window_size), cost=COST)
-        depth_colormap = colormap.apply(dn_u8, "jet")
+        # applyColorMap(disparity_normalized u8, JET) (:1013) runs in the same GPU epilogue
+        dn, disparity, depth_colormap, confidence = engine.stereo_scaled_color(
+            gl, gr, int(min_disp), int(num_disp), int(window_size), colormap.table("jet"), cost=COST)
         colormap.put_text(depth_colormap, f"Scale:{PROCESSING_SCALE:.2f}x Disp:{num_disp}px")
         return dn, disparity, depth_colormap, confidence
     except Exception as e:  # the reference's per-frame error convention (:1031-1041)

@@ -23,6 +23,15 @@ class OracleEngine:
         dn, disp, du, cf = O.create_depth_map_stereo_scaled(gl, gr, min_disp, num_disp, win)
         return dn, disp, du, cf
 
+    def depth_map_color(self, gl, gr, min_disp, num_disp, win, min_depth, max_depth, cmap_bgr,
+                        min_disp_global=None, cost="sad"):
+        depth, disp, norm = self.depth_map(gl, gr, min_disp, num_disp, win, min_depth, max_depth)
+        return depth, disp, np.asarray(cmap_bgr)[norm]
+
+    def stereo_scaled_color(self, gl, gr, min_disp, num_disp, win, cmap_bgr, cost="sad"):
+        dn, disp, du, cf = self.stereo_scaled(gl, gr, min_disp, num_disp, win)
+        return dn, disp, np.asarray(cmap_bgr)[du], cf
+
     def gray(self, bgr):
         return O.bgr_to_gray(bgr)
 
@@ -33,6 +42,9 @@ class FailingEngine(OracleEngine):
 
     def stereo_scaled(self, *a, **k):
         raise SVError("sv_stereo_scaled", -5, "injected")
+
+    depth_map_color = depth_map
+    stereo_scaled_color = stereo_scaled
 
 
 def test_reference_globals_and_signatures():
@@ -68,6 +80,7 @@ def test_create_depth_map_host_flow(monkeypatch):
     np.testing.assert_array_equal(depth, e_depth)
     np.testing.assert_array_equal(disp, e_disp)
     assert cmap.shape == (30, 100, 3) and cmap.dtype == np.uint8
+    np.testing.assert_array_equal(cmap, colormap.table("turbo")[e_norm])
     assert depth.dtype == np.float32 and disp.dtype == np.float32
 
 
@@ -129,5 +142,6 @@ def test_colormaps():
     for name in ("turbo", "jet"):
         c = colormap.apply(u, name)
         assert c.shape == (16, 16, 3) and c.dtype == np.uint8
+        np.testing.assert_array_equal(c, colormap.table(name)[u])
     jet = colormap.apply(np.array([[0, 255]], np.uint8), "jet")
     assert jet[0, 0, 0] > jet[0, 0, 2] and jet[0, 1, 2] > jet[0, 1, 0]   # blue -> red (BGR)

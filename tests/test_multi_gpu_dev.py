@@ -1,0 +1,259 @@
+"""Device-side multi-GPU paths of the C ABI, torch-free.
+
+* sv_multi_gpu_depth_map_dev (C4 from one process): every context computes create_depth_map
+  for its resident frames and all outputs are gathered onto ctxs[0]'s device.
+* sv_depth_map_rows_multi (C5 from one process): one frame row-tiled over the contexts, the
+  bands gathered onto ctxs[0]'s device into the full frame.
+* sv_comm_* (RCCL loaded with dlopen): a communicator per process (init_rank) and a group
+  (init_all) on the devices this box has.
+* the one-process-per-GPU launch of bench.py (torch.distributed.run starts the workers; the
+  workers never import torch): ranks sharing this box's GPU fall back to the file store.
+* the context scratch is ordered across streams (two parameter sets alternating on two
+  streams of one context).
+
+On a 1-GPU box the 8 "devices" are 8 contexts on device 0 (own stream and buffers each; the
+gather degenerates to device copies); on an 8-GPU node the same tests spread them out.
+Bar: bit-exact against the C oracle frame by frame.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import sv_oracle_c as C
+from stereovision_amd.engine import (Communicator, Engine, device_count, depth_map_rows_multi,
+                                     multi_gpu_depth_map_dev)
+from stereovision_amd.synthetic import stereo_pair
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _oracle(L, R, D, win, cost="sad", lo=0.3, hi=2.0):
+    d16 = C.disparity16(L, R, 0, D, win, {"sad": 0, "ssd": 1, "hog": 2}[cost])
+    disp = C.median5_f32(d16)
+    depth, norm = C.depth_post(disp, lo, hi)
+    return disp, depth, norm
+
+
+@pytest.fixture(scope="module")
+def ctxs(engine):
+    nd = max(1, device_count())
+    extra = [Engine(k % nd) for k in range(1, 8)]
+    yield [engine] + extra
+    for e in extra:
+        e.close()
+
+
+def _upload(e, a):
+    p = e.dev_alloc(a.nbytes)
+    e.to_device(p, np.ascontiguousarray(a))
+    return p
+
+
+@pytest.mark.parametrize("ndev,counts,cost,win", [(8, [2, 1, 0, 3, 1, 1, 2, 1], "sad", 9),
+                                                   (3, [1, 2, 1], "sad", 11),
+                                                   (2, [2, 2], "hog", 7),
+                                                   (1, [3], "ssd", 5)])
+def test_multi_gpu_depth_map_dev_gathers_every_frame(ctxs, ndev, counts, cost, win):
+    H, W, D = 45, 320, 64
+    es = ctxs[:ndev]
+    total = sum(counts)
+    frames = [stereo_pair(H, W, D, seed=700 + f)[:2] for f in range(total)]
+    dLs, dRs, f0 = [], [], 0
+    for e, n in zip(es, counts):
+        Ls = np.stack([frames[f0 + z][0] for z in range(n)]) if n else np.zeros((1, H, W), np.uint8)
+        Rs = np.stack([frames[f0 + z][1] for z in range(n)]) if n else np.zeros((1, H, W), np.uint8)
+        dLs.append(_upload(e, Ls))
+        dRs.append(_upload(e, Rs))
+        f0 += n
+    root = es[0]
+    n = H * W
+    o_depth, o_disp, o_norm = root.dev_alloc(4 * n * total), root.dev_alloc(4 * n * total), root.dev_alloc(n * total)
+    try:
+        for _ in range(2):   # twice: the second call reuses every context's scratch
+            multi_gpu_depth_map_dev(es, None, dLs, dRs, counts, H, W, W, H * W, 0, D, win, 0.3, 2.0,
+                                    o_depth, o_disp, o_norm, cost=cost)
+            root.synchronize()
+        depth = root.to_host(o_depth, (total, H, W), np.float32)
+        disp = root.to_host(o_disp, (total, H, W), np.float32)
+        norm = root.to_host(o_norm, (total, H, W), np.uint8)
+        for f, (L, R) in enumerate(frames):
+            e_disp, e_depth, e_norm = _oracle(L, R, D, win, cost)
+            np.testing.assert_array_equal(disp[f], e_disp, err_msg=f"frame {f}")
+            np.testing.assert_array_equal(depth[f], e_depth, err_msg=f"frame {f}")
+            np.testing.assert_array_equal(norm[f], e_norm, err_msg=f"frame {f}")
+    finally:
+        for e, a, b in zip(es, dLs, dRs):
+            e.dev_free(a)
+            e.dev_free(b)
+        for p in (o_depth, o_disp, o_norm):
+            root.dev_free(p)
+
+
+def _rows_multi(es, comms, L, R, D, win, cost="sad"):
+    H, W = L.shape
+    dLs = [_upload(e, L) for e in es]
+    dRs = [_upload(e, R) for e in es]
+    root = es[0]
+    n = H * W
+    o = [root.dev_alloc(4 * n), root.dev_alloc(4 * n), root.dev_alloc(n)]
+    try:
+        depth_map_rows_multi(es, comms, dLs, dRs, H, W, W, 0, D, win, 0.3, 2.0, o[0], o[1], o[2],
+                             cost=cost)
+        root.synchronize()
+        return (root.to_host(o[1], (H, W), np.float32), root.to_host(o[0], (H, W), np.float32),
+                root.to_host(o[2], (H, W), np.uint8))
+    finally:
+        for e, a, b in zip(es, dLs, dRs):
+            e.dev_free(a)
+            e.dev_free(b)
+        for p in o:
+            root.dev_free(p)
+
+
+@pytest.mark.parametrize("ndev,H,cost,win", [(8, 131, "sad", 9), (3, 29, "sad", 15),
+                                               (8, 17, "hog", 5), (2, 64, "ssd", 7), (1, 40, "sad", 9)])
+def test_depth_map_rows_multi_reassembles_bit_exactly(ctxs, ndev, H, cost, win):
+    W, D = 400, 64
+    L, R, _ = stereo_pair(H, W, D, seed=ndev * 100 + H)
+    disp, depth, norm = _rows_multi(ctxs[:ndev], None, L, R, D, win, cost)
+    e_disp, e_depth, e_norm = _oracle(L, R, D, win, cost)
+    np.testing.assert_array_equal(disp, e_disp)
+    np.testing.assert_array_equal(depth, e_depth)
+    np.testing.assert_array_equal(norm, e_norm)
+
+
+def test_c5_row_tiled_over_8_contexts_gathered_on_device_0(ctxs):
+    """C5 (3840x2160, D=256, 15x15): 8 bands, gathered onto the first context's device."""
+    L, R, _ = stereo_pair(2160, 3840, 256, seed=56)
+    disp, depth, norm = _rows_multi(ctxs, None, L, R, 256, 15)
+    e_disp, e_depth, e_norm = _oracle(L, R, 256, 15)
+    np.testing.assert_array_equal(disp, e_disp)
+    np.testing.assert_array_equal(depth, e_depth)
+    np.testing.assert_array_equal(norm, e_norm)
+
+
+def test_multi_device_argument_checks(ctxs):
+    from stereovision_amd.engine import SVError
+    H, W = 16, 64
+    z = np.zeros((H, W), np.uint8)
+    d = _upload(ctxs[0], z)
+    try:
+        with pytest.raises(SVError):      # the same context twice
+            depth_map_rows_multi([ctxs[0], ctxs[0]], None, [d, d], [d, d], H, W, W, 0, 16, 5, 0.3,
+                                 2.0, d, d, d)
+        with pytest.raises(SVError):      # SGBM cannot be row-tiled
+            depth_map_rows_multi(ctxs[:2], None, [d, d], [d, d], H, W, W, 0, 16, 5, 0.3, 2.0, d, d,
+                                 d, cost="sgbm")
+    finally:
+        ctxs[0].dev_free(d)
+
+
+# ---- RCCL communicators --------------------------------------------------------------------
+def test_rccl_single_rank_communicator(engine):
+    assert Communicator.available()
+    uid = Communicator.unique_id()
+    assert len(uid) == 128
+    c = Communicator.init_rank(0, 1, 0, uid)
+    try:
+        assert (c.rank, c.nranks, c.device) == (0, 1, 0)
+        c.barrier()
+        assert c.allreduce_max(3.25) == 3.25
+        # gatherv on one rank: the root's own block is a device copy into place
+        src = np.arange(1000, dtype=np.uint8)
+        d_src, d_dst = _upload(engine, src), engine.dev_alloc(3000)
+        engine.to_device(d_dst, np.zeros(3000, np.uint8))
+        c.gatherv(d_src, 1000, d_dst, [1500], [1000])
+        c.synchronize()
+        out = engine.to_host(d_dst, (3000,), np.uint8)
+        np.testing.assert_array_equal(out[1500:2500], src)
+        assert not out[:1500].any() and not out[2500:].any()
+        engine.dev_free(d_src)
+        engine.dev_free(d_dst)
+    finally:
+        c.close()
+
+
+def test_rccl_group_on_distinct_devices_rows_and_frames(ctxs):
+    """ncclCommInitAll over this box's distinct devices; the gathers of both multi-device
+    entry points then run as RCCL send/recv groups."""
+    nd = max(1, device_count())
+    devs = list(range(min(nd, 8)))
+    comms = Communicator.init_all(devs)
+    es = [next(e for e in ctxs if e.device == d) for d in devs]
+    try:
+        L, R, _ = stereo_pair(97, 350, 64, seed=9)
+        disp, depth, norm = _rows_multi(es, comms, L, R, 64, 9)
+        e_disp, e_depth, e_norm = _oracle(L, R, 64, 9)
+        np.testing.assert_array_equal(disp, e_disp)
+        np.testing.assert_array_equal(depth, e_depth)
+        np.testing.assert_array_equal(norm, e_norm)
+    finally:
+        for c in comms:
+            c.close()
+
+
+# ---- the one-process-per-GPU launch ------------------------------------------------------------
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("mode", ["frames", "rowtile"])
+def test_bench_under_torch_distributed_run_two_ranks(mode):
+    """The driver's N>1 launch: torch.distributed.run starts 2 bench.py workers (torch-free).
+    On a 1-GPU box both ranks share the GPU, so the group falls back to the file store (RCCL
+    refuses two ranks on one device); on a multi-GPU box it is RCCL."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+           "--steps", "3", "--warmup", "1", "--height", "96", "--width", "400", "--num-disp", "64",
+           "--frames", "2", "--batch", "2", "--mode", mode, "--gather", "--no-live-pmc", "--no-aux",
+           "--no-host-path", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    import json
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 2 and res["value"] > 0
+    assert res["scaling"] == ("strong" if mode == "rowtile" else "weak")
+
+
+# ---- cross-stream ordering of the context scratch -----------------------------------
+def test_two_parameter_sets_alternating_on_two_streams(engine):
+    """One context, its post table and int16 scratch used from two streams with two
+    parameter sets in turn: every result matches its own parameter set."""
+    other = Engine(0)
+    try:
+        H, W, D, win = 540, 960, 64, 9
+        L, R, _ = stereo_pair(H, W, D, seed=77)
+        n = H * W
+        dL, dR = _upload(engine, L), _upload(engine, R)
+        outs = [[engine.dev_alloc(4 * n), engine.dev_alloc(4 * n), engine.dev_alloc(n)] for _ in range(6)]
+        params = [(0.3, 2.0), (0.1, 0.9)]
+        streams = [engine.stream, other.stream]
+        exp = [_oracle(L, R, D, win, "sad", lo, hi) for lo, hi in params]
+        for i, o in enumerate(outs):
+            lo, hi = params[i % 2]
+            engine.depth_map_dev(dL, dR, H, W, W, 0, D, win, lo, hi, o[0], o[1], o[2],
+                                 stream=streams[(i // 2) % 2] if i % 3 else streams[i % 2])
+        engine.synchronize()
+        other.synchronize()
+        for i, o in enumerate(outs):
+            e_disp, e_depth, e_norm = exp[i % 2]
+            np.testing.assert_array_equal(engine.to_host(o[1], (H, W), np.float32), e_disp, err_msg=str(i))
+            np.testing.assert_array_equal(engine.to_host(o[0], (H, W), np.float32), e_depth, err_msg=str(i))
+            np.testing.assert_array_equal(engine.to_host(o[2], (H, W), np.uint8), e_norm, err_msg=str(i))
+        for o in outs:
+            for p in o:
+                engine.dev_free(p)
+        engine.dev_free(dL)
+        engine.dev_free(dR)
+    finally:
+        other.close()

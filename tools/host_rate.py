@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""PCIe-inclusive rate of the host-buffer drop-in path: BGR frames in host
-memory -> sv_depth_map (pinned staging, H2D, gray, disparity, median+post, D2H) -> NumPy
-outputs, one call per frame as depth_map.create_depth_map does.  Not the bench metric."""
+"""PCIe-inclusive rates of the host-buffer drop-in path and where the time
+goes: BGR frames in host memory -> engine -> NumPy outputs, one call per frame as
+depth_map.create_depth_map does, plus the pipelined form.  Not the bench metric."""
 import json
 import os
 import sys
@@ -10,8 +10,20 @@ import time
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from stereovision_amd import colormap, depth_map as DM  # noqa: E402
 from stereovision_amd.engine import get_engine  # noqa: E402
+from stereovision_amd.pipeline import DepthMapPipeline  # noqa: E402
 from stereovision_amd.synthetic import stereo_pair, to_bgr  # noqa: E402
+
+
+def rate(fn, n=60, warm=3):
+    for i in range(warm):
+        fn(i)
+    t0 = time.perf_counter()
+    for i in range(n):
+        fn(i)
+    dt = time.perf_counter() - t0
+    return round(n / dt, 1), round(dt * 1e3 / n, 3)
 
 
 def main():
@@ -21,17 +33,40 @@ def main():
         L, R, _ = stereo_pair(H, W, D, seed=s)
         frames.append((to_bgr(L), to_bgr(R)))
     eng = get_engine(0)
-    for i in range(5):
-        eng.depth_map(*frames[i % 4], 0, D, win, 0.3, 2.0)
-    n = 100
-    t0 = time.perf_counter()
-    for i in range(n):
-        eng.depth_map(*frames[i % 4], 0, D, win, 0.3, 2.0)
-    dt = time.perf_counter() - t0
-    print(json.dumps({"path": "host BGR -> sv_depth_map -> host (PCIe-inclusive)",
-                      "size": f"{W}x{H}", "D": D, "win": win, "frames": n,
-                      "frames_per_s": round(n / dt, 1), "ms_per_frame": round(dt * 1e3 / n, 3),
-                      "bytes_per_frame_h2d": 2 * 3 * H * W, "bytes_per_frame_d2h": 9 * H * W}))
+    t = colormap.table("turbo")
+    DM.NUM_DISP, DM.WINDOW_SIZE, DM.MIN_DISP = D, win, 0
+    out = {"size": f"{W}x{H}", "D": D, "win": win}
+    out["engine.depth_map"] = rate(lambda i: eng.depth_map(*frames[i % 4], 0, D, win, 0.3, 2.0))
+    out["engine.depth_map_color"] = rate(lambda i: eng.depth_map_color(*frames[i % 4], 0, D, win, 0.3, 2.0, t))
+    out["create_depth_map"] = rate(lambda i: DM.create_depth_map(*frames[i % 4]))
+    u8 = np.random.default_rng(0).integers(0, 256, (H, W), dtype=np.uint8)
+    out["host colormap.apply"] = rate(lambda i: colormap.apply(u8, "turbo"), n=10)
+    out["host alloc+touch 22.8MB outputs"] = rate(
+        lambda i: (np.empty((H, W), np.float32).fill(0), np.empty((H, W), np.float32).fill(0),
+                   np.empty((H, W, 3), np.uint8).fill(0)), n=30)
+    a = np.random.default_rng(1).integers(0, 256, 6 * H * W, dtype=np.uint8)
+    b = np.empty_like(a)
+    out["host memcpy 12.4MB warm"] = rate(lambda i: np.copyto(b, a), n=30)
+    for depth in (2, 3, 4):
+        pipe = DepthMapPipeline(D, win, depth=depth)
+        try:
+            for i in range(4):
+                pipe.submit(*frames[i % 4]).result()
+            futs, n = [], 120
+            t0 = time.perf_counter()
+            for i in range(n):
+                futs.append(pipe.submit(*frames[i % 4]))
+                if len(futs) > depth:
+                    futs.pop(0).result()
+            for f in futs:
+                f.result()
+            dt = time.perf_counter() - t0
+            out[f"pipeline depth {depth}"] = (round(n / dt, 1), round(dt * 1e3 / n, 3))
+        finally:
+            pipe.close()
+    out["cpu_count"] = os.cpu_count()
+    out["affinity"] = len(os.sched_getaffinity(0))
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":

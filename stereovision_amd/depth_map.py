@@ -7,7 +7,8 @@ keeps the reference's name, arguments, module globals and return tuple
     returns (depth_final float32 HxW, disparity float32 HxW, depth_colormap uint8 HxWx3)
 
 and its never-raise convention for per-frame failures (print, then zero arrays,
-depth_map.py:941-946).  The numeric body — BGR->gray, the disparity engine (which
+depth_map.py:941-946).  Importing the module warms the engine up on a background thread
+(:func:`warmup`; ``SV_WARMUP_AT_IMPORT=0`` disables it).  The numeric body — BGR->gray, the disparity engine (which
 replaces cv2.StereoSGBM), medianBlur(5), depth = 56/(d+1e-6), clip, mask and
 u8 normalisation — runs in one pass of the gfx950 kernels (include/stereovision_amd.h,
 ``sv_depth_map``).  A missing HIP library or GPU is NOT a per-frame failure: it raises
@@ -15,11 +16,13 @@ u8 normalisation — runs in one pass of the gfx950 kernels (include/stereovisio
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from . import colormap
 from . import rectify as _rectify
-from .engine import get_engine
+from .engine import get_engine, start_warmup
 from .preamble import ensure_same_size as _ensure_same_size
 from .preamble import resize_linear as _resize_linear
 from .preamble import to_engine_image
@@ -92,3 +95,17 @@ def create_depth_map(left_img, right_img, stereo_calib=None, min_depth=0.3, max_
         empty_uint8 = np.zeros((h, w), dtype=np.uint8)
         empty_colormap = colormap.apply(empty_uint8, "turbo")
         return np.zeros((h, w), dtype=np.float32), np.zeros((h, w), dtype=np.float32), empty_colormap
+
+
+def warmup(height: int = 480, width: int = 640) -> None:
+    """Create the engine and run create_depth_map's device path once with the module
+    globals (BGR frames of the given size), so the first captured frame does not pay HIP
+    initialisation, code-object loading and staging allocation."""
+    z = np.zeros((height, width, 3), np.uint8)
+    get_engine().depth_map_color(z, z, MIN_DISP, NUM_DISP, WINDOW_SIZE, 0.3, 2.0,
+                                 colormap.table("turbo"), min_disp_global=MIN_DISP, cost=COST)
+
+
+warmup_done = None
+if os.environ.get("SV_WARMUP_AT_IMPORT", "1") != "0":
+    warmup_done = start_warmup(warmup, "sv-warmup-depth-map")

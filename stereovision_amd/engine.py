@@ -971,6 +971,27 @@ class Communicator:
             pass
 
 
+def start_warmup(fn, name: str = "sv-warmup") -> threading.Event:
+    """Run `fn` (engine creation + one pass of the kernels a drop-in will use, at its
+    processing size) on a daemon thread; returns an Event set when it has finished.  The
+    drop-in modules call this at import so the first frame of the reference's loop does not
+    pay HIP initialisation, code-object loading and staging allocation inside its 0.5 s
+    budget (fused_depth_map.py:2671).  Without a GPU (or library) the thread ends silently:
+    the first real call then raises EngineUnavailable loudly."""
+    done = threading.Event()
+
+    def run():
+        try:
+            fn()
+        except Exception:  # no GPU here, or a failing warm-up: the real call reports it
+            pass
+        finally:
+            done.set()
+
+    threading.Thread(target=run, name=name, daemon=True).start()
+    return done
+
+
 _engines: dict[int, Engine] = {}
 _engines_lock = threading.Lock()
 

@@ -12,8 +12,10 @@ caller (fused_depth_map.py:2258-2266) are exposed as :func:`scaled_stereo_params
 
 The reference calls this function from a ThreadPoolExecutor worker and waits at most
 0.5 s (fused_depth_map.py:2591-2598, :2671); :func:`warmup` builds the engine and runs
-every kernel once so the first real frame does not pay context creation and code-object
-loading inside that budget.  It runs at import when ``SV_WARMUP_AT_IMPORT=1``.
+the scaled path once at the processing size, so the first real frame does not pay HIP
+initialisation, context creation, code-object loading and staging allocation inside that
+budget.  It runs at import on a background thread (``warmup_done`` is set when it has
+finished); ``SV_WARMUP_AT_IMPORT=0`` disables it.
 """
 from __future__ import annotations
 
@@ -26,7 +28,7 @@ from . import colormap
 from . import rectify as _rectify
 from .fusion import (calibrate_midas_to_stereo, detect_camera_occlusion,  # noqa: F401
                      normalize_to_stereo_range)
-from .engine import get_engine
+from .engine import get_engine, start_warmup
 from .preamble import ensure_same_size, to_engine_image
 
 STEREO_CALIBRATION_FILE = "output/stereo_calibration_data.pkl"   # fused_depth_map.py:61
@@ -89,11 +91,13 @@ def create_depth_map_stereo_scaled(left_img, right_img, min_disp, num_disp, wind
 
 def warmup(height: int = 356, width: int = 633, processing_scale: float = None) -> None:
     """Create the engine and run the scaled path once at the processing size
-    (default: 1920x1080 at PROCESSING_SCALE 0.33 -> 633x356, D=96, window 5)."""
+    (default: 1920x1080 at PROCESSING_SCALE 0.33 -> 633x356, D=96, window 5), BGR frames as
+    the camera delivers them."""
     nd, ws = scaled_stereo_params(processing_scale)
     z = np.zeros((height, width, 3), np.uint8)
-    get_engine().stereo_scaled(z, z, MIN_DISP_BASE, nd, ws, cost=COST)
+    get_engine().stereo_scaled_color(z, z, MIN_DISP_BASE, nd, ws, colormap.table("jet"), cost=COST)
 
 
-if os.environ.get("SV_WARMUP_AT_IMPORT") == "1":  # pragma: no cover - GPU hosts only
-    warmup()
+warmup_done = None
+if os.environ.get("SV_WARMUP_AT_IMPORT", "1") != "0":
+    warmup_done = start_warmup(warmup, "sv-warmup-fused")

@@ -3,7 +3,7 @@
 # Usage on the GPU box: bash tools/profile.sh [tag] [bench args...]
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${1:-r01}; shift
-ARGS="--no-cpu-baseline --steps ${PSTEPS:-200} --warmup 20 $*"
+ARGS="--no-cpu-baseline --no-live-pmc --no-host-path --no-aux --steps ${PSTEPS:-200} --warmup 20 $*"
 OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp

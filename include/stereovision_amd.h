@@ -17,6 +17,7 @@
  *                                    fused_depth_map.py:1010-1029
  *   sv_depth_map                     the whole numeric body of create_depth_map
  *                                    (depth_map.py:868-937) minus the colormap
+ *   sv_depth_map_color               ... including the colormap (depth_map.py:937)
  *   sv_stereo_scaled                 the whole numeric body of create_depth_map_stereo_scaled
  *                                    (fused_depth_map.py:976-1029) minus colormap/putText
  *   sv_harris, sv_hog_hist           north_star stages with no reference counterpart
@@ -182,6 +183,15 @@ int sv_median_post_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W, int r
                        int mode, float min_depth, float max_depth, float depth_range,
                        float min_disp_global, int min_disp, int num_disp, float* d_disparity,
                        float* d_out_a, uint8_t* d_out_u8, float* d_out_b, void* stream);
+
+/* sv_median_post_dev plus the display colormap in the same epilogue (cv2.applyColorMap of
+ * out_u8: TURBO at depth_map.py:937, JET at fused_depth_map.py:1013): cmap_bgr is the 256 x 3
+ * BGR table in host memory, d_bgr the H x W x 3 output (rows [row0, row1)). */
+int sv_median_post_color_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W, int row0,
+                             int row1, int mode, float min_depth, float max_depth,
+                             float depth_range, float min_disp_global, int min_disp, int num_disp,
+                             const uint8_t* cmap_bgr, float* d_disparity, float* d_out_a,
+                             uint8_t* d_out_u8, float* d_out_b, uint8_t* d_bgr, void* stream);
 
 /* Whole app-1 device path on gray device images: disparity -> median -> depth post. */
 int sv_depth_map_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int H, int W,

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "sv_internal.h"
+#include "sv_pool.h"
 #include "../../include/stereovision_amd.h"
 
 namespace {
@@ -111,6 +112,13 @@ struct sv_ctx {
         sg_hsum, sg_c, sg_l, sg_lt, sg_band, cc_parent, cc_size, hist_copies, cmap, bgr;
     uint8_t cmap_host[768] = {};   // BGR table currently in `cmap`
     bool cmap_valid = false;
+    // host-buffer frame path: int16 medians come back over PCIe and are expanded on the
+    // host with a host copy of the post-processing table (hl_*, valid for hl_key)
+    DevBuf m16;
+    std::vector<float> hl_a, hl_b;
+    std::vector<uint8_t> hl_u8;
+    bool hl_valid = false;
+    hipEvent_t cev[8] = {};
     // SGBM: second stream + fork/join events for the vertical path beside the horizontal ones
     hipStream_t sg_aux = nullptr;
     hipEvent_t sg_ev[2] = {nullptr, nullptr};
@@ -125,7 +133,7 @@ struct sv_ctx {
                    std::memcmp(&rangef, &o.rangef, sizeof(float)) == 0 &&
                    std::memcmp(&mdg, &o.mdg, sizeof(float)) == 0;
         }
-    } lut_key;
+    } lut_key, hl_key;
     hipEvent_t lut_ev = nullptr;
     hipStream_t lut_stream = nullptr;   // stream the table was built on
     HostBuf hin, hout;
@@ -635,11 +643,13 @@ void sv_destroy(sv_ctx* c) {
                           &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->lut,
                           &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1], &c->stats, &c->sel,
                           &c->sg_hsum, &c->sg_c, &c->sg_l, &c->sg_lt, &c->sg_band, &c->cc_parent,
-                          &c->hist_copies, &c->cmap, &c->bgr,
+                          &c->hist_copies, &c->cmap, &c->bgr, &c->m16,
                           &c->cc_size};
         if (c->lut_ev) (void)hipEventDestroy(c->lut_ev);
         if (c->scr_ev) (void)hipEventDestroy(c->scr_ev);
         if (c->xev) (void)hipEventDestroy(c->xev);
+        for (auto e : c->cev)
+            if (e) (void)hipEventDestroy(e);
         if (c->sg_aux) {
             (void)hipStreamSynchronize(c->sg_aux);
             (void)hipStreamDestroy(c->sg_aux);
@@ -712,6 +722,28 @@ int sv_median_post_dev(sv_ctx* c, const int16_t* d_disp16, int H, int W, int row
                                   d_out_a, d_out_u8, d_out_b);
     int lrc = attach_lut(c, pp, s);
     if (lrc) return lrc;
+    SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(d_disp16, H, W, row0, row1, d_disparity, pp, s));
+    return 0;
+}
+
+int sv_median_post_color_dev(sv_ctx* c, const int16_t* d_disp16, int H, int W, int row0, int row1, int mode,
+                             float min_depth, float max_depth, float depth_range, float min_disp_global,
+                             int min_disp, int num_disp, const uint8_t* cmap_bgr, float* d_disparity,
+                             float* d_out_a, uint8_t* d_out_u8, float* d_out_b, uint8_t* d_bgr, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_disp16, H, W) || !d_out_a || !d_out_u8 || !d_bgr || !cmap_bgr)
+        return fail(SV_EINVAL, "bad median arguments");
+    if (mode != SV_POST_DEPTH && mode != SV_POST_SCALED) return fail(SV_EINVAL, "mode must be DEPTH or SCALED");
+    if (mode == SV_POST_SCALED && (!d_out_b || num_disp <= 0)) return fail(SV_EINVAL, "scaled post outputs missing");
+    if (row0 < 0) row0 = 0;
+    if (row1 > H) row1 = H;
+    hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
+    sv::PostParams pp = make_post(mode, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
+                                  d_out_a, d_out_u8, d_out_b);
+    int rc = attach_lut(c, pp, s);
+    if (!rc) rc = attach_cmap(c, pp, cmap_bgr, d_bgr, s);
+    if (rc) return rc;
     SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(d_disp16, H, W, row0, row1, d_disparity, pp, s));
     return 0;
 }
@@ -1354,6 +1386,175 @@ int sv_scaled_post(sv_ctx* c, const float* disparity, int n, int min_disp, int n
     return post_common(c, disparity, n, pp, disparity_normalized, normalized_u8, confidence);
 }
 
+}  // extern "C"
+
+namespace {
+
+// Host memory -> pinned staging -> device, in chunks: the DMA of one chunk runs while the
+// host threads copy the next (one call per frame, as the reference calls the path).
+int stage_image_chunked(sv_ctx* c, const uint8_t* src, int H, size_t row, int stride, uint8_t* stage,
+                        void* dev) {
+    const int nchunk = H >= 64 ? 6 : 1;
+    sv::HostPool& pool = sv::HostPool::get();
+    for (int k = 0; k < nchunk; ++k) {
+        const int y0 = (int)((long long)H * k / nchunk), y1 = (int)((long long)H * (k + 1) / nchunk);
+        if (y1 <= y0) continue;
+        const int parts = pool.threads();
+        pool.parallel_for(parts, [&](int p) {
+            const int a = y0 + (int)((long long)(y1 - y0) * p / parts), b = y0 + (int)((long long)(y1 - y0) * (p + 1) / parts);
+            if (b <= a) return;
+            if ((size_t)stride == row)
+                std::memcpy(stage + (size_t)a * row, src + (size_t)a * row, (size_t)(b - a) * row);
+            else
+                for (int y = a; y < b; ++y) std::memcpy(stage + (size_t)y * row, src + (size_t)y * stride, row);
+        });
+        SV_HIP(hipMemcpyAsync(static_cast<uint8_t*>(dev) + (size_t)y0 * row, stage + (size_t)y0 * row,
+                              (size_t)(y1 - y0) * row, hipMemcpyHostToDevice, c->stream));
+    }
+    return 0;
+}
+
+int stage_pair_chunked(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels, int stride) {
+    if (check_image(left, H, W) || check_image(right, H, W)) return SV_EINVAL;
+    if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
+    const size_t row = (size_t)W * channels;
+    if (stride < (int)row) return fail(SV_EINVAL, "stride smaller than a row");
+    const size_t n = row * H;
+    SV_HIP(c->hin.ensure(2 * n));
+    SV_HIP(c->gray[0].ensure((size_t)H * W));
+    SV_HIP(c->gray[1].ensure((size_t)H * W));
+    const uint8_t* src[2] = {left, right};
+    for (int k = 0; k < 2; ++k) {
+        uint8_t* stage = c->hin.as<uint8_t>() + k * n;
+        void* dst = channels == 1 ? c->gray[k].p : nullptr;
+        if (channels == 3) {
+            SV_HIP(c->img[k].ensure(n));
+            dst = c->img[k].p;
+        }
+        int rc = stage_image_chunked(c, src[k], H, row, stride, stage, dst);
+        if (rc) return rc;
+        if (channels == 3)
+            SV_LAUNCH(c, SV_K_GRAY, c->stream,
+                      sv::launch_gray(c->img[k].as<uint8_t>(), H, W, (int)row, c->gray[k].as<uint8_t>(), c->stream));
+    }
+    return 0;
+}
+
+// Host copy of the context's post-processing table (the one attach_lut attached).
+int host_lut(sv_ctx* c, const sv::PostParams& pp) {
+    if (c->hl_valid && c->hl_key == c->lut_key) return 0;
+    const size_t n = (size_t)pp.lut_n;
+    try {
+        c->hl_a.resize(n);
+        c->hl_b.resize(n);
+        c->hl_u8.resize(n);
+    } catch (...) {
+        return fail(SV_ENOMEM, "host table allocation failed");
+    }
+    SV_HIP(hipMemcpyAsync(c->hl_a.data(), pp.lut_a, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    SV_HIP(hipMemcpyAsync(c->hl_b.data(), pp.lut_b, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    SV_HIP(hipMemcpyAsync(c->hl_u8.data(), pp.lut_u8, n, hipMemcpyDeviceToHost, c->stream));
+    SV_HIP(hipStreamSynchronize(c->stream));
+    c->hl_key = c->lut_key;
+    c->hl_valid = true;
+    return 0;
+}
+
+struct FrameOut {
+    float* a;        // DEPTH: depth_final; SCALED: disparity_normalized
+    float* disp;     // disparity (f32 = median / 16)
+    uint8_t* u8;     // DEPTH: depth_normalized; SCALED: its u8 image (nullable)
+    float* b;        // SCALED: confidence
+    uint8_t* bgr;    // colormap of u8 through `table` (nullable)
+};
+
+// create_depth_map / create_depth_map_stereo_scaled on host buffers (depth_map.py:868-937,
+// fused_depth_map.py:976-1024): the frames go up in chunks, gray + disparity + median run on
+// the device, and only the int16 x16 median map comes back (2 B/px).  The host expands it
+// with the table the device built (bit-identical to the median kernel's epilogue, which
+// reads the same table): disparity = m / 16, the post-processing outputs = table[m - m0],
+// the colormap = table_bgr[u8].  Chunks of rows come back behind events, so the expansion
+// of one chunk runs while the next is in flight.
+int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels, int stride,
+                    int min_disp, int num_disp, int win, int cost, sv::PostParams pp, const uint8_t* table,
+                    FrameOut o) {
+    sv::MatchPlan plan;
+    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    if ((long long)H * W >= (1LL << 30)) return fail(SV_EINVAL, "frame too large");
+    rc = stage_pair_chunked(c, left, right, H, W, channels, stride);
+    if (rc) return rc;
+    const size_t n = (size_t)H * W;
+    SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
+    SV_HIP(c->m16.ensure(n * sizeof(int16_t)));
+    SV_HIP(c->hout.ensure(n * sizeof(int16_t)));
+    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
+                           win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
+    if (rc) return rc;
+    rc = attach_lut(c, pp, c->stream);
+    if (rc) return rc;
+    if (pp.lut_n <= 0) return fail(SV_EINVAL, "no post-processing table for these parameters");
+    rc = host_lut(c, pp);
+    if (rc) return rc;
+    sv::PostParams mp = pp;      // the median kernel writes only the int16 medians
+    mp.mode = SV_POST_NONE;
+    mp.out_m16 = c->m16.as<int16_t>();
+    SV_LAUNCH(c, SV_K_MEDIAN, c->stream, sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, nullptr, mp, c->stream));
+    const int nchunk = H >= 64 ? 8 : 1;
+    for (int k = 0; k < nchunk; ++k) {
+        if (!c->cev[k]) SV_HIP(hipEventCreateWithFlags(&c->cev[k], hipEventDisableTiming));
+        const size_t y0 = (size_t)H * k / nchunk, y1 = (size_t)H * (k + 1) / nchunk;
+        SV_HIP(hipMemcpyAsync(c->hout.as<int16_t>() + y0 * W, c->m16.as<int16_t>() + y0 * W, (y1 - y0) * W * 2,
+                              hipMemcpyDeviceToHost, c->stream));
+        SV_HIP(hipEventRecord(c->cev[k], c->stream));
+    }
+    const int m0 = pp.lut_m0, nl = pp.lut_n;
+    const float* la = c->hl_a.data();
+    const float* lb = c->hl_b.data();
+    const uint8_t* lu = c->hl_u8.data();
+    const int16_t* med = c->hout.as<int16_t>();
+    const bool scaled = pp.mode == SV_POST_SCALED;
+    std::atomic<int> bad{0};
+    sv::HostPool& pool = sv::HostPool::get();
+    for (int k = 0; k < nchunk; ++k) {
+        SV_HIP(hipEventSynchronize(c->cev[k]));
+        const size_t y0 = (size_t)H * k / nchunk, y1 = (size_t)H * (k + 1) / nchunk;
+        const size_t i0 = y0 * W, i1 = y1 * W;
+        const int parts = pool.threads();
+        pool.parallel_for(parts, [&](int p) {
+            const size_t a = i0 + (i1 - i0) * p / parts, b = i0 + (i1 - i0) * (p + 1) / parts;
+            int nbad = 0;
+            for (size_t i = a; i < b; ++i) {
+                const int m = med[i];
+                const uint32_t li = (uint32_t)(m - m0);
+                if (li >= (uint32_t)nl) {
+                    ++nbad;
+                    continue;
+                }
+                o.disp[i] = (float)m / 16.0f;
+                o.a[i] = la[li];
+                const uint8_t u = lu[li];
+                if (o.u8) o.u8[i] = u;
+                if (scaled) o.b[i] = lb[li];
+                if (o.bgr) {
+                    const uint8_t* t = table + 3 * u;
+                    uint8_t* d = o.bgr + 3 * i;
+                    d[0] = t[0];
+                    d[1] = t[1];
+                    d[2] = t[2];
+                }
+            }
+            if (nbad) bad.fetch_add(nbad);
+        });
+    }
+    if (bad.load()) return fail(SV_EHIP, "median value outside the post-processing table");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
 int sv_depth_map(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels, int stride,
                  int min_disp, int num_disp, int win, int cost, float min_depth, float max_depth,
                  float depth_range, float min_disp_global, float* depth_final, float* disparity,
@@ -1361,29 +1562,10 @@ int sv_depth_map(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, in
     SV_ENTER(c);
     SV_SCRATCH(c, c->stream);
     if (!depth_final || !disparity || !depth_normalized) return fail(SV_EINVAL, "null outputs");
-    sv::MatchPlan plan;
-    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
-    if (rc) return rc;
-    rc = stage_pair(c, left, right, H, W, channels, stride);
-    if (rc) return rc;
-    const size_t n = (size_t)H * W;
-    SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
-    SV_HIP(c->fa.ensure(n * sizeof(float)));
-    SV_HIP(c->fb.ensure(n * sizeof(float)));
-    SV_HIP(c->u8.ensure(n));
-    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
-                           win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
-    if (rc) return rc;
     sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
-                                  num_disp, c->fb.as<float>(), c->u8.as<uint8_t>(), nullptr);
-    rc = attach_lut(c, pp, c->stream);
-    if (rc) return rc;
-    SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
-              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fa.as<float>(), pp, c->stream));
-    Out o[] = {{depth_final, c->fb.p, n * sizeof(float)},
-               {disparity, c->fa.p, n * sizeof(float)},
-               {depth_normalized, c->u8.p, n}};
-    return collect(c, o, 3);
+                                  num_disp, nullptr, nullptr, nullptr);
+    return host_frame_path(c, left, right, H, W, channels, stride, min_disp, num_disp, win, cost, pp, nullptr,
+                           FrameOut{depth_final, disparity, depth_normalized, nullptr, nullptr});
 }
 
 int sv_stereo_scaled(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels,
@@ -1393,31 +1575,9 @@ int sv_stereo_scaled(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H
     SV_SCRATCH(c, c->stream);
     if (!disparity_normalized || !disparity || !normalized_u8 || !confidence)
         return fail(SV_EINVAL, "null outputs");
-    sv::MatchPlan plan;
-    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
-    if (rc) return rc;
-    rc = stage_pair(c, left, right, H, W, channels, stride);
-    if (rc) return rc;
-    const size_t n = (size_t)H * W;
-    SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
-    SV_HIP(c->fa.ensure(n * sizeof(float)));
-    SV_HIP(c->fb.ensure(n * sizeof(float)));
-    SV_HIP(c->fc.ensure(n * sizeof(float)));
-    SV_HIP(c->u8.ensure(n));
-    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
-                           win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
-    if (rc) return rc;
-    sv::PostParams pp = make_post(SV_POST_SCALED, 0.f, 0.f, 0.f, 0.f, min_disp, num_disp, c->fb.as<float>(),
-                                  c->u8.as<uint8_t>(), c->fc.as<float>());
-    rc = attach_lut(c, pp, c->stream);
-    if (rc) return rc;
-    SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
-              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fa.as<float>(), pp, c->stream));
-    Out o[] = {{disparity_normalized, c->fb.p, n * sizeof(float)},
-               {disparity, c->fa.p, n * sizeof(float)},
-               {normalized_u8, c->u8.p, n},
-               {confidence, c->fc.p, n * sizeof(float)}};
-    return collect(c, o, 4);
+    sv::PostParams pp = make_post(SV_POST_SCALED, 0.f, 0.f, 0.f, 0.f, min_disp, num_disp, nullptr, nullptr, nullptr);
+    return host_frame_path(c, left, right, H, W, channels, stride, min_disp, num_disp, win, cost, pp, nullptr,
+                           FrameOut{disparity_normalized, disparity, normalized_u8, confidence, nullptr});
 }
 
 int sv_depth_map_color(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels,
@@ -1427,32 +1587,10 @@ int sv_depth_map_color(sv_ctx* c, const uint8_t* left, const uint8_t* right, int
     SV_ENTER(c);
     SV_SCRATCH(c, c->stream);
     if (!depth_final || !disparity || !depth_colormap || !cmap_bgr) return fail(SV_EINVAL, "null outputs");
-    sv::MatchPlan plan;
-    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
-    if (rc) return rc;
-    rc = stage_pair(c, left, right, H, W, channels, stride);
-    if (rc) return rc;
-    const size_t n = (size_t)H * W;
-    SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
-    SV_HIP(c->fa.ensure(n * sizeof(float)));
-    SV_HIP(c->fb.ensure(n * sizeof(float)));
-    SV_HIP(c->u8.ensure(n));
-    SV_HIP(c->bgr.ensure(3 * n));
-    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
-                           win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
-    if (rc) return rc;
     sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
-                                  num_disp, c->fb.as<float>(), c->u8.as<uint8_t>(), nullptr);
-    rc = attach_lut(c, pp, c->stream);
-    if (!rc) rc = attach_cmap(c, pp, cmap_bgr, c->bgr.as<uint8_t>(), c->stream);
-    if (rc) return rc;
-    SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
-              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fa.as<float>(), pp, c->stream));
-    Out o[] = {{depth_final, c->fb.p, n * sizeof(float)},
-               {disparity, c->fa.p, n * sizeof(float)},
-               {depth_colormap, c->bgr.p, 3 * n},
-               {depth_normalized, c->u8.p, n}};
-    return collect(c, o, 4);
+                                  num_disp, nullptr, nullptr, nullptr);
+    return host_frame_path(c, left, right, H, W, channels, stride, min_disp, num_disp, win, cost, pp, cmap_bgr,
+                           FrameOut{depth_final, disparity, depth_normalized, nullptr, depth_colormap});
 }
 
 int sv_stereo_scaled_color(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels,
@@ -1463,34 +1601,9 @@ int sv_stereo_scaled_color(sv_ctx* c, const uint8_t* left, const uint8_t* right,
     SV_SCRATCH(c, c->stream);
     if (!disparity_normalized || !disparity || !confidence || !depth_colormap || !cmap_bgr)
         return fail(SV_EINVAL, "null outputs");
-    sv::MatchPlan plan;
-    int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
-    if (rc) return rc;
-    rc = stage_pair(c, left, right, H, W, channels, stride);
-    if (rc) return rc;
-    const size_t n = (size_t)H * W;
-    SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
-    SV_HIP(c->fa.ensure(n * sizeof(float)));
-    SV_HIP(c->fb.ensure(n * sizeof(float)));
-    SV_HIP(c->fc.ensure(n * sizeof(float)));
-    SV_HIP(c->u8.ensure(n));
-    SV_HIP(c->bgr.ensure(3 * n));
-    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
-                           win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
-    if (rc) return rc;
-    sv::PostParams pp = make_post(SV_POST_SCALED, 0.f, 0.f, 0.f, 0.f, min_disp, num_disp, c->fb.as<float>(),
-                                  c->u8.as<uint8_t>(), c->fc.as<float>());
-    rc = attach_lut(c, pp, c->stream);
-    if (!rc) rc = attach_cmap(c, pp, cmap_bgr, c->bgr.as<uint8_t>(), c->stream);
-    if (rc) return rc;
-    SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
-              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fa.as<float>(), pp, c->stream));
-    Out o[] = {{disparity_normalized, c->fb.p, n * sizeof(float)},
-               {disparity, c->fa.p, n * sizeof(float)},
-               {depth_colormap, c->bgr.p, 3 * n},
-               {confidence, c->fc.p, n * sizeof(float)},
-               {normalized_u8, c->u8.p, n}};
-    return collect(c, o, 5);
+    sv::PostParams pp = make_post(SV_POST_SCALED, 0.f, 0.f, 0.f, 0.f, min_disp, num_disp, nullptr, nullptr, nullptr);
+    return host_frame_path(c, left, right, H, W, channels, stride, min_disp, num_disp, win, cost, pp, cmap_bgr,
+                           FrameOut{disparity_normalized, disparity, normalized_u8, confidence, depth_colormap});
 }
 
 int sv_harris(sv_ctx* c, const uint8_t* gray, int H, int W, int stride, float* out) {

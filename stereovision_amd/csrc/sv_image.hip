@@ -305,6 +305,7 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
         if (pp.out_u8) pp.out_u8 += o;
         if (pp.out_b) pp.out_b += o;
         if (pp.out_bgr) pp.out_bgr += 3 * o;
+        if (pp.out_m16) pp.out_m16 += o;
     }
     const int x0 = blockIdx.x * MQ_W, y0 = row0 + blockIdx.y * MQ_H;
     {   // thread -> one tile column (clamped once), rows g, g+3, ...: 204 of 256 threads load
@@ -389,10 +390,12 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
     const uint32_t i = (uint32_t)y * W + x;
     const bool vec = x + 3 < W && (W & 3) == 0 &&
                      (((uintptr_t)disp | (uintptr_t)pp.out_a | (uintptr_t)pp.out_b) & 15) == 0 &&
-                     (((uintptr_t)pp.out_u8 | (uintptr_t)pp.out_bgr) & 3) == 0;
+                     (((uintptr_t)pp.out_u8 | (uintptr_t)pp.out_bgr) & 3) == 0 && ((uintptr_t)pp.out_m16 & 7) == 0;
     if (vec) {
-        at(reinterpret_cast<float4*>(disp), i >> 2) =
-            make_float4((float)mv[0] / 16.0f, (float)mv[1] / 16.0f, (float)mv[2] / 16.0f, (float)mv[3] / 16.0f);
+        if (disp)
+            at(reinterpret_cast<float4*>(disp), i >> 2) =
+                make_float4((float)mv[0] / 16.0f, (float)mv[1] / 16.0f, (float)mv[2] / 16.0f, (float)mv[3] / 16.0f);
+        if (pp.out_m16) at(reinterpret_cast<uint2*>(pp.out_m16), i >> 2) = raw;
         if (pp.mode == POST_NONE) return;
         PostVals o[4];
 #pragma unroll
@@ -415,7 +418,8 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         if (x + q >= W) break;
-        at(disp, i + q) = (float)mv[q] / 16.0f;
+        if (disp) at(disp, i + q) = (float)mv[q] / 16.0f;
+        if (pp.out_m16) at(pp.out_m16, i + q) = (int16_t)mv[q];
         if (pp.mode == POST_NONE) continue;
         const PostVals o = post_median(pp, mv[q]);
         at(pp.out_a, i + q) = o.a;
@@ -524,6 +528,7 @@ int launch_post_lut(const PostParams& pp, int m0, int n, float* lut_a, uint8_t* 
     q.out_u8 = lut_u8;
     q.out_b = lut_b;
     q.out_bgr = nullptr;
+    q.out_m16 = nullptr;
     q.lut_n = 0;
     hipLaunchKernelGGL(k_post_lut, dim3((n + 255) / 256), dim3(256), 0, s, q, m0, n);
     return (int)hipGetLastError();

@@ -175,6 +175,10 @@ struct PostParams {
     // = the B, G, R bytes of cmap[out_u8[i]] (cmap: 256 entries B | G << 8 | R << 16).
     uint8_t* out_bgr;
     const uint32_t* cmap;
+    // Optional int16 x16 median map (the host paths expand it with the table on the host:
+    // 2 B/px over PCIe instead of 9-11); the f32 disparity output of the median kernel is
+    // then optional (disp == nullptr).
+    int16_t* out_m16;
     // Optional lookup table of the post-processing as a function of the int16 x16 median
     // value m in [lut_m0, lut_m0 + lut_n), built by launch_post_lut with the same f32 ops
     // (bit-identical to evaluating post_one per pixel; replaces two IEEE divisions).

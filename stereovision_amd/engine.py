@@ -43,6 +43,7 @@ EXPORTED = [
     "sv_comm_destroy", "sv_comm_rank", "sv_comm_barrier", "sv_comm_allreduce_max_f64",
     "sv_comm_gatherv", "sv_comm_synchronize", "sv_multi_gpu_depth_map_dev",
     "sv_depth_map_rows_multi", "sv_depth_map_color", "sv_stereo_scaled_color",
+    "sv_median_post_color_dev",
 ]
 COMM_ID_BYTES = 128
 
@@ -229,6 +230,9 @@ def _declare(lib):
                                [_u8p, _f32p, _f32p, _NullableU8, _u8p], _c_int),
         "sv_stereo_scaled_color": ([_vp, _u8p, _u8p] + [_c_int] * 8 +
                                    [_u8p, _f32p, _f32p, _NullableU8, _f32p, _u8p], _c_int),
+        "sv_median_post_color_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                      _c_float, _c_float, _c_float, _c_int, _c_int, _u8p, _vp, _vp,
+                                      _vp, _vp, _vp, _vp], _c_int),
         "sv_profile_enable": ([_vp, _c_int], _c_int),
         "sv_profile_read": ([_vp, _c_int, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_longlong)], _c_int),
@@ -602,6 +606,17 @@ class Engine:
             np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
             np.float32(min_disp_global), int(min_disp), int(num_disp), d_disparity,
             d_out_a or None, d_out_u8 or None, d_out_b or None, stream or None))
+
+    def median_post_color_dev(self, d_disp16: int, H: int, W: int, row0: int, row1: int, mode: int,
+                              cmap_bgr: np.ndarray, d_disparity: int, d_out_a: int, d_out_u8: int,
+                              d_bgr: int, d_out_b: int = 0, min_depth=0.0, max_depth=0.0,
+                              min_disp_global=0.0, min_disp=0, num_disp=0, stream: int = 0):
+        lut = np.ascontiguousarray(cmap_bgr, np.uint8).reshape(256, 3)
+        _check("sv_median_post_color_dev", self.lib.sv_median_post_color_dev(
+            self._h, d_disp16, H, W, int(row0), int(row1), int(mode), np.float32(min_depth),
+            np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
+            np.float32(min_disp_global), int(min_disp), int(num_disp), lut, d_disparity or None,
+            d_out_a, d_out_u8, d_out_b or None, d_bgr, stream or None))
 
     def depth_map_dev(self, d_left: int, d_right: int, H: int, W: int, pitch: int,
                       min_disp: int, num_disp: int, win: int, min_depth: float,

@@ -490,3 +490,35 @@ def test_colormap_fused_in_the_median_epilogue(engine, H, W):
         for got, exp in zip((dn, d2, du, cf), (e[0], e[1], e[2], e[3])):
             np.testing.assert_array_equal(got, exp)
         np.testing.assert_array_equal(cm2, t[e[2]])
+
+
+@pytest.mark.parametrize("H,W", [(70, 400), (33, 130), (17, 63)])
+def test_median_post_color_dev_epilogue(engine, H, W):
+    """sv_median_post_color_dev: the colormap written by the median kernel's epilogue equals
+    the table applied to the oracle's u8 image, for both modes, full frame and row bands."""
+    from stereovision_amd import colormap
+    L, R = _pair(H, W, 64, seed=H * W)
+    d16 = O.disparity16(L, R, 0, 64, 9)
+    disp = O.disparity_f32(d16)
+    _, e_norm = O.depth_post(disp, 0.3, 2.0, 0)
+    _, e_su8, _ = O.scaled_post(disp, 0, 64)
+    n = H * W
+    d_in = engine.dev_alloc(2 * n)
+    bufs = [engine.dev_alloc(4 * n), engine.dev_alloc(4 * n), engine.dev_alloc(n), engine.dev_alloc(4 * n),
+            engine.dev_alloc(3 * n)]
+    try:
+        engine.to_device(d_in, d16)
+        for mode, name, exp_u8 in ((1, "turbo", e_norm), (2, "jet", e_su8)):
+            t = colormap.table(name)
+            for bands in (1, 3):
+                for k in range(bands):
+                    r0, r1 = H * k // bands, H * (k + 1) // bands
+                    engine.median_post_color_dev(d_in, H, W, r0, r1, mode, t, bufs[0], bufs[1], bufs[2],
+                                                 bufs[4], d_out_b=bufs[3], min_depth=0.3, max_depth=2.0,
+                                                 min_disp_global=0, min_disp=0, num_disp=64)
+                engine.synchronize()
+                np.testing.assert_array_equal(engine.to_host(bufs[2], (H, W), np.uint8), exp_u8)
+                np.testing.assert_array_equal(engine.to_host(bufs[4], (H, W, 3), np.uint8), t[exp_u8])
+    finally:
+        for p in [d_in] + bufs:
+            engine.dev_free(p)

@@ -116,9 +116,11 @@ __device__ __forceinline__ Pk<PackCfg<COST, ND>::NW> ld(PackPtr<COST, ND> p) {
         v.w[0] = c.x;
         if constexpr (P::NC > 1) v.w[1] = c.y;
         if constexpr (P::NC > 2) v.w[2] = c.z;
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(p.x, 16));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v.w[P::NC + i] = q[i];
+        const uint4 m = *p.x;       // one ds_read_b128 (8 lanes per LDS cycle)
+        v.w[P::NC] = m.x;
+        v.w[P::NC + 1] = m.y;
+        v.w[P::NC + 2] = m.z;
+        v.w[P::NC + 3] = m.w;
     } else {
         const uint32_t* q = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(p.x, 16));
 #pragma unroll
@@ -504,6 +506,69 @@ __device__ __forceinline__ void reduce_scatter16(uint32_t (&v)[16], int l) {
 #undef SV_RS_STEP
 }
 
+// reduce_scatter16 with the first two butterfly steps as bank-masked DPP: the partner bit of
+// those steps (lane bit 3, then bit 2) is a DPP bank bit, so a lane's keep/send choice is
+// made by which lanes an instruction writes (bank_mask) instead of two v_cndmask per pair:
+// 2 v_min_u32_dpp per pair instead of 1 + 2 selects (33 ops instead of 45 for 16 keys).
+// Inline asm because the masked write must preserve the disabled lanes' destination; each
+// block starts with s_nop 1 (VALU write -> DPP read of the same VGPR needs 2 wait states).
+__device__ __forceinline__ void reduce_scatter16_bm(uint32_t (&v)[16], int l) {
+#define SV_BM_PAIR(A, B, CTRL, M0, M1)                                                          \
+    "v_min_u32_dpp %" #A ", %" #A ", %" #A " " CTRL " row_mask:0xf bank_mask:" M0 "\n\t"      \
+    "v_min_u32_dpp %" #A ", %" #B ", %" #B " " CTRL " row_mask:0xf bank_mask:" M1 "\n\t"
+    // step 1, row_mirror (partner 15 - l): lanes 0-7 (banks 0,1) keep v[k], lanes 8-15 v[k+8]
+    asm volatile("s_nop 1\n\t"
+                 SV_BM_PAIR(0, 8, "row_mirror", "0x3", "0xc") SV_BM_PAIR(1, 9, "row_mirror", "0x3", "0xc")
+                 SV_BM_PAIR(2, 10, "row_mirror", "0x3", "0xc") SV_BM_PAIR(3, 11, "row_mirror", "0x3", "0xc")
+                 SV_BM_PAIR(4, 12, "row_mirror", "0x3", "0xc") SV_BM_PAIR(5, 13, "row_mirror", "0x3", "0xc")
+                 SV_BM_PAIR(6, 14, "row_mirror", "0x3", "0xc") SV_BM_PAIR(7, 15, "row_mirror", "0x3", "0xc")
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+                 : "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
+    // step 2, row_half_mirror (partner l ^ 7): bit-2-clear lanes (banks 0,2) keep v[k]
+    asm volatile("s_nop 1\n\t"
+                 SV_BM_PAIR(0, 4, "row_half_mirror", "0x5", "0xa") SV_BM_PAIR(1, 5, "row_half_mirror", "0x5", "0xa")
+                 SV_BM_PAIR(2, 6, "row_half_mirror", "0x5", "0xa") SV_BM_PAIR(3, 7, "row_half_mirror", "0x5", "0xa")
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])
+                 : "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
+#undef SV_BM_PAIR
+#define SV_RS_STEP(HALF, BIT, CTRL)                                                            \
+    {                                                                                          \
+        const bool hi = (l & (BIT)) != 0;                                                      \
+        _Pragma("unroll") for (int k = 0; k < (HALF); ++k) {                                   \
+            const uint32_t send = hi ? v[k] : v[k + (HALF)];                                   \
+            const uint32_t keep = hi ? v[k + (HALF)] : v[k];                                   \
+            v[k] = min(keep, (uint32_t)__builtin_amdgcn_update_dpp(0u, (int)send, CTRL, 0xF, 0xF, false)); \
+        }                                                                                      \
+    }
+    SV_RS_STEP(2, 2, 0x1B)    // quad_perm 3210:  partner l ^ 3
+    SV_RS_STEP(1, 1, 0xB1)    // quad_perm 1032:  partner l ^ 1
+#undef SV_RS_STEP
+}
+
+// Reduce-scatter of 8 keys over the 16 lanes of a row: on return lanes 2j and 2j+1 hold the
+// min over the row of key j = (l >> 1) & 7 in v[0].  Bank-masked DPP for lane bits 3 and 2,
+// selects for bit 1, then one all-reduce step with lane l ^ 1: 16 ops for 8 keys.
+__device__ __forceinline__ void reduce_scatter8_bm(uint32_t (&v)[8], int l) {
+#define SV_BM_PAIR(A, B, CTRL, M0, M1)                                                          \
+    "v_min_u32_dpp %" #A ", %" #A ", %" #A " " CTRL " row_mask:0xf bank_mask:" M0 "\n\t"      \
+    "v_min_u32_dpp %" #A ", %" #B ", %" #B " " CTRL " row_mask:0xf bank_mask:" M1 "\n\t"
+    asm volatile("s_nop 1\n\t"
+                 SV_BM_PAIR(0, 4, "row_mirror", "0x3", "0xc") SV_BM_PAIR(1, 5, "row_mirror", "0x3", "0xc")
+                 SV_BM_PAIR(2, 6, "row_mirror", "0x3", "0xc") SV_BM_PAIR(3, 7, "row_mirror", "0x3", "0xc")
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])
+                 : "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
+    asm volatile("s_nop 1\n\t"
+                 SV_BM_PAIR(0, 2, "row_half_mirror", "0x5", "0xa") SV_BM_PAIR(1, 3, "row_half_mirror", "0x5", "0xa")
+                 : "+v"(v[0]), "+v"(v[1])
+                 : "v"(v[2]), "v"(v[3]));
+#undef SV_BM_PAIR
+    const bool hi = (l & 2) != 0;
+    const uint32_t send = hi ? v[0] : v[1];
+    const uint32_t keep = hi ? v[1] : v[0];
+    v[0] = min(keep, (uint32_t)__builtin_amdgcn_update_dpp(0u, (int)send, 0x1B, 0xF, 0xF, false));  // l ^ 3
+    v[0] = min(v[0], (uint32_t)__builtin_amdgcn_update_dpp(0u, (int)v[0], 0xB1, 0xF, 0xF, false));  // l ^ 1
+}
+
 // Occupancy target: LDS admits ~3 blocks/CU for the common configs (D <= 128, win <= 11),
 // so cap registers at 3 waves/SIMD (<= 168 VGPRs); the widest packs get 2 waves/SIMD.
 template <int COST, int ND> struct Occ {
@@ -676,6 +741,165 @@ __global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) 
     }
 }
 
+// ---- ring kind: SAD, four rows per lane, win 5..11 (r 2..5) -----------------------------
+// k_match's four-row kind recomputes the LEAVING column's cost at every step (12 v_sad_hi per
+// 4 cells).  Here each lane owns RG_DPL = 4 consecutive disparities and keeps the entering
+// column's four row costs (hi-shifted, as in the key) in a register ring of W2 = 2r+1 steps,
+// so the leaving column's costs are read back instead of recomputed: a step costs 6 v_sad_hi
+// + 4 v_sub + 4 v_add per 4 cells.  Both rings (the W2-step cost ring and the 4-deep right
+// pack ring) have static register indices inside a body of lcm(4, W2) = 4*W2 unrolled steps.
+// The first 2r steps of a segment fill the window (ring starts at zero) and emit nothing.
+// Keys are (cost << 16) | idx; padding disparities (idx >= D)
+// start at cost 0x8000, above every real window cost (<= 121*255 = 30855 for win 11).
+constexpr int RG_DPL = 4;
+
+template <int R>
+__global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
+    using P = PackCfg<COST_SAD4, R>;
+    constexpr int NW = P::NW, NC = P::NC, W2 = 2 * R + 1;
+    static_assert(P::SPLIT && P::CW == 2, "ring kind expects 24-byte split packs");
+    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    if (blockIdx.z) {   // frame batch
+        a.L += blockIdx.z * a.fs_in;
+        a.R += blockIdx.z * a.fs_in;
+        a.out += blockIdx.z * a.fs_out;
+    }
+    const int lane = threadIdx.x;
+    const int LPG = a.lpg;
+    const int S = a.segm;                               // segment width per group (multiple of 4)
+    const int WC = (64 >> a.lpg_log2) * S;
+    constexpr int U = 4 * W2;                           // steps per unrolled body
+    const int nit = (S + 2 * R + U - 1) / U;            // bodies per segment (2r warm-up steps)
+    const int Tn = nit * U;
+    const int NL = WC - S + Tn + 1;                      // + the L prefetch past the last step
+    const int NRlog = WC - S + Tn + 4 * LPG;
+    constexpr int c0 = 1;                               // chunk starts (index = 3 mod 4) meet slot gaps
+    const int NRphys = NRlog + (NRlog + c0) / RG_DPL + 1;
+    uint4* wbase = smem;
+    typename P::CT* cbase = reinterpret_cast<typename P::CT*>(wbase + (size_t)(NL + NRphys));
+    const PackOut<COST_SAD4, R> Lw{wbase, cbase};
+    const PackOut<COST_SAD4, R> Rw{wbase + NL, cbase + NL};
+    const PackPtr<COST_SAD4, R> Lp{Lw.x, Lw.c};
+    const PackPtr<COST_SAD4, R> Rp{Rw.x, Rw.c};
+
+    const int y = a.row0 + (int)blockIdx.y * 4;
+    const int yc = min(y, a.row1 - 1);
+    const int xw = a.X0 + (int)blockIdx.x * WC;
+    const int cL0 = xw - R;                             // L index i -> column cL0 + i
+    const int cR0 = cL0 - a.minD - (4 * LPG - 1);       // R index i -> column cR0 + i
+    build_all_packs<COST_SAD4, R, RG_DPL>(a, yc, cL0, NL, cR0, NRlog, c0, Lw, Rw, lane);
+
+    if (blockIdx.x == 0) {  // columns outside the matched band are invalid
+        const int16_t inv = (int16_t)((a.minD - 1) * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (y + q >= a.row1) break;
+            int16_t* orow = a.out + (size_t)(y + q) * a.opitch;
+            for (int x = lane; x < a.X0; x += 64) orow[x] = inv;
+            for (int x = a.X1 + lane; x < a.W; x += 64) orow[x] = inv;
+        }
+    }
+    __syncthreads();
+    if (y >= a.row1) return;
+
+    const int g = lane >> a.lpg_log2;
+    const int l = lane & (LPG - 1);
+    const int xs = xw + g * S;                          // first output column of the segment
+    // step t enters column xs - r + t; lane l, disparity idx 4l + k reads R index iR0 + t - k
+    const int iR0 = g * S + 4 * (LPG - 1 - l) + 3;
+    uint32_t h[RG_DPL][4];
+#pragma unroll
+    for (int k = 0; k < RG_DPL; ++k) {
+        const int idx = 4 * l + k;
+        const uint32_t base = idx < a.D ? (uint32_t)idx : (0x8000u << 16) | (uint32_t)idx;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) h[k][q] = base;
+    }
+    uint32_t ring[W2][RG_DPL][4];
+#pragma unroll
+    for (int s = 0; s < W2; ++s)
+#pragma unroll
+        for (int k = 0; k < RG_DPL; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ring[s][k][q] = 0u;
+    Pk<NW> rn[RG_DPL];
+#pragma unroll
+    for (int s = 1; s < RG_DPL; ++s) rn[RG_DPL - s] = ld<COST_SAD4, R>(Rp + rslot(iR0 - s, c0, RG_DPL));
+    PackPtr<COST_SAD4, R> rb = Rp + rslot(iR0, c0, RG_DPL);
+    PackPtr<COST_SAD4, R> lb = Lp + g * S;
+    Pk<NW> Lnext = ld<COST_SAD4, R>(lb);
+    // after the reduce-scatter lane l's key is (row jq, step ju) of the chunk; the first 16
+    // lanes of a group emit
+    // (32-bit per-lane state only: output offset of step 0 and the emit window)
+    const int jq = (lane >> 2) & 3, ju = (lane >> 1) & 1;   // key (l >> 1) & 7 = 2 jq + ju
+    const int eb = ju - 2 * R;                          // step t emits column xs + t + eb
+    const int ooff = 2 * ((y + jq) * a.opitch + xs + eb);   // bytes
+    // 32-bit buffer offsets from one SGPR descriptor (no 64-bit per-lane addresses to keep)
+    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFFF, 0x00020000);
+    const int emax = (l < 16 && (l & 1) == 0 && y + jq < a.row1) ? max(0, min(S, a.X1 - xs)) : 0;
+
+    // whole bodies of U = 4*W2 steps (the host picks S so that S + 2r fits nit bodies with
+    // at most 3 idle steps): no exits inside a body, so the rings never need copies
+    for (int it = 0, t0 = 0; it < nit; ++it) {
+#pragma unroll
+        for (int ch = 0; ch < W2; ++ch, t0 += 4) {
+            uint32_t bk[4][2];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int slot = (4 * ch + u) % W2;
+                // this step's packs: L (every k) and the entering right column (k = 0 only)
+                rn[u] = ld<COST_SAD4, R>(rb + (ch * (RG_DPL + 1) + u));
+                const Pk<NW> Lc = Lnext;                 // loaded one step ahead
+                Lnext = ld<COST_SAD4, R>(lb + (4 * ch + u + 1));
+                // the leaving column's costs need no LDS data: subtract them while the loads
+                // are in flight; k = 0 (the fresh right pack) last
+#pragma unroll
+                for (int k = 0; k < RG_DPL; ++k)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) h[k][q] -= ring[slot][k][q];
+#pragma unroll
+                for (int kk = 0; kk < RG_DPL; ++kk) {
+                    const int k = RG_DPL - 1 - kk;
+                    const Pk<NW>& Rk = rn[(u - k) & 3];
+                    uint32_t cn = 0u;
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) cn = __builtin_amdgcn_sad_hi_u8(Lc.w[i], Rk.w[i], cn);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t c = __builtin_amdgcn_sad_hi_u8(Lc.w[NC + q], Rk.w[NC + q], cn);
+                        h[k][q] += c;
+                        ring[slot][k][q] = c;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) bk[q][u & 1] = min(min(h[0][q], h[1][q]), min(h[2][q], h[3][q]));
+                __builtin_amdgcn_sched_barrier(0);
+                if (u & 1) {   // steps u-1, u: 8 keys (row q, step j) at v[2q + j]
+                    uint32_t v[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[i] = bk[i >> 1][i & 1];
+                    reduce_scatter8_bm(v, lane & 15);
+                    uint32_t key = v[0];
+                    if (LPG >= 32) {   // rows 0,1 (and 2,3) of the wave: min with lane ^ 16
+                        const auto p = __builtin_amdgcn_permlane16_swap(key, key, false, false);
+                        key = min(p[0], p[1]);
+                    }
+                    if (LPG == 64) {   // halves: min with lane ^ 32
+                        const auto p = __builtin_amdgcn_permlane32_swap(key, key, false, false);
+                        key = min(p[0], p[1]);
+                    }
+                    const int tt = t0 + u - 1;
+                    if ((unsigned)(tt + eb) < (unsigned)emax)
+                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16), orsrc,
+                                                              ooff + 2 * tt, 0, 0);
+                }
+            }
+        }
+        rb = rb + W2 * (RG_DPL + 1);
+        lb = lb + U;
+    }
+}
+
 __global__ void k_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
@@ -753,6 +977,79 @@ int kind_of(int cost, int win) {
     return cost;
 }
 
+// Ring kind eligibility and geometry.  SV_RING=0 disables it (A/B measurements);
+bool ring_kind(int cost, int win, int num_disp) {
+    static const bool on = [] {
+        const char* e = std::getenv("SV_RING");
+        return !(e && e[0] == '0');
+    }();
+    return on && kind_of(cost, win) == COST_SAD4 && win >= 5 && win <= 9 && num_disp <= 256;
+}
+int ring_lpg(int num_disp) { return num_disp <= 64 ? 16 : num_disp <= 128 ? 32 : 64; }
+// Segment width per group: S = n*U - 2r rounded down to a multiple of 4 (U = 4*(2r+1) steps
+// per unrolled body, 2r warm-up steps).  n minimises the modelled run time: waves run in
+// rounds of 2048 (2 per SIMD), each wave n*U steps long, so time ~ ceil(waves / 2048) * n*U,
+// where the wave count covers the band (idle columns of the last wave per row), the 4-row
+// blocks and the frames; the segment's LDS must leave room for 2 waves per SIMD; ties go to
+// the longer segment.  SV_RING_SEG=<n> forces n (A/B measurements).
+size_t ring_lds_bytes(int lpg, int seg, int r);
+int ring_seg(int lpg, int r, int band, long long blocks) {
+    static const int env = [] {
+        const char* e = std::getenv("SV_RING_SEG");
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 1 && v <= 16 ? v : 0;
+    }();
+    const int u = 4 * (2 * r + 1), G = 64 / lpg;
+    int best = 0;
+    long long best_cost = -1;
+    for (int n = 1; n <= 8; ++n) {
+        const int S = (n * u - 2 * r) & ~3;
+        if (S < 8 || (n > 1 && ring_lds_bytes(lpg, S, r) > 20 * 1024)) continue;
+        const long long waves = (long long)((band + G * S - 1) / (G * S)) * blocks;
+        const long long cost = (waves + 2047) / 2048 * n * u;
+        if (env ? n == env : (best_cost < 0 || cost <= best_cost)) { best = S; best_cost = cost; }
+    }
+    return best;
+}
+size_t ring_lds_bytes(int lpg, int seg, int r) {
+    const int wc = (64 / lpg) * seg;
+    const int u = 4 * (2 * r + 1);
+    const int tn = (seg + 2 * r + u - 1) / u * u;
+    const int nl = wc - seg + tn + 1, nr = wc - seg + tn + 4 * lpg;
+    const int nrp = nr + (nr + 1) / RG_DPL + 1;
+    return (size_t)(nl + nrp) * 24;
+}
+
+template <int R>
+int launch_ring_r(const MatchParams& a, size_t lds, hipStream_t s) {
+    auto fn = k_match_ring<R>;
+    if (lds > 65536) {
+        hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return (int)e;
+    }
+    const int wc = (64 / a.lpg) * a.segm;
+    dim3 grid((a.X1 - a.X0 + wc - 1) / wc, (a.row1 - a.row0 + 3) / 4, a.nf > 1 ? a.nf : 1);
+    hipLaunchKernelGGL(fn, grid, dim3(64), lds, s, a);
+    return (int)hipGetLastError();
+}
+
+int launch_ring(const MatchParams& a0, hipStream_t s) {
+    MatchParams a = a0;
+    a.lpg = ring_lpg(a.D);
+    a.lpg_log2 = a.lpg == 16 ? 4 : a.lpg == 32 ? 5 : 6;
+    a.dbits = 16;
+    a.segm = ring_seg(a.lpg, a.r, a.X1 - a.X0, (long long)((a.row1 - a.row0 + 3) / 4) * (a.nf > 1 ? a.nf : 1));
+    const size_t lds = ring_lds_bytes(a.lpg, a.segm, a.r);
+    if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+    switch (a.r) {
+        case 2: return launch_ring_r<2>(a, lds, s);
+        case 3: return launch_ring_r<3>(a, lds, s);
+        case 4: return launch_ring_r<4>(a, lds, s);
+        case 5: return launch_ring_r<5>(a, lds, s);
+    }
+    return (int)hipErrorInvalidValue;
+}
+
 }  // namespace
 
 uint64_t max_cost(int win, int cost) {
@@ -818,6 +1115,7 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
         }
         return 0;
     }
+    if (ring_kind(cost, a.win, a.D)) return launch_ring(a, s);
     const size_t lds = match_lds_bytes(p, a.r, cost);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
     MatchParams b = a;

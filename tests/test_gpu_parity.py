@@ -66,6 +66,21 @@ def test_four_row_kind_every_height_and_window(engine, win, H):
                                       O.disparity16(L, R, min_disp, D, win))
 
 
+@pytest.mark.parametrize("win", [5, 7, 9])
+@pytest.mark.parametrize("D", [4, 50, 64, 100, 127, 128, 200, 256])
+def test_ring_kind_disparity_counts(engine, D, win):
+    """The cost-ring SAD kind (win 5..9, D <= 256): lanes of 4 disparities with padding
+    inside a lane (D % 4 != 0), 16/32/64 lanes per group, several segments per row and a
+    ragged last segment, negative min_disp."""
+    rng = np.random.default_rng(D * 10 + win)
+    H, W = 11, 1333
+    L = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    R = np.roll(L, -(D // 3), axis=1) ^ rng.integers(0, 8, (H, W), dtype=np.uint8)
+    for min_disp in (0, -3):
+        np.testing.assert_array_equal(engine.disparity(L, R, min_disp, D, win),
+                                      C.disparity16(L, R, min_disp, D, win, 0))
+
+
 def test_disparity_image_narrower_than_band(engine):
     L, R = _pair(20, 50, 64, seed=3)
     got = engine.disparity(L, R, 0, 64, 5)

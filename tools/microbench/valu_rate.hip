@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 
 #define ITERS 2048
 
@@ -47,6 +48,19 @@ OP3(add3, "v_add3_u32 %0, %1, %2, %0")
 OP3(mad_u24, "v_mad_u32_u24 %0, %1, %2, %0")
 OP3(max_u32, "v_max_u32 %0, %1, %0")
 OP3(cndmask, "v_cndmask_b32 %0, %1, %0, vcc")
+
+OP3(sdwa_add, "v_add_u16_sdwa %0, %1, %0 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1")
+OP3(min_dpp, "v_min_u32_dpp %0, %1, %0 row_ror:1 row_mask:0xf bank_mask:0xf")
+OP3(min_dpp_bm, "v_min_u32_dpp %0, %1, %0 row_mirror row_mask:0xf bank_mask:0x3")
+OP3(min_e32, "v_min_u32 %0, %1, %0")
+OP3(lshl_add, "v_lshl_add_u32 %0, %1, 16, %0")
+OP3(pk_min_u16, "v_pk_min_u16 %0, %1, %0")
+OP3(sad_hi_u8, "v_sad_hi_u8 %0, %1, %2, %0")
+// mixed streams: does a VOP2 op hide behind VOP3 ops?
+OP3(mix_sad_sub, "v_sad_u8 %0, %1, %2, %0\n v_sub_u32 %0, %0, %1")
+OP3(mix_sad_sdwa, "v_sad_u8 %0, %1, %2, %0\n v_add_u16_sdwa %0, %1, %0 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1")
+OP3(mix_sad_min, "v_sad_u8 %0, %1, %2, %0\n v_min_u32 %0, %1, %0")
+OP3(plswap, "v_mov_b32 %1, %0\n v_permlane16_swap_b32 %0, %1")
 
 // quad SAD: 64-bit source, 32-bit reference, 64-bit (4 x u16) accumulator
 __global__ __launch_bounds__(256) void k_qsad(uint32_t* out, uint32_t a, uint32_t b) {
@@ -90,11 +104,15 @@ int main() {
         {"v_pk_add_u16", k_pk_add_u16}, {"v_pk_max_u16", k_pk_max_u16}, {"v_pk_sub_u16", k_pk_sub_u16},
         {"v_perm_b32", k_perm}, {"v_alignbyte_b32", k_alignbyte}, {"v_bfe_u32", k_bfe},
         {"v_add3_u32", k_add3}, {"v_mad_u32_u24", k_mad_u24}, {"v_max_u32", k_max_u32},
-        {"v_cndmask_b32", k_cndmask}, {"v_qsad_pk_u16_u8", k_qsad}, {"v_mqsad_u32_u8", k_mqsad},
+        {"v_cndmask_b32", k_cndmask}, {"v_add_u16_sdwa", k_sdwa_add}, {"v_min_u32_dpp", k_min_dpp},
+        {"v_min_u32_dpp bankmask", k_min_dpp_bm}, {"v_min_u32_e32", k_min_e32}, {"v_lshl_add_u32", k_lshl_add},
+        {"v_pk_min_u16", k_pk_min_u16}, {"v_sad_hi_u8", k_sad_hi_u8}, {"mix sad+sub (x2)", k_mix_sad_sub},
+        {"mix sad+sdwa (x2)", k_mix_sad_sdwa}, {"mix sad+min (x2)", k_mix_sad_min}, {"mov+permlane16swap(x2)", k_plswap}, {"v_qsad_pk_u16_u8", k_qsad}, {"v_mqsad_u32_u8", k_mqsad},
     };
     int ncu = 0;
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
-    const int blocks = ncu * 4;   // 16 waves per CU
+    const char* wps = getenv("WPS");
+    const int blocks = ncu * (wps ? atoi(wps) : 4);   // WPS waves per SIMD (default 4)
     uint32_t* out;
     hipMalloc(&out, (size_t)blocks * 256 * 4);
     hipEvent_t e0, e1;

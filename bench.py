@@ -284,7 +284,7 @@ def host_path(H, W, D, win, seconds=3.0):
         from stereovision_amd.pipeline import DepthMapPipeline
     except ImportError:
         return out
-    pipe = DepthMapPipeline(D, win)
+    pipe = DepthMapPipeline(D, win, depth=4)
     try:
         for i in range(4):
             pipe.submit(*frames[i % 4]).result()

@@ -410,6 +410,16 @@ int sv_dev_free(sv_ctx* ctx, void* p);
 int sv_copy_to_device(sv_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 int sv_copy_to_host(sv_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 
+/* Page-lock a host range and make it device-visible (hipHostRegister, portable).  Output
+ * arrays of the host-buffer entry points (sv_depth_map, sv_depth_map_color,
+ * sv_stereo_scaled, sv_stereo_scaled_color) that lie inside registered ranges are filled by
+ * DMA from the device epilogue instead of by the host expansion of the int16 medians; the
+ * results are identical.  A range stays registered until sv_host_unregister(ptr), which
+ * takes the same start pointer.  No reference counterpart: an engine-side optimisation of
+ * the numpy outputs depth_map.py:937-939 returns. */
+int sv_host_register(void* ptr, uint64_t bytes);
+int sv_host_unregister(void* ptr);
+
 /* ---- profiling: HIP events around every kernel this context launches -------------- */
 int sv_profile_enable(sv_ctx* ctx, int on);
 /* Waits for the recorded events and returns the accumulated device time and launch count

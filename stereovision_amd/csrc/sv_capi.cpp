@@ -5,7 +5,9 @@
 // and copy results back; device entry points only enqueue.  No exception crosses the ABI.
 #include <cstdio>
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <thread>
 #include <new>
@@ -104,6 +106,12 @@ struct EvPair {
 
 }  // namespace
 
+// one entry of the host copy of the post-processing table (host-buffer frame path)
+struct HostEnt {
+    float a;          // depth_final / disparity_normalized
+    uint32_t ubgr;    // u8 | B << 8 | G << 16 | R << 24
+};
+
 struct sv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -117,6 +125,7 @@ struct sv_ctx {
     DevBuf m16;
     std::vector<float> hl_a, hl_b;
     std::vector<uint8_t> hl_u8;
+    std::vector<HostEnt> hl_ent;
     bool hl_valid = false;
     hipEvent_t cev[8] = {};
     // SGBM: second stream + fork/join events for the vertical path beside the horizontal ones
@@ -1390,6 +1399,22 @@ int sv_scaled_post(sv_ctx* c, const float* disparity, int n, int min_disp, int n
 
 namespace {
 
+// Host ranges registered through sv_host_register (page-locked and device-visible): the
+// host-buffer frame path DMAs its outputs straight into them instead of expanding the int16
+// medians on the host.
+std::mutex g_reg_mu;
+std::map<uintptr_t, size_t> g_reg;   // start -> bytes
+
+bool host_registered(const void* p, size_t bytes) {
+    if (!p) return false;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.upper_bound(a);
+    if (it == g_reg.begin()) return false;
+    --it;
+    return a >= it->first && a + bytes <= it->first + it->second;
+}
+
 // Host memory -> pinned staging -> device, in chunks: the DMA of one chunk runs while the
 // host threads copy the next (one call per frame, as the reference calls the path).
 int stage_image_chunked(sv_ctx* c, const uint8_t* src, int H, size_t row, int stride, uint8_t* stage,
@@ -1475,15 +1500,74 @@ struct FrameOut {
 // reads the same table): disparity = m / 16, the post-processing outputs = table[m - m0],
 // the colormap = table_bgr[u8].  Chunks of rows come back behind events, so the expansion
 // of one chunk runs while the next is in flight.
+// Pixels [a, b) of the host expansion: disparity = m / 16 (a power of two: exact), the f32
+// output and u8 / BGR from the packed table entry.  The BGR triple goes out as one 4-byte
+// store whose 4th byte the next pixel overwrites (same thread); the last pixel of the range
+// stores 3 bytes, so ranges of different threads never overlap.  Returns the number of
+// medians outside the table (left unwritten).
+template <bool U8, bool SCALED, bool BGR>
+int expand_rows(const int16_t* med, size_t a, size_t b, int m0, int nl, const HostEnt* ent, const float* lb,
+                const FrameOut& o) {
+    for (size_t i = a; i < b; ++i) o.disp[i] = (float)med[i] * 0.0625f;
+    int nbad = 0;
+    for (size_t i = a; i < b; ++i) {
+        const uint32_t li = (uint32_t)(med[i] - m0);
+        if (__builtin_expect(li >= (uint32_t)nl, 0)) {
+            ++nbad;
+            continue;
+        }
+        const HostEnt e = ent[li];
+        o.a[i] = e.a;
+        if (U8) o.u8[i] = (uint8_t)e.ubgr;
+        if (SCALED) o.b[i] = lb[li];
+        if (BGR) {
+            const uint32_t v = e.ubgr >> 8;
+            uint8_t* d = o.bgr + 3 * i;
+            if (i + 1 < b) std::memcpy(d, &v, 4);
+            else std::memcpy(d, &v, 3);
+        }
+    }
+    return nbad;
+}
+
+// SV_HOST_PROFILE=1: stage timings of the host-buffer path on stderr every 200 calls
+// (diagnostic; the default path pays one getenv at first use).
+struct HostProf {
+    bool on = std::getenv("SV_HOST_PROFILE") != nullptr;
+    std::mutex mu;
+    double t[6] = {0, 0, 0, 0, 0, 0};
+    long n = 0;
+    void add(const double* d) {
+        std::lock_guard<std::mutex> lk(mu);
+        for (int i = 0; i < 6; ++i) t[i] += d[i];
+        if (++n % 200 == 0) {
+            std::fprintf(stderr, "[sv host] per call (ms): stage %.3f  issue %.3f  wait-first %.3f  expand %.3f  "
+                         "wait-rest %.3f  total %.3f\n", t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n);
+            for (double& v : t) v = 0;
+            n = 0;
+        }
+    }
+};
+HostProf& host_prof() {
+    static HostProf* p = new HostProf();
+    return *p;
+}
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels, int stride,
                     int min_disp, int num_disp, int win, int cost, sv::PostParams pp, const uint8_t* table,
                     FrameOut o) {
+    const bool prof = host_prof().on;
+    double tm[6] = {0, 0, 0, 0, 0, 0}, t0 = prof ? now_ms() : 0, tp = t0;
     sv::MatchPlan plan;
     int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
     if (rc) return rc;
     if ((long long)H * W >= (1LL << 30)) return fail(SV_EINVAL, "frame too large");
     rc = stage_pair_chunked(c, left, right, H, W, channels, stride);
     if (rc) return rc;
+    if (prof) { const double t = now_ms(); tm[0] = t - tp; tp = t; }
     const size_t n = (size_t)H * W;
     SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
     SV_HIP(c->m16.ensure(n * sizeof(int16_t)));
@@ -1494,6 +1578,46 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
     rc = attach_lut(c, pp, c->stream);
     if (rc) return rc;
     if (pp.lut_n <= 0) return fail(SV_EINVAL, "no post-processing table for these parameters");
+    const bool scaled_mode = pp.mode == SV_POST_SCALED;
+    if (host_registered(o.a, n * 4) && host_registered(o.disp, n * 4) && (!o.u8 || host_registered(o.u8, n)) &&
+        (!scaled_mode || host_registered(o.b, n * 4)) && (!o.bgr || host_registered(o.bgr, 3 * n))) {
+        // registered outputs: the median kernel's epilogue writes every output on the device
+        // and they come back by DMA in row chunks (no host expansion)
+        SV_HIP(c->fa.ensure(n * 4));
+        SV_HIP(c->fb.ensure(n * 4));
+        SV_HIP(c->u8.ensure(n));
+        if (scaled_mode) SV_HIP(c->fc.ensure(n * 4));
+        if (o.bgr) SV_HIP(c->bgr.ensure(3 * n));
+        sv::PostParams dp = pp;
+        dp.out_a = c->fa.as<float>();
+        dp.out_u8 = c->u8.as<uint8_t>();
+        dp.out_b = scaled_mode ? c->fc.as<float>() : nullptr;
+        rc = attach_cmap(c, dp, table, o.bgr ? c->bgr.as<uint8_t>() : nullptr, c->stream);
+        if (rc) return rc;
+        SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
+                  sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fb.as<float>(), dp, c->stream));
+        if (prof) { const double t = now_ms(); tm[1] = t - tp; tp = t; }
+        const int nck = H >= 64 ? 4 : 1;
+        for (int k = 0; k < nck; ++k) {
+            const size_t y0 = (size_t)H * k / nck, y1 = (size_t)H * (k + 1) / nck, i0 = y0 * W, m = (y1 - y0) * W;
+            SV_HIP(hipMemcpyAsync(o.disp + i0, c->fb.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, c->stream));
+            SV_HIP(hipMemcpyAsync(o.a + i0, c->fa.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, c->stream));
+            if (o.u8) SV_HIP(hipMemcpyAsync(o.u8 + i0, c->u8.as<uint8_t>() + i0, m, hipMemcpyDeviceToHost, c->stream));
+            if (scaled_mode)
+                SV_HIP(hipMemcpyAsync(o.b + i0, c->fc.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, c->stream));
+            if (o.bgr)
+                SV_HIP(hipMemcpyAsync(o.bgr + 3 * i0, c->bgr.as<uint8_t>() + 3 * i0, 3 * m, hipMemcpyDeviceToHost,
+                                      c->stream));
+        }
+        SV_HIP(hipStreamSynchronize(c->stream));
+        if (prof) {
+            const double t = now_ms();
+            tm[4] = t - tp;
+            tm[5] = t - t0;
+            host_prof().add(tm);
+        }
+        return 0;
+    }
     rc = host_lut(c, pp);
     if (rc) return rc;
     sv::PostParams mp = pp;      // the median kernel writes only the int16 medians
@@ -1509,43 +1633,52 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
         SV_HIP(hipEventRecord(c->cev[k], c->stream));
     }
     const int m0 = pp.lut_m0, nl = pp.lut_n;
-    const float* la = c->hl_a.data();
+    // one 8-byte entry per table index: the f32 output and (u8, B, G, R) packed, so a pixel
+    // costs one L1 load instead of the dependent u8 -> colormap lookups
+    try {
+        c->hl_ent.resize((size_t)nl);
+    } catch (...) {
+        return fail(SV_ENOMEM, "host table allocation failed");
+    }
+    for (int i = 0; i < nl; ++i) {
+        const uint8_t u = c->hl_u8[i];
+        const uint32_t bgr = table ? (uint32_t)table[3 * u] | (uint32_t)table[3 * u + 1] << 8 |
+                                     (uint32_t)table[3 * u + 2] << 16 : 0u;
+        c->hl_ent[i] = HostEnt{c->hl_a[i], u | bgr << 8};
+    }
+    const HostEnt* ent = c->hl_ent.data();
     const float* lb = c->hl_b.data();
-    const uint8_t* lu = c->hl_u8.data();
     const int16_t* med = c->hout.as<int16_t>();
     const bool scaled = pp.mode == SV_POST_SCALED;
     std::atomic<int> bad{0};
     sv::HostPool& pool = sv::HostPool::get();
     for (int k = 0; k < nchunk; ++k) {
         SV_HIP(hipEventSynchronize(c->cev[k]));
+        if (prof) { const double t = now_ms(); tm[k ? 4 : 2] += t - tp; tp = t; }
         const size_t y0 = (size_t)H * k / nchunk, y1 = (size_t)H * (k + 1) / nchunk;
         const size_t i0 = y0 * W, i1 = y1 * W;
         const int parts = pool.threads();
         pool.parallel_for(parts, [&](int p) {
             const size_t a = i0 + (i1 - i0) * p / parts, b = i0 + (i1 - i0) * (p + 1) / parts;
-            int nbad = 0;
-            for (size_t i = a; i < b; ++i) {
-                const int m = med[i];
-                const uint32_t li = (uint32_t)(m - m0);
-                if (li >= (uint32_t)nl) {
-                    ++nbad;
-                    continue;
-                }
-                o.disp[i] = (float)m / 16.0f;
-                o.a[i] = la[li];
-                const uint8_t u = lu[li];
-                if (o.u8) o.u8[i] = u;
-                if (scaled) o.b[i] = lb[li];
-                if (o.bgr) {
-                    const uint8_t* t = table + 3 * u;
-                    uint8_t* d = o.bgr + 3 * i;
-                    d[0] = t[0];
-                    d[1] = t[1];
-                    d[2] = t[2];
-                }
+            const int nbad = (o.u8 ? 1 : 0) | (scaled ? 2 : 0) | (o.bgr ? 4 : 0);
+            int nb = 0;
+            switch (nbad) {   // the output set picks the instantiation (no per-pixel branches)
+                case 0: nb = expand_rows<false, false, false>(med, a, b, m0, nl, ent, lb, o); break;
+                case 1: nb = expand_rows<true, false, false>(med, a, b, m0, nl, ent, lb, o); break;
+                case 2: nb = expand_rows<false, true, false>(med, a, b, m0, nl, ent, lb, o); break;
+                case 3: nb = expand_rows<true, true, false>(med, a, b, m0, nl, ent, lb, o); break;
+                case 4: nb = expand_rows<false, false, true>(med, a, b, m0, nl, ent, lb, o); break;
+                case 5: nb = expand_rows<true, false, true>(med, a, b, m0, nl, ent, lb, o); break;
+                case 6: nb = expand_rows<false, true, true>(med, a, b, m0, nl, ent, lb, o); break;
+                default: nb = expand_rows<true, true, true>(med, a, b, m0, nl, ent, lb, o); break;
             }
-            if (nbad) bad.fetch_add(nbad);
+            if (nb) bad.fetch_add(nb);
         });
+        if (prof) { const double t = now_ms(); tm[3] += t - tp; tp = t; }
+    }
+    if (prof) {
+        tm[5] = now_ms() - t0;
+        host_prof().add(tm);
     }
     if (bad.load()) return fail(SV_EHIP, "median value outside the post-processing table");
     return 0;
@@ -1554,6 +1687,29 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
 }  // namespace
 
 extern "C" {
+
+int sv_host_register(void* ptr, uint64_t bytes) {
+    if (!ptr || bytes == 0) return fail(SV_EINVAL, "null or empty host range");
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        if (g_reg.count(reinterpret_cast<uintptr_t>(ptr))) return fail(SV_EINVAL, "host range already registered");
+    }
+    SV_HIP(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterPortable));
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg[reinterpret_cast<uintptr_t>(ptr)] = (size_t)bytes;
+    return 0;
+}
+
+int sv_host_unregister(void* ptr) {
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto it = g_reg.find(reinterpret_cast<uintptr_t>(ptr));
+        if (it == g_reg.end()) return fail(SV_EINVAL, "host range not registered");
+        g_reg.erase(it);
+    }
+    SV_HIP(hipHostUnregister(ptr));
+    return 0;
+}
 
 int sv_depth_map(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels, int stride,
                  int min_disp, int num_disp, int win, int cost, float min_depth, float max_depth,

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
 
 import numpy as np
@@ -33,7 +34,7 @@ EXPORTED = [
     "sv_hog_hist", "sv_gray_dev", "sv_disparity_dev", "sv_median_post_dev",
     "sv_depth_map_dev", "sv_harris_dev", "sv_hog_hist_dev", "sv_profile_enable",
     "sv_profile_read", "sv_profile_reset", "sv_disparity_rows", "sv_dev_alloc", "sv_dev_free",
-    "sv_copy_to_device", "sv_copy_to_host", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
+    "sv_copy_to_device", "sv_copy_to_host", "sv_host_register", "sv_host_unregister", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
     "sv_depth_map_batch_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
     "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
     "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
@@ -164,6 +165,8 @@ def _declare(lib):
         "sv_dev_free": ([_vp, _vp], _c_int),
         "sv_copy_to_device": ([_vp, _vp, _vp, ctypes.c_uint64], _c_int),
         "sv_copy_to_host": ([_vp, _vp, _vp, ctypes.c_uint64], _c_int),
+        "sv_host_register": ([_vp, ctypes.c_uint64], _c_int),
+        "sv_host_unregister": ([_vp], _c_int),
         "sv_disparity_batch_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, ctypes.c_int64,
                                     _c_int, _c_int, _c_int, _c_int, _vp, _c_int, ctypes.c_int64,
                                     _vp], _c_int),
@@ -304,6 +307,25 @@ def _image(a: np.ndarray) -> tuple[np.ndarray, int, int, int]:
     raise ValueError(f"expected HxW or HxWx3 image, got shape {a.shape}")
 
 
+def _refs_first(arrs) -> int:
+    for a in arrs:
+        return sys.getrefcount(a)
+    return 0
+
+
+def _set_unreferenced(arrs) -> bool:
+    """True when no array of the recycling slot `arrs` is referenced outside it."""
+    for a in arrs:
+        if sys.getrefcount(a) > _BASE_REFS:
+            return False
+    return True
+
+
+# references of an array held only by a recycling slot, seen from the same loop shape
+# (slot, loop variable, getrefcount's argument): measured, not assumed
+_BASE_REFS = _refs_first([np.empty(1)])
+
+
 class Engine:
     """One libsvhip context (device + stream + cached buffers)."""
 
@@ -319,9 +341,15 @@ class Engine:
         self._h = h
         self.device = device
         self._scratch: dict[str, tuple[int, int]] = {}
+        self._recycle: dict[tuple, list] = {}
+        self._noreg = os.environ.get("SV_REGISTER_OUTPUTS", "1") == "0"
 
     # -- lifetime -------------------------------------------------------------------
     def close(self):
+        for sets in getattr(self, "_recycle", {}).values():
+            for arrs in sets:
+                self._unregister(arrs)
+        self._recycle = {}
         if getattr(self, "_h", None):
             for p, _ in self._scratch.values():
                 self.lib.sv_dev_free(self._h, p)
@@ -338,6 +366,43 @@ class Engine:
             p = self.dev_alloc(max(int(nbytes), 256))
             self._scratch[name] = (p, max(int(nbytes), 256))
         return p
+
+    def outputs(self, specs) -> tuple:
+        """Fresh-looking output arrays for a host-buffer call: ((shape, dtype), ...) ->
+        arrays.  A set this engine returned before is handed out again once the caller holds
+        no reference to any of its arrays (or to views of them), so a steady stream of
+        frames writes into resident pages instead of page-faulting 20+ MB of new memory per
+        1080p frame.  At most 3 sets per shape are kept."""
+        key = tuple((tuple(sh), np.dtype(dt).str) for sh, dt in specs)
+        sets = self._recycle.setdefault(key, [])
+        for arrs in sets:
+            if _set_unreferenced(arrs):
+                self._register(arrs)
+                return tuple(arrs)
+        arrs = [np.empty(sh, dt) for sh, dt in specs]
+        sets.append(arrs)
+        if len(sets) > 3:
+            self._unregister(sets.pop(0))
+        return tuple(arrs)
+
+    def _register(self, arrs):
+        """Page-lock a recycled output set (on its first reuse, so callers that keep every
+        result never pay for it): the C path then DMAs the outputs straight into it."""
+        if getattr(self, "_noreg", False) or not hasattr(self, "lib"):
+            return
+        regs = self.__dict__.setdefault("_registered", {})
+        for a in arrs:
+            if a.nbytes and id(a) not in regs:
+                if self.lib.sv_host_register(a.ctypes.data, a.nbytes) != 0:
+                    self._noreg = True     # e.g. a page-lock limit: keep the host expansion
+                    return
+                regs[id(a)] = a
+
+    def _unregister(self, arrs):
+        regs = self.__dict__.get("_registered", {})
+        for a in arrs:
+            if regs.pop(id(a), None) is not None:
+                self.lib.sv_host_unregister(a.ctypes.data)
 
     def upload(self, name: str, a: np.ndarray) -> int:
         """Copy a host array into the named scratch buffer; returns its device pointer."""
@@ -529,18 +594,24 @@ class Engine:
 
     def depth_map_color(self, left, right, min_disp: int, num_disp: int, win: int,
                         min_depth: float, max_depth: float, cmap_bgr: np.ndarray,
-                        min_disp_global=None, cost="sad", with_normalized: bool = False):
+                        min_disp_global=None, cost="sad", with_normalized: bool = False, out=None):
         """create_depth_map's outputs with the colormap computed on the GPU:
-        (depth_final, disparity, depth_colormap HxWx3 BGR[, depth_normalized])."""
+        (depth_final, disparity, depth_colormap HxWx3 BGR[, depth_normalized]).
+        `out`: optional (depth, disparity, colormap) arrays to fill instead of new ones."""
         left, H, W, C = _image(left)
         right, H2, W2, C2 = _image(right)
         if (H, W, C) != (H2, W2, C2):
             raise ValueError("left/right shapes differ")
         lut = np.ascontiguousarray(cmap_bgr, np.uint8).reshape(256, 3)
         mdg = min_disp if min_disp_global is None else min_disp_global
-        depth = np.empty((H, W), np.float32)
-        disp = np.empty((H, W), np.float32)
-        cmap = np.empty((H, W, 3), np.uint8)
+        if out is not None:
+            depth, disp, cmap = out
+            if (depth.shape, disp.shape, cmap.shape) != ((H, W), (H, W), (H, W, 3)) or \
+                    (depth.dtype, disp.dtype, cmap.dtype) != (np.float32, np.float32, np.uint8) or \
+                    not all(a.flags.c_contiguous for a in out):
+                raise ValueError("out arrays must be C-contiguous (H,W) f32, (H,W) f32, (H,W,3) u8")
+        else:
+            depth, disp, cmap = self.outputs((((H, W), np.float32), ((H, W), np.float32), ((H, W, 3), np.uint8)))
         norm = np.empty((H, W), np.uint8) if with_normalized else None
         _check("sv_depth_map_color", self.lib.sv_depth_map_color(
             self._h, left, right, H, W, C, W * C, int(min_disp), int(num_disp), int(win),
@@ -558,10 +629,8 @@ class Engine:
         if (H, W, C) != (H2, W2, C2):
             raise ValueError("left/right shapes differ")
         lut = np.ascontiguousarray(cmap_bgr, np.uint8).reshape(256, 3)
-        dn = np.empty((H, W), np.float32)
-        disp = np.empty((H, W), np.float32)
-        cf = np.empty((H, W), np.float32)
-        cmap = np.empty((H, W, 3), np.uint8)
+        dn, disp, cf, cmap = self.outputs((((H, W), np.float32), ((H, W), np.float32), ((H, W), np.float32),
+                                           ((H, W, 3), np.uint8)))
         du = np.empty((H, W), np.uint8) if with_normalized else None
         _check("sv_stereo_scaled_color", self.lib.sv_stereo_scaled_color(
             self._h, left, right, H, W, C, W * C, int(min_disp), int(num_disp), int(win),
@@ -955,6 +1024,10 @@ class Communicator:
         return self._h
 
     def close(self):
+        for sets in getattr(self, "_recycle", {}).values():
+            for arrs in sets:
+                self._unregister(arrs)
+        self._recycle = {}
         if getattr(self, "_h", None):
             self.lib.sv_comm_destroy(self._h)
             self._h = None

@@ -537,3 +537,24 @@ def test_median_post_color_dev_epilogue(engine, H, W):
     finally:
         for p in [d_in] + bufs:
             engine.dev_free(p)
+
+
+@pytest.mark.parametrize("scaled", [False, True])
+def test_registered_outputs_dma_path_matches_host_expansion(engine, scaled):
+    """Host-buffer calls whose recycled outputs got page-locked (sv_host_register) take the
+    device-epilogue + DMA path; the first call (fresh arrays) takes the int16 + host table
+    expansion path.  Both must give the same bytes."""
+    from stereovision_amd import colormap
+    L, R, _ = stereo_pair(70, 333, 64, seed=21)
+    Lb, Rb = to_bgr(L), to_bgr(R)
+    t = colormap.table("turbo")
+    call = (lambda: engine.stereo_scaled_color(Lb, Rb, 0, 64, 9, t)) if scaled else \
+        (lambda: engine.depth_map_color(Lb, Rb, 0, 64, 9, 0.3, 2.0, t))
+    first = [a.copy() for a in call()]          # fresh set: host expansion
+    for _ in range(3):                          # released -> reused -> registered -> DMA
+        got = call()
+        for g, e in zip(got, first):
+            np.testing.assert_array_equal(g, e)
+        del got
+    regs = getattr(engine, "_registered", {})
+    assert regs, "no output set was registered"

@@ -1,0 +1,57 @@
+"""Output recycling of the host-buffer entry points (Engine.outputs): a set of output arrays
+is handed out again only when the caller holds no reference to any of them (CPU test: the
+pool logic needs no device)."""
+import numpy as np
+
+from stereovision_amd import engine as EN
+
+
+class _Pool:
+    outputs = EN.Engine.outputs
+    _register = EN.Engine._register      # no library: registration is skipped
+    _unregister = EN.Engine._unregister
+
+    def __init__(self):
+        self._recycle = {}
+
+
+SPEC = (((6, 5), np.float32), ((6, 5), np.float32), ((6, 5, 3), np.uint8))
+
+
+def _ids(arrs):
+    return [id(a) for a in arrs]
+
+
+def test_released_set_is_reused():
+    p = _Pool()
+    a = p.outputs(SPEC)
+    ids = _ids(a)
+    assert [x.shape for x in a] == [(6, 5), (6, 5), (6, 5, 3)]
+    assert [x.dtype for x in a] == [np.float32, np.float32, np.uint8]
+    del a
+    assert _ids(p.outputs(SPEC)) == ids
+
+
+def test_held_arrays_views_and_buffers_block_reuse():
+    p = _Pool()
+    a = p.outputs(SPEC)
+    ids = _ids(a)
+    view = a[0][2:]           # a view keeps its base alive
+    del a
+    assert _ids(p.outputs(SPEC)) != ids
+    del view
+    b = p.outputs(SPEC)
+    assert _ids(b) == ids
+    mv = memoryview(b[2])      # an exported buffer too
+    del b
+    assert _ids(p.outputs(SPEC)) != ids
+    del mv
+
+
+def test_pool_is_bounded_and_keyed_by_shape():
+    p = _Pool()
+    held = [p.outputs(SPEC) for _ in range(5)]
+    assert len(p._recycle[next(iter(p._recycle))]) == 3
+    other = p.outputs((((2, 2), np.float32),))
+    assert other[0].shape == (2, 2) and len(p._recycle) == 2
+    assert len({id(h[0]) for h in held}) == 5   # every held set distinct

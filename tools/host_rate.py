@@ -38,6 +38,9 @@ def main():
     out = {"size": f"{W}x{H}", "D": D, "win": win}
     out["engine.depth_map"] = rate(lambda i: eng.depth_map(*frames[i % 4], 0, D, win, 0.3, 2.0))
     out["engine.depth_map_color"] = rate(lambda i: eng.depth_map_color(*frames[i % 4], 0, D, win, 0.3, 2.0, t))
+    bufs = (np.zeros((H, W), np.float32), np.zeros((H, W), np.float32), np.zeros((H, W, 3), np.uint8))
+    out["engine.depth_map_color reused outputs"] = rate(
+        lambda i: eng.depth_map_color(*frames[i % 4], 0, D, win, 0.3, 2.0, t, out=bufs))
     out["create_depth_map"] = rate(lambda i: DM.create_depth_map(*frames[i % 4]))
     u8 = np.random.default_rng(0).integers(0, 256, (H, W), dtype=np.uint8)
     out["host colormap.apply"] = rate(lambda i: colormap.apply(u8, "turbo"), n=10)

@@ -107,7 +107,11 @@ template <int COST, int ND>
 using PackPtr = PackPtrT<COST, ND, const uint4, const typename PackCfg<COST, ND>::CT>;
 template <int COST, int ND> using PackOut = PackPtrT<COST, ND, uint4, typename PackCfg<COST, ND>::CT>;
 
-template <int COST, int ND>
+// B128: the 16-byte slot as one ds_read_b128 (the ring kind, whose 32-lane groups read
+// slots 80 B apart: as two dword pairs, lanes l and l+16 of a b32 cycle share banks).  The
+// other kinds keep the split dword loads the compiler pairs into ds_read2_b64 (HOG: b128
+// measured 518 -> 655 us per 4K frame).
+template <int COST, int ND, bool B128 = false>
 __device__ __forceinline__ Pk<PackCfg<COST, ND>::NW> ld(PackPtr<COST, ND> p) {
     using P = PackCfg<COST, ND>;
     Pk<P::NW> v;
@@ -116,11 +120,17 @@ __device__ __forceinline__ Pk<PackCfg<COST, ND>::NW> ld(PackPtr<COST, ND> p) {
         v.w[0] = c.x;
         if constexpr (P::NC > 1) v.w[1] = c.y;
         if constexpr (P::NC > 2) v.w[2] = c.z;
-        const uint4 m = *p.x;       // one ds_read_b128 (8 lanes per LDS cycle)
-        v.w[P::NC] = m.x;
-        v.w[P::NC + 1] = m.y;
-        v.w[P::NC + 2] = m.z;
-        v.w[P::NC + 3] = m.w;
+        if constexpr (B128) {
+            const uint4 m = *p.x;
+            v.w[P::NC] = m.x;
+            v.w[P::NC + 1] = m.y;
+            v.w[P::NC + 2] = m.z;
+            v.w[P::NC + 3] = m.w;
+        } else {
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(p.x, 16));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v.w[P::NC + i] = q[i];
+        }
     } else {
         const uint32_t* q = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(p.x, 16));
 #pragma unroll
@@ -824,10 +834,10 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
             for (int q = 0; q < 4; ++q) ring[s][k][q] = 0u;
     Pk<NW> rn[RG_DPL];
 #pragma unroll
-    for (int s = 1; s < RG_DPL; ++s) rn[RG_DPL - s] = ld<COST_SAD4, R>(Rp + rslot(iR0 - s, c0, RG_DPL));
+    for (int s = 1; s < RG_DPL; ++s) rn[RG_DPL - s] = ld<COST_SAD4, R, true>(Rp + rslot(iR0 - s, c0, RG_DPL));
     PackPtr<COST_SAD4, R> rb = Rp + rslot(iR0, c0, RG_DPL);
     PackPtr<COST_SAD4, R> lb = Lp + g * S;
-    Pk<NW> Lnext = ld<COST_SAD4, R>(lb);
+    Pk<NW> Lnext = ld<COST_SAD4, R, true>(lb);
     // after the reduce-scatter lane l's key is (row jq, step ju) of the chunk; the first 16
     // lanes of a group emit
     // (32-bit per-lane state only: output offset of step 0 and the emit window)
@@ -848,9 +858,9 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
             for (int u = 0; u < 4; ++u) {
                 const int slot = (4 * ch + u) % W2;
                 // this step's packs: L (every k) and the entering right column (k = 0 only)
-                rn[u] = ld<COST_SAD4, R>(rb + (ch * (RG_DPL + 1) + u));
+                rn[u] = ld<COST_SAD4, R, true>(rb + (ch * (RG_DPL + 1) + u));
                 const Pk<NW> Lc = Lnext;                 // loaded one step ahead
-                Lnext = ld<COST_SAD4, R>(lb + (4 * ch + u + 1));
+                Lnext = ld<COST_SAD4, R, true>(lb + (4 * ch + u + 1));
                 // the leaving column's costs need no LDS data: subtract them while the loads
                 // are in flight; k = 0 (the fresh right pack) last
 #pragma unroll

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 mkdir -p gpurun_out
 run() {
   local name=$1; shift
-  timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > gpurun_out/cfg_$name.log 2>&1
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-live-pmc --no-host-path "$@" > gpurun_out/cfg_$name.log 2>&1
   local rc=$?
   if [ $rc -ne 0 ]; then echo "$name rc=$rc"; tail -n 5 gpurun_out/cfg_$name.log; exit $rc; fi
   python3 - "$name" gpurun_out/cfg_$name.log <<'PY'

@@ -426,6 +426,12 @@ int sv_profile_enable(sv_ctx* ctx, int on);
  * of kernel `kernel` (sv_kernel) since the last reset. */
 int sv_profile_read(sv_ctx* ctx, int kernel, double* total_ms, long long* count);
 int sv_profile_reset(sv_ctx* ctx);
+/* Device time between two points of a stream (HIP events): sv_timer_begin records the
+ * first, sv_timer_end the second, waits for it and returns the elapsed milliseconds.  For
+ * timing a run of back-to-back launches (one event pair, so small kernels are not
+ * dominated by per-launch event overhead). */
+int sv_timer_begin(sv_ctx* ctx, void* stream);
+int sv_timer_end(sv_ctx* ctx, void* stream, double* ms);
 
 #ifdef __cplusplus
 }

@@ -128,6 +128,7 @@ struct sv_ctx {
     std::vector<HostEnt> hl_ent;
     bool hl_valid = false;
     hipEvent_t cev[8] = {};
+    hipEvent_t tmr[2] = {nullptr, nullptr};   // sv_timer_begin / sv_timer_end
     // SGBM: second stream + fork/join events for the vertical path beside the horizontal ones
     hipStream_t sg_aux = nullptr;
     hipEvent_t sg_ev[2] = {nullptr, nullptr};
@@ -658,6 +659,8 @@ void sv_destroy(sv_ctx* c) {
         if (c->scr_ev) (void)hipEventDestroy(c->scr_ev);
         if (c->xev) (void)hipEventDestroy(c->xev);
         for (auto e : c->cev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto e : c->tmr)
             if (e) (void)hipEventDestroy(e);
         if (c->sg_aux) {
             (void)hipStreamSynchronize(c->sg_aux);
@@ -2245,6 +2248,25 @@ int sv_profile_read(sv_ctx* c, int kernel, double* total_ms, long long* count) {
     c->prof_drain();
     if (total_ms) *total_ms = c->acc_ms[kernel];
     if (count) *count = c->cnt[kernel];
+    return 0;
+}
+
+int sv_timer_begin(sv_ctx* c, void* stream) {
+    SV_ENTER(c);
+    for (auto& e : c->tmr)
+        if (!e) SV_HIP(hipEventCreate(&e));
+    SV_HIP(hipEventRecord(c->tmr[0], pick(c, stream)));
+    return 0;
+}
+
+int sv_timer_end(sv_ctx* c, void* stream, double* ms) {
+    SV_ENTER(c);
+    if (!c->tmr[0] || !ms) return fail(SV_EINVAL, "sv_timer_end without sv_timer_begin");
+    SV_HIP(hipEventRecord(c->tmr[1], pick(c, stream)));
+    SV_HIP(hipEventSynchronize(c->tmr[1]));
+    float f = 0.f;
+    SV_HIP(hipEventElapsedTime(&f, c->tmr[0], c->tmr[1]));
+    *ms = f;
     return 0;
 }
 

@@ -34,7 +34,7 @@ EXPORTED = [
     "sv_hog_hist", "sv_gray_dev", "sv_disparity_dev", "sv_median_post_dev",
     "sv_depth_map_dev", "sv_harris_dev", "sv_hog_hist_dev", "sv_profile_enable",
     "sv_profile_read", "sv_profile_reset", "sv_disparity_rows", "sv_dev_alloc", "sv_dev_free",
-    "sv_copy_to_device", "sv_copy_to_host", "sv_host_register", "sv_host_unregister", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
+    "sv_copy_to_device", "sv_copy_to_host", "sv_host_register", "sv_host_unregister", "sv_timer_begin", "sv_timer_end", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
     "sv_depth_map_batch_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
     "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
     "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
@@ -167,6 +167,8 @@ def _declare(lib):
         "sv_copy_to_host": ([_vp, _vp, _vp, ctypes.c_uint64], _c_int),
         "sv_host_register": ([_vp, ctypes.c_uint64], _c_int),
         "sv_host_unregister": ([_vp], _c_int),
+        "sv_timer_begin": ([_vp, _vp], _c_int),
+        "sv_timer_end": ([_vp, _vp, ctypes.POINTER(ctypes.c_double)], _c_int),
         "sv_disparity_batch_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, ctypes.c_int64,
                                     _c_int, _c_int, _c_int, _c_int, _vp, _c_int, ctypes.c_int64,
                                     _vp], _c_int),
@@ -888,6 +890,15 @@ class Engine:
         return ol, orr
 
     # -- profiling ------------------------------------------------------------------------
+    def timer_begin(self, stream: int = 0):
+        _check("sv_timer_begin", self.lib.sv_timer_begin(self._h, stream or None))
+
+    def timer_end(self, stream: int = 0) -> float:
+        """Device milliseconds since the matching timer_begin on the same stream."""
+        ms = ctypes.c_double()
+        _check("sv_timer_end", self.lib.sv_timer_end(self._h, stream or None, ctypes.byref(ms)))
+        return ms.value
+
     def profile(self, on: bool = True):
         _check("sv_profile_enable", self.lib.sv_profile_enable(self._h, 1 if on else 0))
 

@@ -340,3 +340,42 @@ def test_gpu_dropin_loaders_and_rectification(tmp_path):
     ol3, _ = fused_depth_map.apply_stereo_rectification(bl, br, cs)
     np.testing.assert_array_equal(ol3, RO.remap_linear(RO.resize_linear(bl, 160, 120),
                                                        cs["left_map1"], cs["left_map2"]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size", [(1920, 1080), (1001, 397)])
+def test_gpu_remap_staged_tiles_and_fallback_blocks(engine, size):
+    """k_remap stages each 64x16 output tile's source footprint in LDS when it fits and reads
+    its taps from global memory otherwise.  Calibrated maps (small footprints: staged), a
+    band of invalid map entries (huge footprints: those blocks fall back), ragged edge tiles,
+    BGR and gray sources, the fused gray output over a batch — all bit-exact."""
+    W, H = size
+    K1, D1, K2, D2, R, T = _stereo_setup(4, size)
+    R1, R2, P1, P2, Q, _, _ = calib.stereo_rectify(K1, D1, K2, D2, size, R, T, alpha=0)
+    m1, m2, _, _ = RO.undistort_rectify_map(K1, D1, R1, P1, W, H)
+    m1 = m1.copy()
+    m1[H // 3:H // 3 + 5, W // 4:W // 4 + 70] = (-32768, 32767)     # invalid entries
+    m1[-7:, -3:] = (W + 500, -400)                                  # far outside the image
+    rng = np.random.default_rng(W)
+    bgr = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    gray = np.ascontiguousarray(bgr[..., 1])
+    np.testing.assert_array_equal(engine.remap(bgr, m1, m2), RO.remap_linear(bgr, m1, m2))
+    np.testing.assert_array_equal(engine.remap(gray, m1, m2), RO.remap_linear(gray, m1, m2))
+    nf = 2
+    frames = np.stack([bgr, bgr[::-1].copy()])
+    d_src = engine.dev_alloc(frames.nbytes)
+    d_m1 = engine.dev_alloc(m1.nbytes)
+    d_m2 = engine.dev_alloc(m2.nbytes)
+    d_out = engine.dev_alloc(nf * H * W)
+    try:
+        engine.to_device(d_src, frames)
+        engine.to_device(d_m1, np.ascontiguousarray(m1))
+        engine.to_device(d_m2, np.ascontiguousarray(m2))
+        engine.remap_dev(d_src, H, W, 3, 3 * W, d_m1, d_m2, H, W, d_out, W, gray_out=True,
+                         n_frames=nf, src_frame_stride=3 * H * W, dst_frame_stride=H * W)
+        got = engine.to_host(d_out, (nf, H, W), np.uint8)
+    finally:
+        for p in (d_src, d_m1, d_m2, d_out):
+            engine.dev_free(p)
+    for z in range(nf):
+        np.testing.assert_array_equal(got[z], RO.remap_gray(frames[z], m1, m2))

@@ -779,8 +779,11 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     const int S = a.segm;                               // segment width per group (multiple of 4)
     const int WC = (64 >> a.lpg_log2) * S;
     constexpr int U = 4 * W2;                           // steps per unrolled body
-    const int nit = (S + 2 * R + U - 1) / U;            // bodies per segment (2r warm-up steps)
-    const int Tn = nit * U;
+    // steps per segment: S outputs + 2r warm-up, in chunks of 4; whole bodies of U steps,
+    // the first body entered at chunk e0 (its first e0 chunks skipped)
+    const int Tn = (S + 2 * R + 3) & ~3;
+    const int nit = (Tn + U - 1) / U;
+    const int e0 = (nit * U - Tn) >> 2;
     const int NL = WC - S + Tn + 1;                      // + the L prefetch past the last step
     const int NRlog = WC - S + Tn + 4 * LPG;
     constexpr int c0 = 1;                               // chunk starts (index = 3 mod 4) meet slot gaps
@@ -835,9 +838,11 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     Pk<NW> rn[RG_DPL];
 #pragma unroll
     for (int s = 1; s < RG_DPL; ++s) rn[RG_DPL - s] = ld<COST_SAD4, R, true>(Rp + rslot(iR0 - s, c0, RG_DPL));
-    PackPtr<COST_SAD4, R> rb = Rp + rslot(iR0, c0, RG_DPL);
-    PackPtr<COST_SAD4, R> lb = Lp + g * S;
-    Pk<NW> Lnext = ld<COST_SAD4, R, true>(lb);
+    // pointers of body position 0 (chunk e0 of the first body is step 0; the skipped chunks'
+    // offsets are never dereferenced)
+    PackPtr<COST_SAD4, R> rb = Rp + (rslot(iR0, c0, RG_DPL) - e0 * (RG_DPL + 1));
+    PackPtr<COST_SAD4, R> lb = Lp + (g * S - 4 * e0);
+    Pk<NW> Lnext = ld<COST_SAD4, R, true>(lb + 4 * e0);
     // after the reduce-scatter lane l's key is (row jq, step ju) of the chunk; the first 16
     // lanes of a group emit
     // (32-bit per-lane state only: output offset of step 0 and the emit window)
@@ -848,11 +853,12 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFFF, 0x00020000);
     const int emax = (l < 16 && (l & 1) == 0 && y + jq < a.row1) ? max(0, min(S, a.X1 - xs)) : 0;
 
-    // whole bodies of U = 4*W2 steps (the host picks S so that S + 2r fits nit bodies with
-    // at most 3 idle steps): no exits inside a body, so the rings never need copies
-    for (int it = 0, t0 = 0; it < nit; ++it) {
+    // whole bodies of U = 4*W2 steps, no exits inside a body (an exit per chunk made LLVM
+    // shuffle the rings); the first body skips its first e0 chunks by a uniform branch
+    for (int it = 0, t0 = -4 * e0; it < nit; ++it) {
 #pragma unroll
         for (int ch = 0; ch < W2; ++ch, t0 += 4) {
+            if (t0 < 0) continue;            // the first body's skipped chunks (uniform)
             uint32_t bk[4][2];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -884,7 +890,8 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) bk[q][u & 1] = min(min(h[0][q], h[1][q]), min(h[2][q], h[3][q]));
                 __builtin_amdgcn_sched_barrier(0);
-                if (u & 1) {   // steps u-1, u: 8 keys (row q, step j) at v[2q + j]
+                if ((u & 1) && t0 + u >= 2 * R) {   // steps u-1, u: 8 keys (row q, step j) at v[2q + j]
+                    // (pairs wholly inside the 2r warm-up steps emit nothing: skipped)
                     uint32_t v[8];
 #pragma unroll
                     for (int i = 0; i < 8; ++i) v[i] = bk[i >> 1][i & 1];
@@ -993,38 +1000,35 @@ bool ring_kind(int cost, int win, int num_disp) {
         const char* e = std::getenv("SV_RING");
         return !(e && e[0] == '0');
     }();
-    return on && kind_of(cost, win) == COST_SAD4 && win >= 5 && win <= 9 && num_disp <= 256;
+    return on && kind_of(cost, win) == COST_SAD4 && win >= 5 && win <= 11 && num_disp <= 256;
 }
 int ring_lpg(int num_disp) { return num_disp <= 64 ? 16 : num_disp <= 128 ? 32 : 64; }
-// Segment width per group: S = n*U - 2r rounded down to a multiple of 4 (U = 4*(2r+1) steps
-// per unrolled body, 2r warm-up steps).  n minimises the modelled run time: waves run in
-// rounds of 2048 (2 per SIMD), each wave n*U steps long, so time ~ ceil(waves / 2048) * n*U,
-// where the wave count covers the band (idle columns of the last wave per row), the 4-row
-// blocks and the frames; the segment's LDS must leave room for 2 waves per SIMD; ties go to
-// the longer segment.  SV_RING_SEG=<n> forces n (A/B measurements).
+// Segment width per group: S (a multiple of 4) minimising the steps all waves of a row
+// run, ceil(band / (G*S)) * (S + 2r) (idle columns of the last wave + the 2r warm-up steps
+// of every segment), among segments whose LDS leaves room for 2 waves per SIMD; ties go to
+// the longer segment.  SV_RING_SEG=<S> forces a width (A/B measurements).
 size_t ring_lds_bytes(int lpg, int seg, int r);
 int ring_seg(int lpg, int r, int band, long long blocks) {
     static const int env = [] {
         const char* e = std::getenv("SV_RING_SEG");
         const int v = e ? std::atoi(e) : 0;
-        return v >= 1 && v <= 16 ? v : 0;
+        return v >= 8 && v <= 1024 && v % 4 == 0 ? v : 0;
     }();
-    const int u = 4 * (2 * r + 1), G = 64 / lpg;
-    int best = 0;
+    (void)blocks;
+    if (env) return env;
+    const int G = 64 / lpg;
+    int best = 8;
     long long best_cost = -1;
-    for (int n = 1; n <= 8; ++n) {
-        const int S = (n * u - 2 * r) & ~3;
-        if (S < 8 || (n > 1 && ring_lds_bytes(lpg, S, r) > 20 * 1024)) continue;
-        const long long waves = (long long)((band + G * S - 1) / (G * S)) * blocks;
-        const long long cost = (waves + 2047) / 2048 * n * u;
-        if (env ? n == env : (best_cost < 0 || cost <= best_cost)) { best = S; best_cost = cost; }
+    for (int S = 8; S <= 1024; S += 4) {
+        if (S > 8 && ring_lds_bytes(lpg, S, r) > 20 * 1024) break;
+        const long long cost = (long long)((band + G * S - 1) / (G * S)) * ((S + 2 * r + 3) & ~3);
+        if (best_cost < 0 || cost <= best_cost) { best = S; best_cost = cost; }
     }
     return best;
 }
 size_t ring_lds_bytes(int lpg, int seg, int r) {
     const int wc = (64 / lpg) * seg;
-    const int u = 4 * (2 * r + 1);
-    const int tn = (seg + 2 * r + u - 1) / u * u;
+    const int tn = (seg + 2 * r + 3) & ~3;
     const int nl = wc - seg + tn + 1, nr = wc - seg + tn + 4 * lpg;
     const int nrp = nr + (nr + 1) / RG_DPL + 1;
     return (size_t)(nl + nrp) * 24;

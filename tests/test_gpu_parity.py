@@ -66,10 +66,10 @@ def test_four_row_kind_every_height_and_window(engine, win, H):
                                       O.disparity16(L, R, min_disp, D, win))
 
 
-@pytest.mark.parametrize("win", [5, 7, 9])
+@pytest.mark.parametrize("win", [5, 7, 9, 11])
 @pytest.mark.parametrize("D", [4, 50, 64, 100, 127, 128, 200, 256])
 def test_ring_kind_disparity_counts(engine, D, win):
-    """The cost-ring SAD kind (win 5..9, D <= 256): lanes of 4 disparities with padding
+    """The cost-ring SAD kind (win 5..11, D <= 256): lanes of 4 disparities with padding
     inside a lane (D % 4 != 0), 16/32/64 lanes per group, several segments per row and a
     ragged last segment, negative min_disp."""
     rng = np.random.default_rng(D * 10 + win)

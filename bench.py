@@ -139,7 +139,24 @@ def cpu_baseline(H, W, D, win, cost, seconds, harris=False):
 
     n, dt = rate(aff, seconds, 400)
     n1, dt1 = rate(1, max(1.0, seconds / 4), 20)
+    # the NumPy oracle (BASELINE.md's planned single-process baseline), on strips of 64
+    # output rows (+ the window's halo rows) of the same frame, scaled by the strip share
+    import sv_oracle as NO  # test infrastructure, used here only as the CPU baseline
+    r = win // 2
+    rows, ns, t0 = 64, 0, time.perf_counter()
+    while True:
+        y0 = (ns * rows) % max(1, H - rows - 2 * r)
+        NO.disparity16(L[0, y0:y0 + rows + 2 * r], R[0, y0:y0 + rows + 2 * r], 0, D, win, costi)
+        ns += 1
+        dts = time.perf_counter() - t0
+        if dts >= max(1.0, seconds / 4) or ns >= 40:
+            break
+    numpy_fps = ns * min(rows, H) / H / dts
     return {
+        "numpy_oracle_value": round(numpy_fps, 4),
+        "numpy_oracle_sample": f"{ns} strips of {rows}+{2 * r} rows x {W} (disparity only) of the "
+                               f"NumPy oracle (oracle/sv_oracle.py) in {dts:.1f} s, single process, "
+                               f"scaled by {rows}/{H} rows to frames/s",
         "value": round(n / dt, 3), "unit": "frames/s", "cores": aff, "kind": "port",
         "cpu_count": ncpu, "affinity_cores": aff,
         "single_thread_value": round(n1 / dt1, 4),

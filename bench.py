@@ -401,9 +401,12 @@ def main():
     ap.add_argument("--no-aux", action="store_true", help="skip the aux-kernel rooflines")
     ap.add_argument("--harris", action="store_true",
                     help="C2: also compute the Harris response of every left frame (k_harris)")
-    ap.add_argument("--dist-backend", default="auto", choices=["auto", "rccl", "host"],
-                    help="one-process-per-GPU launch: RCCL (auto falls back to the file store "
-                         "when ranks share a GPU)")
+    ap.add_argument("--dist-backend", default=None, choices=["auto", "rccl", "host"],
+                    help="one-process-per-GPU launch: RCCL or the node-local file store (auto: "
+                         "RCCL unless ranks share a GPU).  Default: auto when a step has a "
+                         "collective (--gather, --mode rowtile); otherwise host, since the "
+                         "frame-sharded path exchanges nothing and the run then needs only the "
+                         "start/end barriers and the max-over-ranks of the elapsed time")
     ap.add_argument("--no-live-pmc", action="store_true", help="skip the rocprofv3 PMC passes")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host_path measurement")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -416,7 +419,8 @@ def main():
     pg = None
     if launched:
         from stereovision_amd.distributed import init_process_group
-        pg = init_process_group(backend=args.dist_backend)
+        backend = args.dist_backend or ("auto" if (args.gather or args.mode == "rowtile") else "host")
+        pg = init_process_group(backend=backend)
         rank, world = pg.rank, pg.world
         devices = [pg.device]
     else:
@@ -538,9 +542,9 @@ def main():
             eng.profile(not args.no_profile)
         step(i)
     sync_all()
+    elapsed = time.perf_counter() - t0     # this rank's; the max over ranks is the run's
     if pg is not None:
         pg.barrier()
-    elapsed = time.perf_counter() - t0
 
     eng.profile(False)
     match_ms, match_n = eng.profile_read("sgbm" if args.cost == "sgbm" else "match")

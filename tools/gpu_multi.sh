@@ -7,7 +7,7 @@ run() {
   local name=$1; shift
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
       --master-addr 127.0.0.1 --master-port ${PORT:-29511} bench.py --gpus 2 --steps 100 \
-      --warmup 10 --dist-backend auto --no-cpu-baseline --no-host-path --no-live-pmc --no-aux "$@" > "gpurun_out/$name.log" 2>&1
+      --warmup 10 --no-cpu-baseline --no-host-path --no-live-pmc --no-aux "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc"; grep -E '^\{' "gpurun_out/$name.log" || tail -n 20 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

@@ -763,11 +763,24 @@ __global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) 
 // start at cost 0x8000, above every real window cost (<= 121*255 = 30855 for win 11).
 constexpr int RG_DPL = 4;
 
+// two u16 lanes of a word (v_pk_add_u16 / v_pk_sub_u16, wrapping mod 2^16)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
+}
+
 template <int R>
 __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     using P = PackCfg<COST_SAD4, R>;
     constexpr int NW = P::NW, NC = P::NC, W2 = 2 * R + 1;
-    static_assert(P::SPLIT && P::CW == 2, "ring kind expects 24-byte split packs");
+    // PK (r 6..7): window and column costs of rows 2j, 2j+1 share a register as two u16
+    // (a window costs at most 57375), updated with v_pk_add/sub_u16: 15 ring steps x 16
+    // cells fit in 120 VGPRs; the argmin keys (cost << 16) | idx are built per step
+    constexpr bool PK = R >= 6;
+    static_assert(P::SPLIT && (P::CW == 2) != PK, "ring kind expects split packs (24 B; 32 B for r 6..7)");
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     if (blockIdx.z) {   // frame batch
         a.L += blockIdx.z * a.fs_in;
@@ -819,22 +832,29 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     const int l = lane & (LPG - 1);
     const int xs = xw + g * S;                          // first output column of the segment
     // step t enters column xs - r + t; lane l, disparity idx 4l + k reads R index iR0 + t - k
-    const int iR0 = g * S + 4 * (LPG - 1 - l) + 3;
-    uint32_t h[RG_DPL][4];
+    // r <= 5: padding disparities (idx >= D) start at cost 0x8000, above any real window.
+    // r 6..7 (window costs up to 57375, no headroom; D a multiple of 4): padding lanes
+    // re-match the last real group D-4..D-1 under their own, larger labels, so on equal
+    // costs the real lane wins every tie
+    const int dl = PK ? min(4 * l, a.D - 4) : 4 * l;
+    const int iR0 = g * S + 4 * (LPG - 1) - dl + 3;
+    constexpr int RQ = PK ? 2 : 4;                      // cost words per k (h and ring slots)
+    uint32_t h[RG_DPL][RQ], lab[RG_DPL];
 #pragma unroll
     for (int k = 0; k < RG_DPL; ++k) {
         const int idx = 4 * l + k;
-        const uint32_t base = idx < a.D ? (uint32_t)idx : (0x8000u << 16) | (uint32_t)idx;
+        const uint32_t base = PK ? 0u : idx < a.D ? (uint32_t)idx : (0x8000u << 16) | (uint32_t)idx;
+        lab[k] = (uint32_t)idx;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) h[k][q] = base;
+        for (int q = 0; q < RQ; ++q) h[k][q] = base;
     }
-    uint32_t ring[W2][RG_DPL][4];
+    uint32_t ring[W2][RG_DPL][RQ];
 #pragma unroll
     for (int s = 0; s < W2; ++s)
 #pragma unroll
         for (int k = 0; k < RG_DPL; ++k)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) ring[s][k][q] = 0u;
+            for (int q = 0; q < RQ; ++q) ring[s][k][q] = 0u;
     Pk<NW> rn[RG_DPL];
 #pragma unroll
     for (int s = 1; s < RG_DPL; ++s) rn[RG_DPL - s] = ld<COST_SAD4, R, true>(Rp + rslot(iR0 - s, c0, RG_DPL));
@@ -872,23 +892,47 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
 #pragma unroll
                 for (int k = 0; k < RG_DPL; ++k)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) h[k][q] -= ring[slot][k][q];
+                    for (int q = 0; q < RQ; ++q)
+                        h[k][q] = PK ? pk_sub16(h[k][q], ring[slot][k][q]) : h[k][q] - ring[slot][k][q];
 #pragma unroll
                 for (int kk = 0; kk < RG_DPL; ++kk) {
                     const int k = RG_DPL - 1 - kk;
                     const Pk<NW>& Rk = rn[(u - k) & 3];
-                    uint32_t cn = 0u;
+                    if constexpr (PK) {
+                        // common rows once, in both halves; row 2j's sad in the low half,
+                        // row 2j+1's in the high half
+                        uint32_t cn = 0u;
 #pragma unroll
-                    for (int i = 0; i < NC; ++i) cn = __builtin_amdgcn_sad_hi_u8(Lc.w[i], Rk.w[i], cn);
+                        for (int i = 0; i < NC; ++i) cn = __builtin_amdgcn_sad_u8(Lc.w[i], Rk.w[i], cn);
+                        cn |= cn << 16;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const uint32_t c = __builtin_amdgcn_sad_hi_u8(Lc.w[NC + q], Rk.w[NC + q], cn);
-                        h[k][q] += c;
-                        ring[slot][k][q] = c;
+                        for (int j = 0; j < 2; ++j) {
+                            const uint32_t c = __builtin_amdgcn_sad_hi_u8(
+                                Lc.w[NC + 2 * j + 1], Rk.w[NC + 2 * j + 1],
+                                __builtin_amdgcn_sad_u8(Lc.w[NC + 2 * j], Rk.w[NC + 2 * j], cn));
+                            h[k][j] = pk_add16(h[k][j], c);
+                            ring[slot][k][j] = c;
+                        }
+                    } else {
+                        uint32_t cn = 0u;
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) cn = __builtin_amdgcn_sad_hi_u8(Lc.w[i], Rk.w[i], cn);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const uint32_t c = __builtin_amdgcn_sad_hi_u8(Lc.w[NC + q], Rk.w[NC + q], cn);
+                            h[k][q] += c;
+                            ring[slot][k][q] = c;
+                        }
                     }
                 }
 #pragma unroll
-                for (int q = 0; q < 4; ++q) bk[q][u & 1] = min(min(h[0][q], h[1][q]), min(h[2][q], h[3][q]));
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t kq[RG_DPL];
+#pragma unroll
+                    for (int k = 0; k < RG_DPL; ++k)
+                        kq[k] = !PK ? h[k][q] : (q & 1) ? (h[k][q >> 1] & 0xFFFF0000u) | lab[k] : (h[k][q >> 1] << 16) | lab[k];
+                    bk[q][u & 1] = min(min(kq[0], kq[1]), min(kq[2], kq[3]));
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 if ((u & 1) && t0 + u >= 2 * R) {   // steps u-1, u: 8 keys (row q, step j) at v[2q + j]
                     // (pairs wholly inside the 2r warm-up steps emit nothing: skipped)
@@ -1000,7 +1044,8 @@ bool ring_kind(int cost, int win, int num_disp) {
         const char* e = std::getenv("SV_RING");
         return !(e && e[0] == '0');
     }();
-    return on && kind_of(cost, win) == COST_SAD4 && win >= 5 && win <= 11 && num_disp <= 256;
+    return on && kind_of(cost, win) == COST_SAD4 && win >= 5 && num_disp <= 256 &&
+           (win <= 11 || (win <= 15 && num_disp % 4 == 0));
 }
 int ring_lpg(int num_disp) { return num_disp <= 64 ? 16 : num_disp <= 128 ? 32 : 64; }
 // Segment width per group: S (a multiple of 4) minimising the steps all waves of a row
@@ -1031,7 +1076,7 @@ size_t ring_lds_bytes(int lpg, int seg, int r) {
     const int tn = (seg + 2 * r + 3) & ~3;
     const int nl = wc - seg + tn + 1, nr = wc - seg + tn + 4 * lpg;
     const int nrp = nr + (nr + 1) / RG_DPL + 1;
-    return (size_t)(nl + nrp) * 24;
+    return (size_t)(nl + nrp) * (r <= 5 ? 24 : 32);
 }
 
 template <int R>
@@ -1060,6 +1105,8 @@ int launch_ring(const MatchParams& a0, hipStream_t s) {
         case 3: return launch_ring_r<3>(a, lds, s);
         case 4: return launch_ring_r<4>(a, lds, s);
         case 5: return launch_ring_r<5>(a, lds, s);
+        case 6: return launch_ring_r<6>(a, lds, s);
+        case 7: return launch_ring_r<7>(a, lds, s);
     }
     return (int)hipErrorInvalidValue;
 }

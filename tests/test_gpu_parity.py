@@ -66,12 +66,13 @@ def test_four_row_kind_every_height_and_window(engine, win, H):
                                       O.disparity16(L, R, min_disp, D, win))
 
 
-@pytest.mark.parametrize("win", [5, 7, 9, 11])
+@pytest.mark.parametrize("win", [5, 7, 9, 11, 13, 15])
 @pytest.mark.parametrize("D", [4, 50, 64, 100, 127, 128, 200, 256])
 def test_ring_kind_disparity_counts(engine, D, win):
-    """The cost-ring SAD kind (win 5..11, D <= 256): lanes of 4 disparities with padding
-    inside a lane (D % 4 != 0), 16/32/64 lanes per group, several segments per row and a
-    ragged last segment, negative min_disp."""
+    """The cost-ring SAD kind (win 5..11, D <= 256; win 13/15 with D % 4 == 0 and a ring of
+    16-bit packed column costs): lanes of 4 disparities with padding inside a lane
+    (D % 4 != 0), padding lanes re-matching the last group (win 13/15), 16/32/64 lanes per
+    group, several segments per row and a ragged last segment, negative min_disp."""
     rng = np.random.default_rng(D * 10 + win)
     H, W = 11, 1333
     L = rng.integers(0, 256, (H, W), dtype=np.uint8)
@@ -96,11 +97,21 @@ def test_flat_images_tie_to_min_disp(engine):
     assert (got[:, 52:] == 4 * 16).all()
 
 
+@pytest.mark.parametrize("D,win", [(200, 15), (68, 13), (256, 15)])
+def test_ring_packed_ties_go_to_the_real_lowest_disparity(engine, D, win):
+    # flat images: every disparity ties, including the padding lanes' re-matched group
+    L = np.full((21, 700), 140, np.uint8)
+    got = engine.disparity(L, L.copy(), -2, D, win)
+    np.testing.assert_array_equal(got, O.disparity16(L, L, -2, D, win))
+    valid = got != -3 * 16
+    assert valid.sum() > 0 and (got[valid] == -2 * 16).all()
+
+
 def test_extreme_contrast_no_overflow(engine):
     # alternating 0/255 columns make every SAD/SSD tap maximal
     L = np.tile(np.array([0, 255], np.uint8), (24, 160))
     R = np.roll(L, 1, axis=1)
-    for cost, D, win in [("sad", 128, 15), ("ssd", 256, 15), ("ssd", 64, 15)]:
+    for cost, D, win in [("sad", 128, 15), ("sad", 256, 15), ("sad", 64, 13), ("ssd", 256, 15), ("ssd", 64, 15)]:
         np.testing.assert_array_equal(engine.disparity(L, R, 0, D, win, cost),
                                       C.disparity16(L, R, 0, D, win, 0 if cost == "sad" else 1))
 

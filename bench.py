@@ -48,7 +48,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from stereovision_amd.engine import (Communicator, device_count, depth_map_rows_multi,  # noqa: E402
+from stereovision_amd.engine import (Communicator, Engine, device_count, depth_map_rows_multi,  # noqa: E402
                                      get_engine, multi_gpu_depth_map_dev)
 from stereovision_amd.synthetic import stereo_batch, stereo_pair, synthetic_calibration, to_bgr  # noqa: E402
 
@@ -398,6 +398,10 @@ def main():
     ap.add_argument("--rectify", action="store_true",
                     help="camera pipeline: raw BGR frames resident in HBM -> rectify+gray "
                          "(k_remap, calibrated CV_16SC2 maps) -> disparity -> median/post")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="frames mode: contexts (HIP streams) per GPU that consecutive steps "
+                         "alternate over, so one step's median/post overlaps the next step's "
+                         "k_match (separate output buffers per stream)")
     ap.add_argument("--no-aux", action="store_true", help="skip the aux-kernel rooflines")
     ap.add_argument("--harris", action="store_true",
                     help="C2: also compute the Harris response of every left frame (k_harris)")
@@ -463,6 +467,13 @@ def main():
     depth = [a.alloc(4 * n_px * out_frames) for a in arenas]
     disp = [a.alloc(4 * n_px * out_frames) for a in arenas]
     norm = [a.alloc(n_px * out_frames) for a in arenas]
+    # --streams S: S-1 extra contexts per GPU (own stream, own outputs) that steps alternate over
+    nstreams = max(1, args.streams) if not (rowtile or args.rectify or args.gather or args.harris) else 1
+    lanes = [(engines, depth, disp, norm)]
+    for _ in range(nstreams - 1):
+        lanes.append(([Engine(d) for d in devices], [a.alloc(4 * n_px * out_frames) for a in arenas],
+                      [a.alloc(4 * n_px * out_frames) for a in arenas], [a.alloc(n_px * out_frames) for a in arenas]))
+    all_engines = [e for ln in lanes for e in ln[0]]
     if rectify:
         rect = make_rectifier(eng, W, H)
         gL, gR = arenas[0].alloc(B * n_px), arenas[0].alloc(B * n_px)
@@ -500,7 +511,8 @@ def main():
                                     [p + f * n_px for p in dR], [B] * len(engines), H, W, W, n_px,
                                     0, D, win, 0.3, 2.0, depth[0], disp[0], norm[0], cost=args.cost)
             return
-        for k, e in enumerate(engines):
+        engs, depth_o, disp_o, norm_o = lanes[i % nstreams]
+        for k, e in enumerate(engs):
             if rectify:
                 for src, m1, m2, g in ((dL[k], m1l, m2l, gL), (dR[k], m1r, m2r, gR)):
                     e.remap_dev(src + f * 3 * n_px, H, W, 3, 3 * W, m1, m2, H, W, g, W,
@@ -510,10 +522,10 @@ def main():
                                       disp[k], norm[k], cost=args.cost)
             elif B == 1:
                 e.depth_map_dev(dL[k] + f * n_px, dR[k] + f * n_px, H, W, W, 0, D, win, 0.3, 2.0,
-                                depth[k], disp[k], norm[k], cost=args.cost)
+                                depth_o[k], disp_o[k], norm_o[k], cost=args.cost)
             else:
                 e.depth_map_batch_dev(dL[k] + f * n_px, dR[k] + f * n_px, B, H, W, W, n_px, 0, D, win,
-                                      0.3, 2.0, depth[k], disp[k], norm[k], cost=args.cost)
+                                      0.3, 2.0, depth_o[k], disp_o[k], norm_o[k], cost=args.cost)
             if harris:      # one launch over the batch's left frames
                 e.harris_batch_dev(gL if rectify else dL[k] + f * n_px, B, H, W, W, n_px, hmaps[k])
         if launched and args.gather and world > 1:
@@ -521,7 +533,7 @@ def main():
             gather_frames(pg, disp[0], B, gather_frames_d or 0, 4 * n_px, stream=eng.stream)
 
     def sync_all():
-        for e in engines:
+        for e in all_engines:
             e.synchronize()
 
     for i in range(args.warmup):

@@ -10,6 +10,7 @@
 //  * k_post        the post-processing alone on an f32 disparity
 // All are HBM-bound stencils: LDS tiles with halos, one read and one write per pixel.
 // Built with -ffp-contract=off so every f32 operation rounds exactly like NumPy's.
+#include <cstdlib>
 #include <type_traits>
 #include "sv_internal.h"
 #include "sv_median_net.h"
@@ -209,6 +210,153 @@ __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g,
                 for (int q = 0; q < 4 && x + q < W; ++q)
 #pragma unroll
                     for (int kk = 0; kk < 5; ++kk) dst[q * 5 + kk] = o[q][kk];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// HOG window histograms, strip form: one wave = 64 consecutive (clamped) columns walking down
+// HS rows; lane j outputs column x0 + j - r for j in [r, 63 - r].  Per row step each lane
+// codes its pixel (bin, magnitude), the row's one-hot records are prefix-summed across the
+// wave by DPP (packed u16 halves: a row prefix is <= 64 * 255, so 32-bit adds never carry
+// between halves), the horizontal window sum is P(j + r) - P(j - r - 1) (two ds_bpermute),
+// and the vertical window sum runs over a register ring of the last 2r+1 row sums (<= 57,375
+// per bin).  No LDS tiles; a row's 50..64 records (contiguous in HBM) are staged in 1.3 KB of
+// LDS and leave as 16-byte stores.  4K, r = 7: 122 us (64x16 LDS tiles) -> 94 us per image.
+constexpr int HS_ROWS = 64, HS_PD = 1;
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t v) {   // v + (lane shifted by CTRL, else 0)
+    return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL, int ROWM>
+__device__ __forceinline__ uint32_t dpp_add_rm(uint32_t v) {
+    return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWM, 0xF, false);
+}
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+template <int r>
+__global__ __launch_bounds__(64) void k_hog_hist_strip(const uint8_t* __restrict__ g, int H, int W, int pitch,
+                                                       int row0, int row1, uint16_t* __restrict__ hist, int hs_rows) {
+    constexpr int W2 = 2 * r + 1, NOUT = 64 - 2 * r;
+    const int lane = threadIdx.x;
+    const int x0 = blockIdx.x * NOUT;                    // first output column of the strip
+    const int ys = row0 + blockIdx.y * hs_rows;          // first output row
+    const int ye = min(ys + hs_rows, row1);
+    const int xx = clampi(x0 - r + lane, 0, W - 1);      // this lane's (clamped) window column
+    const int xm = refl101(xx - 1, W), xp = refl101(xx + 1, W);
+    const int src_hi = (lane + r) << 2, src_lo = (lane - r - 1) << 2;   // bpermute byte addresses
+    const uint32_t lo_mask = lane >= r + 1 ? ~0u : 0u;    // P(j - r - 1) = 0 left of the wave
+    const int xo = x0 + lane - r;
+    const bool out_lane = lane >= r && lane < 64 - r && xo < W;
+    const auto hdst = __builtin_amdgcn_make_buffer_rsrc(hist, 0, 0x7FFFFFFF, 0x00020000);
+    const int nbytes = 20 * min(NOUT, W - x0);           // the strip's record bytes per row
+    __shared__ __attribute__((aligned(16))) uint32_t stage[64 * 5 + 4];
+    // byte loads through one descriptor: uniform row offset + per-lane column (no 64-bit
+    // per-lane address arithmetic)
+    const auto gsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(g), 0, 0x7FFFFFFF, 0x00020000);
+
+    uint32_t ring[W2][5], V[5];
+#pragma unroll
+    for (int s = 0; s < W2; ++s)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) ring[s][k] = 0u;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) V[k] = 0u;
+
+    // step t codes row ys - r + t (clamped) and, from t = 2r on, emits output row ys + t - 2r;
+    // its 8 neighbourhood bytes are loaded HS_PD steps ahead (measured: 1 step 94.9 us per
+    // 4K image, 3 steps 98.7; loading 3 bytes instead of 8 gained 2 us: the step's DPP/LDS
+    // chain, not the loads, sets the pace at ~2.5 waves per SIMD)
+    const int nsteps = ye - ys + 2 * r;
+    auto load_step = [&](int t, int (&n)[8]) {
+        const int c = clampi(ys - r + t, 0, H - 1);
+        const int om = refl101(c - 1, H) * pitch, oc = c * pitch, op = refl101(c + 1, H) * pitch;
+        auto ldb = [&](int col, int row) { return (int)__builtin_amdgcn_raw_buffer_load_b8(gsrc, col, row, 0); };
+        n[0] = ldb(xm, om); n[1] = ldb(xx, om); n[2] = ldb(xp, om);
+        n[3] = ldb(xm, oc); n[4] = ldb(xp, oc);
+        n[5] = ldb(xm, op); n[6] = ldb(xx, op); n[7] = ldb(xp, op);
+    };
+    int nb[HS_PD][8];
+#pragma unroll
+    for (int d = 0; d < HS_PD; ++d) load_step(d, nb[d]);
+    for (int t0 = 0; t0 < nsteps; t0 += W2) {
+#pragma unroll
+        for (int u = 0; u < W2; ++u) {
+            const int t = t0 + u;
+            if (t >= nsteps) break;
+            const int a00 = nb[0][0], a01 = nb[0][1], a02 = nb[0][2], a10 = nb[0][3], a12 = nb[0][4];
+            const int a20 = nb[0][5], a21 = nb[0][6], a22 = nb[0][7];
+#pragma unroll
+            for (int d = 0; d + 1 < HS_PD; ++d)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) nb[d][i] = nb[d + 1][i];
+            load_step(t + HS_PD, nb[HS_PD - 1]);
+            int gx = (a02 + 2 * a12 + a22) - (a00 + 2 * a10 + a20);
+            int gy = (a20 + 2 * a21 + a22) - (a00 + 2 * a01 + a02);
+            const uint32_t m = (uint32_t)(abs(gx) + abs(gy)) >> 3;
+            if (gy < 0 || (gy == 0 && gx < 0)) { gx = -gx; gy = -gy; }
+            int b = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int cy = kHogCos[k] * gy, sx = kHogSin[k] * gx;
+                b += (cy >= sx) + (-cy >= sx);
+            }
+            const uint32_t w = m << ((b & 1) << 4);
+            const uint32_t sel = 1u << (b >> 1);          // dword of the bin, one-hot
+            const int slot = u;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) V[k] -= ring[slot][k];   // the leaving row, first: the
+            uint32_t p[5];                                          // new sum then takes its registers
+#pragma unroll
+            for (int k = 0; k < 5; ++k) p[k] = w & (uint32_t)(((int)(sel << (31 - k))) >> 31);
+            // inclusive prefix over the wave: row_shr 1, 2, 4, 8, then row_bcast 15 / 31
+            // (the five dwords interleaved: no DPP read right after its VALU write)
+#pragma unroll
+            for (int k = 0; k < 5; ++k) p[k] = dpp_add<0x111>(p[k]);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) p[k] = dpp_add<0x112>(p[k]);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) p[k] = dpp_add<0x114>(p[k]);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) p[k] = dpp_add<0x118>(p[k]);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) p[k] = dpp_add_rm<0x142, 0xA>(p[k]);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) p[k] = dpp_add_rm<0x143, 0xC>(p[k]);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_hi, (int)p[k]);
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lo, (int)p[k]);
+                ring[slot][k] = hi - (lo & lo_mask);
+                V[k] += ring[slot][k];
+            }
+            if (t >= 2 * r) {
+                // the strip's records are contiguous in the row: stage them in LDS and leave
+                // as 16-byte stores (20-byte-strided dword stores: 5 partial-line writes each)
+                // (16-byte stores must be 16-byte aligned: the staging starts at the row
+                // start's alignment ra, lane j stores absolute-aligned bytes [16j, 16j+16) of
+                // the staged run, edge lanes dword by dword)
+                const int rs = (ys + t - 2 * r) * W * 20 + x0 * 20;
+                const int ra = rs & 15, ro = rs - ra;
+                if (out_lane)
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) stage[(ra >> 2) + (lane - r) * 5 + k] = V[k];
+                __syncthreads();   // (one wave: orders the staging, fences the compiler)
+                const int e = ra + nbytes;                  // <= 12 + 64 * 20: up to 81 chunks
+                for (int b0 = 16 * lane; b0 < e; b0 += 16 * 64) {
+                    const int b1 = b0 + 16;
+                    if (b0 >= ra && b1 <= e) {
+                        const v4u q = *reinterpret_cast<const v4u*>(stage + (b0 >> 2));
+                        __builtin_amdgcn_raw_buffer_store_b128(q, hdst, b0, ro, 0);
+                    } else if (b1 > ra) {
+                        for (int o = max(b0, ra); o < min(b1, e); o += 4)
+                            __builtin_amdgcn_raw_buffer_store_b32(stage[o >> 2], hdst, o, ro, 0);
+                    }
+                }
+                __syncthreads();
             }
         }
     }
@@ -496,6 +644,25 @@ int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0
     if (row0 < 0) row0 = 0;
     if (row1 > H) row1 = H;
     if (row1 <= row0) return 0;
+    static const int strip = [] {
+        const char* e = std::getenv("SV_HOG_STRIP");
+        return e ? std::atoi(e) : 1;
+    }();
+    // (the strip kernel addresses through 32-bit buffer offsets)
+    if (strip && (long long)H * W * 20 < (1LL << 31) && (long long)H * pitch < (1LL << 31)) {
+        static const int hs_rows = [] {
+            const char* e = std::getenv("SV_HOG_ROWS");
+            const int v = e ? std::atoi(e) : 0;
+            return v >= 8 && v <= 4096 ? v : HS_ROWS;
+        }();
+        const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + hs_rows - 1) / hs_rows);
+        switch (r) {
+#define SV_HOG_S(R) case R: hipLaunchKernelGGL(k_hog_hist_strip<R>, grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows); break;
+            SV_HOG_S(0) SV_HOG_S(1) SV_HOG_S(2) SV_HOG_S(3) SV_HOG_S(4) SV_HOG_S(5) SV_HOG_S(6) SV_HOG_S(7)
+#undef SV_HOG_S
+        }
+        return (int)hipGetLastError();
+    }
     const dim3 grid((W + GT_W - 1) / GT_W, (row1 - row0 + GT_H - 1) / GT_H);
     switch (r) {
 #define SV_HOG_R(R) case R: hipLaunchKernelGGL(k_hog_hist<R>, grid, dim3(256), 0, s, g, H, W, pitch, row0, row1, hist); break;

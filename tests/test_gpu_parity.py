@@ -139,6 +139,17 @@ def test_hog_hist_matches_oracle(engine, win):
     np.testing.assert_array_equal(engine.hog_hist(L, win), O.hog_hist(L, win))
 
 
+@pytest.mark.parametrize("H,W,win", [(1, 1, 3), (2, 70, 15), (150, 211, 15), (131, 64, 13), (97, 130, 5),
+                                     (70, 51, 1), (65, 300, 7)])
+def test_hog_hist_strip_shapes(engine, H, W, win):
+    """The strip kernel: 64-lane column strips with 2r-column overlaps, 64-row strips,
+    images narrower than a strip or than the window, 1-pixel images (reflect-101 of size 1)."""
+    rng = np.random.default_rng(H * 1000 + W + win)
+    g = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    g[:, ::7] = 255                      # strong edges: large magnitudes in every bin
+    np.testing.assert_array_equal(engine.hog_hist(g, win), O.hog_hist(g, win))
+
+
 def test_harris_within_tolerance(engine):
     for H, W, seed in [(50, 70, 0), (1, 40, 1), (17, 1, 2), (128, 300, 3)]:
         rng = np.random.default_rng(seed)

@@ -733,6 +733,28 @@ __global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) 
                 continue;
             }
         }
+        if constexpr (ROWS * DPL == 8) {
+            // 8 keys (HOG, 1-row SAD/SSD with DPL 8, 2-row SAD2 with DPL 4): bank-masked
+            // reduce-scatter over each 16-lane row, then the rows of a group joined by
+            // permlane swaps; lanes 2i of the group's first row emit key i
+            uint32_t v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = bk[i / DPL][i % DPL];
+            reduce_scatter8_bm(v, lane & 15);
+            uint32_t key = v[0];
+            if (LPG >= 32) {
+                const auto p = __builtin_amdgcn_permlane16_swap(key, key, false, false);
+                key = min(p[0], p[1]);
+            }
+            if (LPG == 64) {
+                const auto p = __builtin_amdgcn_permlane32_swap(key, key, false, false);
+                key = min(p[0], p[1]);
+            }
+            const int i = (l >> 1) & 7, q = i / DPL, e = t0 + i % DPL + 1, x = xs + e;
+            if (l < 16 && (l & 1) == 0 && e < S && x < a.X1 && y + q < a.row1)
+                a.out[(size_t)(y + q) * a.opitch + x] = (int16_t)(((int)(key & dmask) + a.minD) * 16);
+            continue;
+        }
         const int e = t0 + j + 1;
         const int x = xs + e;
         const bool emit = j >= 0 && j < DPL && e < S && x < a.X1;

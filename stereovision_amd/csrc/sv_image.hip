@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g,
 // and the vertical window sum runs over a register ring of the last 2r+1 row sums (<= 57,375
 // per bin).  No LDS tiles; a row's 50..64 records (contiguous in HBM) are staged in 1.3 KB of
 // LDS and leave as 16-byte stores.  4K, r = 7: 122 us (64x16 LDS tiles) -> 94 us per image.
-constexpr int HS_ROWS = 64, HS_PD = 1;
+constexpr int HS_ROWS = 64;
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_add(uint32_t v) {   // v + (lane shifted by CTRL, else 0)
@@ -266,10 +266,9 @@ __global__ __launch_bounds__(64) void k_hog_hist_strip(const uint8_t* __restrict
 #pragma unroll
     for (int k = 0; k < 5; ++k) V[k] = 0u;
 
-    // step t codes row ys - r + t (clamped) and, from t = 2r on, emits output row ys + t - 2r;
-    // its 8 neighbourhood bytes are loaded HS_PD steps ahead (measured: 1 step 94.9 us per
-    // 4K image, 3 steps 98.7; loading 3 bytes instead of 8 gained 2 us: the step's DPP/LDS
-    // chain, not the loads, sets the pace at ~2.5 waves per SIMD)
+    // row t codes image row ys - r + t (clamped) and, from t = 2r on, emits output row
+    // ys + t - 2r; its 8 neighbourhood bytes are loaded one step ahead (3 steps ahead measured
+    // slower; loading 3 bytes instead of 8 gained 2 us: the DPP/LDS chain sets the pace)
     const int nsteps = ye - ys + 2 * r;
     auto load_step = [&](int t, int (&n)[8]) {
         const int c = clampi(ys - r + t, 0, H - 1);
@@ -279,84 +278,93 @@ __global__ __launch_bounds__(64) void k_hog_hist_strip(const uint8_t* __restrict
         n[3] = ldb(xm, oc); n[4] = ldb(xp, oc);
         n[5] = ldb(xm, op); n[6] = ldb(xx, op); n[7] = ldb(xp, op);
     };
-    int nb[HS_PD][8];
+    // two rows per step: their code / scan / bpermute chains are independent, so one wave
+    // keeps two in flight (the kernel is latency-bound at ~2.5 waves per SIMD)
+    constexpr int RP = 2;
+    int nb[RP][8];
 #pragma unroll
-    for (int d = 0; d < HS_PD; ++d) load_step(d, nb[d]);
-    for (int t0 = 0; t0 < nsteps; t0 += W2) {
+    for (int rr = 0; rr < RP; ++rr) load_step(rr, nb[rr]);
+    for (int t0 = 0; t0 < nsteps; t0 += RP * W2) {
 #pragma unroll
-        for (int u = 0; u < W2; ++u) {
-            const int t = t0 + u;
-            if (t >= nsteps) break;
-            const int a00 = nb[0][0], a01 = nb[0][1], a02 = nb[0][2], a10 = nb[0][3], a12 = nb[0][4];
-            const int a20 = nb[0][5], a21 = nb[0][6], a22 = nb[0][7];
+        for (int j = 0; j < W2; ++j) {
+            const int tb = t0 + RP * j;
+            if (tb >= nsteps) break;
+            uint32_t p[RP][5];
 #pragma unroll
-            for (int d = 0; d + 1 < HS_PD; ++d)
+            for (int rr = 0; rr < RP; ++rr) {
+                const int a00 = nb[rr][0], a01 = nb[rr][1], a02 = nb[rr][2], a10 = nb[rr][3], a12 = nb[rr][4];
+                const int a20 = nb[rr][5], a21 = nb[rr][6], a22 = nb[rr][7];
+                load_step(tb + RP + rr, nb[rr]);          // the next pair's bytes
+                int gx = (a02 + 2 * a12 + a22) - (a00 + 2 * a10 + a20);
+                int gy = (a20 + 2 * a21 + a22) - (a00 + 2 * a01 + a02);
+                const uint32_t m = (uint32_t)(abs(gx) + abs(gy)) >> 3;
+                if (gy < 0 || (gy == 0 && gx < 0)) { gx = -gx; gy = -gy; }
+                int b = 0;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) nb[d][i] = nb[d + 1][i];
-            load_step(t + HS_PD, nb[HS_PD - 1]);
-            int gx = (a02 + 2 * a12 + a22) - (a00 + 2 * a10 + a20);
-            int gy = (a20 + 2 * a21 + a22) - (a00 + 2 * a01 + a02);
-            const uint32_t m = (uint32_t)(abs(gx) + abs(gy)) >> 3;
-            if (gy < 0 || (gy == 0 && gx < 0)) { gx = -gx; gy = -gy; }
-            int b = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int cy = kHogCos[k] * gy, sx = kHogSin[k] * gx;
-                b += (cy >= sx) + (-cy >= sx);
-            }
-            const uint32_t w = m << ((b & 1) << 4);
-            const uint32_t sel = 1u << (b >> 1);          // dword of the bin, one-hot
-            const int slot = u;
-#pragma unroll
-            for (int k = 0; k < 5; ++k) V[k] -= ring[slot][k];   // the leaving row, first: the
-            uint32_t p[5];                                          // new sum then takes its registers
-#pragma unroll
-            for (int k = 0; k < 5; ++k) p[k] = w & (uint32_t)(((int)(sel << (31 - k))) >> 31);
-            // inclusive prefix over the wave: row_shr 1, 2, 4, 8, then row_bcast 15 / 31
-            // (the five dwords interleaved: no DPP read right after its VALU write)
-#pragma unroll
-            for (int k = 0; k < 5; ++k) p[k] = dpp_add<0x111>(p[k]);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) p[k] = dpp_add<0x112>(p[k]);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) p[k] = dpp_add<0x114>(p[k]);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) p[k] = dpp_add<0x118>(p[k]);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) p[k] = dpp_add_rm<0x142, 0xA>(p[k]);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) p[k] = dpp_add_rm<0x143, 0xC>(p[k]);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_hi, (int)p[k]);
-                const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lo, (int)p[k]);
-                ring[slot][k] = hi - (lo & lo_mask);
-                V[k] += ring[slot][k];
-            }
-            if (t >= 2 * r) {
-                // the strip's records are contiguous in the row: stage them in LDS and leave
-                // as 16-byte stores (20-byte-strided dword stores: 5 partial-line writes each)
-                // (16-byte stores must be 16-byte aligned: the staging starts at the row
-                // start's alignment ra, lane j stores absolute-aligned bytes [16j, 16j+16) of
-                // the staged run, edge lanes dword by dword)
-                const int rs = (ys + t - 2 * r) * W * 20 + x0 * 20;
-                const int ra = rs & 15, ro = rs - ra;
-                if (out_lane)
-#pragma unroll
-                    for (int k = 0; k < 5; ++k) stage[(ra >> 2) + (lane - r) * 5 + k] = V[k];
-                __syncthreads();   // (one wave: orders the staging, fences the compiler)
-                const int e = ra + nbytes;                  // <= 12 + 64 * 20: up to 81 chunks
-                for (int b0 = 16 * lane; b0 < e; b0 += 16 * 64) {
-                    const int b1 = b0 + 16;
-                    if (b0 >= ra && b1 <= e) {
-                        const v4u q = *reinterpret_cast<const v4u*>(stage + (b0 >> 2));
-                        __builtin_amdgcn_raw_buffer_store_b128(q, hdst, b0, ro, 0);
-                    } else if (b1 > ra) {
-                        for (int o = max(b0, ra); o < min(b1, e); o += 4)
-                            __builtin_amdgcn_raw_buffer_store_b32(stage[o >> 2], hdst, o, ro, 0);
-                    }
+                for (int k = 0; k < 4; ++k) {
+                    const int cy = kHogCos[k] * gy, sx = kHogSin[k] * gx;
+                    b += (cy >= sx) + (-cy >= sx);
                 }
-                __syncthreads();
+                const uint32_t w = m << ((b & 1) << 4);
+                const uint32_t sel = 1u << (b >> 1);      // dword of the bin, one-hot
+#pragma unroll
+                for (int k = 0; k < 5; ++k) p[rr][k] = w & (uint32_t)(((int)(sel << (31 - k))) >> 31);
+            }
+            // inclusive prefix over the wave: row_shr 1, 2, 4, 8, then row_bcast 15 / 31 (the
+            // ten dwords interleaved: no DPP read right after its VALU write)
+#define SV_HOG_SCAN(F)                                                                         \
+    _Pragma("unroll") for (int rr = 0; rr < RP; ++rr) _Pragma("unroll") for (int k = 0; k < 5; ++k) p[rr][k] = F(p[rr][k]);
+            SV_HOG_SCAN(dpp_add<0x111>)
+            SV_HOG_SCAN(dpp_add<0x112>)
+            SV_HOG_SCAN(dpp_add<0x114>)
+            SV_HOG_SCAN(dpp_add<0x118>)
+            SV_HOG_SCAN((dpp_add_rm<0x142, 0xA>))
+            SV_HOG_SCAN((dpp_add_rm<0x143, 0xC>))
+#undef SV_HOG_SCAN
+            uint32_t hr[RP][5];
+#pragma unroll
+            for (int rr = 0; rr < RP; ++rr)
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_hi, (int)p[rr][k]);
+                    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lo, (int)p[rr][k]);
+                    hr[rr][k] = hi - (lo & lo_mask);
+                }
+#pragma unroll
+            for (int rr = 0; rr < RP; ++rr) {
+                const int t = tb + rr;
+                if (t >= nsteps) break;
+                const int slot = (RP * j + rr) % W2;      // = t mod W2 (t0 is a multiple of W2)
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    V[k] += hr[rr][k] - ring[slot][k];
+                    ring[slot][k] = hr[rr][k];
+                }
+                if (t >= 2 * r) {
+                    // the strip's records are contiguous in the row: stage them in LDS and
+                    // leave as 16-byte stores (20-byte-strided dword stores: 5 partial-line
+                    // writes each).  16-byte stores must be 16-byte aligned: the staging
+                    // starts at the row start's alignment ra, lane j stores absolute-aligned
+                    // bytes [16j, 16j+16) of the staged run, edge lanes dword by dword.
+                    const int rs = (ys + t - 2 * r) * W * 20 + x0 * 20;
+                    const int ra = rs & 15, ro = rs - ra;
+                    if (out_lane)
+#pragma unroll
+                        for (int k = 0; k < 5; ++k) stage[(ra >> 2) + (lane - r) * 5 + k] = V[k];
+                    __syncthreads();   // (one wave: orders the staging, fences the compiler)
+                    const int e = ra + nbytes;              // <= 12 + 64 * 20: up to 81 chunks
+                    for (int b0 = 16 * lane; b0 < e; b0 += 16 * 64) {
+                        const int b1 = b0 + 16;
+                        if (b0 >= ra && b1 <= e) {
+                            const v4u q = *reinterpret_cast<const v4u*>(stage + (b0 >> 2));
+                            __builtin_amdgcn_raw_buffer_store_b128(q, hdst, b0, ro, 0);
+                        } else if (b1 > ra) {
+                            for (int o = max(b0, ra); o < min(b1, e); o += 4)
+                                __builtin_amdgcn_raw_buffer_store_b32(stage[o >> 2], hdst, o, ro, 0);
+                        }
+                    }
+                    __syncthreads();
+                }
             }
         }
     }

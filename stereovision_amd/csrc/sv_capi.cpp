@@ -302,19 +302,12 @@ int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, in
 
 // Enqueue disparity for rows [row0,row1) of gray device images.
 // nf > 1: a batch of frames, frame z at L/R + z*fs_in bytes and out + z*fs_out elements
-// (one launch over grid.z; HOG runs frame by frame through its histogram scratch).
+// (one launch over grid.z; HOG: one histogram launch over both images of every frame, then
+// one match launch reading frame z's histograms at z * H*W*10).
 int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, int pitch,
                       int min_disp, int num_disp, int win, int cost, int row0, int row1,
                       int16_t* out, int opitch, hipStream_t s, int nf = 1, long long fs_in = 0,
                       long long fs_out = 0) {
-    if (nf > 1 && cost == SV_COST_HOG) {
-        for (int z = 0; z < nf; ++z) {
-            int rc = enqueue_disparity(c, L + z * fs_in, R + z * fs_in, H, W, pitch, min_disp, num_disp,
-                                       win, cost, row0, row1, out + z * fs_out, opitch, s);
-            if (rc) return rc;
-        }
-        return 0;
-    }
     sv::MatchPlan plan;
     int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
     if (rc) return rc;
@@ -358,13 +351,16 @@ int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int 
     a.fs_out = fs_out;
     a.fs_hist = 0;
     if (cost == SV_COST_HOG && a.X1 > a.X0) {
-        const size_t hb = (size_t)H * W * 10 * sizeof(uint16_t);
+        const long long fh = (long long)H * W * 10;   // elements per frame's histograms
+        const size_t hb = (size_t)fh * sizeof(uint16_t) * a.nf;
         SV_HIP(c->hog[0].ensure(hb));
         SV_HIP(c->hog[1].ensure(hb));
-        SV_LAUNCH(c, SV_K_HOG, s, sv::launch_hog_hist(L, H, W, pitch, win, row0, row1, c->hog[0].as<uint16_t>(), s));
-        SV_LAUNCH(c, SV_K_HOG, s, sv::launch_hog_hist(R, H, W, pitch, win, row0, row1, c->hog[1].as<uint16_t>(), s));
+        SV_LAUNCH(c, SV_K_HOG, s,
+                  sv::launch_hog_hist_pairs(L, R, H, W, pitch, win, row0, row1, c->hog[0].as<uint16_t>(),
+                                            c->hog[1].as<uint16_t>(), a.nf, a.nf > 1 ? fs_in : 0, fh, s));
         a.HL = c->hog[0].as<uint16_t>();
         a.HR = c->hog[1].as<uint16_t>();
+        a.fs_hist = a.nf > 1 ? fh : 0;
     }
     SV_LAUNCH(c, SV_K_MATCH, s, sv::launch_match(a, plan, cost, s));
     return 0;

@@ -239,7 +239,18 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 template <int r>
 __global__ __launch_bounds__(64) void k_hog_hist_strip(const uint8_t* __restrict__ g, int H, int W, int pitch,
-                                                       int row0, int row1, uint16_t* __restrict__ hist, int hs_rows) {
+                                                       int row0, int row1, uint16_t* __restrict__ hist, int hs_rows,
+                                                       const uint8_t* __restrict__ g1, uint16_t* __restrict__ hist1,
+                                                       long long fs_in, long long fs_hist) {
+    if (blockIdx.z) {   // image pairs: z = 2 * frame + (0 left, 1 right)
+        const int f = blockIdx.z >> 1;
+        if (blockIdx.z & 1) {
+            g = g1;
+            hist = hist1;
+        }
+        g += f * fs_in;
+        hist += f * fs_hist;
+    }
     constexpr int W2 = 2 * r + 1, NOUT = 64 - 2 * r;
     const int lane = threadIdx.x;
     const int x0 = blockIdx.x * NOUT;                    // first output column of the strip
@@ -665,7 +676,7 @@ int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0
         }();
         const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + hs_rows - 1) / hs_rows);
         switch (r) {
-#define SV_HOG_S(R) case R: hipLaunchKernelGGL(k_hog_hist_strip<R>, grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows); break;
+#define SV_HOG_S(R) case R: hipLaunchKernelGGL(k_hog_hist_strip<R>, grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows, g, hist, 0LL, 0LL); break;
             SV_HOG_S(0) SV_HOG_S(1) SV_HOG_S(2) SV_HOG_S(3) SV_HOG_S(4) SV_HOG_S(5) SV_HOG_S(6) SV_HOG_S(7)
 #undef SV_HOG_S
         }
@@ -676,6 +687,35 @@ int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0
 #define SV_HOG_R(R) case R: hipLaunchKernelGGL(k_hog_hist<R>, grid, dim3(256), 0, s, g, H, W, pitch, row0, row1, hist); break;
         SV_HOG_R(0) SV_HOG_R(1) SV_HOG_R(2) SV_HOG_R(3) SV_HOG_R(4) SV_HOG_R(5) SV_HOG_R(6) SV_HOG_R(7)
 #undef SV_HOG_R
+    }
+    return (int)hipGetLastError();
+}
+
+int launch_hog_hist_pairs(const uint8_t* g0, const uint8_t* g1, int H, int W, int pitch, int win, int row0,
+                          int row1, uint16_t* h0, uint16_t* h1, int nf, long long fs_in, long long fs_hist,
+                          hipStream_t s) {
+    const int r = win / 2;
+    if (r > GR_MAX || nf <= 0) return (int)hipErrorInvalidValue;
+    if (row0 < 0) row0 = 0;
+    if (row1 > H) row1 = H;
+    if (row1 <= row0) return 0;
+    static const int strip = [] {
+        const char* e = std::getenv("SV_HOG_STRIP");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (!(strip && (long long)H * W * 20 < (1LL << 31) && (long long)H * pitch < (1LL << 31))) {
+        for (int z = 0; z < nf; ++z) {   // the tile kernel: image by image
+            int e = launch_hog_hist(g0 + z * fs_in, H, W, pitch, win, row0, row1, h0 + z * fs_hist, s);
+            if (!e) e = launch_hog_hist(g1 + z * fs_in, H, W, pitch, win, row0, row1, h1 + z * fs_hist, s);
+            if (e) return e;
+        }
+        return 0;
+    }
+    const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + HS_ROWS - 1) / HS_ROWS, 2 * nf);
+    switch (r) {
+#define SV_HOG_P(R) case R: hipLaunchKernelGGL(k_hog_hist_strip<R>, grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0, HS_ROWS, g1, h1, fs_in, fs_hist); break;
+        SV_HOG_P(0) SV_HOG_P(1) SV_HOG_P(2) SV_HOG_P(3) SV_HOG_P(4) SV_HOG_P(5) SV_HOG_P(6) SV_HOG_P(7)
+#undef SV_HOG_P
     }
     return (int)hipGetLastError();
 }

@@ -69,6 +69,11 @@ int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStre
                   long long fs_in = 0, long long fs_out = 0);
 int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0, int row1,
                     uint16_t* hist, hipStream_t s);
+// Both images of nf frame pairs in one launch (grid.z = 2 nf): frame z's left/right images at
+// g0/g1 + z*fs_in bytes, their histograms at h0/h1 + z*fs_hist elements.
+int launch_hog_hist_pairs(const uint8_t* g0, const uint8_t* g1, int H, int W, int pitch, int win, int row0,
+                          int row1, uint16_t* h0, uint16_t* h1, int nf, long long fs_in, long long fs_hist,
+                          hipStream_t s);
 
 // Rectification (sv_rectify.hip).  ir = inv(P[:, :3] * R) row-major; k = k1 k2 p1 p2 k3 k4
 // k5 k6 s1 s2 s3 s4 (OpenCV distCoeffs order, zero-padded).

@@ -299,7 +299,7 @@ def test_device_api_band_pipeline(engine):
             engine.dev_free(p)
 
 
-@pytest.mark.parametrize("cost,win", [("sad", 9), ("sad", 11), ("ssd", 5), ("hog", 7)])
+@pytest.mark.parametrize("cost,win", [("sad", 9), ("sad", 11), ("ssd", 5), ("hog", 7), ("hog", 15), ("hog", 1)])
 def test_frame_batch_matches_single_frames(engine, cost, win):
     """sv_*_batch_dev (one launch over grid.z) == the per-frame oracle, frame by frame,
     with a padded input frame stride and a padded output pitch."""

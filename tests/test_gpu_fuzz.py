@@ -73,3 +73,31 @@ def test_random_depth_paths_match_numpy_oracle(engine, seed):
     np.testing.assert_array_equal(disp, disparity, err_msg=f"seed {seed}")
     np.testing.assert_array_equal(depth, e_depth, err_msg=f"seed {seed}")
     np.testing.assert_array_equal(norm, e_norm, err_msg=f"seed {seed}")
+
+
+@pytest.mark.parametrize("seed", range(1, 160, 4))
+def test_random_row_bands_reassemble(engine, seed):
+    """Random row bands (the row-tiled multi-GPU shards) reassemble the full map bit-exactly."""
+    cost, win, D, min_disp, L, R = _case(seed)
+    H = L.shape[0]
+    rng = np.random.default_rng(seed)
+    cuts = sorted({0, H, *[int(c) for c in rng.integers(0, H + 1, 3)]})
+    out = np.full(L.shape, 12345, np.int16)
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        engine.disparity_rows(L, R, min_disp, D, win, r0, r1, cost=cost, out=out)
+    np.testing.assert_array_equal(out, C.disparity16(L, R, min_disp, D, win, COSTS[cost]),
+                                  err_msg=f"seed {seed} cuts {cuts}")
+
+
+@pytest.mark.parametrize("seed", range(2, 160, 4))
+def test_random_scaled_path_matches_numpy_oracle(engine, seed):
+    cost, win, D, min_disp, L, R = _case(seed)
+    if cost == "ssd":
+        cost = "sad"
+    disparity = O.disparity_f32(C.disparity16(L, R, min_disp, D, win, COSTS[cost]))
+    dn, disp, du, cf = engine.stereo_scaled(L, R, min_disp, D, win, cost=cost)
+    e_dn, e_du, e_cf = O.scaled_post(disparity, min_disp, D)
+    np.testing.assert_array_equal(disp, disparity, err_msg=f"seed {seed}")
+    np.testing.assert_array_equal(dn, e_dn, err_msg=f"seed {seed}")
+    np.testing.assert_array_equal(du, e_du, err_msg=f"seed {seed}")
+    np.testing.assert_array_equal(cf, e_cf, err_msg=f"seed {seed}")

@@ -231,20 +231,30 @@ SgbmParams sgbm_reference_params(int win) {
 
 // Enqueue the whole SGBM-3WAY pipeline for one frame (buffers grown in the context).
 // cv2.filterSpeckles on an int16 device map (speckle stage of SGBM, sv_filter_speckles).
+// nf > 1: a batch of maps, map z at d_img + z*fimg (one launch per stage over grid.z).
 int enqueue_speckles(sv_ctx* c, int16_t* d_img, int H, int W, int pitch, int new_val, int max_speckle_size,
-                            int max_diff, hipStream_t s) {
+                     int max_diff, hipStream_t s, int nf = 1, long long fimg = 0) {
     if (max_speckle_size <= 0) return 0;
-    const size_t n = (size_t)H * W;
+    const size_t n = (size_t)H * W * (nf < 1 ? 1 : nf);
     SV_HIP(c->cc_parent.ensure(n * 4));
     SV_HIP(c->cc_size.ensure(n * 4));
     SV_LAUNCH(c, SV_K_SPECKLE, s,
               sv::launch_speckles(d_img, H, W, pitch, new_val, max_speckle_size, max_diff, c->cc_parent.as<int>(),
-                                  c->cc_size.as<int>(), s));
+                                  c->cc_size.as<int>(), s, nf < 1 ? 1 : nf, fimg));
     return 0;
 }
 
+// nf > 1: a batch of frames, frame z at L/R + z*fs_in bytes and out + z*fs_out elements.  The
+// DP kernels are chains of W (or H) dependent steps, so one frame leaves most SIMDs idle;
+// batches run every stage once over grid.z (up to kSgbmChunk frames, or as many as the
+// scratch budget allows: ~1.5 GB of volumes per 1080p D=128 frame with int16 paths).
+constexpr int kSgbmChunk = 32;
+constexpr size_t kSgbmBudget = (size_t)48 << 30;
+
 int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, int pitch, int min_disp,
-                 int num_disp, int win, SgbmParams p, int16_t* out, int opitch, hipStream_t s) {
+                 int num_disp, int win, SgbmParams p, int16_t* out, int opitch, hipStream_t s, int nf = 1,
+                 long long fs_in = 0, long long fs_out = 0) {
+    if (nf < 1) nf = 1;
     if (sv::sgbm_dp(num_disp) < 0) return fail(SV_EINVAL, "num_disp must be in [1, 512]");
     if (W > 16384) return fail(SV_EINVAL, "SGBM: width beyond 16384");
     if (p.P1 < 0 || p.P2 < 0) return fail(SV_EINVAL, "negative P1/P2");
@@ -276,28 +286,51 @@ int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, in
     a.l32 = (cmax > 32767 || p.P2 > 32768) ? 1 : 0;
     a.Dp = sv::sgbm_dp(num_disp);
     const size_t vol = (size_t)H * a.Wb * a.Dp;
-    SV_HIP(c->sg_hsum.ensure(vol * 2 + 256));
-    SV_HIP(c->sg_c.ensure(vol * 2 + 256));
-    SV_HIP(c->sg_l.ensure(vol * (a.l32 ? 8 : 2) + 256));
-    SV_HIP(c->sg_lt.ensure(vol * (a.l32 ? 4 : 2) + 256));
+    // hsum + C (u16), L_lr (int16: in the hsum volume), L_rl (unfused only), L_tb, band
+    const size_t lsz = a.l32 ? 4 : 2;
+    const size_t per_frame = vol * (4 + lsz * 3) + (size_t)H * a.Wb * 8;   // unfused (the larger)
+    int chunk = (int)std::max<size_t>(1, std::min<size_t>({(size_t)nf, (size_t)kSgbmChunk,
+                                                            kSgbmBudget / std::max<size_t>(per_frame, 1)}));
+    const bool fused = sv::sgbm_fused(chunk);
+    if (fused)   // no L_rl volume: a third more frames fit the budget
+        chunk = (int)std::max<size_t>(1, std::min<size_t>({(size_t)nf, (size_t)kSgbmChunk,
+                                                            kSgbmBudget / (per_frame - vol * lsz)}));
+    a.fused = fused ? 1 : 0;
+    SV_HIP(c->sg_hsum.ensure(vol * 2 * chunk + 256));
+    SV_HIP(c->sg_c.ensure(vol * 2 * chunk + 256));
+    const int nl = (a.l32 ? 1 : 0) + (fused ? 0 : 1);   // volumes in sg_l: L_lr (int32), L_rl
+    SV_HIP(c->sg_l.ensure(vol * lsz * nl * chunk + 256));
+    SV_HIP(c->sg_lt.ensure(vol * (a.l32 ? 4 : 2) * chunk + 256));
     if (!c->sg_aux) {
         SV_HIP(hipStreamCreateWithFlags(&c->sg_aux, hipStreamNonBlocking));
         SV_HIP(hipEventCreateWithFlags(&c->sg_ev[0], hipEventDisableTiming));
         SV_HIP(hipEventCreateWithFlags(&c->sg_ev[1], hipEventDisableTiming));
     }
-    SV_HIP(c->sg_band.ensure((size_t)H * a.Wb * 8 + 256 + 64 * 128));
+    const size_t band_bytes = (size_t)H * a.Wb * 8 * chunk;
+    SV_HIP(c->sg_band.ensure(band_bytes + 256 + 64 * 128));
     a.hsum = c->sg_hsum.as<uint16_t>();
     a.C = c->sg_c.as<uint16_t>();
-    // int16 paths: L_lr reuses the hsum volume (dead after the window-row sums)
+    // int16 paths: L_lr reuses the hsum volume (dead after the window-row sums); every volume
+    // holds `chunk` frames at a stride of vol elements of its type (SgbmArgs::select_frame)
     a.Llr = a.l32 ? c->sg_l.p : c->sg_hsum.p;
-    a.Lrl = a.l32 ? (void*)(c->sg_l.as<int32_t>() + vol) : c->sg_l.p;
+    a.Lrl = fused ? nullptr : a.l32 ? (void*)(c->sg_l.as<int32_t>() + vol * chunk) : c->sg_l.p;
     a.Ltb = c->sg_lt.p;
     a.band = c->sg_band.p;
-    a.dummy = c->sg_band.as<uint8_t>() + ((size_t)H * a.Wb * 8 + 255) / 256 * 256;
-    a.out = out;
+    a.dummy = c->sg_band.as<uint8_t>() + (band_bytes + 255) / 256 * 256;
     a.opitch = opitch;
-    SV_LAUNCH(c, SV_K_SGBM, s, sv::launch_sgbm(a, s, c->sg_aux, c->sg_ev[0], c->sg_ev[1]));
-    return enqueue_speckles(c, out, H, W, opitch, (min_disp - 1) * 16, p.speckle_win, 16 * p.speckle_range, s);
+    a.fs_in = fs_in;
+    a.fs_out = fs_out;
+    for (int z0 = 0; z0 < nf; z0 += chunk) {
+        const int n = std::min(chunk, nf - z0);
+        a.L = L + z0 * fs_in;
+        a.R = R + z0 * fs_in;
+        a.out = out + z0 * fs_out;
+        SV_LAUNCH(c, SV_K_SGBM, s, sv::launch_sgbm(a, n, s, c->sg_aux, c->sg_ev[0], c->sg_ev[1]));
+        const int rc = enqueue_speckles(c, a.out, H, W, opitch, (min_disp - 1) * 16, p.speckle_win,
+                                        16 * p.speckle_range, s, n, fs_out);
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 // Enqueue disparity for rows [row0,row1) of gray device images.
@@ -316,12 +349,8 @@ int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int 
     if (row1 <= row0) return 0;
     if (cost == SV_COST_SGBM) {   // the top-down path crosses rows: whole frames only
         if (row0 != 0 || row1 != H) return fail(SV_EINVAL, "SGBM cannot compute a row band (use frames)");
-        for (int z = 0; z < (nf < 1 ? 1 : nf); ++z) {
-            rc = enqueue_sgbm(c, L + z * fs_in, R + z * fs_in, H, W, pitch, min_disp, num_disp, win,
-                              sgbm_reference_params(win), out + z * fs_out, opitch, s);
-            if (rc) return rc;
-        }
-        return 0;
+        return enqueue_sgbm(c, L, R, H, W, pitch, min_disp, num_disp, win, sgbm_reference_params(win), out, opitch,
+                            s, nf, fs_in, fs_out);
     }
     sv::MatchParams a{};
     a.L = L;

@@ -153,18 +153,42 @@ struct SgbmArgs {
     void* Lrl;
     void* Ltb;                 // [H][Wb][Dp] top->bottom path costs (same type as Llr)
     int l32;
+    int fused;                 // R->L path fused with the WTA (L_rl never stored; see sgbm_fused)
     void* band;                // [H][Wb] {int16 x16 disparity after uniqueness + sub-pixel,
                                //  int16 argmin index, int32 min cost (INT_MAX: not unique)}
     int16_t* out;              // [H][opitch] final int16 x16 map
     int opitch;
     void* dummy;               // >= 64 x 128 bytes: store target of the padding lanes
+    // frame batch (grid.z = frame): frame z reads L/R + z*fs_in bytes, writes out + z*fs_out
+    // elements, and owns volume z (H*Wb*Dp elements of each volume's type) and band z
+    long long fs_in, fs_out;
+    __device__ __forceinline__ void select_frame(int z) {
+        const size_t vol = (size_t)H * Wb * Dp * z;
+        L += z * fs_in;
+        R += z * fs_in;
+        out += z * fs_out;
+        hsum += vol;
+        C += vol;
+        const size_t lb = vol * (l32 ? 4 : 2);
+        Llr = static_cast<char*>(Llr) + lb;
+        Lrl = static_cast<char*>(Lrl) + lb;
+        Ltb = static_cast<char*>(Ltb) + lb;
+        band = static_cast<char*>(band) + (size_t)H * Wb * 8 * z;
+    }
 };
-int sgbm_dp(int D);                  // per-pixel volume stride for D disparities, -1 if D > 512
+int sgbm_dp(int D);
+// Whether launches of nf frames fuse the R->L path with the WTA (k_sgbm_rl_wta, L_rl never
+// stored): batches of >= 8 frames, where the extra work per step hides behind other waves'
+// chains (one frame: both paths in k_sgbm_hpath, concurrent, then k_sgbm_wta).
+// SV_SGBM_FUSED=0 / 1 forces either form.
+bool sgbm_fused(int nf);                  // per-pixel volume stride for D disparities, -1 if D > 512
 // aux / fork / join: a second stream and two events for the concurrent vertical path (aux =
 // nullptr: everything on s)
-int launch_sgbm(const SgbmArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
+// nf frames per launch (grid.z), laid out as described at SgbmArgs::select_frame
+int launch_sgbm(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
+// nf maps, map z at img + z*fimg; parent/size hold H*W ints per map
 int launch_speckles(int16_t* img, int H, int W, int pitch, int newv, int maxsize, int maxdiff, int* parent,
-                    int* size, hipStream_t s);
+                    int* size, hipStream_t s, int nf = 1, long long fimg = 0);
 
 // Post-processing modes for the median kernel.
 enum PostMode { POST_NONE = 0, POST_DEPTH = 1, POST_SCALED = 2 };

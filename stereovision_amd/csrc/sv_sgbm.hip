@@ -136,6 +136,7 @@ __device__ __forceinline__ int bt_cost(const uint4 l, const uint4 r) {
 
 template <int R>
 __global__ __launch_bounds__(256) void k_sgbm_hsum_tiled(SgbmArgs a) {
+    if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
     extern __shared__ uint4 rec[];
     constexpr int W2 = 2 * R + 1;
     const int y = blockIdx.y, t = threadIdx.x;
@@ -193,6 +194,7 @@ __global__ __launch_bounds__(256) void k_sgbm_hsum_tiled(SgbmArgs a) {
 
 // window rows: C(y) = sum_{j=-r..r} hsum(clamp(y + j))
 __global__ __launch_bounds__(256) void k_sgbm_vsum(SgbmArgs a) {
+    if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
     const size_t plane = (size_t)a.Wb * a.Dp;
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= plane) return;
@@ -236,6 +238,7 @@ __device__ __forceinline__ uint4 add4(uint4 s, uint4 a, uint4 b) {
 
 template <int R>   // window radius: the 2R+1 rows of the window stay in a register ring
 __global__ __launch_bounds__(256) void k_sgbm_vsum8(SgbmArgs a, int vb) {
+    if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
     constexpr int W2 = 2 * R + 1;
     const size_t p8 = (size_t)a.Wb * a.Dp / 8;        // uint4 per row plane
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -371,6 +374,7 @@ __device__ __forceinline__ int lane_min(const int (&v)[DPL]) {
 // right->left into Lrl.
 template <int DPL, int LPC, typename LT, int PF>
 __global__ __launch_bounds__(64) void k_sgbm_hpath(SgbmArgs a) {
+    if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
     constexpr int NL = 64 / LPC;
     const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
     const int y = blockIdx.x * NL + g, dir = blockIdx.y;
@@ -479,6 +483,7 @@ __device__ __forceinline__ BandOut wta_line(const SgbmArgs& a, const int (&s)[DP
 // chains of dependent steps that leave most of a SIMD idle).
 template <int DPL, int LPC, typename LT, int PF>
 __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
+    if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
     constexpr int NL = 64 / LPC;
     const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
     const int xb = blockIdx.x * NL + g;
@@ -529,6 +534,7 @@ __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
 // fused vertical-path kernel on ~900 waves).
 template <int DPL, int LPC, typename LT>
 __global__ __launch_bounds__(64) void k_sgbm_wta(SgbmArgs a) {
+    if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
     constexpr int NL = 64 / LPC;
     const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
     const size_t npx = (size_t)a.H * a.Wb;
@@ -548,8 +554,78 @@ __global__ __launch_bounds__(64) void k_sgbm_wta(SgbmArgs a) {
     if (p < npx && j == 0) reinterpret_cast<BandOut*>(a.band)[p] = o;
 }
 
+// Right->left path fused with the winner-take-all: the line walks x = Wb-1 .. 0 like
+// k_sgbm_hpath's second direction, and at every step sums its fresh L_rl[x] with L_lr[x]
+// and L_tb[x] (prefetched in register rings beside C) and runs wta_line on the sum.  L_rl
+// is never stored, so the R->L volume's write and the WTA's read of it (2 of the pipeline's
+// volume passes) disappear, and so does the WTA launch.  The WTA work hangs off the DP
+// chain (only `prev` and the path minimum are loop-carried), so it fills the chain's gaps.
+template <int DPL, typename LT, int PF>
+__global__ __launch_bounds__(64) void k_sgbm_rl_wta(SgbmArgs a) {
+    if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
+    constexpr int LPC = 16, NL = 64 / LPC;
+    const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
+    const int y = blockIdx.x * NL + g;
+    const int D = a.D, Wb = a.Wb, Dp = a.Dp, dbase = j * DPL;
+    const int yc = min(y, a.H - 1);
+    const size_t x0 = (size_t)(Wb - 1) * Dp;
+    const size_t row = (size_t)yc * Wb * Dp + (dbase < D ? dbase : 0) + x0;
+    const uint16_t* Cp = a.C + row;
+    const LT* Ap = static_cast<const LT*>(a.Llr) + row;
+    const LT* Bp = static_cast<const LT*>(a.Ltb) + row;
+    BandOut* bout = reinterpret_cast<BandOut*>(a.band) + (size_t)yc * Wb + (Wb - 1);
+    const bool emit = y < a.H && j == 0;
+    __shared__ int lds_s[64 * DPL];
+    using CP = Pack<uint16_t, DPL>;
+    using LP = Pack<LT, DPL>;
+    CP rc[PF];
+    LP ra[PF], rb[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+        const ptrdiff_t o = -(ptrdiff_t)min(p, Wb - 1) * Dp;
+        rc[p] = *reinterpret_cast<const CP*>(Cp + o);
+        ra[p] = *reinterpret_cast<const LP*>(Ap + o);
+        rb[p] = *reinterpret_cast<const LP*>(Bp + o);
+    }
+    ptrdiff_t on = -(ptrdiff_t)min(PF, Wb - 1) * Dp;   // next load: step PF, clamped to x = 0
+    int prev[DPL], pad[DPL];
+    pad_init<DPL>(pad, dbase, D);
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) prev[k] = dbase + k < D ? 0 : kInf;
+    int mn = 0;
+    auto step = [&](int t, const CP& cp, const LP& lp, const LP& tp) {
+        int c[DPL];
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) c[k] = (int)cp.v[k];
+        path_step<DPL, LPC>(prev, c, mn, a.P1, a.P2, pad, j);
+        mn = line_min<LPC>(lane_min<DPL>(prev));
+        int s[DPL];
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) s[k] = prev[k] + (int)lp.v[k] + (int)tp.v[k];
+        const BandOut o = wta_line<DPL, LPC>(a, s, dbase, lds_s + lane * DPL, lds_s + g * LPC * DPL);
+        if (emit) bout[-t] = o;
+    };
+    int s0 = 0;
+    for (; s0 + PF <= Wb; s0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const CP cc = rc[u];
+            const LP la = ra[u], lb = rb[u];
+            rc[u] = *reinterpret_cast<const CP*>(Cp + on);
+            ra[u] = *reinterpret_cast<const LP*>(Ap + on);
+            rb[u] = *reinterpret_cast<const LP*>(Bp + on);
+            on -= s0 + u + PF < Wb - 1 ? Dp : 0;
+            step(s0 + u, cc, la, lb);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (s0 + u < Wb) step(s0 + u, rc[u], ra[u], rb[u]);
+}
+
 // Left-right consistency (disp12MaxDiff) and band borders: one workgroup per row.
 __global__ __launch_bounds__(256) void k_sgbm_lrcheck(SgbmArgs a) {
+    if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
     extern __shared__ unsigned long long keys[];
     const int y = blockIdx.x, t = threadIdx.x, W = a.W, Wb = a.Wb;
     for (int x = t; x < W; x += 256) keys[x] = ~0ull;
@@ -631,7 +707,10 @@ __device__ __forceinline__ void uf_unite(int* p, int a, int b) {
 // everywhere else).
 constexpr int kCT = 32;
 __global__ __launch_bounds__(256) void k_cc_local(const int16_t* img, int H, int W, int pitch, int newv,
-                                                  int maxdiff, int* parent, int* size) {
+                                                  int maxdiff, int* parent, int* size, long long fimg) {
+    img += blockIdx.z * fimg;   // map z of a batch; its forest at z*H*W
+    parent += (size_t)blockIdx.z * H * W;
+    size += (size_t)blockIdx.z * H * W;
     __shared__ int lp[kCT * kCT];
     __shared__ int lc[kCT * kCT];
     __shared__ int16_t lv[kCT * kCT];
@@ -685,7 +764,11 @@ __global__ __launch_bounds__(256) void k_cc_local(const int16_t* img, int H, int
 // joined (parent[p] is always a local root of p's tree, whose size[] is a local size).
 // This drops the background's border edges, which otherwise all contend for one root.
 __global__ __launch_bounds__(256) void k_cc_border(const int16_t* img, int H, int W, int pitch, int newv,
-                                                   int maxdiff, int maxsize, int* parent, const int* size) {
+                                                   int maxdiff, int maxsize, int* parent, const int* size,
+                                                   long long fimg) {
+    img += blockIdx.z * fimg;
+    parent += (size_t)blockIdx.z * H * W;
+    size += (size_t)blockIdx.z * H * W;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= H * W) return;
     const int y = i / W, x = i % W;
@@ -710,6 +793,8 @@ __global__ __launch_bounds__(256) void k_cc_border(const int16_t* img, int H, in
 // count already exceeds maxsize (the decision size <= maxsize stays exact).  Non-roots
 // keep size 0 and the roots' own entries start at their local size.
 __global__ __launch_bounds__(256) void k_cc_count(int H, int W, int maxsize, int* parent, int* size) {
+    parent += (size_t)blockIdx.z * H * W;
+    size += (size_t)blockIdx.z * H * W;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= H * W) return;
     const int s = size[i];
@@ -719,7 +804,10 @@ __global__ __launch_bounds__(256) void k_cc_count(int H, int W, int maxsize, int
 }
 
 __global__ __launch_bounds__(256) void k_cc_apply(int16_t* img, int H, int W, int pitch, int newv, int maxsize,
-                                                  int* parent, const int* size) {
+                                                  int* parent, const int* size, long long fimg) {
+    img += blockIdx.z * fimg;
+    parent += (size_t)blockIdx.z * H * W;
+    size += (size_t)blockIdx.z * H * W;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= H * W || parent[i] < 0) return;
     if (size[uf_find(parent, i)] <= maxsize) img[(size_t)(i / W) * pitch + i % W] = (int16_t)newv;
@@ -753,11 +841,12 @@ PathPlan vpath_plan(int D) {
 PathPlan hpath_plan(int D) { return hpath16_plan(D); }
 
 template <typename LT>
-int launch_paths_t(const SgbmArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
+int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
     const PathPlan ph = hpath_plan(a.D), pv = vpath_plan(a.D), pw = pv;
-    const dim3 gh((a.H + 3) / 4, 2), gv((a.Wb + 64 / pv.lpc - 1) / (64 / pv.lpc));
+    const bool fused = a.fused != 0;
+    const dim3 gh((a.H + 3) / 4, fused ? 1 : 2, nf), gv((a.Wb + 64 / pv.lpc - 1) / (64 / pv.lpc), 1, nf);
     const size_t npx = (size_t)a.H * a.Wb;
-    const dim3 gw((unsigned)((npx + 64 / pw.lpc - 1) / (64 / pw.lpc)));
+    const dim3 gw((unsigned)((npx + 64 / pw.lpc - 1) / (64 / pw.lpc)), 1, nf);
     // vertical path on the second stream, beside the horizontal paths
     hipStream_t sv = aux ? aux : s;
     if (aux) {
@@ -784,6 +873,17 @@ int launch_paths_t(const SgbmArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t
     SV_HPATH(16, 16, 8) SV_HPATH(16, 20, 6) SV_HPATH(16, 24, 6) SV_HPATH(16, 32, 4)
 #undef SV_HPATH
     if (aux && hipStreamWaitEvent(s, join, 0) != hipSuccess) return (int)hipErrorLaunchFailure;
+    if (fused) {
+        const dim3 gf((a.H + 3) / 4, 1, nf);
+#define SV_RLWTA(N, PF)                                                              \
+        if (!w && ph.dpl == N) {                                                     \
+            hipLaunchKernelGGL((k_sgbm_rl_wta<N, LT, PF>), gf, dim3(64), 0, s, a);   \
+            w = true;                                                                \
+        }
+        SV_RLWTA(1, 16) SV_RLWTA(2, 16) SV_RLWTA(4, 12) SV_RLWTA(8, 8) SV_RLWTA(12, 6) SV_RLWTA(16, 4)
+        SV_RLWTA(20, 3) SV_RLWTA(24, 3) SV_RLWTA(32, 2)
+#undef SV_RLWTA
+    }
 #define SV_WTA(L, N)                                                                 \
     if (!w && pw.lpc == L && pw.dpl == N) {                                          \
         hipLaunchKernelGGL((k_sgbm_wta<N, L, LT>), gw, dim3(64), 0, s, a);           \
@@ -798,6 +898,14 @@ int launch_paths_t(const SgbmArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t
 
 }  // namespace
 
+bool sgbm_fused(int nf) {
+    static const int force = [] {
+        const char* e = std::getenv("SV_SGBM_FUSED");
+        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+    }();
+    return force >= 0 ? force == 1 : nf >= 8;
+}
+
 int sgbm_dp(int D) {
     if (D < 1 || D > 512) return -1;
     int x = hpath_plan(D).dpl, y = vpath_plan(D).dpl;   // Dp: a multiple of both lane widths
@@ -811,11 +919,11 @@ int sgbm_dp(int D) {
     return (D + l - 1) / l * l;
 }
 
-int launch_sgbm(const SgbmArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
-    if (a.H <= 0 || a.W <= 0) return 0;
+int launch_sgbm(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
+    if (a.H <= 0 || a.W <= 0 || nf <= 0) return 0;
     if (a.Wb > 0) {
         if (a.r > kMaxR) return (int)hipErrorInvalidValue;
-        const dim3 grid((unsigned)((a.Wb + kHX - 1) / kHX), (unsigned)a.H);
+        const dim3 grid((unsigned)((a.Wb + kHX - 1) / kHX), (unsigned)a.H, (unsigned)nf);
         const size_t lds = (size_t)(2 * kHX + 4 * a.r + a.D - 1) * sizeof(uint4);
         switch (a.r) {
 #define SV_HSUM_R(R) case R: hipLaunchKernelGGL(k_sgbm_hsum_tiled<R>, grid, dim3(256), lds, s, a); break;
@@ -828,9 +936,9 @@ int launch_sgbm(const SgbmArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fo
             // enough bands for ~4 waves per SIMD (4 waves per block), each >= 64 rows so the
             // per-band warm-up of 2r+1 rows stays small
             const size_t blocks = (plane / 8 + 255) / 256;
-            const int nb = (int)std::max<size_t>(1, std::min<size_t>((size_t)a.H / 64, (1024 + blocks - 1) / blocks));
+            const int nb = (int)std::max<size_t>(1, std::min<size_t>((size_t)a.H / 64, (1024 + blocks * nf - 1) / (blocks * nf)));
             const int vb = (a.H + nb - 1) / nb;
-            const dim3 grid8((unsigned)blocks, (unsigned)((a.H + vb - 1) / vb));
+            const dim3 grid8((unsigned)blocks, (unsigned)((a.H + vb - 1) / vb), (unsigned)nf);
             switch (a.r) {
 #define SV_VSUM_R(R) case R: hipLaunchKernelGGL(k_sgbm_vsum8<R>, grid8, dim3(256), 0, s, a, vb); break;
                 SV_VSUM_R(0) SV_VSUM_R(1) SV_VSUM_R(2) SV_VSUM_R(3) SV_VSUM_R(4) SV_VSUM_R(5) SV_VSUM_R(6)
@@ -838,26 +946,26 @@ int launch_sgbm(const SgbmArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fo
 #undef SV_VSUM_R
             }
         } else {
-            hipLaunchKernelGGL(k_sgbm_vsum, dim3((unsigned)((plane + 255) / 256)), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(k_sgbm_vsum, dim3((unsigned)((plane + 255) / 256), 1, (unsigned)nf), dim3(256), 0, s, a);
         }
-        const int e = a.l32 ? launch_paths_t<int32_t>(a, s, aux, fork, join)
-                            : launch_paths_t<int16_t>(a, s, aux, fork, join);
+        const int e = a.l32 ? launch_paths_t<int32_t>(a, nf, s, aux, fork, join)
+                            : launch_paths_t<int16_t>(a, nf, s, aux, fork, join);
         if (e) return e;
     }
-    hipLaunchKernelGGL(k_sgbm_lrcheck, dim3(a.H), dim3(256), (size_t)a.W * 8, s, a);
+    hipLaunchKernelGGL(k_sgbm_lrcheck, dim3(a.H, 1, nf), dim3(256), (size_t)a.W * 8, s, a);
     return (int)hipGetLastError();
 }
 
 int launch_speckles(int16_t* img, int H, int W, int pitch, int newv, int maxsize, int maxdiff, int* parent,
-                    int* size, hipStream_t s) {
-    if (H <= 0 || W <= 0 || maxsize <= 0) return 0;
-    const unsigned n = (unsigned)(((size_t)H * W + 255) / 256);
-    dim3 tiles((W + kCT - 1) / kCT, (H + kCT - 1) / kCT);
-    hipLaunchKernelGGL(k_cc_local, tiles, dim3(256), 0, s, img, H, W, pitch, newv, maxdiff, parent, size);
-    hipLaunchKernelGGL(k_cc_border, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, maxdiff, maxsize, parent,
-                       size);
-    hipLaunchKernelGGL(k_cc_count, dim3(n), dim3(256), 0, s, H, W, maxsize, parent, size);
-    hipLaunchKernelGGL(k_cc_apply, dim3(n), dim3(256), 0, s, img, H, W, pitch, newv, maxsize, parent, size);
+                    int* size, hipStream_t s, int nf, long long fimg) {
+    if (H <= 0 || W <= 0 || maxsize <= 0 || nf <= 0) return 0;
+    const dim3 n((unsigned)(((size_t)H * W + 255) / 256), 1, (unsigned)nf);
+    dim3 tiles((W + kCT - 1) / kCT, (H + kCT - 1) / kCT, (unsigned)nf);
+    hipLaunchKernelGGL(k_cc_local, tiles, dim3(256), 0, s, img, H, W, pitch, newv, maxdiff, parent, size, fimg);
+    hipLaunchKernelGGL(k_cc_border, n, dim3(256), 0, s, img, H, W, pitch, newv, maxdiff, maxsize, parent,
+                       size, fimg);
+    hipLaunchKernelGGL(k_cc_count, n, dim3(256), 0, s, H, W, maxsize, parent, size);
+    hipLaunchKernelGGL(k_cc_apply, n, dim3(256), 0, s, img, H, W, pitch, newv, maxsize, parent, size, fimg);
     return (int)hipGetLastError();
 }
 

@@ -191,3 +191,40 @@ def test_gpu_sgbm_tall_frames_row_bands(engine, H, W, D, win):
     band re-summing its first window; band seams must be invisible."""
     L, R, _ = stereo_pair(H, W, D, seed=H + W)
     np.testing.assert_array_equal(engine.sgbm(L, R, 0, D, win), SG.sgbm(L, R, 0, D, win))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nf,H,W,D,win,minD", [(11, 37, 150, 32, 5, 0),     # fused R->L + WTA
+                                                (9, 29, 133, 48, 15, -3),   # fused, int32 paths
+                                                (3, 29, 133, 48, 15, -3),   # unfused, int32
+                                                (2, 64, 200, 64, 9, 4),     # unfused
+                                                (8, 16, 380, 320, 7, 0),    # fused, DPL 20
+                                                (8, 12, 560, 512, 5, 0)])   # fused, DPL 32
+def test_gpu_sgbm_frame_batch(engine, nf, H, W, D, win, minD):
+    """Frame batches (every SGBM stage and the speckle filter over grid.z; batches of >= 8
+    frames fuse the R->L path with the WTA): each frame of a pitched, strided stack bit-exact against the
+    oracle run on that frame alone."""
+    pitch, fs = W + 24, (H + 3) * (W + 24)
+    Ls = np.zeros((nf, H + 3, pitch), np.uint8)
+    Rs = np.zeros_like(Ls)
+    for z in range(nf):
+        L, R, _ = stereo_pair(H, W, D, seed=100 + z)
+        if z % 3 == 2:   # flat / noise frames beside textured ones
+            R = np.random.default_rng(z).integers(0, 256, (H, W), dtype=np.uint8)
+        Ls[z, :H, :W], Rs[z, :H, :W] = L, R
+    opitch, ofs = W + 8, H * (W + 8) + 40
+    dL, dR = engine.dev_alloc(Ls.nbytes), engine.dev_alloc(Rs.nbytes)
+    dO = engine.dev_alloc(nf * ofs * 2)
+    try:
+        engine.to_device(dL, Ls)
+        engine.to_device(dR, Rs)
+        engine.disparity_batch_dev(dL, dR, nf, H, W, pitch, fs, minD, D, win, "sgbm", dO, opitch, ofs)
+        engine.synchronize()
+        flat = engine.to_host(dO, (nf * ofs,), np.int16)
+        for z in range(nf):
+            got = flat[z * ofs:z * ofs + H * opitch].reshape(H, opitch)[:, :W]
+            exp = SG.sgbm(Ls[z, :H, :W], Rs[z, :H, :W], minD, D, win)
+            np.testing.assert_array_equal(got, exp, err_msg=f"frame {z}")
+    finally:
+        for p in (dL, dR, dO):
+            engine.dev_free(p)

@@ -601,7 +601,11 @@ def main():
         write = pmc.get("WRITE_SIZE")
         traffic = round((fetch + write) * 1024) if fetch is not None and write is not None else None
         roofline = {
-            "kernel": k_name, "bound": "hbm", "achieved": round(achieved, 2),
+            # bound: what limits the kernel (VALU issue); achieved/peak/frac stay
+            # the contract's HBM figures (algorithmic bytes by SURVEY.md §8(d)), the VALU
+            # roofline is the `valu` object below
+            "kernel": k_name, "bound": "valu" if args.cost != "sgbm" else "hbm",
+            "frac_basis": "hbm", "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": traffic,
             "bytes_per_launch": k_bytes,
@@ -609,7 +613,6 @@ def main():
             "kernel_bytes_per_launch": k_bytes_kernel,
             "frac_kernel_bytes": round(k_bytes_kernel / k_avg_s / 1e9 / HBM_PEAK_GBS, 5),
             "avg_launch_us": round(k_avg_s * 1e6, 2), "launches": match_n,
-            "limiter": "valu",
             # what actually bounds k_match: VALU issue.  SQ_INSTS_VALU per
             # launch from the live rocprofv3 pass over the live launch time, against the
             # full-rate issue peak (1 wave64 instruction / 2 cycles / SIMD); v_sad_u8 and the

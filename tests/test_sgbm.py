@@ -199,7 +199,12 @@ def test_gpu_sgbm_tall_frames_row_bands(engine, H, W, D, win):
                                                 (3, 29, 133, 48, 15, -3),   # unfused, int32
                                                 (2, 64, 200, 64, 9, 4),     # unfused
                                                 (8, 16, 380, 320, 7, 0),    # fused, DPL 20
-                                                (8, 12, 560, 512, 5, 0)])   # fused, DPL 32
+                                                (8, 12, 560, 512, 5, 0),    # fused, DPL 32
+                                                (8, 21, 90, 16, 3, 0),      # fused, DPL 1
+                                                (8, 19, 230, 128, 9, -2),   # fused, DPL 8
+                                                (8, 14, 300, 192, 5, 0),    # fused, DPL 12
+                                                (8, 13, 330, 256, 7, 3),    # fused, DPL 16
+                                                (8, 11, 450, 384, 3, 0)])   # fused, DPL 24
 def test_gpu_sgbm_frame_batch(engine, nf, H, W, D, win, minD):
     """Frame batches (every SGBM stage and the speckle filter over grid.z; batches of >= 8
     frames fuse the R->L path with the WTA): each frame of a pitched, strided stack bit-exact against the

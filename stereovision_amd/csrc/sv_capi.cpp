@@ -117,7 +117,7 @@ struct sv_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut, rmap1, rmap2, rdst[2], stats, sel,
-        sg_hsum, sg_c, sg_l, sg_lt, sg_band, cc_parent, cc_size, hist_copies, cmap, bgr;
+        sg_hsum, sg_c, sg_l, sg_lt, sg_band, sg_rec, cc_parent, cc_size, hist_copies, cmap, bgr;
     uint8_t cmap_host[768] = {};   // BGR table currently in `cmap`
     bool cmap_valid = false;
     // host-buffer frame path: int16 medians come back over PCIe and are expanded on the
@@ -288,7 +288,9 @@ int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, in
     const size_t vol = (size_t)H * a.Wb * a.Dp;
     // hsum + C (u16), L_lr (int16: in the hsum volume), L_rl (unfused only), L_tb, band
     const size_t lsz = a.l32 ? 4 : 2;
-    const size_t per_frame = vol * (4 + lsz * 3) + (size_t)H * a.Wb * 8;   // unfused (the larger)
+    const bool cost1 = sv::sgbm_cost_fused(num_disp, a.r);   // k_sgbm_cost: per-pixel record planes
+    const size_t rec_frame = cost1 ? (size_t)2 * H * W * 16 : 0;
+    const size_t per_frame = vol * (4 + lsz * 3) + (size_t)H * a.Wb * 8 + rec_frame;   // unfused (the larger)
     int chunk = (int)std::max<size_t>(1, std::min<size_t>({(size_t)nf, (size_t)kSgbmChunk,
                                                             kSgbmBudget / std::max<size_t>(per_frame, 1)}));
     const bool fused = sv::sgbm_fused(chunk);
@@ -316,6 +318,11 @@ int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, in
     a.Lrl = fused ? nullptr : a.l32 ? (void*)(c->sg_l.as<int32_t>() + vol * chunk) : c->sg_l.p;
     a.Ltb = c->sg_lt.p;
     a.band = c->sg_band.p;
+    a.recs = nullptr;
+    if (cost1) {
+        SV_HIP(c->sg_rec.ensure(rec_frame * chunk + 256));
+        a.recs = c->sg_rec.as<uint4>();
+    }
     a.dummy = c->sg_band.as<uint8_t>() + (band_bytes + 255) / 256 * 256;
     a.opitch = opitch;
     a.fs_in = fs_in;

@@ -154,6 +154,7 @@ struct SgbmArgs {
     void* Ltb;                 // [H][Wb][Dp] top->bottom path costs (same type as Llr)
     int l32;
     int fused;                 // R->L path fused with the WTA (L_rl never stored; see sgbm_fused)
+    uint4* recs;               // [2][H][W] per-pixel BT records of L, R (k_sgbm_cost path)
     void* band;                // [H][Wb] {int16 x16 disparity after uniqueness + sub-pixel,
                                //  int16 argmin index, int32 min cost (INT_MAX: not unique)}
     int16_t* out;              // [H][opitch] final int16 x16 map
@@ -174,6 +175,7 @@ struct SgbmArgs {
         Lrl = static_cast<char*>(Lrl) + lb;
         Ltb = static_cast<char*>(Ltb) + lb;
         band = static_cast<char*>(band) + (size_t)H * Wb * 8 * z;
+        if (recs) recs += (size_t)2 * H * W * z;
     }
 };
 int sgbm_dp(int D);
@@ -181,7 +183,10 @@ int sgbm_dp(int D);
 // stored): batches of >= 8 frames, where the extra work per step hides behind other waves'
 // chains (one frame: both paths in k_sgbm_hpath, concurrent, then k_sgbm_wta).
 // SV_SGBM_FUSED=0 / 1 forces either form.
-bool sgbm_fused(int nf);                  // per-pixel volume stride for D disparities, -1 if D > 512
+bool sgbm_fused(int nf);
+// r <= 4: pixel cost and both window sums in one pass (k_sgbm_cost, no hsum
+// volume); SV_SGBM_COST=0 restores k_sgbm_hsum_tiled + k_sgbm_vsum8
+bool sgbm_cost_fused(int D, int r);                  // per-pixel volume stride for D disparities, -1 if D > 512
 // aux / fork / join: a second stream and two events for the concurrent vertical path (aux =
 // nullptr: everything on s)
 // nf frames per launch (grid.z), laid out as described at SgbmArgs::select_frame

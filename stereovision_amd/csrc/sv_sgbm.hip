@@ -272,6 +272,166 @@ __global__ __launch_bounds__(256) void k_sgbm_vsum8(SgbmArgs a, int vb) {
     }
 }
 
+// Pixel cost + both window sums in one pass (r <= 4): the hsum volume never leaves the
+// chip.  Every wave is independent (no workgroup barriers): it owns 64 consecutive
+// disparities (lane = d, so its stores coalesce), a chunk of CL band columns and a band of
+// output rows, and walks the rows top to bottom.  Per input row it copies that row's
+// {value, BT lo, BT hi} records (from k_sgbm_records' planes, prefetched into registers one
+// row ahead) into its own LDS slice, forms the CL window-column sums of the chunk with a
+// horizontal running sum (CL + 2R pixel costs per lane) and keeps the last 2R+1 rows of them
+// in a register ring of packed u16 pairs: C(y) = C(y-1) + hsum(y+R) - hsum(y-R-1), by
+// v_pk_add/sub_u16 (exact: every window sum fits 16 bits, enqueue_sgbm checks).  Rows are
+// clamped like k_sgbm_vsum's, columns like k_sgbm_hsum_tiled's.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {   // v_pk_add_u16 (mod 2^16)
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {   // v_pk_sub_u16 (mod 2^16)
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
+}
+
+// Per-pixel {value, BT lo, BT hi} records of both images (k_sgbm_cost stages rows of them)
+__global__ __launch_bounds__(256) void k_sgbm_records(SgbmArgs a) {
+    if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y >> 1, img = blockIdx.y & 1;
+    if (x >= a.W) return;
+    a.recs[((size_t)img * a.H + y) * a.W + x] = bt_record(a, img ? a.R : a.L, y, x);
+}
+
+template <int R> struct CostCfg {
+    static constexpr int CL = R <= 2 ? 32 : 16;           // columns per lane (ring: (2R+1)*CL/2 VGPRs)
+    static constexpr int NREC = 2 * (CL + 2 * R) + 63;    // records per row of a wave
+    static constexpr int NRT = (NREC + 63) / 64;          // per lane
+};
+
+// wave-scope ordering of the LDS slice (LDS instructions of one wave execute in order; this
+// keeps the compiler from moving accesses across)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int R>
+__global__ __launch_bounds__(64, 2) void k_sgbm_cost(SgbmArgs a, int vb, int ndg) {
+    if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
+    constexpr int W2 = 2 * R + 1, CL = CostCfg<R>::CL, CP = CL / 2, NRT = CostCfg<R>::NRT;
+    __shared__ uint4 rec[2 * CostCfg<R>::NREC];
+    const int lane = threadIdx.x, D = a.D, Wb = a.Wb, H = a.H;
+    const int dg = (int)blockIdx.y % ndg, band = (int)blockIdx.y / ndg;
+    const int d = 64 * dg + lane, dmax = min(64 * dg + 63, D - 1);
+    const int xs = (int)blockIdx.x * CL;                 // first band column of the chunk
+    const int y0 = band * vb, n = min(H, y0 + vb) - y0;
+    const bool active = d < D;
+    // records: left band columns xs-R .. xs+CL+R-1 (band-clamped), right image columns
+    // xr0 .. xr1 that those columns reach at d = dmax .. 64*dg
+    const int xr0 = a.X0 + max(xs - R, 0) - a.minD - dmax;
+    const int xr1 = a.X0 + min(xs + CL + R - 1, Wb - 1) - a.minD - 64 * dg;
+    const int nL = CL + 2 * R;
+    const int nrec = nL + (xr1 - xr0 + 1);
+    const int roff = a.X0 - a.minD - min(d, dmax) - xr0;
+    const uint4* recLg = a.recs;                          // [H][W] left records, then right
+    const uint4* recRg = a.recs + (size_t)H * a.W;
+    uint32_t nx[NRT][4];   // scalar words (a uint4 array stayed in scratch)
+    auto load = [&](int iy) {
+        const uint4* lrow = recLg + (size_t)iy * a.W;
+        const uint4* rrow = recRg + (size_t)iy * a.W;
+#pragma unroll
+        for (int q = 0; q < NRT; ++q) {   // unconditional (clamped) loads keep nx in VGPRs
+            const int i = min(lane + 64 * q, nrec - 1);
+            const uint4 v = i < nL ? lrow[a.X0 + min(max(xs - R + i, 0), Wb - 1)] : rrow[xr0 + (i - nL)];
+            nx[q][0] = v.x;
+            nx[q][1] = v.y;
+            nx[q][2] = v.z;
+            nx[q][3] = v.w;
+        }
+    };
+    auto put = [&](uint4* buf) {
+#pragma unroll
+        for (int q = 0; q < NRT; ++q) {
+            const int i = lane + 64 * q;
+            if (i < nrec) buf[i] = make_uint4(nx[q][0], nx[q][1], nx[q][2], nx[q][3]);
+        }
+        wave_lds_sync();
+    };
+    // window-column sums of this lane's CL cells from the row in `buf`, packed in pairs;
+    // interior chunks (no band clamp among their columns) read with immediate offsets
+    const bool interior = xs - R >= 0 && xs + CL + R - 1 <= Wb - 1;
+    // (left records as uniform scalar loads instead of LDS broadcasts: 275 -> 700 us per 1080p
+    // frame, the loads' latency exposed)
+    auto hrow = [&](const uint4* buf, uint32_t (&hp)[CP]) {
+        int pcs[CL + 2 * R];
+        if (interior) {
+            const uint4* rb = buf + nL + (xs - R + roff);
+#pragma unroll
+            for (int k = 0; k < CL + 2 * R; ++k) pcs[k] = bt_cost(buf[k], rb[k]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < CL + 2 * R; ++k)
+                pcs[k] = bt_cost(buf[k], buf[nL + min(max(xs - R + k, 0), Wb - 1) + roff]);
+        }
+        int hs = 0;
+#pragma unroll
+        for (int k = 0; k < W2; ++k) hs += pcs[k];
+        int lo = hs;
+#pragma unroll
+        for (int j = 1; j < CL; ++j) {
+            hs += pcs[j + 2 * R] - pcs[j - 1];
+            if (j & 1) hp[j >> 1] = (uint32_t)(lo & 0xFFFF) | ((uint32_t)hs << 16);
+            else lo = hs;
+        }
+    };
+    // stores through a per-row buffer descriptor: 32-bit lane offsets, the column step as the
+    // uniform soffset (no per-column 64-bit addresses to keep live)
+    const int voff = 2 * (xs * a.Dp + d);
+    auto store = [&](int y, const uint32_t (&cp)[CP]) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.C + (size_t)y * Wb * a.Dp, 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < CL; ++j)
+            if (xs + j < Wb)
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(cp[j >> 1] >> (16 * (j & 1))), rs, voff,
+                                                      2 * j * a.Dp, 0);
+    };
+    constexpr int NB = CostCfg<R>::NREC;
+    int cur = 0;   // LDS buffer of the row being summed: rec + cur * NB
+    // warm-up: rows clamp(y0-R .. y0+R) into the ring, C(y0) = their sum
+    uint32_t ring[W2][CP], acc[CP];
+#pragma unroll
+    for (int j = 0; j < CP; ++j) acc[j] = 0u;
+    load(min(max(y0 - R, 0), H - 1));
+    put(rec);
+#pragma unroll
+    for (int k = 0; k < W2; ++k) {
+        const int ny = k < W2 - 1 ? y0 - R + k + 1 : y0 + 1 + R;
+        load(min(max(ny, 0), H - 1));
+        hrow(rec + cur * NB, ring[k]);
+#pragma unroll
+        for (int j = 0; j < CP; ++j) acc[j] = pk_add16(acc[j], ring[k][j]);
+        put(rec + (cur ^ 1) * NB);
+        cur ^= 1;
+    }
+    if (active) store(y0, acc);
+    // output row y0 + t adds row clamp(y0 + t + R) and drops ring slot (t - 1) mod W2
+    for (int t0 = 1; t0 < n; t0 += W2) {
+#pragma unroll
+        for (int u = 0; u < W2; ++u) {
+            if (t0 + u < n) {   // uniform across the wave
+                load(min(y0 + t0 + u + 1 + R, H - 1));
+                uint32_t hp[CP];
+                hrow(rec + cur * NB, hp);
+#pragma unroll
+                for (int j = 0; j < CP; ++j) {
+                    acc[j] = pk_sub16(pk_add16(acc[j], hp[j]), ring[u][j]);
+                    ring[u][j] = hp[j];
+                }
+                if (active) store(y0 + t0 + u, acc);
+                put(rec + (cur ^ 1) * NB);
+                cur ^= 1;
+            }
+        }
+    }
+}
+
 // The path kernels run one line's DP (a chain of W or H dependent steps: the path minimum
 // of step s feeds step s+1) in a 16-lane row of a wave, so a wave advances 4 lines at once
 // and the loop-carried chain per step is ~11 VALU ops: the d+-1 neighbours by row_shr/shl
@@ -898,6 +1058,16 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
 
 }  // namespace
 
+bool sgbm_cost_fused(int D, int r) {
+    static const bool off = [] {
+        const char* e = std::getenv("SV_SGBM_COST");
+        return e && e[0] == '0';
+    }();
+    // r >= 5: the ring no longer fits the registers of 2 waves per SIMD (spills), and the 13/15-
+    // row bodies of r 6..7 are too large to unroll
+    return !off && D >= 1 && D <= 512 && r <= 4;
+}
+
 bool sgbm_fused(int nf) {
     static const int force = [] {
         const char* e = std::getenv("SV_SGBM_FUSED");
@@ -921,7 +1091,26 @@ int sgbm_dp(int D) {
 
 int launch_sgbm(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
     if (a.H <= 0 || a.W <= 0 || nf <= 0) return 0;
-    if (a.Wb > 0) {
+    if (a.Wb > 0 && sgbm_cost_fused(a.D, a.r)) {
+        if (a.r > kMaxR) return (int)hipErrorInvalidValue;
+        // pixel cost + window sums in one pass (k_sgbm_cost): one wave per (CL-column chunk,
+        // 64 disparities, row band, frame); bands of >= 32 rows (the ring warm-up is 2r+1 rows)
+        const int cl = a.r <= 2 ? 32 : 16;                  // CostCfg<R>::CL
+        const int chunks = (a.Wb + cl - 1) / cl, ndg = (a.D + 63) / 64;
+        const long long per_band = (long long)chunks * ndg * nf;
+        const int nb = (int)std::max<long long>(1, std::min<long long>(a.H / 32, (16384 + per_band - 1) / per_band));
+        const int vb = (a.H + nb - 1) / nb;
+        const dim3 grid((unsigned)chunks, (unsigned)(ndg * ((a.H + vb - 1) / vb)), (unsigned)nf);
+        hipLaunchKernelGGL(k_sgbm_records, dim3((a.W + 255) / 256, 2 * a.H, nf), dim3(256), 0, s, a);
+        switch (a.r) {
+#define SV_COST_R(R) case R: hipLaunchKernelGGL(k_sgbm_cost<R>, grid, dim3(64), 0, s, a, vb, ndg); break;
+            SV_COST_R(0) SV_COST_R(1) SV_COST_R(2) SV_COST_R(3) SV_COST_R(4)
+#undef SV_COST_R
+        }
+        const int e = a.l32 ? launch_paths_t<int32_t>(a, nf, s, aux, fork, join)
+                            : launch_paths_t<int16_t>(a, nf, s, aux, fork, join);
+        if (e) return e;
+    } else if (a.Wb > 0) {
         if (a.r > kMaxR) return (int)hipErrorInvalidValue;
         const dim3 grid((unsigned)((a.Wb + kHX - 1) / kHX), (unsigned)a.H, (unsigned)nf);
         const size_t lds = (size_t)(2 * kHX + 4 * a.r + a.D - 1) * sizeof(uint4);

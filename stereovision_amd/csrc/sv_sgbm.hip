@@ -532,8 +532,10 @@ __device__ __forceinline__ int lane_min(const int (&v)[DPL]) {
 
 // Horizontal paths: 64/LPC rows per wave; blockIdx.y = 0: left->right into Llr, 1:
 // right->left into Lrl.
-template <int DPL, int LPC, typename LT, int PF>
-__global__ __launch_bounds__(64) void k_sgbm_hpath(SgbmArgs a) {
+// WPE: waves per SIMD the register budget allows (2 for frame batches, where ~2 lines' waves
+// share a SIMD; 1 with deeper prefetch for single frames, whose ~540 waves leave SIMDs idle)
+template <int DPL, int LPC, typename LT, int PF, int WPE>
+__global__ __launch_bounds__(64, WPE) void k_sgbm_hpath(SgbmArgs a) {
     if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
     constexpr int NL = 64 / LPC;
     const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
@@ -720,8 +722,9 @@ __global__ __launch_bounds__(64) void k_sgbm_wta(SgbmArgs a) {
 // is never stored, so the R->L volume's write and the WTA's read of it (2 of the pipeline's
 // volume passes) disappear, and so does the WTA launch.  The WTA work hangs off the DP
 // chain (only `prev` and the path minimum are loop-carried), so it fills the chain's gaps.
+// 2 waves per SIMD (256 VGPRs) where that does not spill: batches put ~2 lines' waves on a SIMD
 template <int DPL, typename LT, int PF>
-__global__ __launch_bounds__(64) void k_sgbm_rl_wta(SgbmArgs a) {
+__global__ __launch_bounds__(64, DPL <= 16 ? 2 : 1) void k_sgbm_rl_wta(SgbmArgs a) {
     if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
     constexpr int LPC = 16, NL = 64 / LPC;
     const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
@@ -1024,13 +1027,19 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
     SV_VPATH(32, 12, 4) SV_VPATH(32, 16, 3)
 #undef SV_VPATH
     if (aux && hipEventRecord(join, aux) != hipSuccess) return (int)hipErrorLaunchFailure;
-#define SV_HPATH(L, N, PF)                                                           \
+#define SV_HPATH(L, N, PF, WPE)                                                      \
     if (!h && ph.lpc == L && ph.dpl == N) {                                          \
-        hipLaunchKernelGGL((k_sgbm_hpath<N, L, LT, PF>), gh, dim3(64), 0, s, a);    \
+        hipLaunchKernelGGL((k_sgbm_hpath<N, L, LT, PF, WPE>), gh, dim3(64), 0, s, a); \
         h = true;                                                                    \
     }
-    SV_HPATH(16, 1, 24) SV_HPATH(16, 2, 24) SV_HPATH(16, 4, 16) SV_HPATH(16, 8, 16) SV_HPATH(16, 12, 10)
-    SV_HPATH(16, 16, 8) SV_HPATH(16, 20, 6) SV_HPATH(16, 24, 6) SV_HPATH(16, 32, 4)
+    if (fused) {   // batches: 2 waves per SIMD
+        SV_HPATH(16, 1, 24, 2) SV_HPATH(16, 2, 24, 2) SV_HPATH(16, 4, 16, 2) SV_HPATH(16, 8, 12, 2)
+        SV_HPATH(16, 12, 8, 2) SV_HPATH(16, 16, 6, 2) SV_HPATH(16, 20, 4, 2) SV_HPATH(16, 24, 4, 2)
+        SV_HPATH(16, 32, 4, 1)
+    }
+    SV_HPATH(16, 1, 24, 1) SV_HPATH(16, 2, 24, 1) SV_HPATH(16, 4, 16, 1) SV_HPATH(16, 8, 16, 1)
+    SV_HPATH(16, 12, 10, 1) SV_HPATH(16, 16, 8, 1) SV_HPATH(16, 20, 6, 1) SV_HPATH(16, 24, 6, 1)
+    SV_HPATH(16, 32, 4, 1)
 #undef SV_HPATH
     if (aux && hipStreamWaitEvent(s, join, 0) != hipSuccess) return (int)hipErrorLaunchFailure;
     if (fused) {
@@ -1040,7 +1049,7 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
             hipLaunchKernelGGL((k_sgbm_rl_wta<N, LT, PF>), gf, dim3(64), 0, s, a);   \
             w = true;                                                                \
         }
-        SV_RLWTA(1, 16) SV_RLWTA(2, 16) SV_RLWTA(4, 12) SV_RLWTA(8, 8) SV_RLWTA(12, 6) SV_RLWTA(16, 4)
+        SV_RLWTA(1, 16) SV_RLWTA(2, 16) SV_RLWTA(4, 8) SV_RLWTA(8, 4) SV_RLWTA(12, 3) SV_RLWTA(16, 2)
         SV_RLWTA(20, 3) SV_RLWTA(24, 3) SV_RLWTA(32, 2)
 #undef SV_RLWTA
     }

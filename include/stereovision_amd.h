@@ -206,7 +206,10 @@ int sv_depth_map_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
  * one launch per kernel fills the GPU even for small frames.  Outputs are dense per frame
  * (frame z of an H x W output at + z*H*W elements) except sv_disparity_batch_dev's int16
  * map, which takes an explicit out_pitch / out_frame_stride (elements).  The context's
- * internal scratch (sv_depth_map_batch_dev) assumes calls on one context use one stream. */
+ * internal scratch is ordered across streams (a call on another stream waits for the
+ * previous user of the scratch).  cost = SV_COST_SGBM runs every SGBM stage once per chunk of
+ * up to 32 frames (volumes of ~1.5 GB per 1080p D=128 frame, within a 48 GiB scratch budget);
+ * chunks of >= 8 frames fuse the right-to-left path with the winner-take-all. */
 int sv_disparity_batch_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
                            int n_frames, int H, int W, int pitch, int64_t frame_stride,
                            int min_disp, int num_disp, int win, int cost, int16_t* d_disp16,

@@ -179,6 +179,82 @@ def verify01_sel(net, outs, n_real, ranks):
     return True
 
 
+# optimal 5-comparator sorting network for 4 inputs
+SORT4 = [(0, 1), (2, 3), (0, 2), (1, 3), (1, 2)]
+
+
+def sorted_column_inputs():
+    """Bit-sliced 0-1 inputs of the 20 shared values v[i*5+j] (row i of the 4, column j of
+    the 5) whose columns are sorted (v[j] <= v[5+j] <= v[10+j] <= v[15+j]): 5^5 = 3125 cases,
+    one bit each.  Thresholding an integer input with sorted columns gives one of these, and
+    min/max networks commute with thresholding, so a network that selects the right ranks
+    for all of them selects them for every integer input with sorted columns."""
+    import itertools
+    cases = list(itertools.product(range(5), repeat=5))   # ones per column
+    wires = [0] * 20
+    for t, ks in enumerate(cases):
+        for j, k in enumerate(ks):
+            for i in range(4 - k, 4):
+                wires[i * 5 + j] |= 1 << t
+    return cases, wires
+
+
+def build_sel20s(ranks, seeds=range(8)):
+    """Ranks of the 20 shared values when each column of 4 arrives sorted (the columns are
+    sorted once in LDS and shared by the 5 windows that read them).  Start: Batcher on 32
+    wires with the 5 columns on its first five 4-wire blocks (+inf pads above), so its
+    first two levels are exactly the column sorts; then drop comparators greedily (seeded
+    order) while the outputs stay correct on every sorted-column 0-1 input; the cheapest
+    seed (min/max op count after liveness pruning) wins."""
+    import random
+    cases, w0 = sorted_column_inputs()
+    exp = []
+    for k in ranks:
+        m = 0
+        for t, ks in enumerate(cases):
+            if 20 - sum(ks) <= k:
+                m |= 1 << t
+        exp.append(m)
+    base, outs = build_sel(20, 32, 0, ranks)
+    v_of = {w: (w % 4) * 5 + (w // 4) for w in range(20)}   # Batcher wire -> v index
+    net0 = [(v_of[a], v_of[b]) for a, b, _ in base]
+    outs = [v_of[o] for o in outs]
+
+    def ok(net):
+        v = list(w0)
+        for a, b in net:
+            v[a], v[b] = v[a] & v[b], v[a] | v[b]
+        return all(v[o] == e for o, e in zip(outs, exp))
+
+    def liveness(net):
+        live, kept, ops = set(outs), [], 0
+        for a, b in reversed(net):
+            na, nb = a in live, b in live
+            if na or nb:
+                kept.append((a, b, int(na) | (int(nb) << 1)))
+                ops += 2 if na and nb else 1
+                live.update((a, b))
+        kept.reverse()
+        return ops, kept
+
+    assert ok(net0)
+    best = None
+    for seed in seeds:
+        rng = random.Random(seed)
+        net = list(net0)
+        order = list(range(len(net)))
+        rng.shuffle(order)
+        drop = set()
+        for i in order:
+            if ok([c for k, c in enumerate(net) if k not in drop and k != i]):
+                drop.add(i)
+        ops, kept = liveness([c for k, c in enumerate(net) if k not in drop])
+        if best is None or ops < best[0]:
+            best = (ops, kept)
+    assert ok([(a, b) for a, b, _ in best[1]])
+    return best[1], outs, best[0]
+
+
 # optimal 9-comparator sorting network for 5 inputs (Knuth, TAOCP 5.3.4)
 SORT5 = [(0, 1), (3, 4), (2, 4), (2, 3), (1, 4), (0, 3), (0, 2), (1, 3), (1, 2)]
 
@@ -208,6 +284,13 @@ def main(check: bool = True):
         assert v == sorted(vals)
     if check:
         assert verify01_sel(sel, sel_out, 20, ranks), "SEL20 0-1 check failed"
+    # SEL20S: the same ranks when every column of 4 is pre-sorted (k_median_i16)
+    sels, sels_out, sels_ops = build_sel20s(ranks)
+    for _ in range(4000):
+        vals = [rng.randint(-40, 40) for _ in range(20)]
+        cols = [sorted(vals[j::5]) for j in range(5)]
+        srt = [cols[j][i] for i in range(4) for j in range(5)]
+        assert run_sel(sels, sels_out, srt) == sorted(vals)[7:13]
     here = os.path.dirname(os.path.abspath(__file__))
     lines = [
         "// Generated by gen_median_net.py — do not edit.",
@@ -237,12 +320,29 @@ def main(check: bool = True):
     for a, b, u in sel:
         lines.append(f"  {{{a}, {b}, {u}}},")
     lines.append("};")
+    lines += [
+        "",
+        f"// Ranks 7..12 (sorted) of 20 values v[i*5+j] whose 5 columns (i = 0..3) arrive",
+        f"// sorted: {len(sels)} comparators ({sels_ops} min/max ops), Batcher on 32 wires",
+        "// (columns on its first five 4-wire blocks) greedily pruned; verified over every",
+        "// sorted-column 0-1 input (0-1 principle restricted to sorted columns).",
+        f"#define SV_SEL20S_NCMP {len(sels)}",
+        "static constexpr unsigned char SV_SEL20S_OUT[6] = {" + ", ".join(map(str, sels_out)) + "};",
+        "static constexpr unsigned char SV_SEL20S_NET[SV_SEL20S_NCMP][3] = {",
+    ]
+    for a, b, u in sels:
+        lines.append(f"  {{{a}, {b}, {u}}},")
+    lines.append("};")
+    lines += ["", "// optimal 5-comparator sort of 4 values",
+              "static constexpr unsigned char SV_SORT4_NET[5][2] = {" +
+              ", ".join(f"{{{a}, {b}}}" for a, b in SORT4) + "};"]
     lines += ["", "// optimal 9-comparator sort of 5 values",
               "static constexpr unsigned char SV_SORT5_NET[9][2] = {" +
               ", ".join(f"{{{a}, {b}}}" for a, b in SORT5) + "};"]
     with open(os.path.join(here, "sv_median_net.h"), "w") as f:
         f.write("\n".join(lines) + "\n")
-    print(f"{len(net)} comparators, output wire {out_slot}; SEL20 {len(sel)} comparators")
+    print(f"{len(net)} comparators, output wire {out_slot}; SEL20 {len(sel)} comparators; "
+          f"SEL20S {len(sels)} comparators ({sels_ops} ops)")
 
 
 if __name__ == "__main__":

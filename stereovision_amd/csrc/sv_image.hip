@@ -427,11 +427,14 @@ __device__ __forceinline__ void post_one(const PostParams& pp, size_t i, float d
 // Median-of-25 for the int16 map, 4 output rows per lane.
 // Two vertically adjacent 5x5 windows (rows y, y+1) share 20 of their 25 values (rows
 // y-1..y+2).  The 13th smallest of a window lies in ranks 7..12 of the shared 20 or among
-// its 5 unique values, so: SEL20 (89 comparators) sorts ranks 7..12 of the shared 20 once
-// per row pair, each window sorts its unique row (9 comparators), and the median is the
-// 6th smallest of (6 sorted + 5 sorted) = min_i max(C_i, U_{6-i}) (10 ops).  Each lane
-// packs two row pairs (rows y,y+1 | y+2,y+3) into short2 halves, so one v_pk_min/max_i16
-// serves both: ~55 ops per output instead of 113 for the plain 25-input network.
+// its 5 unique values.  The shared 20 are 5 columns of 4, and each column is read by 5
+// horizontally adjacent windows, so every column is sorted once (5 comparators, in LDS),
+// and SEL20S (59 comparators, 104 ops; 164 for the unsorted SEL20) takes ranks 7..12 of
+// the 5 sorted columns once per row pair; each window sorts its unique row (9 comparators),
+// and the median is the 6th smallest of (6 sorted + 5 sorted) = min_i max(C_i, U_{6-i})
+// (10 ops).  Each lane packs two row pairs (rows y,y+1 | y+2,y+3) into short2 halves, so
+// one v_pk_min/max_i16 serves both: ~43 ops per output (55 without the column sorts, 113
+// for the plain 25-input network).
 typedef short s2 __attribute__((ext_vector_type(2)));
 constexpr int MT_W = 64, MT_H = 8;        // k_median_f32 tile
 constexpr int MQ_W = 64, MQ_H = 16;       // k_median_i16: 64 columns x 16 rows per block
@@ -464,6 +467,8 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
                                                     PostParams pp, long long fs_in, long long fs_out) {
     // t2[r][c] = (tile row r, tile row r+2) of column x0-2+c; tile row r = image row y0-2+r
     __shared__ uint32_t t2[MQ_H + 2][MQ_W + 4];
+    // srt[g][i][c]: rank i of column c over the shared pair rows 4g+1..4g+4 of t2
+    __shared__ uint32_t srt[MQ_H / 4][4][MQ_W + 4];
     if (blockIdx.z) {   // frame batch
         in += blockIdx.z * fs_in;
         const long long o = blockIdx.z * fs_out;
@@ -506,15 +511,36 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
     // every thread computes (the tile is clamped, so columns/rows past the edge read valid
     // data); only in-range pixels are written, after the LDS transpose below
     const int tx = threadIdx.x % MQ_W, tb = 4 * (threadIdx.x / MQ_W);
+    {   // sort each column of the 4 shared pair rows once (5 comparators); the 5 windows
+        // that read a column share the sort.  Thread (tb, tx) sorts column tx of its row
+        // group; the 4 columns past 64 of each group go to the first 16 lanes of wave 0
+        auto sort_col = [&](int g4, int c) {
+            s2 w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w[i] = as_s2(t2[g4 + 1 + i][c]);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const int a = SV_SORT4_NET[k][0], b = SV_SORT4_NET[k][1];
+                const s2 lo = __builtin_elementwise_min(w[a], w[b]);
+                w[b] = __builtin_elementwise_max(w[a], w[b]);
+                w[a] = lo;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) srt[g4 >> 2][i][c] = __builtin_bit_cast(uint32_t, w[i]);
+        };
+        sort_col(tb, tx);
+        if (threadIdx.x < 16) sort_col(4 * (threadIdx.x >> 2), MQ_W + (threadIdx.x & 3));
+    }
+    __syncthreads();
 
     s2 v[20];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 5; ++j) v[i * 5 + j] = as_s2(t2[tb + 1 + i][tx + j]);
+        for (int j = 0; j < 5; ++j) v[i * 5 + j] = as_s2(srt[tb >> 2][i][tx + j]);
 #pragma unroll
-    for (int c = 0; c < SV_SEL20_NCMP; ++c) {
-        const int a = SV_SEL20_NET[c][0], b = SV_SEL20_NET[c][1], use = SV_SEL20_NET[c][2];
+    for (int c = 0; c < SV_SEL20S_NCMP; ++c) {
+        const int a = SV_SEL20S_NET[c][0], b = SV_SEL20S_NET[c][1], use = SV_SEL20S_NET[c][2];
         const s2 lo = __builtin_elementwise_min(v[a], v[b]);
         const s2 hi = __builtin_elementwise_max(v[a], v[b]);
         if (use & 1) v[a] = lo;
@@ -533,10 +559,10 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
             u[b] = __builtin_elementwise_max(u[a], u[b]);
             u[a] = lo;
         }
-        s2 r = v[SV_SEL20_OUT[5]];
+        s2 r = v[SV_SEL20S_OUT[5]];
 #pragma unroll
         for (int i = 0; i < 5; ++i)
-            r = __builtin_elementwise_min(r, __builtin_elementwise_max(v[SV_SEL20_OUT[i]], u[4 - i]));
+            r = __builtin_elementwise_min(r, __builtin_elementwise_max(v[SV_SEL20S_OUT[i]], u[4 - i]));
         m[h] = r;
     }
     // m[0] = (row y, row y+2), m[1] = (row y+1, row y+3): park the four medians in LDS, then

@@ -893,7 +893,20 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     const int ooff = 2 * ((y + jq) * a.opitch + xs + eb);   // bytes
     // 32-bit buffer offsets from one SGPR descriptor (no 64-bit per-lane addresses to keep)
     const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFFF, 0x00020000);
-    const int emax = (l < 16 && (l & 1) == 0 && y + jq < a.row1) ? max(0, min(S, a.X1 - xs)) : 0;
+    // 32-lane groups (D 65..128) join the two DPP rows of a chunk's two step pairs with ONE
+    // v_permlane16_swap of the pairs' keys (instead of a mov + swap + min per pair): the
+    // rows then hold different pairs, and both rows emit.  Which row receives which pair is
+    // read off the swap itself once (pofs = the step offset of the lane's pair in its chunk).
+    // (r <= 4: r 5 has no register left for the held key)
+    constexpr bool J2 = R <= 4;
+    const bool join2 = J2 && LPG == 32;
+    int pofs = 0;
+    if (join2) {
+        const auto p = __builtin_amdgcn_permlane16_swap((uint32_t)lane, (uint32_t)lane + 64u, false, false);
+        // min(p[0], p[1]) of a lane comes from the first operand's values iff both p[k] < 64
+        pofs = (max(p[0], p[1]) < 64u) ? 0 : 2;
+    }
+    const int emax = ((l & 1) == 0 && (join2 || l < 16) && y + jq < a.row1) ? max(0, min(S, a.X1 - xs)) : 0;
 
     // whole bodies of U = 4*W2 steps, no exits inside a body (an exit per chunk made LLVM
     // shuffle the rings); the first body skips its first e0 chunks by a uniform branch
@@ -902,6 +915,7 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
         for (int ch = 0; ch < W2; ++ch, t0 += 4) {
             if (t0 < 0) continue;            // the first body's skipped chunks (uniform)
             uint32_t bk[4][2];
+            uint32_t kA;                     // join2: key of the chunk's first pair (set at u = 1)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int slot = (4 * ch + u) % W2;
@@ -956,25 +970,39 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                     bk[q][u & 1] = min(min(kq[0], kq[1]), min(kq[2], kq[3]));
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                if ((u & 1) && t0 + u >= 2 * R) {   // steps u-1, u: 8 keys (row q, step j) at v[2q + j]
-                    // (pairs wholly inside the 2r warm-up steps emit nothing: skipped)
+                // steps u-1, u: 8 keys (row q, step j) at v[2q + j]; pairs wholly inside the 2r
+                // warm-up steps emit nothing and are skipped (LPG 32: chunks wholly inside them)
+                if ((u & 1) && t0 + (join2 ? 3 : u) >= 2 * R) {
                     uint32_t v[8];
 #pragma unroll
                     for (int i = 0; i < 8; ++i) v[i] = bk[i >> 1][i & 1];
                     reduce_scatter8_bm(v, lane & 15);
                     uint32_t key = v[0];
-                    if (LPG >= 32) {   // rows 0,1 (and 2,3) of the wave: min with lane ^ 16
-                        const auto p = __builtin_amdgcn_permlane16_swap(key, key, false, false);
-                        key = min(p[0], p[1]);
+                    if (join2) {
+                        if (u == 1) {
+                            kA = key;
+                        } else {   // pair (0,1) in kA, pair (2,3) in key: one swap joins both
+                            const auto p = __builtin_amdgcn_permlane16_swap(kA, key, false, false);
+                            key = min(p[0], p[1]);
+                            const int tt = t0 + pofs;
+                            if ((unsigned)(tt + eb) < (unsigned)emax)
+                                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16),
+                                                                      orsrc, ooff + 2 * tt, 0, 0);
+                        }
+                    } else {
+                        if (LPG >= 32) {   // rows 0,1 (and 2,3) of the wave: min with lane ^ 16
+                            const auto p = __builtin_amdgcn_permlane16_swap(key, key, false, false);
+                            key = min(p[0], p[1]);
+                        }
+                        if (LPG == 64) {   // halves: min with lane ^ 32
+                            const auto p = __builtin_amdgcn_permlane32_swap(key, key, false, false);
+                            key = min(p[0], p[1]);
+                        }
+                        const int tt = t0 + u - 1;
+                        if ((unsigned)(tt + eb) < (unsigned)emax)
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16),
+                                                                  orsrc, ooff + 2 * tt, 0, 0);
                     }
-                    if (LPG == 64) {   // halves: min with lane ^ 32
-                        const auto p = __builtin_amdgcn_permlane32_swap(key, key, false, false);
-                        key = min(p[0], p[1]);
-                    }
-                    const int tt = t0 + u - 1;
-                    if ((unsigned)(tt + eb) < (unsigned)emax)
-                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16), orsrc,
-                                                              ooff + 2 * tt, 0, 0);
                 }
             }
         }

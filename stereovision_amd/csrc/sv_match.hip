@@ -897,16 +897,18 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     // v_permlane16_swap of the pairs' keys (instead of a mov + swap + min per pair): the
     // rows then hold different pairs, and both rows emit.  Which row receives which pair is
     // read off the swap itself once (pofs = the step offset of the lane's pair in its chunk).
-    // (r <= 4: r 5 has no register left for the held key)
-    constexpr bool J2 = R <= 4;
-    const bool join2 = J2 && LPG == 32;
+    // 64-lane groups (D 129..256) do the same and then join the wave's halves with one
+    // v_permlane32_swap; rows 0 and 1 emit.  (r <= 4 and the packed r 6..7: r 5 has no
+    // register left for the held key)
+    constexpr bool J2 = R <= 4 || PK;
+    const bool join2 = J2 && LPG >= 32;
     int pofs = 0;
     if (join2) {
         const auto p = __builtin_amdgcn_permlane16_swap((uint32_t)lane, (uint32_t)lane + 64u, false, false);
         // min(p[0], p[1]) of a lane comes from the first operand's values iff both p[k] < 64
         pofs = (max(p[0], p[1]) < 64u) ? 0 : 2;
     }
-    const int emax = ((l & 1) == 0 && (join2 || l < 16) && y + jq < a.row1) ? max(0, min(S, a.X1 - xs)) : 0;
+    const int emax = ((l & 1) == 0 && l < (join2 ? 32 : 16) && y + jq < a.row1) ? max(0, min(S, a.X1 - xs)) : 0;
 
     // whole bodies of U = 4*W2 steps, no exits inside a body (an exit per chunk made LLVM
     // shuffle the rings); the first body skips its first e0 chunks by a uniform branch
@@ -982,8 +984,12 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                         if (u == 1) {
                             kA = key;
                         } else {   // pair (0,1) in kA, pair (2,3) in key: one swap joins both
-                            const auto p = __builtin_amdgcn_permlane16_swap(kA, key, false, false);
+                            auto p = __builtin_amdgcn_permlane16_swap(kA, key, false, false);
                             key = min(p[0], p[1]);
+                            if (LPG == 64) {   // rows 0 and 2 hold the same pair (1 and 3 the other)
+                                p = __builtin_amdgcn_permlane32_swap(key, key, false, false);
+                                key = min(p[0], p[1]);
+                            }
                             const int tt = t0 + pofs;
                             if ((unsigned)(tt + eb) < (unsigned)emax)
                                 __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16),

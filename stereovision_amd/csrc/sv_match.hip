@@ -889,18 +889,15 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     // lanes of a group emit
     // (32-bit per-lane state only: output offset of step 0 and the emit window)
     const int jq = (lane >> 2) & 3, ju = (lane >> 1) & 1;   // key (l >> 1) & 7 = 2 jq + ju
-    const int eb = ju - 2 * R;                          // step t emits column xs + t + eb
-    const int ooff = 2 * ((y + jq) * a.opitch + xs + eb);   // bytes
-    // 32-bit buffer offsets from one SGPR descriptor (no 64-bit per-lane addresses to keep)
-    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFFF, 0x00020000);
     // 32-lane groups (D 65..128) join the two DPP rows of a chunk's two step pairs with ONE
     // v_permlane16_swap of the pairs' keys (instead of a mov + swap + min per pair): the
     // rows then hold different pairs, and both rows emit.  Which row receives which pair is
-    // read off the swap itself once (pofs = the step offset of the lane's pair in its chunk).
-    // 64-lane groups (D 129..256) do the same and then join the wave's halves with one
-    // v_permlane32_swap; rows 0 and 1 emit.  (r <= 4 and the packed r 6..7: r 5 has no
-    // register left for the held key)
-    constexpr bool J2 = R <= 4 || PK;
+    // read off the swap itself once (pofs = the step offset of the lane's pair in its chunk,
+    // folded into eb).  64-lane groups (D 129..256) do the same and then join the wave's
+    // halves with one v_permlane32_swap; rows 0 and 1 emit.  Not for r 5 (254 VGPRs): with
+    // the join in its body the compiler spills ~1,000 VGPRs (the held key parked in LDS
+    // instead does not change that).
+    constexpr bool J2 = R != 5;
     const bool join2 = J2 && LPG >= 32;
     int pofs = 0;
     if (join2) {
@@ -908,6 +905,12 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
         // min(p[0], p[1]) of a lane comes from the first operand's values iff both p[k] < 64
         pofs = (max(p[0], p[1]) < 64u) ? 0 : 2;
     }
+    // step t emits column xs + t + eb (join2: the chunk starting at step t emits the lane's
+    // pair at column xs + t + eb)
+    const int eb = ju - 2 * R + pofs;
+    const int ooff = 2 * ((y + jq) * a.opitch + xs + eb);   // bytes
+    // 32-bit buffer offsets from one SGPR descriptor (no 64-bit per-lane addresses to keep)
+    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFFF, 0x00020000);
     const int emax = ((l & 1) == 0 && l < (join2 ? 32 : 16) && y + jq < a.row1) ? max(0, min(S, a.X1 - xs)) : 0;
 
     // whole bodies of U = 4*W2 steps, no exits inside a body (an exit per chunk made LLVM
@@ -990,7 +993,7 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                                 p = __builtin_amdgcn_permlane32_swap(key, key, false, false);
                                 key = min(p[0], p[1]);
                             }
-                            const int tt = t0 + pofs;
+                            const int tt = t0;
                             if ((unsigned)(tt + eb) < (unsigned)emax)
                                 __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16),
                                                                       orsrc, ooff + 2 * tt, 0, 0);

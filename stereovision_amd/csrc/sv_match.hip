@@ -794,7 +794,7 @@ __device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
 }
 
-template <int R>
+template <int R, int LPGT>
 __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     using P = PackCfg<COST_SAD4, R>;
     constexpr int NW = P::NW, NC = P::NC, W2 = 2 * R + 1;
@@ -810,9 +810,10 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
         a.out += blockIdx.z * a.fs_out;
     }
     const int lane = threadIdx.x;
-    const int LPG = a.lpg;
+    constexpr int LPG = LPGT;                           // lanes per group (template: no
+                                                        // branches between the steps)
     const int S = a.segm;                               // segment width per group (multiple of 4)
-    const int WC = (64 >> a.lpg_log2) * S;
+    const int WC = (64 / LPG) * S;
     constexpr int U = 4 * W2;                           // steps per unrolled body
     // steps per segment: S outputs + 2r warm-up, in chunks of 4; whole bodies of U steps,
     // the first body entered at chunk e0 (its first e0 chunks skipped)
@@ -850,7 +851,7 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     __syncthreads();
     if (y >= a.row1) return;
 
-    const int g = lane >> a.lpg_log2;
+    const int g = lane / LPG;
     const int l = lane & (LPG - 1);
     const int xs = xw + g * S;                          // first output column of the segment
     // step t enters column xs - r + t; lane l, disparity idx 4l + k reads R index iR0 + t - k
@@ -894,11 +895,10 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     // rows then hold different pairs, and both rows emit.  Which row receives which pair is
     // read off the swap itself once (pofs = the step offset of the lane's pair in its chunk,
     // folded into eb).  64-lane groups (D 129..256) do the same and then join the wave's
-    // halves with one v_permlane32_swap; rows 0 and 1 emit.  Not for r 5 (254 VGPRs): with
-    // the join in its body the compiler spills ~1,000 VGPRs (the held key parked in LDS
-    // instead does not change that).
-    constexpr bool J2 = R != 5;
-    const bool join2 = J2 && LPG >= 32;
+    // halves with one v_permlane32_swap; rows 0 and 1 emit.  (r 5 fits it since LPG is a
+    // template parameter and the body has no branches: 244 VGPRs; with a runtime LPG and
+    // branches around the reductions the allocator spilled ~1,000.)
+    constexpr bool join2 = LPG >= 32;
     int pofs = 0;
     if (join2) {
         const auto p = __builtin_amdgcn_permlane16_swap((uint32_t)lane, (uint32_t)lane + 64u, false, false);
@@ -975,9 +975,11 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                     bk[q][u & 1] = min(min(kq[0], kq[1]), min(kq[2], kq[3]));
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                // steps u-1, u: 8 keys (row q, step j) at v[2q + j]; pairs wholly inside the 2r
-                // warm-up steps emit nothing and are skipped (LPG 32: chunks wholly inside them)
-                if ((u & 1) && t0 + (join2 ? 3 : u) >= 2 * R) {
+                // steps u-1, u: 8 keys (row q, step j) at v[2q + j].  Warm-up pairs are reduced
+                // too (their keys are not emitted): no branch, so a chunk is one basic block and
+                // the scheduler can interleave a reduction's DPP / permlane chain with the next
+                // step's independent cost work
+                if (u & 1) {
                     uint32_t v[8];
 #pragma unroll
                     for (int i = 0; i < 8; ++i) v[i] = bk[i >> 1][i & 1];
@@ -994,9 +996,11 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                                 key = min(p[0], p[1]);
                             }
                             const int tt = t0;
-                            if ((unsigned)(tt + eb) < (unsigned)emax)
-                                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16),
-                                                                      orsrc, ooff + 2 * tt, 0, 0);
+                            // non-emitting lanes store past the buffer's range (dropped by the
+                            // hardware bounds check, as in composable_kernel): no exec-mask branch
+                            const int off = (unsigned)(tt + eb) < (unsigned)emax ? ooff + 2 * tt : (int)0x80000000u;
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16),
+                                                                  orsrc, off, 0, 0);
                         }
                     } else {
                         if (LPG >= 32) {   // rows 0,1 (and 2,3) of the wave: min with lane ^ 16
@@ -1008,9 +1012,9 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                             key = min(p[0], p[1]);
                         }
                         const int tt = t0 + u - 1;
-                        if ((unsigned)(tt + eb) < (unsigned)emax)
-                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16),
-                                                                  orsrc, ooff + 2 * tt, 0, 0);
+                        const int off = (unsigned)(tt + eb) < (unsigned)emax ? ooff + 2 * tt : (int)0x80000000u;
+                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16),
+                                                              orsrc, off, 0, 0);
                     }
                 }
             }
@@ -1138,9 +1142,9 @@ size_t ring_lds_bytes(int lpg, int seg, int r) {
     return (size_t)(nl + nrp) * (r <= 5 ? 24 : 32);
 }
 
-template <int R>
-int launch_ring_r(const MatchParams& a, size_t lds, hipStream_t s) {
-    auto fn = k_match_ring<R>;
+template <int R, int LPG>
+int launch_ring_rl(const MatchParams& a, size_t lds, hipStream_t s) {
+    auto fn = k_match_ring<R, LPG>;
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return (int)e;
@@ -1149,6 +1153,15 @@ int launch_ring_r(const MatchParams& a, size_t lds, hipStream_t s) {
     dim3 grid((a.X1 - a.X0 + wc - 1) / wc, (a.row1 - a.row0 + 3) / 4, a.nf > 1 ? a.nf : 1);
     hipLaunchKernelGGL(fn, grid, dim3(64), lds, s, a);
     return (int)hipGetLastError();
+}
+template <int R>
+int launch_ring_r(const MatchParams& a, size_t lds, hipStream_t s) {
+    switch (a.lpg) {
+        case 16: return launch_ring_rl<R, 16>(a, lds, s);
+        case 32: return launch_ring_rl<R, 32>(a, lds, s);
+        case 64: return launch_ring_rl<R, 64>(a, lds, s);
+    }
+    return (int)hipErrorInvalidValue;
 }
 
 int launch_ring(const MatchParams& a0, hipStream_t s) {

@@ -49,7 +49,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from stereovision_amd.engine import (Communicator, Engine, device_count, depth_map_rows_multi,  # noqa: E402
-                                     get_engine, multi_gpu_depth_map_dev)
+                                     depth_map_rows_scatter, get_engine, multi_gpu_depth_map_dev)
 from stereovision_amd.synthetic import stereo_batch, stereo_pair, synthetic_calibration, to_bgr  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -368,8 +368,85 @@ def live_pmc(args, kernel_tag="k_match", timeout=150):
     return res
 
 
+# ---- verification of the timed outputs (after the timed region) --------------------------
+class Verifier:
+    """Bit-exact check of maps the timed steps produced against the C oracle
+    (oracle/sv_oracle.c, the engine's semantics; test infrastructure used here only as the
+    checker): (depth_final, disparity, depth_normalized) of create_depth_map per frame
+    (depth_map.py:909-936), the Harris response within 1e-4 (north_star)."""
+
+    def __init__(self, D, win, cost, threads):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import sv_oracle_c as C  # test infrastructure: the checker only
+        self.C, self.D, self.win, self.threads = C, D, win, threads
+        self.cost = {"sad": 0, "ssd": 1, "hog": 2}[cost]
+        self.checked, self.failed = [], []
+
+    def frame(self, tag, L, R, got_depth, got_disp, got_norm):
+        e_depth, e_disp, e_norm = self.C.depth_map(L, R, 0, self.D, self.win, self.cost, 0.3, 2.0,
+                                                   self.threads)
+        ok = (np.array_equal(got_disp, e_disp) and np.array_equal(got_depth, e_depth)
+              and np.array_equal(got_norm, e_norm))
+        self.checked.append(tag)
+        if not ok:
+            bad = int((got_disp != e_disp).sum())
+            self.failed.append(f"{tag}: {bad} disparity pixels differ")
+        return ok
+
+    def harris(self, tag, L, got):
+        exp = self.C.harris(L)
+        err = float(np.max(np.abs(got.astype(np.float64) - exp))) if exp.size else 0.0
+        self.checked.append(tag + " harris")
+        if not err <= 1e-4:
+            self.failed.append(f"{tag}: Harris max |diff| {err:.3g} > 1e-4")
+
+    def result(self):
+        return not self.failed
+
+
+def fetch_maps(eng, d_depth, d_disp, d_norm, index, n_px, H, W):
+    """Frame `index` of dense per-frame output stacks -> host (depth, disparity, norm)."""
+    return (eng.to_host(d_depth + 4 * n_px * index, (H, W), np.float32),
+            eng.to_host(d_disp + 4 * n_px * index, (H, W), np.float32),
+            eng.to_host(d_norm + n_px * index, (H, W), np.uint8))
+
+
+def dist_summary(ngpu, launched, pg=None, comms=None, gather=False, rowtile=False,
+                 gather_ms=0.0, gather_n=0, scatter_ms=0.0, scatter_n=0, gather_wall_s=0.0,
+                 steps=0, gather_bytes=0, scatter_bytes=0, reason=""):
+    """The multi-GPU fields of the bench line (None for one GPU): the backend the run used,
+    how many ranks the RCCL communicator saw (0 + the reason when it fell back), and the
+    gather / scatter time per step from HIP events on the root's stream (these include the
+    wait for the slowest rank's maps)."""
+    if ngpu <= 1:
+        return None
+    if launched:
+        backend = pg.backend
+        rccl_ranks = pg.rccl_ranks
+        why = pg.reason
+    else:
+        backend = "rccl" if comms else "peer"
+        rccl_ranks = len(comms) if comms else 0
+        why = "" if comms else (reason or "RCCL group not requested")
+    out = {"backend": backend, "rccl_ranks": rccl_ranks, "rccl_reason": why or None,
+           "process_model": "one process per GPU" if launched else "one process, all devices",
+           "gather": bool(gather or rowtile),
+           "gather_us_per_step": round(gather_ms * 1e3 / gather_n, 2) if gather_n else None,
+           "gather_events": gather_n,
+           "gather_bytes_per_step": gather_bytes or None,
+           "gather_wall_us_per_step": (round(gather_wall_s * 1e6 / steps, 2)
+                                       if (gather_wall_s and steps) else None)}
+    if out["gather_us_per_step"] and gather_bytes:
+        out["gather_GBps"] = round(gather_bytes / (gather_ms * 1e-3 / gather_n) / 1e9, 1)
+    if rowtile:
+        out["scatter_us_per_step"] = round(scatter_ms * 1e3 / scatter_n, 2) if scatter_n else None
+        out["scatter_bytes_per_step"] = scatter_bytes or None
+        out["inputs"] = "band-only: each rank receives its band + halo rows from rank 0 inside the step"
+    return out
+
+
 # ---- main ----------------------------------------------------------------------------------
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -392,9 +469,17 @@ def main():
                          "event record costs a few us of queue time; 1 = every step)")
     ap.add_argument("--mode", default="frames", choices=["frames", "rowtile"],
                     help="frames: independent frames per GPU (C4, weak scaling); rowtile: one "
-                         "frame row-tiled across GPUs + RCCL band gather (C5, strong scaling)")
+                         "frame row-tiled across GPUs, band inputs scattered from GPU 0 and the "
+                         "bands gathered back (C5, strong scaling)")
     ap.add_argument("--gather", action="store_true",
-                    help="frames mode: gather every step's output maps to GPU 0 over xGMI")
+                    help="(default for --gpus N > 1) gather every step's output maps to GPU 0")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="frames mode, N > 1: no gather (the compute-only weak-scaling curve)")
+    ap.add_argument("--full-frame-inputs", action="store_true",
+                    help="rowtile: every GPU holds the full frame (no input scatter in the step)")
+    ap.add_argument("--allow-peer-copies", action="store_true",
+                    help="one process, N devices: gather with peer copies if RCCL cannot start "
+                         "(default: exit non-zero)")
     ap.add_argument("--rectify", action="store_true",
                     help="camera pipeline: raw BGR frames resident in HBM -> rectify+gray "
                          "(k_remap, calibrated CV_16SC2 maps) -> disparity -> median/post")
@@ -407,24 +492,32 @@ def main():
                     help="C2: also compute the Harris response of every left frame (k_harris)")
     ap.add_argument("--dist-backend", default=None, choices=["auto", "rccl", "host"],
                     help="one-process-per-GPU launch: RCCL or the node-local file store (auto: "
-                         "RCCL unless ranks share a GPU).  Default: auto when a step has a "
-                         "collective (--gather, --mode rowtile); otherwise host, since the "
-                         "frame-sharded path exchanges nothing and the run then needs only the "
-                         "start/end barriers and the max-over-ranks of the elapsed time")
+                         "RCCL unless ranks share a GPU).  Default: auto, and RCCL is then "
+                         "required whenever the ranks are on distinct devices and a step has "
+                         "a collective (the gather / the row-tile scatter)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the bit-exact check of the timed steps' outputs")
     ap.add_argument("--no-live-pmc", action="store_true", help="skip the rocprofv3 PMC passes")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host_path measurement")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.pmc_child:
         args.no_cpu_baseline = args.no_aux = args.no_live_pmc = args.no_host_path = True
-        args.no_profile = True
+        args.no_profile = args.no_verify = True
+    return args
 
+
+def main():
+    args = parse_args()
     launched = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    rowtile = args.mode == "rowtile"
     pg = None
     if launched:
         from stereovision_amd.distributed import init_process_group
-        backend = args.dist_backend or ("auto" if (args.gather or args.mode == "rowtile") else "host")
-        pg = init_process_group(backend=backend)
+        world_env = int(os.environ["WORLD_SIZE"])
+        collective = rowtile or (world_env > 1 and not args.no_gather)
+        backend = args.dist_backend or "auto"
+        pg = init_process_group(backend=backend, strict=collective)
         rank, world = pg.rank, pg.world
         devices = [pg.device]
     else:
@@ -442,33 +535,40 @@ def main():
     F = max(1, args.frames)
     B = max(1, min(args.batch, F))
     F = (F // B) * B
-    rowtile = args.mode == "rowtile"
     rectify = args.rectify and not rowtile
     if rectify and len(devices) > 1:
         raise SystemExit("--rectify runs one GPU per process (use the torch.distributed.run launch)")
     harris = args.harris and not rowtile
     n_px = H * W
     arenas = [DevArena(e) for e in engines]
+    gather_on = (not rowtile) and ngpu > 1 and not args.no_gather
+    band_inputs = rowtile and ngpu > 1 and not args.full_frame_inputs
 
-    # resident inputs: F distinct frames per GPU (rowtile: the SAME frame on every GPU)
-    dL, dR = [], []
+    # resident inputs: F distinct frames per GPU (rowtile: ONE frame, on GPU 0 only unless
+    # --full-frame-inputs; the other GPUs receive their band rows inside each step)
+    dL, dR, hostL, hostR = [], [], [], []
     for k, (e, a) in enumerate(zip(engines, arenas)):
         if rowtile:
             L, R = stereo_batch(1, H, W, D, seed=4242)
         else:
             L, R = stereo_batch(F, H, W, D, seed=1000 * (rank * len(devices) + k))
+        hostL.append(L)
+        hostR.append(R)
+        if band_inputs and (rank if launched else k) != 0:
+            dL.append(0)
+            dR.append(0)
+            continue
         if rectify:
             L, R = np.repeat(L[..., None], 3, axis=3), np.repeat(R[..., None], 3, axis=3)
         dL.append(a.upload(L))
         dR.append(a.upload(R))
-    nb_out = B if not rowtile else 1
-    gather_all = args.gather and not rowtile and len(engines) > 1
-    out_frames = nb_out * (len(engines) if gather_all else 1)
+    gather_all = gather_on and not launched and len(engines) > 1
+    out_frames = (1 if rowtile else B) * (len(engines) if gather_all else 1)
     depth = [a.alloc(4 * n_px * out_frames) for a in arenas]
     disp = [a.alloc(4 * n_px * out_frames) for a in arenas]
     norm = [a.alloc(n_px * out_frames) for a in arenas]
     # --streams S: S-1 extra contexts per GPU (own stream, own outputs) that steps alternate over
-    nstreams = max(1, args.streams) if not (rowtile or args.rectify or args.gather or args.harris) else 1
+    nstreams = max(1, args.streams) if not (rowtile or args.rectify or gather_on or args.harris) else 1
     lanes = [(engines, depth, disp, norm)]
     for _ in range(nstreams - 1):
         lanes.append(([Engine(d) for d in devices], [a.alloc(4 * n_px * out_frames) for a in arenas],
@@ -485,23 +585,43 @@ def main():
         from stereovision_amd.distributed import RowTiledDepthMap
         tile = RowTiledDepthMap(H, W, D, win, cost=args.cost, device=devices[0], rank=rank,
                                 world=world, engine=eng)
-    comms = None
-    if not launched and len(engines) > 1 and (args.gather or rowtile):
+    comms, comm_reason = None, ""
+    if not launched and len(engines) > 1 and (gather_on or rowtile):
         try:
             comms = Communicator.init_all(devices)
-        except Exception as ex:  # peer copies instead
+        except Exception as ex:
+            comm_reason = f"ncclCommInitAll failed: {ex}"
+            if not args.allow_peer_copies:
+                raise SystemExit(f"RCCL group over devices {devices} unavailable ({ex}); "
+                                 "pass --allow-peer-copies to gather with peer copies")
             log(f"RCCL group unavailable ({ex}); gathering with peer copies")
-    gather_frames_d = None
-    if launched and args.gather and not rowtile and world > 1 and rank == 0:
-        gather_frames_d = arenas[0].alloc(4 * n_px * B * world)
+    gathered = None   # launched frames mode: rank 0's stacks of every rank's frames
+    if launched and gather_on:
+        if rank == 0:
+            gathered = (arenas[0].alloc(4 * n_px * B * world), arenas[0].alloc(4 * n_px * B * world),
+                        arenas[0].alloc(n_px * B * world))
+        else:
+            gathered = (0, 0, 0)
+    gather_wall = [0.0]
 
     def step(i):
         f = (i * B) % F
         if rowtile:
             if launched:
-                tile.compute(dL[0], dR[0])
+                if band_inputs and world > 1:
+                    eng.profile_region_begin("scatter", eng.stream)
+                    tile.scatter(pg, dL[0], dR[0])
+                    eng.profile_region_end(eng.stream)
+                    tile.compute()
+                else:
+                    tile.compute(dL[0], dR[0])
                 if world > 1:
+                    eng.profile_region_begin("gather", eng.stream)
                     tile.gather(pg, stream=eng.stream)
+                    eng.profile_region_end(eng.stream)
+            elif band_inputs:
+                depth_map_rows_scatter(engines, comms, dL[0], dR[0], H, W, W, 0, D, win, 0.3, 2.0,
+                                       depth[0], disp[0], norm[0], cost=args.cost)
             else:
                 depth_map_rows_multi(engines, comms, dL, dR, H, W, W, 0, D, win, 0.3, 2.0,
                                      depth[0], disp[0], norm[0], cost=args.cost)
@@ -528,9 +648,15 @@ def main():
                                       0.3, 2.0, depth_o[k], disp_o[k], norm_o[k], cost=args.cost)
             if harris:      # one launch over the batch's left frames
                 e.harris_batch_dev(gL if rectify else dL[k] + f * n_px, B, H, W, W, n_px, hmaps[k])
-        if launched and args.gather and world > 1:
+        if gathered is not None:   # every rank's maps -> rank 0 (RCCL over xGMI)
             from stereovision_amd.distributed import gather_frames
-            gather_frames(pg, disp[0], B, gather_frames_d or 0, 4 * n_px, stream=eng.stream)
+            t_g = time.perf_counter()
+            eng.profile_region_begin("gather", eng.stream)
+            for src, dst, nb in ((depth[0], gathered[0], 4), (disp[0], gathered[1], 4),
+                                 (norm[0], gathered[2], 1)):
+                gather_frames(pg, src, B, dst, nb * n_px, stream=eng.stream)
+            eng.profile_region_end(eng.stream)
+            gather_wall[0] += time.perf_counter() - t_g
 
     def sync_all():
         for e in all_engines:
@@ -541,6 +667,7 @@ def main():
     sync_all()
     eng.profile(False)
     eng.profile_reset()
+    gather_wall[0] = 0.0
     every = max(1, args.profile_every)
 
     if pg is not None:
@@ -563,6 +690,8 @@ def main():
     med_ms, med_n = eng.profile_read("median")
     remap_ms, remap_n = eng.profile_read("remap")
     harris_ms, harris_n = eng.profile_read("harris")
+    gath_ms, gath_n = eng.profile_read("gather")
+    scat_ms, scat_n = eng.profile_read("scatter")
     k_name = "sgbm pipeline (k_sgbm_*)" if args.cost == "sgbm" else "k_match"
     if pg is not None:
         elapsed = pg.allreduce_max(elapsed)
@@ -573,6 +702,72 @@ def main():
     if args.pmc_child:
         print(json.dumps({"pmc_child": True, "value": value}), flush=True)
         return
+
+    # ---- the timed steps' own outputs, checked bit-exactly (outside the timed region) ----
+    verified, verify_info = None, None
+    if not args.no_verify and args.cost != "sgbm":
+        t_v = time.perf_counter()
+        ver = Verifier(D, win, args.cost, host_cores()[0])
+        last = args.steps - 1 if args.steps > 0 else max(0, args.warmup - 1)
+        f0 = (last * B) % F
+        zs = sorted({0, B - 1})
+        if rowtile:
+            if launched:
+                if rank == 0:
+                    ver.frame("full frame gathered on rank 0", hostL[0][0], hostR[0][0],
+                              eng.to_host(tile.out_a, (H, W), np.float32),
+                              eng.to_host(tile.disp, (H, W), np.float32),
+                              eng.to_host(tile.out_u8, (H, W), np.uint8))
+            else:
+                ver.frame("full frame gathered on device 0", hostL[0][0], hostR[0][0],
+                          *fetch_maps(eng, depth[0], disp[0], norm[0], 0, n_px, H, W))
+        elif gather_all:
+            for k in range(len(engines)):
+                for z in zs:
+                    ver.frame(f"device {k} frame {f0 + z} (gathered on device 0)", hostL[k][f0 + z],
+                              hostR[k][f0 + z], *fetch_maps(eng, depth[0], disp[0], norm[0], k * B + z,
+                                                            n_px, H, W))
+        else:
+            engs, depth_o, disp_o, norm_o = lanes[last % nstreams]
+            for k, e in enumerate(engs):
+                for z in zs:
+                    Lz, Rz = hostL[k][f0 + z], hostR[k][f0 + z]
+                    if rectify:
+                        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+                        import sv_rectify_oracle as RO  # test infrastructure: the checker only
+                        lm1, lm2, rm1, rm2 = rect.host_maps()
+                        Lz = RO.remap_gray(np.repeat(Lz[..., None], 3, axis=2), lm1, lm2)
+                        Rz = RO.remap_gray(np.repeat(Rz[..., None], 3, axis=2), rm1, rm2)
+                    ver.frame(f"rank {rank} device {k} frame {f0 + z}", Lz, Rz,
+                              *fetch_maps(e, depth_o[k], disp_o[k], norm_o[k], z, n_px, H, W))
+                    if harris:
+                        ver.harris(f"rank {rank} device {k} frame {f0 + z}", Lz,
+                                   e.to_host(hmaps[k] + 4 * n_px * z, (H, W), np.float32))
+            if gathered is not None and rank == 0:
+                from stereovision_amd.synthetic import stereo_pair
+                for r in range(world):
+                    for z in zs:
+                        if r == 0:
+                            Lz, Rz = hostL[0][f0 + z], hostR[0][f0 + z]
+                        else:   # rank r's inputs, regenerated from its seed
+                            Lz, Rz, _ = stereo_pair(H, W, D, seed=1000 * r + f0 + z)
+                        ver.frame(f"rank {r} frame {f0 + z} (gathered on rank 0)", Lz, Rz,
+                                  *fetch_maps(eng, gathered[0], gathered[1], gathered[2], r * B + z,
+                                              n_px, H, W))
+        ok = ver.result()
+        if pg is not None:
+            ok = pg.allreduce_max(0.0 if ok else 1.0) == 0.0
+        verified = bool(ok)
+        verify_info = {"checked": ver.checked if rank == 0 else len(ver.checked),
+                       "failures": ver.failed or None,
+                       "against": "oracle/sv_oracle.c (the engine's semantics), bit-exact"
+                                  + (" + Harris within 1e-4" if harris else ""),
+                       "when": "after the timed region: maps of the LAST timed step",
+                       "seconds": round(time.perf_counter() - t_v, 2)}
+    elif args.cost == "sgbm":
+        verify_info = {"skipped": "SGBM mode: the NumPy SGBM-3WAY oracle takes ~15 s per 1080p "
+                                  "frame; tests/test_sgbm.py checks the kernels bit-exactly"}
+
     # pixels of one k_match launch: the batch (frames) or this GPU's band + median halo
     npx = n_px * B
     if rowtile:
@@ -633,8 +828,26 @@ def main():
             "median_post_avg_us": round(med_ms / med_n * 1e3, 2) if med_n else None,
         }
 
-    parallelism = (f"row-tiled x{ngpu} + band gather" if rowtile else
-                   f"frame-sharded x{ngpu}" + (" + gather" if args.gather else ""))
+    # per step: bytes received by the root (N-1 peers' maps; rowtile: N-1 bands of the three
+    # outputs) and, rowtile with band inputs, bytes sent from the root (both images' rows)
+    gbytes = sbytes = 0
+    if ngpu > 1:
+        if rowtile:
+            from stereovision_amd.distributed import band_layout
+            for k in range(1, ngpu):
+                b = band_layout(H, k, ngpu, win)
+                gbytes += 9 * (b["r1"] - b["r0"]) * W
+                if band_inputs:
+                    sbytes += 2 * (b["in1"] - b["in0"]) * W
+        elif gather_on:
+            gbytes = 9 * n_px * B * (ngpu - 1)
+    dist = dist_summary(ngpu, launched, pg, comms, gather=gather_on, rowtile=rowtile,
+                        gather_ms=gath_ms, gather_n=gath_n, scatter_ms=scat_ms, scatter_n=scat_n,
+                        gather_wall_s=gather_wall[0], steps=args.steps, gather_bytes=gbytes,
+                        scatter_bytes=sbytes, reason=comm_reason)
+    parallelism = (f"row-tiled x{ngpu}" + (" (band inputs scattered from GPU 0)" if band_inputs else "")
+                   + " + band gather" if rowtile else
+                   f"frame-sharded x{ngpu}" + (" + gather to GPU 0" if gather_on else ""))
     if ngpu > 1:
         parallelism += (f" ({'one process per GPU, ' + pg.backend if launched else 'one process, ' + ('RCCL group' if comms else 'peer copies')})")
     result = {
@@ -655,6 +868,9 @@ def main():
                    "frames_resident_per_gpu": 1 if rowtile else F,
                    "frames_per_step_per_gpu": 1 if rowtile else B,
                    "parallelism": parallelism},
+        "verified": verified,
+        "verify": verify_info,
+        "distributed": dist,
         "hbm_gbs_frame_path": round(frame_bytes * value / 1e9, 2),
         # BASELINE.md's fixed roofline formulas, per GPU: 6*H*W algorithmic bytes and
         # H*W*D*win^2 SAD taps per frame against 8.0e12 B/s and 157.3e12 taps/s.  The
@@ -704,6 +920,9 @@ def main():
             c.close()
     if pg is not None:
         pg.close()
+    if verified is False:
+        log("bench outputs do NOT match the oracle: " + "; ".join(verify_info["failures"] or ["(other rank)"]))
+        sys.exit(3)
 
 
 if __name__ == "__main__":

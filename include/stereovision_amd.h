@@ -89,7 +89,9 @@ enum sv_kernel {
     SV_K_GRAY = 0, SV_K_HARRIS = 1, SV_K_HOG = 2, SV_K_MATCH = 3, SV_K_MEDIAN = 4, SV_K_POST = 5,
     SV_K_REMAP = 6, SV_K_UNDISTORT = 7, SV_K_RESIZE = 8, SV_K_STATS = 9, SV_K_SELECT = 10,
     SV_K_AFFINE = 11, SV_K_SGBM = 12, SV_K_SPECKLE = 13,
-    SV_NKERNELS = 14
+    SV_K_GATHER = 14,   /* multi-GPU gathers to the root (RCCL / peer copies), root stream */
+    SV_K_SCATTER = 15,  /* multi-GPU input scatters (row bands + halos), per context stream */
+    SV_NKERNELS = 16
 };
 
 int sv_version(void);
@@ -98,6 +100,11 @@ int sv_device_count(int* n);
 int sv_create(int device, sv_ctx** out);
 void sv_destroy(sv_ctx* ctx);
 int sv_synchronize(sv_ctx* ctx);
+/* Waits for the context's work and frees its grow-only device scratch (disparity, HOG and
+ * SGBM volumes, band buffers); the next call allocates what it needs again.  SGBM batches
+ * size their volumes to SV_SGBM_BUDGET_GB, default a quarter of the device's free memory
+ * (at most 48 GiB). */
+int sv_release_scratch(sv_ctx* ctx);
 void* sv_stream(sv_ctx* ctx);
 
 /* Engine plan for a configuration: disparities per lane, lanes per group, LDS bytes per
@@ -208,7 +215,8 @@ int sv_depth_map_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
  * map, which takes an explicit out_pitch / out_frame_stride (elements).  The context's
  * internal scratch is ordered across streams (a call on another stream waits for the
  * previous user of the scratch).  cost = SV_COST_SGBM runs every SGBM stage once per chunk of
- * up to 32 frames (volumes of ~1.5 GB per 1080p D=128 frame, within a 48 GiB scratch budget);
+ * up to 32 frames (volumes of ~1.5 GB per 1080p D=128 frame, within the scratch budget of
+ * sv_release_scratch);
  * chunks of >= 8 frames fuse the right-to-left path with the winner-take-all. */
 int sv_disparity_batch_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
                            int n_frames, int H, int W, int pitch, int64_t frame_stride,
@@ -251,7 +259,8 @@ int sv_multi_gpu_batch(sv_ctx* const* ctxs, int ndev, const uint8_t* left, const
  *   sv_comm_gatherv     rank k's send_bytes land at d_recv + recv_offsets[k] on `root`
  *                       (ncclSend/ncclRecv in one group; the root's own block is a device
  *                       copy unless it is already in place); enqueued on `stream` (NULL =
- *                       the communicator's stream) */
+ *                       the communicator's own stream, which nothing orders against the
+ *                       caller's compute streams: pass the stream the data was produced on) */
 typedef struct sv_comm sv_comm;
 #define SV_COMM_ID_BYTES 128
 int sv_comm_available(void);
@@ -264,6 +273,13 @@ int sv_comm_barrier(sv_comm* comm);
 int sv_comm_allreduce_max_f64(sv_comm* comm, double* value);
 int sv_comm_gatherv(sv_comm* comm, const void* d_send, uint64_t send_bytes, void* d_recv,
                     const uint64_t* recv_offsets, const uint64_t* recv_bytes, int root, void* stream);
+/* The inverse of sv_comm_gatherv: the root's send_bytes[k] bytes at d_send + send_offsets[k]
+ * land in rank k's d_recv (recv_bytes); the root's own block is a device copy unless it is
+ * already in place.  Enqueued on `stream` (NULL = the communicator's stream: the caller then
+ * orders it against its own streams). */
+int sv_comm_scatterv(sv_comm* comm, const void* d_send, const uint64_t* send_offsets,
+                     const uint64_t* send_bytes, void* d_recv, uint64_t recv_bytes, int root,
+                     void* stream);
 int sv_comm_synchronize(sv_comm* comm);
 
 /* C4 on device-resident frames, one process driving ndev contexts: context k computes
@@ -293,6 +309,23 @@ int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev
                             float min_depth, float max_depth, float depth_range,
                             float min_disp_global, float* d_depth, float* d_disparity,
                             uint8_t* d_norm);
+
+/* C5 with the frame resident on ctxs[0]'s device only: context k > 0 first receives just the
+ * input rows its band reads (sv_band_rows_in: the band, the median halo and the window halo)
+ * from the root (RCCL send/recv over xGMI, or peer copies), into its own scratch; then as
+ * sv_depth_map_rows_multi.  Profiled as SV_K_SCATTER / SV_K_GATHER on the root stream. */
+int sv_depth_map_rows_scatter(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
+                              const uint8_t* d_left, const uint8_t* d_right, int H, int W,
+                              int pitch, int min_disp, int num_disp, int win, int cost,
+                              float min_depth, float max_depth, float depth_range,
+                              float min_disp_global, float* d_depth, float* d_disparity,
+                              uint8_t* d_norm);
+/* Row bands of a `world`-way row tiling for rank `rank`: out6 = {r0, r1 (output rows), h0, h1
+ * (disparity rows incl. the median halo), in0, in1 (input rows the band reads)}.  Device
+ * buffers holding only input rows [in0, in1) must keep SV_BAND_MARGIN spare rows above and
+ * below them (read-ahead of the row pipelines; never used as data). */
+#define SV_BAND_MARGIN 8
+int sv_band_rows_in(int H, int rank, int world, int win, int cost, int* out6);
 
 int sv_harris_dev(sv_ctx* ctx, const uint8_t* d_gray, int H, int W, int pitch, float* d_out,
                   void* stream);
@@ -435,6 +468,11 @@ int sv_profile_reset(sv_ctx* ctx);
  * dominated by per-launch event overhead). */
 int sv_timer_begin(sv_ctx* ctx, void* stream);
 int sv_timer_end(sv_ctx* ctx, void* stream, double* ms);
+/* Caller-delimited profiling region on `stream` (NULL = the context's stream), counted under
+ * `kernel` like a launch when profiling is enabled (a no-op otherwise): e.g. the RCCL gather a
+ * process enqueues itself through sv_comm_gatherv (SV_K_GATHER).  Regions do not nest. */
+int sv_profile_region_begin(sv_ctx* ctx, int kernel, void* stream);
+int sv_profile_region_end(sv_ctx* ctx, void* stream);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,9 @@ def lib():
         L.svo_hog_hist.restype = None
         L.svo_gray.argtypes = [_u8p, _i, _i, _i, _u8p]
         L.svo_gray.restype = None
+        L.svo_depth_map.argtypes = [_u8p, _u8p, _i, _i, _i, _i, _i, _i, _f, _f, _f, _f32p, _f32p,
+                                    _u8p, _i]
+        L.svo_depth_map.restype = _i
         L.svo_max_threads.argtypes = []
         L.svo_max_threads.restype = _i
         _lib = L
@@ -112,6 +115,23 @@ def gray(bgr):
     out = np.empty((H, W), np.uint8)
     lib().svo_gray(bgr, H, W, W * 3, out)
     return out
+
+
+def depth_map(L, R, min_disp, num_disp, win, cost=0, min_depth=0.3, max_depth=2.0, nthreads=0):
+    """The whole app-1 path of one gray pair (svo_depth_map): (depth_final, disparity,
+    depth_normalized) with create_depth_map's float32 casts (depth_map.py:909-936)."""
+    L = np.ascontiguousarray(L, np.uint8)
+    R = np.ascontiguousarray(R, np.uint8)
+    H, W = L.shape
+    depth = np.empty((H, W), np.float32)
+    disp = np.empty((H, W), np.float32)
+    norm = np.empty((H, W), np.uint8)
+    rc = lib().svo_depth_map(L, R, H, W, min_disp, num_disp, win, cost, np.float32(min_depth),
+                             np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
+                             depth, disp, norm, nthreads)
+    if rc != 0:
+        raise ValueError(f"svo_depth_map failed: {rc}")
+    return depth, disp, norm
 
 
 def max_threads() -> int:

@@ -4,6 +4,7 @@
 // Host entry points stage into pinned memory, run the whole chain on the context stream
 // and copy results back; device entry points only enqueue.  No exception crosses the ABI.
 #include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -154,12 +155,15 @@ struct sv_ctx {
     hipStream_t scr_stream = nullptr;
     hipEvent_t scr_ev = nullptr;
     hipEvent_t xev = nullptr;   // multi-device entry points: this context's part is enqueued
+    hipEvent_t sev = nullptr;   // sv_depth_map_rows_scatter: the root's inputs are ready
     bool prof = false;
     std::vector<EvPair> pending;
     std::vector<hipEvent_t> pool;
     double acc_ms[SV_NKERNELS] = {};
     long long cnt[SV_NKERNELS] = {};
     EvPair cur{};
+    EvPair region{};            // sv_profile_region_begin/end (separate from `cur`: kernels
+    bool region_open = false;   // launched inside a region keep their own pairs)
 
     hipEvent_t get_event() {
         if (!pool.empty()) {
@@ -249,7 +253,20 @@ int enqueue_speckles(sv_ctx* c, int16_t* d_img, int H, int W, int pitch, int new
 // batches run every stage once over grid.z (up to kSgbmChunk frames, or as many as the
 // scratch budget allows: ~1.5 GB of volumes per 1080p D=128 frame with int16 paths).
 constexpr int kSgbmChunk = 32;
-constexpr size_t kSgbmBudget = (size_t)48 << 30;
+// Scratch budget of a batch's volumes: SV_SGBM_BUDGET_GB (GiB) if set, else a quarter of the
+// device's free memory at the call (capped at 48 GiB), so several contexts on one device do
+// not each pin tens of GB; sv_release_scratch returns them after a large batch
+size_t sgbm_budget(int device) {
+    static const long long env_gb = [] {
+        const char* e = std::getenv("SV_SGBM_BUDGET_GB");
+        return e ? std::atoll(e) : 0LL;
+    }();
+    if (env_gb > 0) return (size_t)env_gb << 30;
+    size_t fr = 0, tot = 0;
+    (void)device;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr == 0) return (size_t)8 << 30;
+    return std::min<size_t>(fr / 4, (size_t)48 << 30);
+}
 
 int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, int pitch, int min_disp,
                  int num_disp, int win, SgbmParams p, int16_t* out, int opitch, hipStream_t s, int nf = 1,
@@ -291,6 +308,9 @@ int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, in
     const bool cost1 = sv::sgbm_cost_fused(num_disp, a.r);   // k_sgbm_cost: per-pixel record planes
     const size_t rec_frame = cost1 ? (size_t)2 * H * W * 16 : 0;
     const size_t per_frame = vol * (4 + lsz * 3) + (size_t)H * a.Wb * 8 + rec_frame;   // unfused (the larger)
+    // volumes already held count towards the budget (they are reused, not added to)
+    const size_t held = c->sg_hsum.cap + c->sg_c.cap + c->sg_l.cap + c->sg_lt.cap + c->sg_band.cap + c->sg_rec.cap;
+    const size_t kSgbmBudget = std::max(sgbm_budget(c->device) + held, per_frame);
     int chunk = (int)std::max<size_t>(1, std::min<size_t>({(size_t)nf, (size_t)kSgbmChunk,
                                                             kSgbmBudget / std::max<size_t>(per_frame, 1)}));
     const bool fused = sv::sgbm_fused(chunk);
@@ -686,10 +706,15 @@ void sv_destroy(sv_ctx* c) {
                           &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1], &c->stats, &c->sel,
                           &c->sg_hsum, &c->sg_c, &c->sg_l, &c->sg_lt, &c->sg_band, &c->cc_parent,
                           &c->hist_copies, &c->cmap, &c->bgr, &c->m16,
-                          &c->cc_size};
+                          &c->cc_size, &c->sg_rec};
         if (c->lut_ev) (void)hipEventDestroy(c->lut_ev);
         if (c->scr_ev) (void)hipEventDestroy(c->scr_ev);
         if (c->xev) (void)hipEventDestroy(c->xev);
+        if (c->sev) (void)hipEventDestroy(c->sev);
+        if (c->region_open) {
+            (void)hipEventDestroy(c->region.a);
+            (void)hipEventDestroy(c->region.b);
+        }
         for (auto e : c->cev)
             if (e) (void)hipEventDestroy(e);
         for (auto e : c->tmr)
@@ -706,6 +731,19 @@ void sv_destroy(sv_ctx* c) {
         (void)hipStreamDestroy(c->stream);
     }
     delete c;
+}
+
+int sv_release_scratch(sv_ctx* c) {
+    SV_ENTER(c);
+    SV_HIP(hipStreamSynchronize(c->stream));
+    if (c->sg_aux) SV_HIP(hipStreamSynchronize(c->sg_aux));
+    // the grow-only work buffers (not the post table, colormap or staging): the next call
+    // allocates what it needs again
+    DevBuf* bufs[] = {&c->img[0], &c->img[1], &c->gray[0], &c->gray[1], &c->d16, &c->fa, &c->fb, &c->fc,
+                      &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->sg_hsum, &c->sg_c,
+                      &c->sg_l, &c->sg_lt, &c->sg_band, &c->sg_rec, &c->cc_parent, &c->cc_size, &c->m16};
+    for (auto* b : bufs) b->release();
+    return 0;
 }
 
 int sv_synchronize(sv_ctx* c) {
@@ -1005,6 +1043,23 @@ struct MultiLock {
     }
 };
 
+// Row bands of a row-tiled frame: output rows [r0, r1) of `rank`,
+// disparity rows [h0, h1) (+ the 5x5 median's 2-row halo) and the input rows [in0, in1) the
+// kernels read for them: the matching window's r rows, the four-row waves' 3 extra rows below
+// a band's last row and the HOG histograms' Sobel row (r + 4 each side, clamped).
+struct SvRows {
+    int r0 = 0, r1 = 0, h0 = 0, h1 = 0, in0 = 0, in1 = 0;
+};
+void band_rows_of(int H, int rank, int world, int win, SvRows& b) {
+    b.r0 = (int)((long long)H * rank / world);
+    b.r1 = (int)((long long)H * (rank + 1) / world);
+    b.h0 = b.r0 - 2 > 0 ? b.r0 - 2 : 0;
+    b.h1 = b.r1 + 2 < H ? b.r1 + 2 : H;
+    const int halo = win / 2 + 4;
+    b.in0 = b.h0 - halo > 0 ? b.h0 - halo : 0;
+    b.in1 = b.h1 + halo < H ? b.h1 + halo : H;
+}
+
 // Scratch hazard (ScratchUse) for an explicit device/stream, and the join event.
 int scratch_wait(sv_ctx* c, hipStream_t s) {
     if (c->scr_stream && c->scr_stream != s && c->scr_ev) SV_HIP(hipStreamWaitEvent(s, c->scr_ev, 0));
@@ -1064,7 +1119,34 @@ struct Block {
 
 // Gather the blocks of contexts 1..ndev-1 into the root's buffers: RCCL send/recv in one
 // group (comms) or peer copies; the root stream then waits for every part.
-int gather_blocks(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const std::vector<std::vector<Block>>& blocks) {
+int gather_blocks_impl(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
+                       const std::vector<std::vector<Block>>& blocks);
+
+// ... timed on the root stream as SV_K_GATHER (from the point where the root's own work is
+// enqueued to the last part's arrival: includes waiting for the slowest context), and every
+// context's scratch-ready event recorded AFTER its sends / peer copies were enqueued, so a
+// later call on another stream cannot overwrite fa/fb/u8 while the gather still reads them.
+int gather_blocks(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const std::vector<std::vector<Block>>& blocks,
+                  const std::vector<int>& active) {
+    sv_ctx* root = ctxs[0];
+    SV_HIP(hipSetDevice(root->device));
+    const bool timed = ndev > 1 && root->prof && !root->region_open;
+    if (timed) root->prof_begin(SV_K_GATHER, root->stream);
+    int rc = gather_blocks_impl(ctxs, comms, ndev, blocks);
+    if (rc) return rc;
+    SV_HIP(hipSetDevice(root->device));
+    if (timed) root->prof_end(root->stream);
+    for (int k : active) {
+        SV_HIP(hipSetDevice(ctxs[k]->device));
+        rc = scratch_mark(ctxs[k], ctxs[k]->stream);
+        if (rc) return rc;
+    }
+    SV_HIP(hipSetDevice(root->device));
+    return 0;
+}
+
+int gather_blocks_impl(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
+                       const std::vector<std::vector<Block>>& blocks) {
     sv_ctx* root = ctxs[0];
     if (comms && ndev > 1) {
         int rc = sv::comm_group_start();
@@ -1134,8 +1216,10 @@ int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int n
     if (!lock.ok) return fail(SV_ENOMEM, "lock allocation failed");
     const size_t n = (size_t)H * W;
     std::vector<std::vector<Block>> blocks;
+    std::vector<int> active;
     try {
         blocks.resize(ndev);
+        active.reserve(ndev);
     } catch (...) {
         return fail(SV_ENOMEM, "allocation failed");
     }
@@ -1172,14 +1256,13 @@ int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int n
         SV_LAUNCH(c, SV_K_MEDIAN, s,
                   sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, o_disp, pp, s, nf, (long long)n,
                                         (long long)n));
-        rc = scratch_mark(c, s);
-        if (rc) return rc;
+        active.push_back(k);
         if (k > 0)
             blocks[k] = {{d_depth + off * n, o_depth, (size_t)nf * n * sizeof(float)},
                          {d_disparity + off * n, o_disp, (size_t)nf * n * sizeof(float)},
                          {d_norm + off * n, o_norm, (size_t)nf * n}};
     }
-    return gather_blocks(ctxs, comms, ndev, blocks);
+    return gather_blocks(ctxs, comms, ndev, blocks, active);
 }
 
 int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
@@ -1200,8 +1283,10 @@ int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev
     if (!lock.ok) return fail(SV_ENOMEM, "lock allocation failed");
     const size_t n = (size_t)H * W;
     std::vector<std::vector<Block>> blocks;
+    std::vector<int> active;
     try {
         blocks.resize(ndev);
+        active.reserve(ndev);
     } catch (...) {
         return fail(SV_ENOMEM, "allocation failed");
     }
@@ -1234,8 +1319,7 @@ int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev
         rc = attach_lut(c, pp, s);
         if (rc) return rc;
         SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(c->d16.as<int16_t>(), H, W, r0, r1, o_disp, pp, s));
-        rc = scratch_mark(c, s);
-        if (rc) return rc;
+        active.push_back(k);
         if (k > 0) {
             const size_t o = (size_t)r0 * W, m = (size_t)(r1 - r0) * W;
             blocks[k] = {{d_depth + o, o_depth + o, m * sizeof(float)},
@@ -1243,7 +1327,146 @@ int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev
                          {d_norm + o, o_norm + o, m}};
         }
     }
-    return gather_blocks(ctxs, comms, ndev, blocks);
+    return gather_blocks(ctxs, comms, ndev, blocks, active);
+}
+
+int sv_depth_map_rows_scatter(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* d_left,
+                              const uint8_t* d_right, int H, int W, int pitch, int min_disp, int num_disp, int win,
+                              int cost, float min_depth, float max_depth, float depth_range, float min_disp_global,
+                              float* d_depth, float* d_disparity, uint8_t* d_norm) {
+    if (!d_left || !d_right || !d_depth || !d_disparity || !d_norm) return fail(SV_EINVAL, "null arguments");
+    int rc = multi_prologue(ctxs, comms, ndev);
+    if (rc) return rc;
+    sv::MatchPlan plan;
+    rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
+    if (rc) return rc;
+    if (cost == SV_COST_SGBM && ndev > 1) return fail(SV_EINVAL, "SGBM cannot be row-tiled (top-down path)");
+    if (pitch < W) return fail(SV_EINVAL, "pitch smaller than width");
+    MultiLock lock(ctxs, ndev);
+    if (!lock.ok) return fail(SV_ENOMEM, "lock allocation failed");
+    const size_t n = (size_t)H * W;
+    std::vector<std::vector<Block>> blocks;
+    std::vector<int> active;
+    std::vector<SvRows> rows;
+    try {
+        blocks.resize(ndev);
+        active.reserve(ndev);
+        rows.resize(ndev);
+    } catch (...) {
+        return fail(SV_ENOMEM, "allocation failed");
+    }
+    sv_ctx* root = ctxs[0];
+    for (int k = 0; k < ndev; ++k) band_rows_of(H, k, ndev, win, rows[k]);
+    // 1. scatter: context k > 0 receives input rows [in0, in1) of both images into its scratch
+    //    (img[0], img[1]: SV_BAND_MARGIN spare rows above and below, never read as data)
+    for (int k = 1; k < ndev; ++k) {
+        sv_ctx* c = ctxs[k];
+        if (rows[k].r1 <= rows[k].r0) continue;
+        SV_HIP(hipSetDevice(c->device));
+        rc = scratch_wait(c, c->stream);
+        if (rc) return rc;
+        const size_t bytes = (size_t)(rows[k].in1 - rows[k].in0 + 2 * SV_BAND_MARGIN) * pitch;
+        SV_HIP(c->img[0].ensure(bytes));
+        SV_HIP(c->img[1].ensure(bytes));
+    }
+    SV_HIP(hipSetDevice(root->device));
+    const bool timed = ndev > 1 && root->prof && !root->region_open;
+    if (timed) root->prof_begin(SV_K_SCATTER, root->stream);
+    if (comms && ndev > 1) {
+        rc = sv::comm_group_start();
+        if (rc) return rc;
+        int erc = 0;
+        for (int k = 1; k < ndev && !erc; ++k) {
+            if (rows[k].r1 <= rows[k].r0) continue;
+            const size_t off = (size_t)rows[k].in0 * pitch, bytes = (size_t)(rows[k].in1 - rows[k].in0) * pitch;
+            for (int i = 0; i < 2 && !erc; ++i) {
+                const uint8_t* src = (i ? d_right : d_left) + off;
+                uint8_t* dst = ctxs[k]->img[i].as<uint8_t>() + (size_t)SV_BAND_MARGIN * pitch;
+                erc = sv::comm_send(comms[0], src, bytes, k, root->stream);
+                if (!erc) erc = sv::comm_recv(comms[k], dst, bytes, 0, ctxs[k]->stream);
+            }
+        }
+        rc = sv::comm_group_end();
+        if (erc) return erc;
+        if (rc) return rc;
+    } else if (ndev > 1) {
+        if (!root->sev) SV_HIP(hipEventCreateWithFlags(&root->sev, hipEventDisableTiming));
+        SV_HIP(hipEventRecord(root->sev, root->stream));
+        for (int k = 1; k < ndev; ++k) {
+            sv_ctx* c = ctxs[k];
+            if (rows[k].r1 <= rows[k].r0) continue;
+            SV_HIP(hipSetDevice(c->device));
+            SV_HIP(hipStreamWaitEvent(c->stream, root->sev, 0));
+            const size_t off = (size_t)rows[k].in0 * pitch, bytes = (size_t)(rows[k].in1 - rows[k].in0) * pitch;
+            for (int i = 0; i < 2; ++i) {
+                rc = peer_copy(c, root, ctxs[k]->img[i].as<uint8_t>() + (size_t)SV_BAND_MARGIN * pitch,
+                               (i ? d_right : d_left) + off, bytes, c->stream);
+                if (rc) return rc;
+            }
+        }
+    }
+    SV_HIP(hipSetDevice(root->device));
+    if (timed) root->prof_end(root->stream);
+    // 2. every context: disparity of its band + median halo, median + post of its band
+    for (int k = 0; k < ndev; ++k) {
+        sv_ctx* c = ctxs[k];
+        const SvRows& b = rows[k];
+        if (b.r1 <= b.r0) continue;
+        SV_HIP(hipSetDevice(c->device));
+        hipStream_t s = c->stream;
+        if (k == 0) {
+            rc = scratch_wait(c, s);
+            if (rc) return rc;
+        }
+        // band images addressed as full frames: row y of the frame at base + y * pitch for
+        // y in [in0, in1) (the kernels clamp rows to [0, H) and read only [in0, in1))
+        const ptrdiff_t shift = ((ptrdiff_t)SV_BAND_MARGIN - b.in0) * pitch;
+        const uint8_t* L = k ? c->img[0].as<uint8_t>() + shift : d_left;
+        const uint8_t* R = k ? c->img[1].as<uint8_t>() + shift : d_right;
+        SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
+        float* o_depth = d_depth;
+        float* o_disp = d_disparity;
+        uint8_t* o_norm = d_norm;
+        if (k > 0) {
+            SV_HIP(c->fa.ensure(n * sizeof(float)));
+            SV_HIP(c->fb.ensure(n * sizeof(float)));
+            SV_HIP(c->u8.ensure(n));
+            o_depth = c->fb.as<float>();
+            o_disp = c->fa.as<float>();
+            o_norm = c->u8.as<uint8_t>();
+        }
+        rc = enqueue_disparity(c, L, R, H, W, pitch, min_disp, num_disp, win, cost, b.h0, b.h1,
+                               c->d16.as<int16_t>(), W, s);
+        if (rc) return rc;
+        sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                                      num_disp, o_depth, o_norm, nullptr);
+        rc = attach_lut(c, pp, s);
+        if (rc) return rc;
+        SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(c->d16.as<int16_t>(), H, W, b.r0, b.r1, o_disp, pp, s));
+        active.push_back(k);
+        if (k > 0) {
+            const size_t o = (size_t)b.r0 * W, m = (size_t)(b.r1 - b.r0) * W;
+            blocks[k] = {{d_depth + o, o_depth + o, m * sizeof(float)},
+                         {d_disparity + o, o_disp + o, m * sizeof(float)},
+                         {d_norm + o, o_norm + o, m}};
+        }
+    }
+    // 3. bands -> the root's full-frame outputs
+    return gather_blocks(ctxs, comms, ndev, blocks, active);
+}
+
+int sv_band_rows_in(int H, int rank, int world, int win, int cost, int* out6) {
+    if (!out6 || H <= 0 || world < 1 || rank < 0 || rank >= world || win < 1) return fail(SV_EINVAL, "bad band arguments");
+    (void)cost;
+    SvRows b;
+    band_rows_of(H, rank, world, win, b);
+    out6[0] = b.r0;
+    out6[1] = b.r1;
+    out6[2] = b.h0;
+    out6[3] = b.h1;
+    out6[4] = b.in0;
+    out6[5] = b.in1;
+    return 0;
 }
 
 int sv_harris_dev(sv_ctx* c, const uint8_t* d_gray, int H, int W, int pitch, float* d_out, void* stream) {
@@ -2299,6 +2522,28 @@ int sv_timer_end(sv_ctx* c, void* stream, double* ms) {
     float f = 0.f;
     SV_HIP(hipEventElapsedTime(&f, c->tmr[0], c->tmr[1]));
     *ms = f;
+    return 0;
+}
+
+int sv_profile_region_begin(sv_ctx* c, int kernel, void* stream) {
+    SV_ENTER(c);
+    if (kernel < 0 || kernel >= SV_NKERNELS) return fail(SV_EINVAL, "kernel id out of range");
+    if (c->region_open) return fail(SV_EINVAL, "profiling regions do not nest");
+    if (!c->prof) return 0;
+    c->region.a = c->get_event();
+    c->region.b = c->get_event();
+    c->region.kid = kernel;
+    SV_HIP(hipEventRecord(c->region.a, pick(c, stream)));
+    c->region_open = true;
+    return 0;
+}
+
+int sv_profile_region_end(sv_ctx* c, void* stream) {
+    SV_ENTER(c);
+    if (!c->region_open) return 0;   // profiling was off at the matching begin
+    c->region_open = false;
+    SV_HIP(hipEventRecord(c->region.b, pick(c, stream)));
+    c->pending.push_back(c->region);
     return 0;
 }
 

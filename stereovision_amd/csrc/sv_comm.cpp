@@ -308,6 +308,36 @@ int sv_comm_gatherv(sv_comm* c, const void* d_send, uint64_t send_bytes, void* d
     return 0;
 }
 
+int sv_comm_scatterv(sv_comm* c, const void* d_send, const uint64_t* send_offsets, const uint64_t* send_bytes,
+                     void* d_recv, uint64_t recv_bytes, int root, void* stream) {
+    if (!c || root < 0 || root >= c->nranks) return comm_fail(SV_EINVAL, "bad scatter arguments");
+    if (recv_bytes && !d_recv) return comm_fail(SV_EINVAL, "null receive buffer");
+    if (c->rank == root && (!d_send || !send_offsets || !send_bytes)) return comm_fail(SV_EINVAL, "root needs send layout");
+    if (c->rank == root && send_bytes[root] != recv_bytes) return comm_fail(SV_EINVAL, "root's own block size differs");
+    Rccl* r = rccl();
+    if (!r) return comm_fail(SV_ENODEV, "RCCL unavailable");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    SV_CHIP(hipSetDevice(c->device));
+    SV_NCCL(r, r->group_start());
+    ncclResult_t e = ncclSuccess;
+    if (c->rank == root) {
+        for (int k = 0; k < c->nranks && e == ncclSuccess; ++k) {
+            if (k == root || send_bytes[k] == 0) continue;
+            e = r->send(static_cast<const uint8_t*>(d_send) + send_offsets[k], send_bytes[k], ncclChar, k, c->comm, s);
+        }
+    } else if (recv_bytes) {
+        e = r->recv(d_recv, recv_bytes, ncclChar, root, c->comm, s);
+    }
+    ncclResult_t e2 = r->group_end();
+    if (e != ncclSuccess) return nccl_fail(r, e, "ncclSend/ncclRecv");
+    if (e2 != ncclSuccess) return nccl_fail(r, e2, "ncclGroupEnd");
+    if (c->rank == root && recv_bytes) {
+        const uint8_t* src = static_cast<const uint8_t*>(d_send) + send_offsets[root];
+        if (src != d_recv) SV_CHIP(hipMemcpyAsync(d_recv, src, recv_bytes, hipMemcpyDeviceToDevice, s));
+    }
+    return 0;
+}
+
 int sv_comm_synchronize(sv_comm* c) {
     if (!c) return comm_fail(SV_EINVAL, "null communicator");
     SV_CHIP(hipSetDevice(c->device));

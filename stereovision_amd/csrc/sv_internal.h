@@ -178,7 +178,7 @@ struct SgbmArgs {
         if (recs) recs += (size_t)2 * H * W * z;
     }
 };
-int sgbm_dp(int D);
+int sgbm_dp(int D);   // per-pixel volume stride for D disparities, -1 if D > 512
 // Whether launches of nf frames fuse the R->L path with the WTA (k_sgbm_rl_wta, L_rl never
 // stored): batches of >= 8 frames, where the extra work per step hides behind other waves'
 // chains (one frame: both paths in k_sgbm_hpath, concurrent, then k_sgbm_wta).
@@ -186,7 +186,7 @@ int sgbm_dp(int D);
 bool sgbm_fused(int nf);
 // r <= 4: pixel cost and both window sums in one pass (k_sgbm_cost, no hsum
 // volume); SV_SGBM_COST=0 restores k_sgbm_hsum_tiled + k_sgbm_vsum8
-bool sgbm_cost_fused(int D, int r);                  // per-pixel volume stride for D disparities, -1 if D > 512
+bool sgbm_cost_fused(int D, int r);
 // aux / fork / join: a second stream and two events for the concurrent vertical path (aux =
 // nullptr: everything on s)
 // nf frames per launch (grid.z), laid out as described at SgbmArgs::select_frame

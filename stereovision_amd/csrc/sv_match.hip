@@ -1248,7 +1248,11 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
         }
         return 0;
     }
-    if (ring_kind(cost, a.win, a.D)) return launch_ring(a, s);
+    // the ring kind stores through one buffer descriptor with 32-bit byte offsets
+    // (2 * (row * out_pitch + x) per frame); maps whose last row lies past 2^31 bytes take
+    // the size_t-addressed four-row kind instead
+    const bool ring_fits = 2LL * ((long long)(a.row1 + 3) * a.opitch + a.W + 64) < 0x7FFFFFFFLL;
+    if (ring_kind(cost, a.win, a.D) && ring_fits) return launch_ring(a, s);
     const size_t lds = match_lds_bytes(p, a.r, cost);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
     MatchParams b = a;

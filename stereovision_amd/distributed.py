@@ -35,7 +35,7 @@ import time
 
 import numpy as np
 
-from .engine import POST_DEPTH, POST_SCALED, Communicator, get_engine
+from .engine import BAND_MARGIN, POST_DEPTH, POST_SCALED, Communicator, get_engine
 
 
 # ---- partition arithmetic -----------------------------------------------------------------
@@ -47,6 +47,33 @@ def band_rows(H: int, rank: int, world: int) -> tuple[int, int]:
 def median_halo(r0: int, r1: int, H: int, halo: int = 2) -> tuple[int, int]:
     """Disparity rows a band needs for its 5x5 median (replicate border at the image edge)."""
     return max(0, r0 - halo), min(H, r1 + halo)
+
+
+def input_rows(h0: int, h1: int, H: int, win: int) -> tuple[int, int]:
+    """Input rows the kernels of disparity rows [h0, h1) read (sv_band_rows_in): the window's
+    r rows, the four-row waves' 3 extra rows below the last one and the HOG Sobel row,
+    i.e. r + 4 each side, clamped to the frame."""
+    halo = win // 2 + 4
+    return max(0, h0 - halo), min(H, h1 + halo)
+
+
+def band_layout(H: int, rank: int, world: int, win: int) -> dict:
+    """Output rows r0:r1, disparity rows h0:h1 (median halo) and input rows in0:in1 of a
+    rank's band (the same numbers as the C ABI's sv_band_rows_in)."""
+    r0, r1 = band_rows(H, rank, world)
+    h0, h1 = median_halo(r0, r1, H)
+    in0, in1 = input_rows(h0, h1, H, win)
+    return {"r0": r0, "r1": r1, "h0": h0, "h1": h1, "in0": in0, "in1": in1}
+
+
+def scatter_layout(H: int, world: int, win: int, row_nbytes: int) -> tuple[list[int], list[int]]:
+    """Byte offsets (into a full frame) and sizes of every rank's input rows."""
+    offs, sizes = [], []
+    for k in range(world):
+        b = band_layout(H, k, world, win)
+        offs.append(b["in0"] * row_nbytes)
+        sizes.append((b["in1"] - b["in0"]) * row_nbytes)
+    return offs, sizes
 
 
 def frame_indices(n_frames: int, rank: int, world: int) -> list[int]:
@@ -193,10 +220,26 @@ class ProcessGroup:
     buffers: RCCL (`backend == "rccl"`) or the file store with host staging ("host")."""
 
     def __init__(self, rank: int, world: int, device: int, store: FileStore | None,
-                 comm: Communicator | None, engine=None):
+                 comm: Communicator | None, engine=None, devices=None, reason: str = ""):
         self.rank, self.world, self.device = rank, world, device
         self.store, self.comm, self.engine = store, comm, engine
         self.backend = "rccl" if comm is not None else ("host" if world > 1 else "local")
+        self.devices = list(devices) if devices is not None else [device]
+        # why RCCL is not used ("" when it is): ranks sharing a GPU, library missing, "host"
+        # requested
+        self.reason = reason
+
+    @property
+    def rccl_ranks(self) -> int:
+        """Ranks of the RCCL communicator (0 when the group runs on the file store)."""
+        return self.comm.nranks if self.comm is not None else 0
+
+    def _stream(self, stream: int) -> int:
+        """stream 0 = this rank's engine stream (the one compute() enqueues on), never the
+        communicator's own stream: the gather must follow the kernels that write the data."""
+        if stream:
+            return stream
+        return (self.engine or get_engine(self.device)).stream
 
     def barrier(self):
         if self.comm is not None:
@@ -214,7 +257,8 @@ class ProcessGroup:
     def gatherv(self, d_send: int, send_bytes: int, d_recv: int, offsets, sizes, root: int = 0,
                 stream: int = 0):
         if self.comm is not None:
-            self.comm.gatherv(d_send, send_bytes, d_recv, offsets, sizes, root=root, stream=stream)
+            self.comm.gatherv(d_send, send_bytes, d_recv, offsets, sizes, root=root,
+                              stream=self._stream(stream))
             return
         eng = self.engine or get_engine(self.device)
         if self.world == 1 or self.store is None:
@@ -243,6 +287,37 @@ class ProcessGroup:
                 eng.to_device(d_recv + offsets[k], data)
         self.store.set(f"{t}.done", b"1")
 
+    def scatterv(self, d_send: int, offsets, sizes, d_recv: int, recv_bytes: int, root: int = 0,
+                 stream: int = 0):
+        """The root's block k (d_send + offsets[k], sizes[k] bytes) -> rank k's d_recv."""
+        if self.comm is not None:
+            self.comm.scatterv(d_send, offsets, sizes, d_recv, recv_bytes, root=root,
+                               stream=self._stream(stream))
+            return
+        eng = self.engine or get_engine(self.device)
+        if self.world == 1 or self.store is None:
+            if recv_bytes and d_recv != d_send + offsets[self.rank]:
+                eng.synchronize()
+                eng.to_device(d_recv, eng.to_host(d_send + offsets[self.rank], (recv_bytes,), np.uint8))
+            return
+        # host staging through the store (fallback when RCCL cannot run)
+        eng.synchronize()
+        t = self.store._tag("scatterv")
+        if self.rank == root:
+            for k in range(self.world):
+                host = eng.to_host(d_send + offsets[k], (sizes[k],), np.uint8) if sizes[k] else np.empty(0, np.uint8)
+                if k == root:
+                    if sizes[k] and d_recv != d_send + offsets[k]:
+                        eng.to_device(d_recv, host)
+                else:
+                    self.store.set(f"{t}.{k}", host.tobytes())
+            return
+        data = np.frombuffer(self.store.get(f"{t}.{self.rank}"), np.uint8)
+        if data.size != recv_bytes:
+            raise RuntimeError(f"scatterv: rank {self.rank} got {data.size} bytes, expected {recv_bytes}")
+        if data.size:
+            eng.to_device(d_recv, data)
+
     def close(self):
         if self.comm is not None:
             self.comm.close()
@@ -257,10 +332,12 @@ def _log(msg: str):
 
 
 def init_process_group(device: int | None = None, backend: str = "auto",
-                       timeout: float = 300.0, engine=None) -> ProcessGroup:
+                       timeout: float = 300.0, engine=None, strict: bool = False) -> ProcessGroup:
     """Process group of a torch.distributed.run-style launch, from RANK / WORLD_SIZE /
     LOCAL_RANK (world 1 when unset).  backend: "auto" (RCCL unless it cannot run: ranks
-    sharing a GPU, library missing), "rccl" (required), "host" (file store only)."""
+    sharing a GPU, library missing), "rccl" (required), "host" (file store only).
+    strict: with "auto", ranks on DISTINCT devices must get RCCL (RuntimeError otherwise);
+    only ranks sharing a GPU (a 1-GPU rehearsal) may fall back to the file store."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -269,7 +346,7 @@ def init_process_group(device: int | None = None, backend: str = "auto",
         nd = max(1, device_count())
         device = local % nd
     if world == 1:
-        return ProcessGroup(0, 1, device, None, None, engine)
+        return ProcessGroup(0, 1, device, None, None, engine, reason="world size 1")
     store = FileStore(default_store_path(), rank, world, timeout)
     # collective decision (a rank must never be left alone inside ncclCommInitRank)
     ok = backend != "host" and Communicator.available()
@@ -278,9 +355,13 @@ def init_process_group(device: int | None = None, backend: str = "auto",
     all_ok = all(struct.unpack("<ii", v)[1] for v in info)
     dup = len(set(devs)) < len(devs)
     use_rccl = all_ok and not dup
+    reason = ("file store requested (backend='host')" if backend == "host" else
+              f"ranks share a GPU (devices {devs})" if dup else
+              "librccl.so.1 not loadable on every rank" if not all_ok else "")
     if backend == "rccl" and not use_rccl:
-        raise RuntimeError(f"RCCL backend requested but unusable (devices {devs}, "
-                           f"library on every rank: {all_ok})")
+        raise RuntimeError(f"RCCL backend requested but unusable: {reason}")
+    if strict and backend == "auto" and not use_rccl and not dup:
+        raise RuntimeError(f"RCCL required on distinct devices {devs} but unusable: {reason}")
     comm = None
     if use_rccl:
         if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
@@ -288,17 +369,22 @@ def init_process_group(device: int | None = None, backend: str = "auto",
         uid = store.broadcast(Communicator.unique_id() if rank == 0 else None)
         comm = Communicator.init_rank(device, world, rank, uid)
     elif rank == 0:
-        _log(f"RCCL not used (devices {devs}, RCCL loadable on every rank: {all_ok}); "
-             "barriers/reductions through the file store, gathers through host staging")
-    return ProcessGroup(rank, world, device, store, comm, engine)
+        _log(f"RCCL not used ({reason}); barriers/reductions through the file store, "
+             "gathers through host staging")
+    return ProcessGroup(rank, world, device, store, comm, engine, devices=devs, reason=reason)
 
 
 class RowTiledDepthMap:
     """Row-tiled app-1 / app-2 device path for one frame across the ranks of a group.
 
-    Each rank owns full-frame gray inputs in HBM (device pointers) and computes its band:
-    disparity for the band plus the median halo (sv_disparity_dev), then median + post for
-    the band (sv_median_post_dev); :meth:`gather` moves the bands into rank 0's buffers.
+    Inputs either as full frames on every rank (:meth:`compute` with full-frame pointers), or
+    band-only (:meth:`scatter` from the root's full frame: rank k receives just the input rows
+    [in0, in1) its band reads into :attr:`band_left` / :attr:`band_right`, then
+    :meth:`compute` without arguments).  Each rank computes disparity for its band plus the
+    median halo (sv_disparity_dev), then median + post for the band (sv_median_post_dev);
+    :meth:`gather` moves the bands into rank 0's buffers.  Every operation is enqueued on
+    the engine's stream unless a stream is passed, so scatter -> compute -> gather are ordered
+    on one stream (the RCCL calls included).
     """
 
     def __init__(self, H: int, W: int, num_disp: int, win: int, min_disp: int = 0,
@@ -307,8 +393,9 @@ class RowTiledDepthMap:
         self.num_disp, self.win, self.min_disp, self.cost = num_disp, win, min_disp, cost
         self.rank, self.world = rank, world
         self.engine = engine or get_engine(device)
-        self.r0, self.r1 = band_rows(H, rank, world)
-        self.h0, self.h1 = median_halo(self.r0, self.r1, H)
+        b = band_layout(H, rank, world, win)
+        self.r0, self.r1, self.h0, self.h1 = b["r0"], b["r1"], b["h0"], b["h1"]
+        self.in0, self.in1 = b["in0"], b["in1"]
         e, n = self.engine, H * W
         self.d16 = e.dev_alloc(2 * n)
         self.disp = e.dev_alloc(4 * n)
@@ -316,28 +403,54 @@ class RowTiledDepthMap:
         self.out_b = e.dev_alloc(4 * n)
         self.out_u8 = e.dev_alloc(n)
         self.rows = self.r1 - self.r0
+        # band-only inputs: input rows [in0, in1) with BAND_MARGIN spare rows either side
+        self.band_bytes = (self.in1 - self.in0) * W
+        nb = self.band_bytes + 2 * BAND_MARGIN * W
+        self._band = [e.dev_alloc(max(256, nb)), e.dev_alloc(max(256, nb))]
+        self.band_left, self.band_right = (p + BAND_MARGIN * W for p in self._band)
 
-    def compute(self, d_left: int, d_right: int, mode: int = POST_DEPTH, min_depth: float = 0.3,
+    def _stream(self, stream: int) -> int:
+        return stream or self.engine.stream
+
+    def scatter(self, pg: "ProcessGroup", d_full_left: int = 0, d_full_right: int = 0,
+                root: int = 0, stream: int = 0):
+        """Input rows of every rank's band from the root's full-frame gray images (device
+        pointers, used on the root only) into each rank's band buffers."""
+        offs, sizes = scatter_layout(self.H, pg.world, self.win, self.W)
+        s = self._stream(stream)
+        for full, band in ((d_full_left, self.band_left), (d_full_right, self.band_right)):
+            pg.scatterv(full, offs, sizes, band, self.band_bytes, root=root, stream=s)
+
+    def compute(self, d_left: int = 0, d_right: int = 0, mode: int = POST_DEPTH, min_depth: float = 0.3,
                 max_depth: float = 2.0, min_disp_global=None, stream: int = 0):
         """Enqueue this rank's band; outputs at their full-frame row offsets of self.disp /
-        self.out_a / self.out_u8 (/ self.out_b for POST_SCALED)."""
+        self.out_a / self.out_u8 (/ self.out_b for POST_SCALED).  d_left/d_right: full-frame
+        gray images, or 0 for the band buffers filled by :meth:`scatter`."""
         e, H, W = self.engine, self.H, self.W
+        s = self._stream(stream)
+        if not d_left:   # band buffer addressed as a full frame (row y at base + y * W)
+            d_left = self.band_left - self.in0 * W
+            d_right = self.band_right - self.in0 * W
         e.disparity_dev(d_left, d_right, H, W, W, self.min_disp, self.num_disp, self.win, self.cost,
-                        self.h0, self.h1, self.d16, W, stream=stream)
+                        self.h0, self.h1, self.d16, W, stream=s)
         mdg = self.min_disp if min_disp_global is None else min_disp_global
         e.median_post_dev(self.d16, H, W, self.r0, self.r1, mode, self.disp, self.out_a,
                           self.out_u8, self.out_b if mode == POST_SCALED else 0,
                           min_depth=min_depth, max_depth=max_depth, min_disp_global=mdg,
-                          min_disp=self.min_disp, num_disp=self.num_disp, stream=stream)
+                          min_disp=self.min_disp, num_disp=self.num_disp, stream=s)
 
-    def gather(self, pg: ProcessGroup, root: int = 0, stream: int = 0, outputs=("disp", "out_a", "out_u8")):
-        """Bands of every rank into the root's full-frame buffers (in place)."""
+    def gather(self, pg: "ProcessGroup", root: int = 0, stream: int = 0,
+               outputs=("disp", "out_a", "out_u8")):
+        """Bands of every rank into the root's full-frame buffers (in place), on the engine
+        stream unless `stream` is given (never the communicator's own stream: ADVICE r02)."""
+        s = self._stream(stream)
         for name in outputs:
             elem = 1 if name == "out_u8" else 4
-            gather_rows(pg, getattr(self, name), self.H, self.W * elem, root=root, stream=stream)
+            gather_rows(pg, getattr(self, name), self.H, self.W * elem, root=root, stream=s)
 
     def close(self):
-        for p in (self.d16, self.disp, self.out_a, self.out_b, self.out_u8):
+        for p in (self.d16, self.disp, self.out_a, self.out_b, self.out_u8, *self._band):
             if p:
                 self.engine.dev_free(p)
         self.d16 = self.disp = self.out_a = self.out_b = self.out_u8 = 0
+        self._band = []

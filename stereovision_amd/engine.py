@@ -10,6 +10,7 @@ while the main thread keeps working.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import sys
@@ -24,7 +25,7 @@ COSTS = {"sad": 0, "ssd": 1, "hog": 2, "sgbm": 3}
 POST_NONE, POST_DEPTH, POST_SCALED = 0, 1, 2
 KERNELS = {"gray": 0, "harris": 1, "hog": 2, "match": 3, "median": 4, "post": 5, "remap": 6,
            "undistort": 7, "resize": 8, "stats": 9, "select": 10, "affine": 11, "sgbm": 12,
-           "speckle": 13}
+           "speckle": 13, "gather": 14, "scatter": 15}
 
 # Every symbol include/stereovision_amd.h declares (checked by tests/test_capi.py).
 EXPORTED = [
@@ -44,8 +45,10 @@ EXPORTED = [
     "sv_comm_destroy", "sv_comm_rank", "sv_comm_barrier", "sv_comm_allreduce_max_f64",
     "sv_comm_gatherv", "sv_comm_synchronize", "sv_multi_gpu_depth_map_dev",
     "sv_depth_map_rows_multi", "sv_depth_map_color", "sv_stereo_scaled_color",
-    "sv_median_post_color_dev",
+    "sv_median_post_color_dev", "sv_profile_region_begin", "sv_profile_region_end",
+    "sv_comm_scatterv", "sv_depth_map_rows_scatter", "sv_band_rows_in", "sv_release_scratch",
 ]
+BAND_MARGIN = 8   # SV_BAND_MARGIN: spare rows around a band-only input buffer
 COMM_ID_BYTES = 128
 
 
@@ -125,6 +128,7 @@ def _declare(lib):
         "sv_create": ([_c_int, ctypes.POINTER(_vp)], _c_int),
         "sv_destroy": ([_vp], None),
         "sv_synchronize": ([_vp], _c_int),
+        "sv_release_scratch": ([_vp], _c_int),
         "sv_stream": ([_vp], _vp),
         "sv_plan": ([_c_int, _c_int, _c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),
                      ctypes.POINTER(_c_int)], _c_int),
@@ -222,6 +226,12 @@ def _declare(lib):
         "sv_comm_gatherv": ([_vp, _vp, ctypes.c_uint64, _vp, ctypes.POINTER(ctypes.c_uint64),
                              ctypes.POINTER(ctypes.c_uint64), _c_int, _vp], _c_int),
         "sv_comm_synchronize": ([_vp], _c_int),
+        "sv_comm_scatterv": ([_vp, _vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                              _vp, ctypes.c_uint64, _c_int, _vp], _c_int),
+        "sv_depth_map_rows_scatter": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int, _vp, _vp,
+                                       _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                       _c_float, _c_float, _c_float, _c_float, _vp, _vp, _vp], _c_int),
+        "sv_band_rows_in": ([_c_int, _c_int, _c_int, _c_int, _c_int, ctypes.POINTER(_c_int)], _c_int),
         "sv_multi_gpu_depth_map_dev": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
                                         ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                                         ctypes.POINTER(_c_int), _c_int, _c_int, _c_int,
@@ -242,6 +252,8 @@ def _declare(lib):
         "sv_profile_read": ([_vp, _c_int, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_longlong)], _c_int),
         "sv_profile_reset": ([_vp], _c_int),
+        "sv_profile_region_begin": ([_vp, _c_int, _vp], _c_int),
+        "sv_profile_region_end": ([_vp, _vp], _c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -430,6 +442,10 @@ class Engine:
 
     def synchronize(self):
         _check("sv_synchronize", self.lib.sv_synchronize(self._h))
+
+    def release_scratch(self):
+        """Free the context's grow-only device scratch (e.g. after a large SGBM batch)."""
+        _check("sv_release_scratch", self.lib.sv_release_scratch(self._h))
 
     # -- host-memory entry points -----------------------------------------------------
     def gray(self, bgr: np.ndarray) -> np.ndarray:
@@ -902,6 +918,16 @@ class Engine:
     def profile(self, on: bool = True):
         _check("sv_profile_enable", self.lib.sv_profile_enable(self._h, 1 if on else 0))
 
+    def profile_region_begin(self, kernel: str | int, stream: int = 0):
+        """Open a caller-delimited profiling region on `stream` (counted under `kernel`,
+        e.g. "gather" around an RCCL gatherv this process enqueues); no-op unless profiling
+        is on."""
+        k = KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
+        _check("sv_profile_region_begin", self.lib.sv_profile_region_begin(self._h, k, stream or None))
+
+    def profile_region_end(self, stream: int = 0):
+        _check("sv_profile_region_end", self.lib.sv_profile_region_end(self._h, stream or None))
+
     def profile_reset(self):
         _check("sv_profile_reset", self.lib.sv_profile_reset(self._h))
 
@@ -993,6 +1019,30 @@ def depth_map_rows_multi(engines, comms, d_left, d_right, H: int, W: int, pitch:
         *_depth_args(min_depth, max_depth, min_disp, min_disp_global), d_depth, d_disp, d_norm))
 
 
+def depth_map_rows_scatter(engines, comms, d_left: int, d_right: int, H: int, W: int, pitch: int,
+                           min_disp: int, num_disp: int, win: int, min_depth: float, max_depth: float,
+                           d_depth: int, d_disp: int, d_norm: int, cost="sad", min_disp_global=None):
+    """C5 from ONE process with the frame resident on engines[0]'s device only
+    (sv_depth_map_rows_scatter): each other engine receives just the input rows of its band
+    (+ halos, :func:`band_rows_in`), computes its band, and the bands are gathered back into
+    the full-frame outputs on engines[0]'s device.  Enqueue only."""
+    engines = list(engines)
+    lib = engines[0].lib
+    ch = None if comms is None else _handles([c.handle for c in comms])
+    _check("sv_depth_map_rows_scatter", lib.sv_depth_map_rows_scatter(
+        _handles(engines), ch, len(engines), d_left, d_right, H, W, pitch, int(min_disp),
+        int(num_disp), int(win), _cost(cost), *_depth_args(min_depth, max_depth, min_disp, min_disp_global),
+        d_depth, d_disp, d_norm))
+
+
+def band_rows_in(H: int, rank: int, world: int, win: int, cost="sad") -> dict:
+    """Row bands of a `world`-way tiling (sv_band_rows_in): output rows r0:r1, disparity rows
+    h0:h1 (with the median halo) and the input rows in0:in1 the band's kernels read."""
+    out = (_c_int * 6)()
+    _check("sv_band_rows_in", load_library().sv_band_rows_in(H, rank, world, win, _cost(cost), out))
+    return dict(zip(("r0", "r1", "h0", "h1", "in0", "in1"), list(out)))
+
+
 class Communicator:
     """An RCCL communicator of libsvhip (sv_comm_*): rank `rank` of `nranks` on `device`."""
 
@@ -1060,6 +1110,15 @@ class Communicator:
                                                           d_recv or None, off, sz, int(root),
                                                           stream or None))
 
+    def scatterv(self, d_send: int, offsets, sizes, d_recv: int, recv_bytes: int, root: int = 0,
+                 stream: int = 0):
+        n = self.nranks
+        off = (ctypes.c_uint64 * n)(*[int(v) for v in offsets]) if offsets is not None else None
+        sz = (ctypes.c_uint64 * n)(*[int(v) for v in sizes]) if sizes is not None else None
+        _check("sv_comm_scatterv", self.lib.sv_comm_scatterv(self._h, d_send or None, off, sz,
+                                                            d_recv or None, int(recv_bytes), int(root),
+                                                            stream or None))
+
     def synchronize(self):
         _check("sv_comm_synchronize", self.lib.sv_comm_synchronize(self._h))
 
@@ -1076,7 +1135,10 @@ def start_warmup(fn, name: str = "sv-warmup") -> threading.Event:
     drop-in modules call this at import so the first frame of the reference's loop does not
     pay HIP initialisation, code-object loading and staging allocation inside its 0.5 s
     budget (fused_depth_map.py:2671).  Without a GPU (or library) the thread ends silently:
-    the first real call then raises EngineUnavailable loudly."""
+    the first real call then raises EngineUnavailable loudly.  The warm-up initialises the GPU
+    in the importing process: a host application that forks or execs worker processes after
+    importing the drop-ins sets SV_WARMUP_AT_IMPORT=0 (the first call then pays the start-up).
+    Interpreter exit waits for an unfinished warm-up (at most 30 s)."""
     done = threading.Event()
 
     def run():
@@ -1087,7 +1149,11 @@ def start_warmup(fn, name: str = "sv-warmup") -> threading.Event:
         finally:
             done.set()
 
-    threading.Thread(target=run, name=name, daemon=True).start()
+    t = threading.Thread(target=run, name=name, daemon=True)
+    t.start()
+    # a short-lived script must not tear the interpreter down while the warm-up is still
+    # inside a HIP call: wait for it at exit (bounded)
+    atexit.register(done.wait, 30.0)
     return done
 
 

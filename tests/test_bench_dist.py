@@ -1,0 +1,166 @@
+"""CPU tests of the multi-GPU bench contract and the band-only row tiling (no GPU).
+
+* bench.py's N > 1 line: the gather is on by default, and the `distributed` object carries
+  backend / rccl_ranks / rccl_reason / gather_us_per_step (dist_summary, fed by a file-store
+  process group of 2 spawned ranks, the 1-GPU rehearsal of the driver's launch);
+* init_process_group(strict=True) refuses a file-store fallback on distinct devices and
+  allows it when the ranks share a GPU;
+* ProcessGroup / RowTiledDepthMap default to the ENGINE stream for their collectives
+  (never the communicator's own stream);
+* band-only inputs: the Python layout equals the C ABI's sv_band_rows_in, and a band
+  computed by the C oracle from ONLY its input rows (everything else poisoned) equals the
+  full-frame result, for every rank of several tilings.
+"""
+import multiprocessing as mp
+import os
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+import sv_oracle_c as C
+from stereovision_amd import distributed as SD
+from stereovision_amd import engine as E
+from stereovision_amd.synthetic import stereo_pair
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_gather_is_the_default_for_multi_gpu_frames():
+    a = bench.parse_args(["--gpus", "2"])
+    assert not a.no_gather and a.mode == "frames"
+    assert bench.parse_args(["--gpus", "2", "--no-gather"]).no_gather
+    assert not bench.parse_args([]).no_verify
+
+
+def _dist_worker(rank, world, path, q):
+    os.environ.update({"WORLD_SIZE": str(world), "RANK": str(rank), "LOCAL_RANK": str(rank),
+                       "SV_RDZV_DIR": path})
+    # both ranks on "device 0": the 1-GPU rehearsal, where the file store is legitimate
+    pg = SD.init_process_group(device=0, backend="auto", timeout=60, strict=True)
+    d = bench.dist_summary(2, True, pg, gather=True, gather_ms=1.5, gather_n=3,
+                           gather_wall_s=0.002, steps=4, gather_bytes=9 * 1920 * 1080)
+    q.put((rank, d, "torch" in sys.modules))
+    pg.close()
+
+
+def test_dist_fields_under_the_file_store_rehearsal():
+    path = tempfile.mkdtemp(prefix="sv_bench_dist_")
+    os.rmdir(path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_dist_worker, args=(k, 2, path, q)) for k in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((r, (d, t)) for r, d, t in (q.get(timeout=120) for _ in range(2)))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    d, torch_loaded = res[0]
+    assert not torch_loaded
+    assert d["backend"] == "host" and d["rccl_ranks"] == 0
+    assert "share a GPU" in d["rccl_reason"]
+    assert d["gather"] is True and d["gather_us_per_step"] == 500.0 and d["gather_events"] == 3
+    assert d["gather_bytes_per_step"] == 9 * 1920 * 1080 and d["gather_GBps"] > 0
+    assert d["gather_wall_us_per_step"] == 500.0
+
+
+def test_dist_summary_one_process_modes():
+    assert bench.dist_summary(1, False) is None
+
+    class Comm:
+        pass
+    d = bench.dist_summary(8, False, comms=[Comm()] * 8, gather=True)
+    assert d["backend"] == "rccl" and d["rccl_ranks"] == 8 and d["rccl_reason"] is None
+    d = bench.dist_summary(4, False, comms=None, rowtile=True, scatter_ms=2.0, scatter_n=4,
+                           reason="ncclCommInitAll failed: x")
+    assert d["backend"] == "peer" and d["rccl_ranks"] == 0 and "ncclCommInitAll" in d["rccl_reason"]
+    assert d["scatter_us_per_step"] == 500.0 and "band-only" in d["inputs"]
+
+
+def _strict_worker(rank, world, path, q):
+    os.environ.update({"WORLD_SIZE": str(world), "RANK": str(rank), "LOCAL_RANK": str(rank),
+                       "SV_RDZV_DIR": path})
+    E.Communicator.available = staticmethod(lambda: False)    # "librccl.so.1 missing"
+    try:
+        SD.init_process_group(device=rank, backend="auto", timeout=60, strict=True)
+        q.put((rank, "no error"))
+    except RuntimeError as e:
+        q.put((rank, str(e)))
+
+
+def test_strict_group_refuses_file_store_on_distinct_devices():
+    path = tempfile.mkdtemp(prefix="sv_bench_strict_")
+    os.rmdir(path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_strict_worker, args=(k, 2, path, q)) for k in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in ps:
+        p.join(timeout=60)
+    assert all("RCCL required on distinct devices" in msg for _, msg in res), res
+
+
+class _FakeEngine:
+    stream = 0xABC
+
+
+class _FakeComm:
+    nranks = 2
+
+    def __init__(self):
+        self.streams = []
+
+    def gatherv(self, *a, stream=0, **k):
+        self.streams.append(stream)
+
+    def scatterv(self, *a, stream=0, **k):
+        self.streams.append(stream)
+
+
+def test_collectives_default_to_the_engine_stream():
+    comm = _FakeComm()
+    pg = SD.ProcessGroup(0, 2, 0, None, comm, engine=_FakeEngine())
+    assert pg.backend == "rccl" and pg.rccl_ranks == 2
+    SD.gather_rows(pg, 0, 10, 4)                 # the documented default-stream call
+    SD.gather_frames(pg, 0, 1, 0, 4)
+    pg.scatterv(0, [0, 0], [1, 1], 0, 1)
+    pg.gatherv(0, 1, 0, [0, 1], [1, 1], stream=77)
+    assert comm.streams == [0xABC, 0xABC, 0xABC, 77]
+
+
+def test_python_band_layout_equals_the_c_abi():
+    lib = E.load_library()
+    assert lib is not None
+    for H in (1, 7, 29, 270, 1080, 2160):
+        for world in (1, 2, 3, 8):
+            for win in (1, 5, 9, 15):
+                for k in range(world):
+                    assert SD.band_layout(H, k, world, win) == E.band_rows_in(H, k, world, win), (H, world, win, k)
+    offs, sizes = SD.scatter_layout(2160, 8, 15, 3840)
+    b = SD.band_layout(2160, 3, 8, 15)
+    assert offs[3] == b["in0"] * 3840 and sizes[3] == (b["in1"] - b["in0"]) * 3840
+
+
+@pytest.mark.parametrize("world,H,win,cost", [(2, 64, 9, 0), (3, 41, 15, 0), (8, 131, 5, 0),
+                                               (4, 50, 11, 1), (3, 37, 7, 2)])
+def test_band_from_its_input_rows_only_matches_the_full_frame(world, H, win, cost):
+    W, D = 160, 48
+    L, R, _ = stereo_pair(H, W, D, seed=world * 1000 + H)
+    ref = C.disparity16(L, R, 0, D, win, cost)
+    ref_med = C.median5_f32(ref)
+    for k in range(world):
+        b = SD.band_layout(H, k, world, win)
+        Lp = np.full_like(L, 0xA5)
+        Rp = np.full_like(R, 0x5A)
+        Lp[b["in0"]:b["in1"]] = L[b["in0"]:b["in1"]]
+        Rp[b["in0"]:b["in1"]] = R[b["in0"]:b["in1"]]
+        d16 = C.disparity16(Lp, Rp, 0, D, win, cost, rows=(b["h0"], b["h1"]))
+        np.testing.assert_array_equal(d16[b["h0"]:b["h1"]], ref[b["h0"]:b["h1"]])
+        med = C.median5_f32(d16[b["h0"]:b["h1"]])[b["r0"] - b["h0"]:b["r1"] - b["h0"]]
+        np.testing.assert_array_equal(med, ref_med[b["r0"]:b["r1"]])

@@ -580,3 +580,27 @@ def test_registered_outputs_dma_path_matches_host_expansion(engine, scaled):
         del got
     regs = getattr(engine, "_registered", {})
     assert regs, "no output set was registered"
+
+
+@pytest.mark.parametrize("win,D", [(9, 128), (15, 256)])
+def test_ring_kind_huge_out_pitch_falls_back_exactly(engine, win, D):
+    """the ring kernel's 32-bit buffer offsets cannot address an int16 map whose
+    rows lie past 2^31 bytes; such maps take the size_t-addressed four-row kind, bit-exact."""
+    H, W = 40, 400
+    opitch = (1 << 26) + 64                       # 2 * 40 * 2^26 bytes = 5.4 GB of map span
+    L, R, _ = stereo_pair(H, W, D, seed=31)
+    exp = O.disparity16(L, R, 0, D, win)
+    dL, dR = engine.dev_alloc(H * W), engine.dev_alloc(H * W)
+    engine.to_device(dL, L)
+    engine.to_device(dR, R)
+    span = 2 * ((H - 1) * opitch + W)
+    d16 = engine.dev_alloc(span)
+    try:
+        engine.disparity_dev(dL, dR, H, W, W, 0, D, win, "sad", 0, H, d16, opitch)
+        engine.synchronize()
+        for y in (0, 1, H // 2, H - 2, H - 1):
+            row = engine.to_host(d16 + 2 * y * opitch, (W,), np.int16)
+            np.testing.assert_array_equal(row, exp[y], err_msg=f"row {y}")
+    finally:
+        for p in (dL, dR, d16):
+            engine.dev_free(p)

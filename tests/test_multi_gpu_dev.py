@@ -137,6 +137,74 @@ def test_c5_row_tiled_over_8_contexts_gathered_on_device_0(ctxs):
     np.testing.assert_array_equal(norm, e_norm)
 
 
+def _rows_scatter(es, comms, L, R, D, win, cost="sad"):
+    """sv_depth_map_rows_scatter: the frame on es[0]'s device only; bands + halos scattered."""
+    from stereovision_amd.engine import depth_map_rows_scatter
+    H, W = L.shape
+    root = es[0]
+    dL, dR = _upload(root, L), _upload(root, R)
+    n = H * W
+    o = [root.dev_alloc(4 * n), root.dev_alloc(4 * n), root.dev_alloc(n)]
+    try:
+        depth_map_rows_scatter(es, comms, dL, dR, H, W, W, 0, D, win, 0.3, 2.0, o[0], o[1], o[2],
+                               cost=cost)
+        root.synchronize()
+        return (root.to_host(o[1], (H, W), np.float32), root.to_host(o[0], (H, W), np.float32),
+                root.to_host(o[2], (H, W), np.uint8))
+    finally:
+        root.dev_free(dL)
+        root.dev_free(dR)
+        for p in o:
+            root.dev_free(p)
+
+
+@pytest.mark.parametrize("ndev,H,cost,win", [(8, 131, "sad", 9), (3, 29, "sad", 15),
+                                               (8, 57, "hog", 5), (2, 64, "ssd", 7), (1, 40, "sad", 9),
+                                               (4, 96, "sad", 11), (8, 300, "hog", 15)])
+def test_depth_map_rows_scatter_band_only_inputs(ctxs, ndev, H, cost, win):
+    """Band-only inputs: context k > 0 holds just the input rows of its band (+ halos), in a
+    scratch buffer whose spare rows hold the PREVIOUS call's frame (first call: a different
+    frame), so any read outside the band's rows would break bit-exactness."""
+    W, D = 400, 64
+    Lx, Rx, _ = stereo_pair(H, W, D, seed=ndev * 100 + H + 1)
+    _rows_scatter(ctxs[:ndev], None, Lx, Rx, D, win, cost)          # leaves stale rows behind
+    L, R, _ = stereo_pair(H, W, D, seed=ndev * 100 + H)
+    disp, depth, norm = _rows_scatter(ctxs[:ndev], None, L, R, D, win, cost)
+    e_disp, e_depth, e_norm = _oracle(L, R, D, win, cost)
+    np.testing.assert_array_equal(disp, e_disp)
+    np.testing.assert_array_equal(depth, e_depth)
+    np.testing.assert_array_equal(norm, e_norm)
+
+
+def test_c5_row_tiled_band_inputs_over_8_contexts(ctxs):
+    """C5 (3840x2160, D=256, 15x15) with band-only inputs scattered from the first context."""
+    L, R, _ = stereo_pair(2160, 3840, 256, seed=57)
+    disp, depth, norm = _rows_scatter(ctxs, None, L, R, 256, 15)
+    e_disp, e_depth, e_norm = _oracle(L, R, 256, 15)
+    np.testing.assert_array_equal(disp, e_disp)
+    np.testing.assert_array_equal(depth, e_depth)
+    np.testing.assert_array_equal(norm, e_norm)
+
+
+def test_rccl_group_scatter_band_inputs(ctxs):
+    """The scatter + gather of sv_depth_map_rows_scatter as RCCL groups over this box's
+    distinct devices."""
+    nd = max(1, device_count())
+    devs = list(range(min(nd, 8)))
+    comms = Communicator.init_all(devs)
+    es = [next(e for e in ctxs if e.device == d) for d in devs]
+    try:
+        L, R, _ = stereo_pair(97, 350, 64, seed=19)
+        disp, depth, norm = _rows_scatter(es, comms, L, R, 64, 9)
+        e_disp, e_depth, e_norm = _oracle(L, R, 64, 9)
+        np.testing.assert_array_equal(disp, e_disp)
+        np.testing.assert_array_equal(depth, e_depth)
+        np.testing.assert_array_equal(norm, e_norm)
+    finally:
+        for c in comms:
+            c.close()
+
+
 def test_multi_device_argument_checks(ctxs):
     from stereovision_amd.engine import SVError
     H, W = 16, 64
@@ -210,11 +278,13 @@ def _port():
 def test_bench_under_torch_distributed_run_two_ranks(mode):
     """The driver's N>1 launch: torch.distributed.run starts 2 bench.py workers (torch-free).
     On a 1-GPU box both ranks share the GPU, so the group falls back to the file store (RCCL
-    refuses two ranks on one device); on a multi-GPU box it is RCCL."""
+    refuses two ranks on one device); on a multi-GPU box it is RCCL.  The gather is on by
+    default; rank 0 checks every rank's gathered maps (frames) / the reassembled frame from
+    band-only inputs (rowtile) against the C oracle: `verified` must be true."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
            "--steps", "3", "--warmup", "1", "--height", "96", "--width", "400", "--num-disp", "64",
-           "--frames", "2", "--batch", "2", "--mode", mode, "--gather", "--no-live-pmc", "--no-aux",
+           "--frames", "2", "--batch", "2", "--mode", mode, "--no-live-pmc", "--no-aux",
            "--no-host-path", "--no-cpu-baseline"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
@@ -223,6 +293,30 @@ def test_bench_under_torch_distributed_run_two_ranks(mode):
     res = json.loads(line)
     assert res["n_gpus"] == 2 and res["value"] > 0
     assert res["scaling"] == ("strong" if mode == "rowtile" else "weak")
+    assert res["verified"] is True, res["verify"]
+    d = res["distributed"]
+    assert d["gather"] is True and d["process_model"] == "one process per GPU"
+    if device_count() == 1:
+        assert d["backend"] == "host" and d["rccl_ranks"] == 0 and "share a GPU" in d["rccl_reason"]
+    else:
+        assert d["backend"] == "rccl" and d["rccl_ranks"] == 2
+    checked = res["verify"]["checked"]
+    if mode == "frames":     # both ranks' first and last frame, from rank 0's gathered stacks
+        assert sum("gathered on rank 0" in c for c in checked) == 4, checked
+    else:
+        assert checked == ["full frame gathered on rank 0"]
+
+
+def test_bench_single_gpu_verifies_its_timed_outputs():
+    cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--height", "120",
+           "--width", "400", "--num-disp", "64", "--frames", "4", "--batch", "2", "--no-live-pmc",
+           "--no-aux", "--no-host-path", "--no-cpu-baseline", "--harris"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    import json
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["verified"] is True and res["distributed"] is None
+    assert len(res["verify"]["checked"]) == 4     # frames 0 and B-1: maps + Harris each
 
 
 # ---- cross-stream ordering of the context scratch -----------------------------------

@@ -258,6 +258,13 @@ def aux_kernels(eng, H, W, B, med_ms, med_n, reps=20, blocker=None):
         ms, n = timed(lambda: eng.frame_stats_dev(dst, dst + H * W, H, W, 1, W, st, st + 8 * nb,
                                                   st + 16 * nb))
         out["k_frame_stats"] = hbm_entry("k_frame_stats", 2 * H * W, ms, n)
+        # the same statistics for a batch of B pairs in one launch + one fold
+        # (sv_frame_stats_batch_dev): the queued-frames form
+        gpair = arena.upload(rng.integers(0, 256, (B, 2, H, W), dtype=np.uint8))
+        stb = arena.alloc(4 * 2 * B * (2 * nb + 256))
+        ms, n = timed(lambda: eng.frame_stats_batch_dev(gpair, gpair + H * W, B, 2 * H * W, H, W, 1, W, stb,
+                                                        stb + 8 * B * nb, stb + 16 * B * nb))
+        out["k_frame_stats_batch"] = hbm_entry(f"k_frame_stats ({B} pairs per launch)", 2 * H * W * B, ms, n)
         # one radix-select pass over a float32 disparity map (4 B/px).  select_count returns
         # its counts to the host (a synchronising call), so this one is timed per launch by
         # the context's kernel events

@@ -417,6 +417,16 @@ int sv_frame_stats_dev(sv_ctx* ctx, const uint8_t* d_img0, const uint8_t* d_img1
                        int channels, int pitch, uint32_t* d_block_sum, uint32_t* d_block_sq,
                        uint32_t* d_hist, void* stream);
 
+/* sv_frame_stats_dev over a batch of n_frames images or pairs in one launch (image z of the
+ * batch: img0 / img1 of frame z / per at + (z / per) * frame_stride bytes, per = 2 with
+ * d_img1, else 1); outputs dense per image z: block moments [n_img][bh*bw], hist [n_img][256].
+ * detect_camera_occlusion runs once per checked frame (fused_depth_map.py:2515-2522); a
+ * stream of queued frames is one launch plus one fold. */
+int sv_frame_stats_batch_dev(sv_ctx* ctx, const uint8_t* d_img0, const uint8_t* d_img1, int n_frames,
+                             int64_t frame_stride, int H, int W, int channels, int pitch,
+                             uint32_t* d_block_sum, uint32_t* d_block_sq, uint32_t* d_hist,
+                             void* stream);
+
 /* Order statistics of a float32 device array for np.percentile (calibrate_midas_to_stereo
  * fused_depth_map.py:1169-1257, normalize_to_stereo_range :1503-1554) with the reference's
  * masks as predicates: mask_mode 0 = all elements, 1 = elements > 0 (stereo_disparity > 0),

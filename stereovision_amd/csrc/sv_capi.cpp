@@ -2243,6 +2243,41 @@ int sv_frame_stats_dev(sv_ctx* c, const uint8_t* d_img0, const uint8_t* d_img1, 
     a.W = W;
     a.pitch = pitch;
     a.cn = channels;
+    a.per = nimg;
+    a.fs = 0;
+    stats_blocks(H, W, &a.bh, &a.bw);
+    a.block_sum = d_block_sum;
+    a.block_sq = d_block_sq;
+    a.hist = d_hist;
+    SV_LAUNCH(c, SV_K_STATS, s, sv::launch_frame_stats(a, nimg, s));
+    return 0;
+}
+
+int sv_frame_stats_batch_dev(sv_ctx* c, const uint8_t* d_img0, const uint8_t* d_img1, int n_frames,
+                             int64_t frame_stride, int H, int W, int channels, int pitch, uint32_t* d_block_sum,
+                             uint32_t* d_block_sq, uint32_t* d_hist, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_img0, H, W) || !d_block_sum || !d_block_sq || !d_hist || n_frames < 1)
+        return fail(SV_EINVAL, "bad frame-stats arguments");
+    if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
+    if (pitch < W * channels) return fail(SV_EINVAL, "pitch smaller than a row");
+    if (n_frames > 1 && frame_stride < (int64_t)pitch * H) return fail(SV_EINVAL, "frame stride smaller than a frame");
+    const int per = d_img1 ? 2 : 1;
+    if ((long long)n_frames * per > 65535) return fail(SV_EINVAL, "too many images in one batch");
+    hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
+    const int nimg = n_frames * per;
+    SV_HIP(c->hist_copies.ensure_zeroed((size_t)sv::kHistCopies * nimg * 256 * sizeof(uint32_t)));
+    sv::FrameStatsArgs a{};
+    a.hist_copies = c->hist_copies.as<uint32_t>();
+    a.img0 = d_img0;
+    a.img1 = d_img1;
+    a.H = H;
+    a.W = W;
+    a.pitch = pitch;
+    a.cn = channels;
+    a.per = per;
+    a.fs = n_frames > 1 ? frame_stride : 0;
     stats_blocks(H, W, &a.bh, &a.bw);
     a.block_sum = d_block_sum;
     a.block_sq = d_block_sq;
@@ -2282,6 +2317,8 @@ int sv_frame_stats(sv_ctx* c, const uint8_t* img0, const uint8_t* img1, int H, i
     a.W = W;
     a.pitch = (int)row;
     a.cn = channels;
+    a.per = nimg;
+    a.fs = 0;
     a.bh = bh;
     a.bw = bw;
     a.block_sum = d;

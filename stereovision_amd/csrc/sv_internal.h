@@ -102,6 +102,10 @@ struct FrameStatsArgs {
     uint32_t* block_sq;
     uint32_t* hist;           // [nimg][256], written whole by the fold kernel
     uint32_t* hist_copies;    // accumulators [kHistCopies][nimg][256], zero on entry and exit
+    // frame batches: image z of the launch (grid.z) is image z % per (img0 / img1) of frame
+    // z / per, at + (z / per) * fs bytes; outputs are dense per image z
+    int per;                  // images per frame: 1 or 2
+    long long fs;
 };
 // Global histograms are accumulated into kHistCopies copies (block b adds into copy
 // b % kHistCopies: hundreds of same-address atomics serialise at L2) and folded after.

@@ -32,6 +32,7 @@
 //   HOG   9-bin u16 window histograms as packs compared with v_sad_u16 (no running window).
 #include "sv_internal.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -1183,6 +1184,522 @@ int launch_ring(const MatchParams& a0, hipStream_t s) {
     return (int)hipErrorInvalidValue;
 }
 
+
+// ---- stream kind: persistent waves walking whole rows (SAD, win 5..9, 65 <= D <= 256) -------
+// The ring kind above spends 2r warm-up steps per segment of S = 128 columns (6% of its steps
+// at the metric config) because a segment's right packs (S + D + 2r of them) must fit in LDS
+// at once, and its 30k waves per 16-frame launch leave a partly filled last round.  Here a
+// launch is exactly as many waves as the chip holds (8 per CU) and each wave takes an equal
+// contiguous share of the launch's work, measured in bodies of U = 4*W2 steps of a row bundle
+// (G = 64/LPG vertically adjacent row quads, one per lane group, walking the same columns in
+// lockstep).  Packs live in per-group LDS rings that are refilled one body ahead:
+//   * at the top of a body every producer lane issues the global loads of one 4-column unit
+//     of the NEXT body's packs (2r+4 dword rows; right units of group gg, then left units);
+//   * the body's U steps run exactly as in the ring kind (static register rings, one basic
+//     block);
+//   * at the bottom the units are transposed into packs and written to the rings.
+// A row starts with a burst build of the packs its first body needs (the right stream needs
+// D + 3 packs of history per lane group); the running window sums need no reset (a window
+// sum is exactly the sum of its ring entries), only the first 2r steps of a row emit nothing.
+// A wave whose share starts inside a row first runs a prologue of the 2r (rounded to 4)
+// steps before it, without reductions or stores.  Rows are padded to whole bodies.
+// Right ring: position p <-> column xR0 + p of the bundle's row, slot phys(p mod RL) with one
+// empty slot per 4 (phase c0: every lane's chunk reads 4 consecutive slots, 16 lanes of a
+// group on distinct banks), the first TPR slots mirrored after the period so a body's reads
+// never wrap.  Left ring: position s <-> column xL0 + s, broadcast reads, TL slots mirrored.
+struct StreamParams {
+    const uint8_t* img;        // min(L, R): one buffer resource covers both images
+    int offL, offR;            // byte offsets of L and R from img (host-checked < 2^31)
+    int img_span;              // bytes from img through the end of the later image
+    int16_t* out;
+    int H, W, pitch, opitch;
+    int minD, D, X0, X1, row0, row1;
+    long long fs_in, fs_out;
+    int xl0, xr0, delta, c0;   // stream origins (4-aligned), right read offset, gap phase
+    int nb;                    // bodies per row bundle
+    int nq, nbund;             // row quads / bundles per frame
+    long long total;           // bodies of the launch (nf * nbund * nb)
+};
+
+template <int R, int LPG> struct StreamCfg {
+    static constexpr int W2 = 2 * R + 1, U = 4 * W2, G = 64 / LPG;
+    static constexpr int PRE = (2 * R + 3) / 4 * 4;                 // prologue steps
+    static constexpr int RL = (4 * (LPG - 1) + U + PRE + 9 + 3) & ~3;   // right ring positions
+    static constexpr int RPER = RL + RL / 4;                         // ... slots per period
+    static constexpr int TPR = 5 * W2;                               // mirrored slots
+    static constexpr int RSL = RPER + TPR;
+    static constexpr int LL = (U + PRE + 3 + 3) & ~3;                // left ring positions
+    static constexpr int TL = U;
+    static constexpr int LSL = LL + TL;
+    static constexpr int GROUP_BYTES = 24 * (RSL + LSL);
+    static constexpr int LDS_BYTES = G * GROUP_BYTES + 32;           // + one dummy slot pair
+    static constexpr int NROW = 2 * R + 4;                          // image rows of a pack
+};
+
+// Unit geometry of a producer lane: which group's ring, which image, which unit column.
+struct StreamUnit {
+    int gg;        // group whose ring receives the unit (-1: idle lane)
+    int right;     // 1: right image / ring
+    int col;       // first image column of the unit (4-aligned, may lie outside [0, W))
+    int yq;        // top output row of the group's row quad
+};
+
+// Loads of one unit: NROW dwords, rows clamp(yq - R + j), columns clamp(col, 0, W - 4) (the
+// edge bytes are replicated by stream_store's v_perm when the unit crosses an image border).
+// ONE load per row through one resource covering both images (per-lane image offset), so
+// the loaded registers are not touched until the transposes at the end of the body.
+// fast: rows of every producer group inside the image (uniform): row j = soffset j * pitch.
+template <int R>
+__device__ __forceinline__ void stream_load(const StreamParams& p, __amdgpu_buffer_rsrc_t rs, const StreamUnit& u,
+                                            bool fast, uint32_t (&rw)[2 * R + 4]) {
+    constexpr int NROW = 2 * R + 4;
+    const int OOR = 0x7FFF0000;
+    const int io = u.right ? p.offR : p.offL;
+    const int cl = clampi(u.col, 0, p.W - 4);
+    if (fast) {
+        const int base = u.gg >= 0 ? io + (u.yq - R) * p.pitch + cl : OOR;
+#pragma unroll
+        for (int j = 0; j < NROW; ++j) rw[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, base, j * p.pitch, 0);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < NROW; ++j) {
+        const int off = u.gg >= 0 ? io + clampi(u.yq - R + j, 0, p.H - 1) * p.pitch + cl : OOR;
+        rw[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+    }
+}
+
+// v_perm selector replicating the edge bytes of a unit that starts at column `col`
+__device__ __forceinline__ uint32_t stream_edge_sel(int col, int W) {
+    const int cl = clampi(col, 0, W - 4);
+    uint32_t sel = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sel |= (uint32_t)(clampi(col + i, 0, W - 1) - cl) << (8 * i);
+    return sel;
+}
+
+// Ring slots of a unit's 4 packs (positions 4 m .. 4 m + 3 of its stream) and the writes,
+// mirrored slots included; idle lanes write the dummy slot.
+template <int R, int LPG>
+__device__ __forceinline__ void stream_store(char* lds, const StreamUnit& u, int m, int c0, uint32_t (&rw)[2 * R + 4],
+                                             bool edges, int W) {
+    using C = StreamCfg<R, LPG>;
+    constexpr int NC = PackCfg<COST_SAD4, R>::NC, NCR = 2 * R - 2;
+    if (edges) {   // a unit of this batch may cross an image border (uniform)
+        const uint32_t sel = stream_edge_sel(u.col, W);
+#pragma unroll
+        for (int j = 0; j < 2 * R + 4; ++j) rw[j] = __builtin_amdgcn_perm(rw[j], rw[j], sel);
+    }
+    // slot byte offsets of the 4 packs (main array; the common array is at +cofs, half the
+    // stride) and of their mirrors (the dummy slot when not mirrored / idle lane)
+    const int dummy = C::G * C::GROUP_BYTES;
+    const int gb = u.gg * C::GROUP_BYTES;
+    int s0[4], s1[4];
+    const int cofs = u.right ? 16 * C::RSL : 16 * C::LSL;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (u.right) {
+            const int q = (4 * m) % C::RL + k;
+            const int ph = q + ((q + c0) >> 2);
+            s0[k] = ph;
+            s1[k] = ph < C::TPR ? ph + C::RPER : -1;
+        } else {
+            const int q = (4 * m) % C::LL + k;
+            s0[k] = q;
+            s1[k] = q < C::TL ? q + C::LL : -1;
+        }
+    }
+    const int abase = gb + (u.right ? 0 : 24 * C::RSL);
+    // common words first (rows 3 .. 2r), written before the custom words are formed: the
+    // unit's live registers stay near NROW + 8 while the body's register rings are live
+    {
+        uint32_t w[NC][4];
+#pragma unroll
+        for (int mm = 0; mm < NC; ++mm) {
+            uint32_t d[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) d[t] = 4 * mm + t < NCR ? rw[3 + 4 * mm + t] : 0u;
+            transpose4(d[0], d[1], d[2], d[3], w[mm]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint2 v = make_uint2(w[0][k], NC > 1 ? w[NC > 1 ? 1 : 0][k] : 0u);
+            const int a0 = u.gg < 0 ? dummy + 16 : abase + cofs + 8 * s0[k];
+            const int a1 = (u.gg < 0 || s1[k] < 0) ? dummy + 16 : abase + cofs + 8 * s1[k];
+            *reinterpret_cast<uint2*>(lds + a0) = v;
+            *reinterpret_cast<uint2*>(lds + a1) = v;
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+        uint32_t w[4][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t d[3];
+            int n = 0;
+#pragma unroll
+            for (int j = q; j <= 2; ++j) d[n++] = rw[j];
+#pragma unroll
+            for (int j = 2 * R + 1; j <= 2 * R + q; ++j) d[n++] = rw[j];
+            transpose4(d[0], d[1], d[2], 0u, w[q]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = make_uint4(w[0][k], w[1][k], w[2][k], w[3][k]);
+            const int a0 = u.gg < 0 ? dummy : abase + 16 * s0[k];
+            const int a1 = (u.gg < 0 || s1[k] < 0) ? dummy : abase + 16 * s1[k];
+            *reinterpret_cast<uint4*>(lds + a0) = v;
+            *reinterpret_cast<uint4*>(lds + a1) = v;
+        }
+    }
+}
+
+template <int R, int LPG>
+__global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
+    using P = PackCfg<COST_SAD4, R>;
+    using C = StreamCfg<R, LPG>;
+    constexpr int NW = P::NW, NC = P::NC, W2 = C::W2, U = C::U, G = C::G;
+    constexpr int RQ = 4;
+    static_assert(LPG >= 32 && R >= 2 && R <= 4, "stream kind: LPG 32/64, r 2..4");
+    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    char* lds = reinterpret_cast<char*>(smem);
+    const int lane = threadIdx.x;
+    const int g = lane / LPG, l = lane & (LPG - 1);
+    const int band = p.X1 - p.X0;
+
+    // this wave's share of the launch: bodies [b_lo, b_hi)
+    const long long b_lo = p.total * (long long)blockIdx.x / gridDim.x;
+    const long long b_hi = p.total * (long long)(blockIdx.x + 1) / gridDim.x;
+
+    // per-lane constants of the step loop
+    const int dl = p.delta - 4 * l;                      // right position offset of the lane
+    uint32_t h[RG_DPL][RQ], ring[W2][RG_DPL][RQ];
+    const int jq = (lane >> 2) & 3, ju = (lane >> 1) & 1;
+    int pofs;
+    {
+        const auto pp = __builtin_amdgcn_permlane16_swap((uint32_t)lane, (uint32_t)lane + 64u, false, false);
+        pofs = (max(pp[0], pp[1]) < 64u) ? 0 : 2;
+    }
+    const int el0 = p.xl0 + ju + pofs - R - p.X0;        // + step: column - X0 of the lane's pair
+    const bool emit_lane = (l & 1) == 0 && l < 32;   // LPG 64: rows 0, 1 of the group
+    // producer lane roles (fixed): unit kk of group gg, right units first
+    const int NUR = W2 + ((p.delta & 3) ? 1 : 0);
+    const int per_g = NUR + W2;
+    const int pg_ = lane / per_g, pk_ = lane % per_g;
+    const bool prod = pg_ < G;
+    const int p_right = pk_ < NUR ? 1 : 0;
+    const int p_k = p_right ? pk_ : pk_ - NUR;
+
+    const int gbase = g * C::GROUP_BYTES;
+    const int rmain = gbase, rcom = gbase + 16 * C::RSL;
+    const int lmain = gbase + 24 * C::RSL, lcom = lmain + 16 * C::LSL;
+
+    long long b = b_lo;
+    bool first_row = true;
+    Pk<NW> rn[RG_DPL], Lnext;
+    while (b < b_hi) {
+        // ---- row setup -------------------------------------------------------------------
+        const long long bund = b / p.nb;
+        const int jb0 = (int)(b - bund * p.nb);
+        const long long b_end = min(b_hi, (bund + 1) * (long long)p.nb);
+        const int frame = (int)(bund / p.nbund);
+        const int bq = (int)(bund - (long long)frame * p.nbund);
+        const int yq = p.row0 + (bq * G + g) * 4;            // this lane's group row quad
+        const bool gvalid = bq * G + g < p.nq;
+        const auto rsI = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.img + frame * p.fs_in), 0, p.img_span,
+                                                          0x00020000);
+        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(p.out + frame * p.fs_out, 0, 0x7FFFFFFF, 0x00020000);
+        // rows of every group inside the image (uniform): fast producer loads
+        const int ytop = p.row0 + bq * G * 4;
+        const bool rows_in = ytop - R >= 0 && ytop + 4 * G - 1 + R <= p.H - 1;
+        // producer lane's unit rows
+        const int p_yq = p.row0 + (bq * G + min(pg_, G - 1)) * 4;
+        // emission: lane's output offset at step 0 and its column window
+        const int band_l = (gvalid && yq + jq < p.row1) ? band : 0;
+        const int ooff0 = 2 * ((yq + jq) * p.opitch + p.xl0 + ju + pofs - R);
+
+        __syncthreads();   // the previous row's reads are done before its rings are rebuilt
+        if (jb0 == 0) {     // invalid columns outside the matched band, rows of every group
+            const int ninv = p.X0 + (p.W - p.X1);
+            const int16_t inv = (int16_t)((p.minD - 1) * 16);
+            for (int i = lane; i < G * 4 * ninv; i += 64) {
+                const int gq = i / ninv, c = i - gq * ninv;
+                const int x = c < p.X0 ? c : p.X1 + (c - p.X0);
+                const int y = p.row0 + (bq * G + gq / 4) * 4 + (gq & 3);
+                if (bq * G + gq / 4 < p.nq && y < p.row1)
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)inv, orsrc, 2 * (y * p.opitch + x), 0, 0);
+            }
+        }
+        // ---- burst: the packs of the first (partial) body --------------------------------
+        const int pre = (jb0 > 0 && first_row) ? C::PRE : 0;
+        const int s_first = jb0 * U - pre;                 // first step this wave runs in the row
+        const int s_end = jb0 * U + U;                     // ... through the end of its first body
+        {
+            const int r_lo = (s_first + p.delta - 4 * (LPG - 1) - 3) >> 2;   // right units
+            const int r_hi = (s_end + p.delta + 3) >> 2;
+            const int l_lo = s_first >> 2, l_hi = (s_end + 3) >> 2;          // left units
+            const int nr = r_hi - r_lo, nl = l_hi - l_lo, nug = nr + nl;
+            for (int i = lane; i < G * nug; i += 64) {
+                const int gg = i / nug, kk = i - gg * nug;
+                StreamUnit u;
+                u.gg = gg;
+                u.right = kk < nr ? 1 : 0;
+                const int m = u.right ? r_lo + kk : l_lo + (kk - nr);
+                u.col = (u.right ? p.xr0 : p.xl0) + 4 * m;
+                u.yq = p.row0 + (bq * G + gg) * 4;
+                uint32_t rw[C::NROW];
+                stream_load<R>(p, rsI, u, false, rw);
+                stream_store<R, LPG>(lds, u, m, p.c0, rw, true, p.W);
+            }
+        }
+        __syncthreads();
+        // running window state of the row, (re)started after the burst so the previous row's
+        // state is dead while the burst holds its unit registers (a window sum is the sum of
+        // its ring entries: keys idx + 0, padding disparities idx + 0x8000 << 16)
+#pragma unroll
+        for (int k = 0; k < RG_DPL; ++k) {
+            const int idx = 4 * l + k;
+            const uint32_t base = idx < p.D ? (uint32_t)idx : (0x8000u << 16) | (uint32_t)idx;
+#pragma unroll
+            for (int q = 0; q < RQ; ++q) h[k][q] = base;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < W2; ++s2)
+#pragma unroll
+            for (int k = 0; k < RG_DPL; ++k)
+#pragma unroll
+                for (int q = 0; q < RQ; ++q) ring[s2][k][q] = 0u;
+        // register rings of the first step: rn[4 - k] = right pack of step s_first - k
+        {
+            int q = (s_first % C::RL) + dl;
+            q = q >= C::RL ? q - C::RL : q;
+            const int ph = q + ((q + p.c0) >> 2);
+#pragma unroll
+            for (int k = 1; k < RG_DPL; ++k) {
+                int a = ph - k - 1;
+                a = a < 0 ? a + C::RPER : a;
+                const PackPtr<COST_SAD4, R> rp{reinterpret_cast<const uint4*>(lds + rmain) + a,
+                                               reinterpret_cast<const typename P::CT*>(lds + rcom) + a};
+                rn[RG_DPL - k] = ld<COST_SAD4, R, true>(rp);
+            }
+        }
+        // ---- prologue: the window's 2r steps before a share that starts inside a row -----
+        if (pre) {
+            int q = (s_first % C::RL) + dl;
+            q = q >= C::RL ? q - C::RL : q;
+            const int ph = q + ((q + p.c0) >> 2);
+            const PackPtr<COST_SAD4, R> rb{reinterpret_cast<const uint4*>(lds + rmain) + ph,
+                                           reinterpret_cast<const typename P::CT*>(lds + rcom) + ph};
+            const int lq = s_first % C::LL;
+            const PackPtr<COST_SAD4, R> lb{reinterpret_cast<const uint4*>(lds + lmain) + lq,
+                                           reinterpret_cast<const typename P::CT*>(lds + lcom) + lq};
+#pragma unroll
+            for (int c = 0; c < C::PRE / 4; ++c) {
+                const int ch = W2 - C::PRE / 4 + c;       // ring slots of the body's last chunks
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int slot = (4 * ch + u) % W2;
+                    rn[u] = ld<COST_SAD4, R, true>(rb + (5 * c + u));
+                    const Pk<NW> Lc = ld<COST_SAD4, R, true>(lb + (4 * c + u));
+#pragma unroll
+                    for (int k = 0; k < RG_DPL; ++k)
+#pragma unroll
+                        for (int q2 = 0; q2 < RQ; ++q2) h[k][q2] -= ring[slot][k][q2];
+#pragma unroll
+                    for (int k = 0; k < RG_DPL; ++k) {
+                        const Pk<NW>& Rk = rn[(u - k) & 3];
+                        uint32_t cn = 0u;
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) cn = __builtin_amdgcn_sad_hi_u8(Lc.w[i], Rk.w[i], cn);
+#pragma unroll
+                        for (int q2 = 0; q2 < 4; ++q2) {
+                            const uint32_t cc = __builtin_amdgcn_sad_hi_u8(Lc.w[NC + q2], Rk.w[NC + q2], cn);
+                            h[k][q2] += cc;
+                            ring[slot][k][q2] = cc;
+                        }
+                    }
+                }
+            }
+        }
+        first_row = false;
+
+        // ---- bodies ----------------------------------------------------------------------
+        for (int jb = jb0; b < b_end; ++b, ++jb) {
+            const int s_b = jb * U;
+            const bool has_next = b + 1 < b_end;
+            // producer unit of the next body: loads now, transposes + writes after the steps
+            StreamUnit pu;
+            pu.gg = (prod && has_next) ? pg_ : -1;
+            pu.right = p_right;
+            const int pm = p_right ? ((s_b + U + p.delta) >> 2) + p_k : ((s_b + U) >> 2) + p_k;
+            pu.col = (p_right ? p.xr0 : p.xl0) + 4 * pm;
+            // laundered per body: the border path's 2r+4 clamped row offsets must not be
+            // hoisted out of the body loop (they would hold 2r+4 VGPRs for the whole row)
+            int pyq = p_yq;
+            asm volatile("" : "+v"(pyq));
+            pu.yq = pyq;
+            // units of this batch crossing an image border (uniform): their edge bytes are
+            // replicated in stream_store
+            const int rc_lo = p.xr0 + 4 * ((s_b + U + p.delta) >> 2), rc_hi = rc_lo + 4 * NUR;
+            const int lc_lo = p.xl0 + s_b + U, lc_hi = lc_lo + 4 * W2;
+            const bool edges = rc_lo < 0 || rc_hi > p.W || lc_lo < 0 || lc_hi > p.W;
+            uint32_t praw[C::NROW];
+            if (has_next) stream_load<R>(p, rsI, pu, rows_in, praw);
+
+            // ring bases of this body
+            int q = (s_b % C::RL) + dl;
+            q = q >= C::RL ? q - C::RL : q;
+            const int ph = q + ((q + p.c0) >> 2);
+            const PackPtr<COST_SAD4, R> rb{reinterpret_cast<const uint4*>(lds + rmain) + ph,
+                                           reinterpret_cast<const typename P::CT*>(lds + rcom) + ph};
+            const int lq = s_b % C::LL;
+            const PackPtr<COST_SAD4, R> lb{reinterpret_cast<const uint4*>(lds + lmain) + lq,
+                                           reinterpret_cast<const typename P::CT*>(lds + lcom) + lq};
+            Lnext = ld<COST_SAD4, R, true>(lb);
+            const int eb = el0 + s_b;
+            const int ob = ooff0 + 2 * s_b;
+            const int emax = emit_lane ? band_l : 0;
+#pragma unroll
+            for (int ch = 0; ch < W2; ++ch) {
+                // a uniform branch that never skips: one basic block per chunk (as in the ring
+                // kind) lets the register allocator keep r = 4 at ~225 VGPRs; the whole body
+                // as one block needed > 256
+                if (s_b + 4 * ch < 0) continue;
+                uint32_t bk[4][2];
+                uint32_t kA = 0u;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int slot = (4 * ch + u) % W2;
+                    rn[u] = ld<COST_SAD4, R, true>(rb + (5 * ch + u));
+                    const Pk<NW> Lc = Lnext;
+                    if (ch < W2 - 1 || u < 3) Lnext = ld<COST_SAD4, R, true>(lb + (4 * ch + u + 1));
+#pragma unroll
+                    for (int k = 0; k < RG_DPL; ++k)
+#pragma unroll
+                        for (int q2 = 0; q2 < RQ; ++q2) h[k][q2] -= ring[slot][k][q2];
+#pragma unroll
+                    for (int kk = 0; kk < RG_DPL; ++kk) {
+                        const int k = RG_DPL - 1 - kk;
+                        const Pk<NW>& Rk = rn[(u - k) & 3];
+                        uint32_t cn = 0u;
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) cn = __builtin_amdgcn_sad_hi_u8(Lc.w[i], Rk.w[i], cn);
+#pragma unroll
+                        for (int q2 = 0; q2 < 4; ++q2) {
+                            const uint32_t cc = __builtin_amdgcn_sad_hi_u8(Lc.w[NC + q2], Rk.w[NC + q2], cn);
+                            h[k][q2] += cc;
+                            ring[slot][k][q2] = cc;
+                        }
+                    }
+#pragma unroll
+                    for (int q2 = 0; q2 < 4; ++q2) bk[q2][u & 1] = min(min(h[0][q2], h[1][q2]), min(h[2][q2], h[3][q2]));
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (u & 1) {
+                        uint32_t v[8];
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) v[i] = bk[i >> 1][i & 1];
+                        reduce_scatter8_bm(v, lane & 15);
+                        if (u == 1) {
+                            kA = v[0];
+                        } else {   // pair (0,1) in kA, pair (2,3) in v[0]: one swap joins both
+                            auto pr = __builtin_amdgcn_permlane16_swap(kA, v[0], false, false);
+                            uint32_t key = min(pr[0], pr[1]);
+                            if (LPG == 64) {
+                                pr = __builtin_amdgcn_permlane32_swap(key, key, false, false);
+                                key = min(pr[0], pr[1]);
+                            }
+                            const int tt = 4 * ch;
+                            const int off = (unsigned)(eb + tt) < (unsigned)emax ? ob + 2 * tt : (int)0x80000000u;
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + p.minD) * 16),
+                                                                  orsrc, off, 0, 0);
+                        }
+                    }
+                }
+            }
+            if (has_next) {
+                __builtin_amdgcn_sched_barrier(0);
+                stream_store<R, LPG>(lds, pu, pm, p.c0, praw, edges, p.W);
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Stream kind eligibility (SV_STREAM=0 disables it, for A/B runs): SAD with 5 <= win <= 9,
+// 65 <= D <= 256, 4-aligned images and widths (dword unit loads), 32-bit output offsets.
+bool stream_kind(const MatchParams& a) {
+    static const bool on = [] {
+        const char* e = std::getenv("SV_STREAM");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || a.win < 5 || a.win > 9 || a.D <= 64 || a.D > 256 || (a.W & 3) || (a.pitch & 3) || a.X1 - a.X0 < 4 ||
+        ((reinterpret_cast<uintptr_t>(a.L) | reinterpret_cast<uintptr_t>(a.R)) & 3u))
+        return false;
+    // one 32-bit buffer resource spans both images of every frame of the batch
+    const long long gap = a.L < a.R ? (long long)(a.R - a.L) : (long long)(a.L - a.R);
+    const long long span = gap + (long long)(a.H - 1) * a.pitch + a.W + (long long)((a.nf > 1 ? a.nf : 1) - 1) * a.fs_in;
+    return span < 0x7FFF0000LL;
+}
+
+int device_cus() {
+    static const int n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return 256;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) return 256;
+        return v;
+    }();
+    return n;
+}
+
+template <int R, int LPG>
+int launch_stream_rl(const MatchParams& a, hipStream_t s) {
+    using C = StreamCfg<R, LPG>;
+    StreamParams p{};
+    const uint8_t* lo = a.L < a.R ? a.L : a.R;
+    p.img = lo;
+    p.offL = (int)(a.L - lo);
+    p.offR = (int)(a.R - lo);
+    p.img_span = (int)(std::max(p.offL, p.offR) + (long long)(a.H - 1) * a.pitch + a.W);
+    p.out = a.out;
+    p.H = a.H;
+    p.W = a.W;
+    p.pitch = a.pitch;
+    p.opitch = a.opitch;
+    p.minD = a.minD;
+    p.D = a.D;
+    p.X0 = a.X0;
+    p.X1 = a.X1;
+    p.row0 = a.row0;
+    p.row1 = a.row1;
+    p.fs_in = a.fs_in;
+    p.fs_out = a.fs_out;
+    p.xl0 = (a.X0 - R) & ~3;                                   // floor to a multiple of 4
+    p.xr0 = (p.xl0 - a.minD - 4 * (LPG - 1) - 3) & ~3;
+    p.delta = p.xl0 - a.minD - p.xr0;
+    p.c0 = (4 - (p.delta & 3)) & 3;
+    const int ns = a.X1 + R - p.xl0;                           // steps through the last output
+    p.nb = (ns + C::U - 1) / C::U;
+    p.nq = (a.row1 - a.row0 + 3) / 4;
+    p.nbund = (p.nq + C::G - 1) / C::G;
+    const int nf = a.nf > 1 ? a.nf : 1;
+    p.total = (long long)nf * p.nbund * p.nb;
+    const int per_cu = std::min(8, (160 * 1024) / C::LDS_BYTES);
+    const long long waves = std::min<long long>(p.total, (long long)per_cu * device_cus());
+    hipLaunchKernelGGL((k_match_stream<R, LPG>), dim3((unsigned)waves), dim3(64), C::LDS_BYTES, s, p);
+    return (int)hipGetLastError();
+}
+template <int R>
+int launch_stream_r(const MatchParams& a, hipStream_t s) {
+    return a.D <= 128 ? launch_stream_rl<R, 32>(a, s) : launch_stream_rl<R, 64>(a, s);
+}
+int launch_stream(const MatchParams& a, hipStream_t s) {
+    switch (a.r) {
+        case 2: return launch_stream_r<2>(a, s);
+        case 3: return launch_stream_r<3>(a, s);
+        case 4: return launch_stream_r<4>(a, s);
+    }
+    return (int)hipErrorInvalidValue;
+}
 }  // namespace
 
 uint64_t max_cost(int win, int cost) {
@@ -1252,6 +1769,7 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
     // (2 * (row * out_pitch + x) per frame); maps whose last row lies past 2^31 bytes take
     // the size_t-addressed four-row kind instead
     const bool ring_fits = 2LL * ((long long)(a.row1 + 3) * a.opitch + a.W + 64) < 0x7FFFFFFFLL;
+    if (ring_kind(cost, a.win, a.D) && ring_fits && stream_kind(a)) return launch_stream(a, s);
     if (ring_kind(cost, a.win, a.D) && ring_fits) return launch_ring(a, s);
     const size_t lds = match_lds_bytes(p, a.r, cost);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;

@@ -59,7 +59,8 @@ __device__ __forceinline__ uint32_t gray_at(const uint8_t* p, int cn) {
 __global__ __launch_bounds__(256) void k_frame_stats(FrameStatsArgs a) {
     __shared__ uint32_t hist[4][256];
     const int z = blockIdx.z;
-    const uint8_t* img = z == 0 ? a.img0 : a.img1;
+    const int f = a.per == 2 ? z >> 1 : z;
+    const uint8_t* img = (a.per == 2 && (z & 1) ? a.img1 : a.img0) + f * a.fs;
     const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
     for (int i = t; i < 4 * 256; i += 256) (&hist[0][0])[i] = 0;
     __syncthreads();

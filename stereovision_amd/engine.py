@@ -47,6 +47,7 @@ EXPORTED = [
     "sv_depth_map_rows_multi", "sv_depth_map_color", "sv_stereo_scaled_color",
     "sv_median_post_color_dev", "sv_profile_region_begin", "sv_profile_region_end",
     "sv_comm_scatterv", "sv_depth_map_rows_scatter", "sv_band_rows_in", "sv_release_scratch",
+    "sv_frame_stats_batch_dev",
 ]
 BAND_MARGIN = 8   # SV_BAND_MARGIN: spare rows around a band-only input buffer
 COMM_ID_BYTES = 128
@@ -204,6 +205,8 @@ def _declare(lib):
                            _c_int),
         "sv_frame_stats_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
                                _c_int),
+        "sv_frame_stats_batch_dev": ([_vp, _vp, _vp, _c_int, ctypes.c_int64, _c_int, _c_int, _c_int,
+                                      _c_int, _vp, _vp, _vp, _vp], _c_int),
         "sv_select_count": ([_vp, _vp, ctypes.c_int64, _c_int, _vp, _c_float,
                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)], _c_int),
         "sv_select_ranks": ([_vp, _vp, ctypes.c_int64, _c_int, _vp, _c_float, _i64p, _c_int, _f32p],
@@ -867,6 +870,15 @@ class Engine:
         _check("sv_frame_stats_dev", self.lib.sv_frame_stats_dev(
             self._h, d_img0, d_img1 or None, H, W, channels, pitch, d_block_sum, d_block_sq, d_hist,
             stream or None))
+
+    def frame_stats_batch_dev(self, d_img0: int, d_img1: int, n_frames: int, frame_stride: int, H: int,
+                              W: int, channels: int, pitch: int, d_block_sum: int, d_block_sq: int,
+                              d_hist: int, stream: int = 0):
+        """detect_camera_occlusion's image statistics for a batch of frames (or pairs) in one
+        launch: outputs dense per image (frame-major, img0 before img1)."""
+        _check("sv_frame_stats_batch_dev", self.lib.sv_frame_stats_batch_dev(
+            self._h, d_img0, d_img1 or None, int(n_frames), int(frame_stride), H, W, channels, pitch,
+            d_block_sum, d_block_sq, d_hist, stream or None))
 
     def select_count(self, d_x: int, n: int, mask_mode: int = 0, d_mask: int = 0,
                      thr: float = 0.0) -> tuple[int, int]:

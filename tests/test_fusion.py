@@ -162,6 +162,44 @@ def test_gpu_frame_stats_exact(engine, shape, channels):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nf,shape,channels,pair", [(8, (1080, 1920), 1, True), (3, (47, 61), 3, True),
+                                                    (5, (480, 640), 1, False), (1, (96, 144), 1, True)])
+def test_gpu_frame_stats_batch_equals_per_frame(engine, nf, shape, channels, pair):
+    """sv_frame_stats_batch_dev: one launch over nf frames (pairs) == nf single calls."""
+    H, W = shape
+    rng = np.random.default_rng(nf * 1000 + H)
+    ext = (3,) if channels == 3 else ()
+    a = rng.integers(0, 256, (nf,) + shape + ext, dtype=np.uint8)
+    b = rng.integers(0, 256, (nf,) + shape + ext, dtype=np.uint8)
+    a[0] = 17                                         # a flat frame: one histogram bin
+    fs = H * W * channels
+    dA, dB = engine.dev_alloc(a.nbytes), engine.dev_alloc(b.nbytes)
+    engine.to_device(dA, a)
+    engine.to_device(dB, b)
+    bh, bw = max(1, H // 48), max(1, W // 48)
+    per = 2 if pair else 1
+    nimg = nf * per
+    dbs, dbq, dh = engine.dev_alloc(4 * nimg * bh * bw), engine.dev_alloc(4 * nimg * bh * bw), engine.dev_alloc(4 * nimg * 256)
+    try:
+        for _ in range(2):   # twice: the fold leaves the accumulators zeroed
+            engine.frame_stats_batch_dev(dA, dB if pair else 0, nf, fs, H, W, channels, W * channels, dbs, dbq, dh)
+            engine.synchronize()
+        bs = engine.to_host(dbs, (nimg, bh, bw), np.uint32)
+        bq = engine.to_host(dbq, (nimg, bh, bw), np.uint32)
+        hist = engine.to_host(dh, (nimg, 256), np.uint32)
+        for f in range(nf):
+            e_bs, e_bq, e_h = engine.frame_stats(a[f], b[f]) if pair else engine.frame_stats(a[f])
+            for k in range(per):
+                z = f * per + k
+                np.testing.assert_array_equal(bs[z], e_bs[k], err_msg=f"frame {f} image {k}")
+                np.testing.assert_array_equal(bq[z], e_bq[k])
+                np.testing.assert_array_equal(hist[z], e_h[k])
+    finally:
+        for p in (dA, dB, dbs, dbq, dh):
+            engine.dev_free(p)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kinds", [("texture", "texture"), ("covered", "texture"),
                                    ("texture", "covered"), ("covered", "covered"), ("flat", "noise")])
 def test_gpu_detect_camera_occlusion(kinds):

@@ -276,6 +276,17 @@ def aux_kernels(eng, H, W, B, med_ms, med_n, reps=20, blocker=None):
         eng.profile(False)
         ms, n = eng.profile_read("select")
         out["k_select_hist"] = hbm_entry("k_select_hist", 4 * H * W, ms, n)
+        # one pass over a batch of B maps per launch (sv_select_count_batch: grid.y = map)
+        Bm = min(B, 16)
+        dm = arena.upload(rng.random((Bm, H, W), dtype=np.float32))
+        eng.select_count_batch(dm, H * W, H * W, Bm, 1)
+        eng.profile_reset()
+        eng.profile(True)
+        for _ in range(reps):
+            eng.select_count_batch(dm, H * W, H * W, Bm, 1)
+        eng.profile(False)
+        ms, n = eng.profile_read("select")
+        out["k_select_hist_batch"] = hbm_entry(f"k_select_hist ({Bm} maps per launch)", 4 * H * W * Bm, ms, n)
     finally:
         arena.free()
     return out

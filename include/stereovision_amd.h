@@ -439,6 +439,16 @@ int sv_select_count(sv_ctx* ctx, const float* d_x, int64_t n, int mask_mode, con
                     float thr, int64_t* selected, int64_t* nans);
 int sv_select_ranks(sv_ctx* ctx, const float* d_x, int64_t n, int mask_mode, const float* d_mask,
                     float thr, const int64_t* ranks, int nranks, float* values);
+/* The same over a batch of n_arrays <= 16 arrays of n elements (array y at d_x + y * x_stride
+ * elements, its mask at d_mask + y * mask_stride): one launch + one fold per radix pass for
+ * the whole batch (e.g. the disparity maps of queued frames).  selected / nans: [n_arrays];
+ * ranks / values: [n_arrays][nranks]. */
+int sv_select_count_batch(sv_ctx* ctx, const float* d_x, int64_t n, int64_t x_stride, int n_arrays,
+                          int mask_mode, const float* d_mask, int64_t mask_stride, float thr,
+                          int64_t* selected, int64_t* nans);
+int sv_select_ranks_batch(sv_ctx* ctx, const float* d_x, int64_t n, int64_t x_stride, int n_arrays,
+                          int mask_mode, const float* d_mask, int64_t mask_stride, float thr,
+                          const int64_t* ranks, int nranks, float* values);
 /* Elementwise epilogues: mode 0: out = fc + ((x - fa) / fb) * fd in float32, op by op;
  * mode 1: out = float32(float64(x) * ds + doff); mode 2: out = fc. */
 int sv_affine_f32_dev(sv_ctx* ctx, const float* d_x, int64_t n, int mode, float fa, float fb,

@@ -2330,31 +2330,103 @@ int sv_frame_stats(sv_ctx* c, const uint8_t* img0, const uint8_t* img1, int H, i
     return collect(c, o, 3);
 }
 
-static int check_select(const float* d_x, int64_t n, int mask_mode, const float* d_mask) {
-    if (!d_x || n < 0) return fail(SV_EINVAL, "bad select arguments");
-    if (mask_mode < 0 || mask_mode > 2) return fail(SV_EINVAL, "mask_mode must be 0, 1 or 2");
-    if (mask_mode == 2 && !d_mask) return fail(SV_EINVAL, "mask_mode 2 needs a mask array");
-    return 0;
-}
-
-// One select pass over the context stream: ghist[nranks][2048] back on the host.
+// One select pass over the context stream (a batch of a.narr arrays): hist [narr][kMaxRanks]
+// [2048] and counts [narr][2] back on the host.
 static int select_pass(sv_ctx* c, sv::SelectArgs& a, uint32_t* hist_host, unsigned long long* counts_host) {
-    // device: [copies][kMaxRanks][2048] accumulators | count slots | folded hist | counts
+    // device: [narr][copies][kMaxRanks][2048] accumulators | [narr] count slots | folded
+    // hist [narr][kMaxRanks][2048] | counts [narr][2]
+    const size_t na = (size_t)(a.narr > 0 ? a.narr : 1);
     const size_t hb = (size_t)sv::kMaxRanks * 2048 * sizeof(uint32_t);
-    const size_t ab = sv::kHistCopies * hb;
-    const size_t cb = (size_t)sv::kCountSlots * 16 * sizeof(unsigned long long);
-    SV_HIP(c->sel.ensure_zeroed(ab + cb + hb + 16));
+    const size_t ab = na * sv::kHistCopies * hb;
+    const size_t cb = na * sv::kCountSlots * 16 * sizeof(unsigned long long);
+    const size_t ob = na * hb + na * 16;
+    SV_HIP(c->sel.ensure_zeroed(ab + cb + ob));
     uint8_t* base = c->sel.as<uint8_t>();
     a.ghist = reinterpret_cast<uint32_t*>(base);
     a.counts = reinterpret_cast<unsigned long long*>(base + ab);
     a.hist_out = reinterpret_cast<uint32_t*>(base + ab + cb);
-    a.counts_out = reinterpret_cast<unsigned long long*>(base + ab + cb + hb);
+    a.counts_out = reinterpret_cast<unsigned long long*>(base + ab + cb + na * hb);
     SV_LAUNCH(c, SV_K_SELECT, c->stream, sv::launch_select_hist(a, c->stream));
-    SV_HIP(c->hout.ensure(hb + 16));
-    SV_HIP(hipMemcpyAsync(c->hout.p, a.hist_out, hb + 16, hipMemcpyDeviceToHost, c->stream));
+    SV_HIP(c->hout.ensure(ob));
+    SV_HIP(hipMemcpyAsync(c->hout.p, a.hist_out, ob, hipMemcpyDeviceToHost, c->stream));
     SV_HIP(hipStreamSynchronize(c->stream));
-    std::memcpy(hist_host, c->hout.p, (size_t)a.nranks * 2048 * sizeof(uint32_t));
-    if (counts_host) std::memcpy(counts_host, c->hout.as<uint8_t>() + hb, 16);
+    std::memcpy(hist_host, c->hout.p, na * hb);
+    if (counts_host) std::memcpy(counts_host, c->hout.as<uint8_t>() + na * hb, na * 16);
+    return 0;
+}
+
+// np.percentile's order statistics of a batch of narr arrays (array y at d_x + y * x_stride,
+// its mask at d_mask + y * mask_stride): selected / nan counts (nullable) and, with nranks
+// > 0, the values of ranks[y][r] (radix select in three passes of 11/11/10 bits, one launch
+// + one fold per pass for the whole batch).
+static int select_batch(sv_ctx* c, const float* d_x, int64_t n, int64_t x_stride, int narr, int mask_mode,
+                        const float* d_mask, int64_t mask_stride, float thr, const int64_t* ranks, int nranks,
+                        float* values, int64_t* selected, int64_t* nans) {
+    if (!d_x || n < 0) return fail(SV_EINVAL, "bad select arguments");
+    if (mask_mode < 0 || mask_mode > 2) return fail(SV_EINVAL, "mask_mode must be 0, 1 or 2");
+    if (mask_mode == 2 && !d_mask) return fail(SV_EINVAL, "mask_mode 2 needs a mask array");
+    if (narr < 1 || narr > sv::kSelBatch) return fail(SV_EINVAL, "1..16 arrays per batch");
+    if (narr > 1 && (x_stride < n || (mask_mode == 2 && mask_stride < n))) return fail(SV_EINVAL, "array stride below n");
+    if (nranks < 0 || nranks > sv::kMaxRanks || (nranks > 0 && (!ranks || !values))) return fail(SV_EINVAL, "0..4 ranks");
+    sv::SelectArgs a{};
+    a.x = d_x;
+    a.mask = mask_mode == 2 ? d_mask : nullptr;
+    a.thr = thr;
+    a.mask_mode = mask_mode;
+    a.n = (size_t)n;
+    a.narr = narr;
+    a.xstride = narr > 1 ? (size_t)x_stride : 0;
+    a.mstride = narr > 1 ? (size_t)mask_stride : 0;
+    std::vector<uint32_t> h((size_t)narr * sv::kMaxRanks * 2048);
+    std::vector<unsigned long long> cnt((size_t)narr * 2, 0ull);
+    const size_t hs = (size_t)sv::kMaxRanks * 2048;
+    uint32_t prefix[sv::kSelBatch][sv::kMaxRanks] = {};
+    int64_t rem[sv::kSelBatch][sv::kMaxRanks];
+    for (int y = 0; y < narr; ++y)
+        for (int r = 0; r < nranks; ++r) {
+            if (ranks[(size_t)y * nranks + r] < 0) return fail(SV_EINVAL, "negative rank");
+            rem[y][r] = ranks[(size_t)y * nranks + r];
+        }
+    const int shifts[3] = {21, 10, 0}, bits[3] = {11, 11, 10};
+    const int passes = nranks > 0 ? 3 : 1;
+    for (int p = 0; p < passes; ++p) {
+        a.shift = shifts[p];
+        a.bits = bits[p];
+        a.nranks = p == 0 ? 1 : nranks;          // pass 0: one histogram serves every rank
+        for (int y = 0; y < narr; ++y)
+            for (int r = 0; r < sv::kMaxRanks; ++r) a.prefix[y][r] = p == 0 ? 0u : prefix[y][r];
+        if (n > 0) {
+            int rc = select_pass(c, a, h.data(), p == 0 ? cnt.data() : nullptr);
+            if (rc) return rc;
+        }
+        if (p == 0) {
+            for (int y = 0; y < narr; ++y) {
+                if (selected) selected[y] = (int64_t)cnt[2 * y];
+                if (nans) nans[y] = (int64_t)cnt[2 * y + 1];
+                for (int r = 0; r < nranks; ++r)
+                    if ((unsigned long long)rem[y][r] >= cnt[2 * y]) return fail(SV_ERANGE, "rank beyond the selection");
+            }
+        }
+        for (int y = 0; y < narr; ++y)
+            for (int r = 0; r < nranks; ++r) {
+                const uint32_t* hr = h.data() + (size_t)y * hs + (p == 0 ? 0 : r) * 2048;
+                int64_t acc = 0;
+                int d = 0;
+                for (; d < (1 << bits[p]); ++d) {
+                    if (acc + (int64_t)hr[d] > rem[y][r]) break;
+                    acc += hr[d];
+                }
+                if (d == (1 << bits[p])) return fail(SV_EHIP, "select: histogram inconsistent (data changed?)");
+                rem[y][r] -= acc;
+                prefix[y][r] = (prefix[y][r] << bits[p]) | (uint32_t)d;
+            }
+    }
+    for (int y = 0; y < narr; ++y)
+        for (int r = 0; r < nranks; ++r) {
+            const uint32_t k = prefix[y][r];
+            const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+            std::memcpy(&values[(size_t)y * nranks + r], &u, sizeof(float));
+        }
     return 0;
 }
 
@@ -2362,80 +2434,35 @@ int sv_select_count(sv_ctx* c, const float* d_x, int64_t n, int mask_mode, const
                     int64_t* selected, int64_t* nans) {
     SV_ENTER(c);
     SV_SCRATCH(c, c->stream);
-    int rc = check_select(d_x, n, mask_mode, d_mask);
-    if (rc) return rc;
-    sv::SelectArgs a{};
-    a.x = d_x;
-    a.mask = d_mask;
-    a.thr = thr;
-    a.mask_mode = mask_mode;
-    a.n = (size_t)n;
-    a.shift = 21;
-    a.bits = 11;
-    a.nranks = 1;
-    std::vector<uint32_t> h(2048);
-    unsigned long long cnt[2] = {0, 0};
-    if (n > 0) {
-        rc = select_pass(c, a, h.data(), cnt);
-        if (rc) return rc;
-    }
-    if (selected) *selected = (int64_t)cnt[0];
-    if (nans) *nans = (int64_t)cnt[1];
-    return 0;
+    if (selected) *selected = 0;
+    if (nans) *nans = 0;
+    return select_batch(c, d_x, n, n, 1, mask_mode, d_mask, n, thr, nullptr, 0, nullptr, selected, nans);
 }
 
 int sv_select_ranks(sv_ctx* c, const float* d_x, int64_t n, int mask_mode, const float* d_mask, float thr,
                     const int64_t* ranks, int nranks, float* values) {
     SV_ENTER(c);
     SV_SCRATCH(c, c->stream);
-    int rc = check_select(d_x, n, mask_mode, d_mask);
-    if (rc) return rc;
     if (!ranks || !values || nranks < 1 || nranks > sv::kMaxRanks) return fail(SV_EINVAL, "1..4 ranks");
-    sv::SelectArgs a{};
-    a.x = d_x;
-    a.mask = d_mask;
-    a.thr = thr;
-    a.mask_mode = mask_mode;
-    a.n = (size_t)n;
-    uint32_t prefix[sv::kMaxRanks] = {};
-    int64_t rem[sv::kMaxRanks];
-    for (int r = 0; r < nranks; ++r) {
-        if (ranks[r] < 0) return fail(SV_EINVAL, "negative rank");
-        rem[r] = ranks[r];
-    }
-    std::vector<uint32_t> h((size_t)sv::kMaxRanks * 2048);
-    unsigned long long cnt[2] = {0, 0};
-    const int shifts[3] = {21, 10, 0}, bits[3] = {11, 11, 10};
-    for (int p = 0; p < 3; ++p) {
-        a.shift = shifts[p];
-        a.bits = bits[p];
-        a.nranks = p == 0 ? 1 : nranks;          // pass 0: one histogram serves every rank
-        for (int r = 0; r < nranks; ++r) a.prefix[r] = p == 0 ? 0u : prefix[r];
-        rc = select_pass(c, a, h.data(), p == 0 ? cnt : nullptr);
-        if (rc) return rc;
-        if (p == 0) {
-            for (int r = 0; r < nranks; ++r)
-                if ((unsigned long long)rem[r] >= cnt[0]) return fail(SV_ERANGE, "rank beyond the selection");
-        }
-        for (int r = 0; r < nranks; ++r) {
-            const uint32_t* hr = h.data() + (p == 0 ? 0 : r) * 2048;
-            int64_t acc = 0;
-            int d = 0;
-            for (; d < (1 << bits[p]); ++d) {
-                if (acc + (int64_t)hr[d] > rem[r]) break;
-                acc += hr[d];
-            }
-            if (d == (1 << bits[p])) return fail(SV_EHIP, "select: histogram inconsistent (data changed?)");
-            rem[r] -= acc;
-            prefix[r] = (prefix[r] << bits[p]) | (uint32_t)d;
-        }
-    }
-    for (int r = 0; r < nranks; ++r) {
-        const uint32_t k = prefix[r];
-        const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
-        std::memcpy(&values[r], &u, sizeof(float));
-    }
-    return 0;
+    return select_batch(c, d_x, n, n, 1, mask_mode, d_mask, n, thr, ranks, nranks, values, nullptr, nullptr);
+}
+
+int sv_select_count_batch(sv_ctx* c, const float* d_x, int64_t n, int64_t x_stride, int n_arrays, int mask_mode,
+                          const float* d_mask, int64_t mask_stride, float thr, int64_t* selected, int64_t* nans) {
+    SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
+    return select_batch(c, d_x, n, x_stride, n_arrays, mask_mode, d_mask, mask_stride, thr, nullptr, 0, nullptr,
+                        selected, nans);
+}
+
+int sv_select_ranks_batch(sv_ctx* c, const float* d_x, int64_t n, int64_t x_stride, int n_arrays, int mask_mode,
+                          const float* d_mask, int64_t mask_stride, float thr, const int64_t* ranks, int nranks,
+                          float* values) {
+    SV_ENTER(c);
+    SV_SCRATCH(c, c->stream);
+    if (!ranks || !values || nranks < 1 || nranks > sv::kMaxRanks) return fail(SV_EINVAL, "1..4 ranks");
+    return select_batch(c, d_x, n, x_stride, n_arrays, mask_mode, d_mask, mask_stride, thr, ranks, nranks, values,
+                        nullptr, nullptr);
 }
 
 int sv_affine_f32_dev(sv_ctx* c, const float* d_x, int64_t n, int mode, float fa, float fb, float fc, float fd,

@@ -114,6 +114,7 @@ int launch_frame_stats(const FrameStatsArgs& a, int nimg, hipStream_t s);
 
 enum SelectMask { SEL_ALL = 0, SEL_POSITIVE = 1, SEL_MASK_GT = 2 };
 constexpr int kMaxRanks = 4;
+constexpr int kSelBatch = 16;   // arrays per batched select launch
 struct SelectArgs {
     const float* x;
     const float* mask;        // SEL_MASK_GT: element i selected iff mask[i] > thr
@@ -122,11 +123,15 @@ struct SelectArgs {
     size_t n;
     int shift, bits;          // digit = (key >> shift) & ((1 << bits) - 1)
     int nranks;
-    uint32_t prefix[kMaxRanks];   // key >> (shift + bits) of each rank's target
-    uint32_t* ghist;          // accumulators [kHistCopies][kMaxRanks][2048], zero on entry and exit
-    unsigned long long* counts;   // accumulators [kCountSlots][16] (slot = {selected, nan, pad})
-    uint32_t* hist_out;       // [nranks][2048], folded by the launcher's second kernel
-    unsigned long long* counts_out;   // [selected, nan]
+    // batches (grid.y = array y of narr): x + y * xstride, mask + y * mstride; every
+    // accumulator / output below is per array (array y's block at + y * its size)
+    int narr;
+    size_t xstride, mstride;
+    uint32_t prefix[kSelBatch][kMaxRanks];   // key >> (shift + bits) of each rank's target
+    uint32_t* ghist;          // accumulators [narr][kHistCopies][kMaxRanks][2048], zero on entry and exit
+    unsigned long long* counts;   // accumulators [narr][kCountSlots][16] (slot = {selected, nan, pad})
+    uint32_t* hist_out;       // [narr][kMaxRanks][2048], folded by the launcher's second kernel
+    unsigned long long* counts_out;   // [narr][2]: selected, nan
 };
 constexpr int kCountSlots = 32;   // blocks add their counts into slot blockIdx % 32 (128 B apart)
 int launch_select_hist(const SelectArgs& a, hipStream_t s);

@@ -146,8 +146,8 @@ __device__ __forceinline__ uint32_t f32_key(float f) {
 // Pass 0 (shift = 21, all prefixes empty) also counts selected elements and NaNs.
 constexpr int kSelVec = 4;   // float4 loads per thread per iteration (16 elements)
 
-__device__ __forceinline__ void select_one(const SelectArgs& a, uint32_t (*h)[2048], int nb, float v, float m,
-                                           uint32_t& cnt, uint32_t& nan) {
+__device__ __forceinline__ void select_one(const SelectArgs& a, const uint32_t* prefix, uint32_t (*h)[2048], int nb,
+                                           float v, float m, uint32_t& cnt, uint32_t& nan) {
     if (a.mask_mode == SEL_MASK_GT && !(m > a.thr)) return;   // confidence > 0.7
     if (v != v) {                                               // NaN in the selection -> nan
         nan += a.mask_mode != SEL_POSITIVE;
@@ -159,7 +159,7 @@ __device__ __forceinline__ void select_one(const SelectArgs& a, uint32_t (*h)[20
     const uint32_t d = (k >> a.shift) & (uint32_t)(nb - 1);
     const uint32_t hi = a.shift + a.bits >= 32 ? 0u : (k >> (a.shift + a.bits));
     for (int r = 0; r < a.nranks; ++r)
-        if (hi == a.prefix[r]) hist_add<4>(h[r], d);
+        if (hi == prefix[r]) hist_add<4>(h[r], d);
 }
 
 // Pass `shift` of the select: histogram of digit (key >> shift) & (nbins-1) over the
@@ -168,6 +168,12 @@ __device__ __forceinline__ void select_one(const SelectArgs& a, uint32_t (*h)[20
 // Each thread loads kSelVec float4s (and mask float4s) before using any of them.
 __global__ __launch_bounds__(256) void k_select_hist(SelectArgs a) {
     __shared__ uint32_t h[kMaxRanks][2048];
+    const int y = blockIdx.y;                   // array of a batch
+    const uint32_t* prefix = a.prefix[y];
+    a.x += y * a.xstride;
+    if (a.mask) a.mask += y * a.mstride;
+    a.ghist += (size_t)y * kHistCopies * kMaxRanks * 2048;
+    a.counts += (size_t)y * kCountSlots * 16;
     const int nb = 1 << a.bits;
     for (int r = 0; r < a.nranks; ++r)
         for (int i = threadIdx.x; i < nb; i += 256) h[r][i] = 0;
@@ -191,16 +197,16 @@ __global__ __launch_bounds__(256) void k_select_hist(SelectArgs a) {
 #pragma unroll
         for (int k = 0; k < kSelVec; ++k) {
             if (base + (size_t)k * 256 < n4) {
-                select_one(a, h, nb, v[k].x, m[k].x, cnt, nan);
-                select_one(a, h, nb, v[k].y, m[k].y, cnt, nan);
-                select_one(a, h, nb, v[k].z, m[k].z, cnt, nan);
-                select_one(a, h, nb, v[k].w, m[k].w, cnt, nan);
+                select_one(a, prefix, h, nb, v[k].x, m[k].x, cnt, nan);
+                select_one(a, prefix, h, nb, v[k].y, m[k].y, cnt, nan);
+                select_one(a, prefix, h, nb, v[k].z, m[k].z, cnt, nan);
+                select_one(a, prefix, h, nb, v[k].w, m[k].w, cnt, nan);
             }
         }
     }
     // scalar elements: the tail after the float4s, or everything when unaligned
     for (size_t i = 4 * n4 + (size_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (size_t)gridDim.x * 256)
-        select_one(a, h, nb, a.x[i], use_mask ? a.mask[i] : 0.f, cnt, nan);
+        select_one(a, prefix, h, nb, a.x[i], use_mask ? a.mask[i] : 0.f, cnt, nan);
     __syncthreads();
     for (int r = 0; r < a.nranks; ++r)
         for (int i = threadIdx.x; i < nb; i += 256)
@@ -225,6 +231,11 @@ __global__ __launch_bounds__(256) void k_select_hist(SelectArgs a) {
 // hist_out = sum of the accumulator copies (nranks x 2048 bins, 8 blocks per rank), counts_out
 // = sum of the count slots; every accumulator read is zeroed for the next pass.
 __global__ __launch_bounds__(256) void k_select_fold(SelectArgs a) {
+    const int y = blockIdx.y;
+    a.ghist += (size_t)y * kHistCopies * kMaxRanks * 2048;
+    a.counts += (size_t)y * kCountSlots * 16;
+    a.hist_out += (size_t)y * kMaxRanks * 2048;
+    a.counts_out += (size_t)y * 2;
     const int i = blockIdx.x * 256 + threadIdx.x;   // < nranks * 2048
     uint32_t v = 0;
     for (int k = 0; k < kHistCopies; ++k) {
@@ -277,9 +288,10 @@ int launch_select_hist(const SelectArgs& a, hipStream_t s) {
     // 16 elements per thread: each block zeroes and merges a 2048-bin histogram per rank
     int blocks = (int)((a.n + 256 * 4 * kSelVec - 1) / (256 * 4 * kSelVec));
     if (blocks > 1024) blocks = 1024;
-    if (a.n > 0) hipLaunchKernelGGL(k_select_hist, dim3(blocks), dim3(256), 0, s, a);
+    const int narr = a.narr > 0 ? a.narr : 1;
+    if (a.n > 0) hipLaunchKernelGGL(k_select_hist, dim3(blocks, narr), dim3(256), 0, s, a);
     // the fold runs for n = 0 too: it writes the (empty) result
-    hipLaunchKernelGGL(k_select_fold, dim3(a.nranks * 8), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_select_fold, dim3(a.nranks * 8, narr), dim3(256), 0, s, a);
     return (int)hipGetLastError();
 }
 

@@ -7,11 +7,13 @@ to a worker pool).  The build's sharding:
 * **frame sharding** (config C4): independent frames, frame i -> rank i % world.  No
   collective in the data path; finished maps may be gathered to rank 0 over RCCL/xGMI.
 * **row tiling** (config C5): one large frame, rank k computes output rows
-  [H*k/world, H*(k+1)/world).  Every rank holds the full input frame, so the matching
-  window's halo rows (and the 5x5 median's 2-row halo, :func:`median_halo`) are read
-  locally: bands reassemble bit-exactly (the border policy applies only at the true image
-  border).  :func:`gather_rows` moves every band into rank 0's full-frame buffer with one
-  RCCL send/recv group (unequal bands, no padding).
+  [H*k/world, H*(k+1)/world).  Rank 0 holds the frame; :meth:`RowTiledDepthMap.scatter`
+  sends every rank only the input rows its band reads (:func:`band_layout`: the band, the
+  5x5 median's 2-row halo and the matching window's halo), so the halo rows are read
+  locally and bands reassemble bit-exactly (the border policy applies only at the true
+  image border).  :func:`gather_rows` moves every band into rank 0's full-frame buffer with
+  one RCCL send/recv group (unequal bands, no padding).  Ranks that already hold the full
+  frame skip the scatter (``compute(d_left, d_right)``).
 
 Two ways to run N GPUs:
 

@@ -47,7 +47,7 @@ EXPORTED = [
     "sv_depth_map_rows_multi", "sv_depth_map_color", "sv_stereo_scaled_color",
     "sv_median_post_color_dev", "sv_profile_region_begin", "sv_profile_region_end",
     "sv_comm_scatterv", "sv_depth_map_rows_scatter", "sv_band_rows_in", "sv_release_scratch",
-    "sv_frame_stats_batch_dev",
+    "sv_frame_stats_batch_dev", "sv_select_count_batch", "sv_select_ranks_batch",
 ]
 BAND_MARGIN = 8   # SV_BAND_MARGIN: spare rows around a band-only input buffer
 COMM_ID_BYTES = 128
@@ -207,6 +207,10 @@ def _declare(lib):
                                _c_int),
         "sv_frame_stats_batch_dev": ([_vp, _vp, _vp, _c_int, ctypes.c_int64, _c_int, _c_int, _c_int,
                                       _c_int, _vp, _vp, _vp, _vp], _c_int),
+        "sv_select_count_batch": ([_vp, _vp, ctypes.c_int64, ctypes.c_int64, _c_int, _c_int, _vp,
+                                   ctypes.c_int64, _c_float, _i64p, _i64p], _c_int),
+        "sv_select_ranks_batch": ([_vp, _vp, ctypes.c_int64, ctypes.c_int64, _c_int, _c_int, _vp,
+                                   ctypes.c_int64, _c_float, _i64p, _c_int, _f32p], _c_int),
         "sv_select_count": ([_vp, _vp, ctypes.c_int64, _c_int, _vp, _c_float,
                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)], _c_int),
         "sv_select_ranks": ([_vp, _vp, ctypes.c_int64, _c_int, _vp, _c_float, _i64p, _c_int, _f32p],
@@ -894,6 +898,28 @@ class Engine:
         out = np.empty(r.size, np.float32)
         _check("sv_select_ranks", self.lib.sv_select_ranks(
             self._h, d_x, int(n), int(mask_mode), d_mask or None, np.float32(thr), r, r.size, out))
+        return out
+
+    def select_count_batch(self, d_x: int, n: int, x_stride: int, n_arrays: int, mask_mode: int = 0,
+                           d_mask: int = 0, mask_stride: int = 0, thr: float = 0.0):
+        """select_count of n_arrays arrays (array y at d_x + 4 * y * x_stride) in one pass."""
+        sel = np.zeros(n_arrays, np.int64)
+        nan = np.zeros(n_arrays, np.int64)
+        _check("sv_select_count_batch", self.lib.sv_select_count_batch(
+            self._h, d_x, int(n), int(x_stride), int(n_arrays), int(mask_mode), d_mask or None,
+            int(mask_stride), np.float32(thr), sel, nan))
+        return sel, nan
+
+    def select_ranks_batch(self, d_x: int, n: int, x_stride: int, ranks, mask_mode: int = 0,
+                           d_mask: int = 0, mask_stride: int = 0, thr: float = 0.0) -> np.ndarray:
+        """ranks: [n_arrays][nranks] -> values [n_arrays][nranks] (three passes for the batch)."""
+        r = np.ascontiguousarray(np.asarray(ranks, np.int64))
+        if r.ndim != 2:
+            raise ValueError("ranks must be [n_arrays][nranks]")
+        out = np.empty(r.shape, np.float32)
+        _check("sv_select_ranks_batch", self.lib.sv_select_ranks_batch(
+            self._h, d_x, int(n), int(x_stride), r.shape[0], int(mask_mode), d_mask or None,
+            int(mask_stride), np.float32(thr), r.ravel(), r.shape[1], out.ravel()))
         return out
 
     def affine_f32_dev(self, d_x: int, n: int, mode: int, d_out: int, fa=0.0, fb=1.0, fc=0.0,

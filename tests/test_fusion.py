@@ -289,3 +289,32 @@ def test_gpu_resize_f32(engine, src, dst):
     engine.resize_f32_dev(d_a, src[0], src[1], d_o, dst[0], dst[1])
     got = engine.to_host(d_o, dst, np.float32)
     np.testing.assert_array_equal(got, FO.resize_linear_f32(a, dst[1], dst[0]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("narr,n,mode", [(16, 1 << 18, 0), (3, 1000003, 1), (5, 4097, 2), (1, 777, 0)])
+def test_gpu_select_batch_equals_single(engine, narr, n, mode):
+    """sv_select_count_batch / sv_select_ranks_batch: per-array results == single calls."""
+    rng = np.random.default_rng(narr * 31 + n)
+    x = (rng.normal(size=(narr, n)) * 100).astype(np.float32)
+    x[0, :7] = np.nan
+    m = rng.random((narr, n)).astype(np.float32)
+    dx, dm = engine.dev_alloc(x.nbytes), engine.dev_alloc(m.nbytes)
+    engine.to_device(dx, x)
+    engine.to_device(dm, m)
+    try:
+        sel, nan = engine.select_count_batch(dx, n, n, narr, mode, dm, n, 0.7)
+        ranks = []
+        for y in range(narr):
+            s1, n1 = engine.select_count(dx + 4 * y * n, n, mode, dm + 4 * y * n, 0.7)
+            assert (sel[y], nan[y]) == (s1, n1), y
+            ranks.append([0, s1 // 3, s1 // 2, max(0, s1 - 1)])
+        vals = engine.select_ranks_batch(dx, n, n, ranks, mode, dm, n, 0.7)
+        for y in range(narr):
+            single = engine.select_ranks(dx + 4 * y * n, n, ranks[y], mode, dm + 4 * y * n, 0.7)
+            np.testing.assert_array_equal(vals[y], single, err_msg=f"array {y}")
+            sel_y = x[y][(~np.isnan(x[y])) & ((x[y] > 0) if mode == 1 else (m[y] > 0.7) if mode == 2 else True)]
+            np.testing.assert_array_equal(vals[y], np.sort(sel_y)[ranks[y]])
+    finally:
+        engine.dev_free(dx)
+        engine.dev_free(dm)

@@ -411,6 +411,12 @@ class Verifier:
             self.failed.append(f"{tag}: {bad} disparity pixels differ")
         return ok
 
+    def disparity(self, tag, L, R, got_disp):
+        _, e_disp, _ = self.C.depth_map(L, R, 0, self.D, self.win, self.cost, 0.3, 2.0, self.threads)
+        self.checked.append(tag)
+        if not np.array_equal(got_disp, e_disp):
+            self.failed.append(f"{tag}: {int((got_disp != e_disp).sum())} disparity pixels differ")
+
     def harris(self, tag, L, got):
         exp = self.C.harris(L)
         err = float(np.max(np.abs(got.astype(np.float64) - exp))) if exp.size else 0.0
@@ -431,7 +437,7 @@ def fetch_maps(eng, d_depth, d_disp, d_norm, index, n_px, H, W):
 
 def dist_summary(ngpu, launched, pg=None, comms=None, gather=False, rowtile=False,
                  gather_ms=0.0, gather_n=0, scatter_ms=0.0, scatter_n=0, gather_wall_s=0.0,
-                 steps=0, gather_bytes=0, scatter_bytes=0, reason=""):
+                 steps=0, gather_bytes=0, scatter_bytes=0, reason="", gathered_maps=None):
     """The multi-GPU fields of the bench line (None for one GPU): the backend the run used,
     how many ranks the RCCL communicator saw (0 + the reason when it fell back), and the
     gather / scatter time per step from HIP events on the root's stream (these include the
@@ -449,6 +455,7 @@ def dist_summary(ngpu, launched, pg=None, comms=None, gather=False, rowtile=Fals
     out = {"backend": backend, "rccl_ranks": rccl_ranks, "rccl_reason": why or None,
            "process_model": "one process per GPU" if launched else "one process, all devices",
            "gather": bool(gather or rowtile),
+           "gathered_maps": gathered_maps,
            "gather_us_per_step": round(gather_ms * 1e3 / gather_n, 2) if gather_n else None,
            "gather_events": gather_n,
            "gather_bytes_per_step": gather_bytes or None,
@@ -618,13 +625,18 @@ def main():
                 raise SystemExit(f"RCCL group over devices {devices} unavailable ({ex}); "
                                  "pass --allow-peer-copies to gather with peer copies")
             log(f"RCCL group unavailable ({ex}); gathering with peer copies")
-    gathered = None   # launched frames mode: rank 0's stacks of every rank's frames
+    # launched frames mode with the gather: every step's disparity maps (f32, the reference's
+    # returned disparity) go to rank 0 on a communication stream of their own, double-buffered,
+    # so step i's gather overlaps step i+1's kernels; rank 0 receives them into one stack per
+    # buffer (rank-major).  Event slots of `eng`: 2s = set s computed, 2s+1 = set s gathered.
+    gathered, ceng, cstream = None, None, 0
     if launched and gather_on:
-        if rank == 0:
-            gathered = (arenas[0].alloc(4 * n_px * B * world), arenas[0].alloc(4 * n_px * B * world),
-                        arenas[0].alloc(n_px * B * world))
-        else:
-            gathered = (0, 0, 0)
+        ceng = Engine(devices[0])
+        cstream = ceng.stream
+        all_engines.append(ceng)
+        gset = [(depth[0], disp[0], norm[0]),
+                (arenas[0].alloc(4 * n_px * B), arenas[0].alloc(4 * n_px * B), arenas[0].alloc(n_px * B))]
+        gathered = [arenas[0].alloc(4 * n_px * B * world) if rank == 0 else 0 for _ in range(2)]
     gather_wall = [0.0]
 
     def step(i):
@@ -655,6 +667,11 @@ def main():
                                     0, D, win, 0.3, 2.0, depth[0], disp[0], norm[0], cost=args.cost)
             return
         engs, depth_o, disp_o, norm_o = lanes[i % nstreams]
+        if gathered is not None:   # double-buffered output sets; set s free once its gather ran
+            gs = i % 2
+            if i >= 2:
+                eng.stream_wait_event(2 * gs + 1, eng.stream)
+            depth_o, disp_o, norm_o = [gset[gs][0]], [gset[gs][1]], [gset[gs][2]]
         for k, e in enumerate(engs):
             if rectify:
                 for src, m1, m2, g in ((dL[k], m1l, m2l, gL), (dR[k], m1r, m2r, gR)):
@@ -671,14 +688,15 @@ def main():
                                       0.3, 2.0, depth_o[k], disp_o[k], norm_o[k], cost=args.cost)
             if harris:      # one launch over the batch's left frames
                 e.harris_batch_dev(gL if rectify else dL[k] + f * n_px, B, H, W, W, n_px, hmaps[k])
-        if gathered is not None:   # every rank's maps -> rank 0 (RCCL over xGMI)
+        if gathered is not None:   # every rank's disparity maps -> rank 0 (RCCL over xGMI)
             from stereovision_amd.distributed import gather_frames
             t_g = time.perf_counter()
-            eng.profile_region_begin("gather", eng.stream)
-            for src, dst, nb in ((depth[0], gathered[0], 4), (disp[0], gathered[1], 4),
-                                 (norm[0], gathered[2], 1)):
-                gather_frames(pg, src, B, dst, nb * n_px, stream=eng.stream)
-            eng.profile_region_end(eng.stream)
+            eng.event_record(2 * gs, eng.stream)        # set gs computed
+            eng.stream_wait_event(2 * gs, cstream)      # the gather follows it
+            ceng.profile_region_begin("gather", cstream)
+            gather_frames(pg, gset[gs][1], B, gathered[gs], 4 * n_px, stream=cstream)
+            ceng.profile_region_end(cstream)
+            eng.event_record(2 * gs + 1, cstream)       # set gs free again
             gather_wall[0] += time.perf_counter() - t_g
 
     def sync_all():
@@ -694,8 +712,9 @@ def main():
             sync_all()    # the time test sees device progress, not just enqueued steps
     sync_all()
     warm_s = time.perf_counter() - t_w
-    eng.profile(False)
-    eng.profile_reset()
+    for pe in [eng] + ([ceng] if ceng is not None else []):
+        pe.profile(False)
+        pe.profile_reset()
     gather_wall[0] = 0.0
     every = max(1, args.profile_every)
 
@@ -703,23 +722,26 @@ def main():
         pg.barrier()
     sync_all()
     t0 = time.perf_counter()
+    prof_engs = [eng] + ([ceng] if ceng is not None else [])
     for i in range(args.steps):
-        if not args.no_profile and every > 1:
-            eng.profile(i % every == 0)        # host-side toggle, no GPU work
-        elif i == 0:
-            eng.profile(not args.no_profile)
+        for pe in prof_engs:
+            if not args.no_profile and every > 1:
+                pe.profile(i % every == 0)        # host-side toggle, no GPU work
+            elif i == 0:
+                pe.profile(not args.no_profile)
         step(i)
     sync_all()
     elapsed = time.perf_counter() - t0     # this rank's; the max over ranks is the run's
     if pg is not None:
         pg.barrier()
 
-    eng.profile(False)
+    for pe in prof_engs:
+        pe.profile(False)
     match_ms, match_n = eng.profile_read("sgbm" if args.cost == "sgbm" else "match")
     med_ms, med_n = eng.profile_read("median")
     remap_ms, remap_n = eng.profile_read("remap")
     harris_ms, harris_n = eng.profile_read("harris")
-    gath_ms, gath_n = eng.profile_read("gather")
+    gath_ms, gath_n = (ceng or eng).profile_read("gather")
     scat_ms, scat_n = eng.profile_read("scatter")
     k_name = "sgbm pipeline (k_sgbm_*)" if args.cost == "sgbm" else "k_match"
     if pg is not None:
@@ -758,6 +780,9 @@ def main():
                                                             n_px, H, W))
         else:
             engs, depth_o, disp_o, norm_o = lanes[last % nstreams]
+            if gathered is not None:
+                gs = last % 2
+                depth_o, disp_o, norm_o = [gset[gs][0]], [gset[gs][1]], [gset[gs][2]]
             for k, e in enumerate(engs):
                 for z in zs:
                     Lz, Rz = hostL[k][f0 + z], hostR[k][f0 + z]
@@ -780,9 +805,9 @@ def main():
                             Lz, Rz = hostL[0][f0 + z], hostR[0][f0 + z]
                         else:   # rank r's inputs, regenerated from its seed
                             Lz, Rz, _ = stereo_pair(H, W, D, seed=1000 * r + f0 + z)
-                        ver.frame(f"rank {r} frame {f0 + z} (gathered on rank 0)", Lz, Rz,
-                                  *fetch_maps(eng, gathered[0], gathered[1], gathered[2], r * B + z,
-                                              n_px, H, W))
+                        ver.disparity(f"rank {r} frame {f0 + z} (gathered on rank 0)", Lz, Rz,
+                                      eng.to_host(gathered[last % 2] + 4 * n_px * (r * B + z), (H, W),
+                                                  np.float32))
         ok = ver.result()
         if pg is not None:
             ok = pg.allreduce_max(0.0 if ok else 1.0) == 0.0
@@ -868,12 +893,17 @@ def main():
                 gbytes += 9 * (b["r1"] - b["r0"]) * W
                 if band_inputs:
                     sbytes += 2 * (b["in1"] - b["in0"]) * W
-        elif gather_on:
-            gbytes = 9 * n_px * B * (ngpu - 1)
+        elif gather_on:   # launched: the f32 disparity maps; one process: all three outputs
+            gbytes = (4 if launched else 9) * n_px * B * (ngpu - 1)
     dist = dist_summary(ngpu, launched, pg, comms, gather=gather_on, rowtile=rowtile,
                         gather_ms=gath_ms, gather_n=gath_n, scatter_ms=scat_ms, scatter_n=scat_n,
                         gather_wall_s=gather_wall[0], steps=args.steps, gather_bytes=gbytes,
-                        scatter_bytes=sbytes, reason=comm_reason)
+                        scatter_bytes=sbytes, reason=comm_reason,
+                        gathered_maps=("rows of depth f32 + disparity f32 + depth u8" if rowtile else
+                                       "disparity f32 of every frame, overlapped with the next step "
+                                       "(communication stream, double-buffered maps)" if launched else
+                                       "depth f32 + disparity f32 + depth u8 of every frame")
+                        if (gather_on or rowtile) else None)
     parallelism = (f"row-tiled x{ngpu}" + (" (band inputs scattered from GPU 0)" if band_inputs else "")
                    + " + band gather" if rowtile else
                    f"frame-sharded x{ngpu}" + (" + gather to GPU 0" if gather_on else ""))

@@ -105,6 +105,12 @@ int sv_synchronize(sv_ctx* ctx);
  * size their volumes to SV_SGBM_BUDGET_GB, default a quarter of the device's free memory
  * (at most 48 GiB). */
 int sv_release_scratch(sv_ctx* ctx);
+/* Cross-stream ordering on the context's device (NULL stream = the context stream), with 16
+ * event slots per context: sv_event_record marks the work enqueued on `stream` so far;
+ * sv_stream_wait_event makes work enqueued on `stream` afterwards wait for that mark (e.g.
+ * a gather on a communication stream overlapping the next frame batch's kernels). */
+int sv_event_record(sv_ctx* ctx, int slot, void* stream);
+int sv_stream_wait_event(sv_ctx* ctx, int slot, void* stream);
 void* sv_stream(sv_ctx* ctx);
 
 /* Engine plan for a configuration: disparities per lane, lanes per group, LDS bytes per

@@ -156,6 +156,7 @@ struct sv_ctx {
     hipEvent_t scr_ev = nullptr;
     hipEvent_t xev = nullptr;   // multi-device entry points: this context's part is enqueued
     hipEvent_t sev = nullptr;   // sv_depth_map_rows_scatter: the root's inputs are ready
+    hipEvent_t wev[16] = {};    // sv_event_record / sv_stream_wait_event slots
     bool prof = false;
     std::vector<EvPair> pending;
     std::vector<hipEvent_t> pool;
@@ -711,6 +712,8 @@ void sv_destroy(sv_ctx* c) {
         if (c->scr_ev) (void)hipEventDestroy(c->scr_ev);
         if (c->xev) (void)hipEventDestroy(c->xev);
         if (c->sev) (void)hipEventDestroy(c->sev);
+        for (auto e : c->wev)
+            if (e) (void)hipEventDestroy(e);
         if (c->region_open) {
             (void)hipEventDestroy(c->region.a);
             (void)hipEventDestroy(c->region.b);
@@ -731,6 +734,22 @@ void sv_destroy(sv_ctx* c) {
         (void)hipStreamDestroy(c->stream);
     }
     delete c;
+}
+
+int sv_event_record(sv_ctx* c, int slot, void* stream) {
+    SV_ENTER(c);
+    if (slot < 0 || slot >= 16) return fail(SV_EINVAL, "event slot must be in [0, 16)");
+    hipEvent_t& e = c->wev[slot];
+    if (!e) SV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    SV_HIP(hipEventRecord(e, pick(c, stream)));
+    return 0;
+}
+
+int sv_stream_wait_event(sv_ctx* c, int slot, void* stream) {
+    SV_ENTER(c);
+    if (slot < 0 || slot >= 16 || !c->wev[slot]) return fail(SV_EINVAL, "event slot never recorded");
+    SV_HIP(hipStreamWaitEvent(pick(c, stream), c->wev[slot], 0));
+    return 0;
 }
 
 int sv_release_scratch(sv_ctx* c) {

@@ -47,7 +47,8 @@ EXPORTED = [
     "sv_depth_map_rows_multi", "sv_depth_map_color", "sv_stereo_scaled_color",
     "sv_median_post_color_dev", "sv_profile_region_begin", "sv_profile_region_end",
     "sv_comm_scatterv", "sv_depth_map_rows_scatter", "sv_band_rows_in", "sv_release_scratch",
-    "sv_frame_stats_batch_dev", "sv_select_count_batch", "sv_select_ranks_batch",
+    "sv_frame_stats_batch_dev", "sv_select_count_batch", "sv_select_ranks_batch", "sv_event_record",
+    "sv_stream_wait_event",
 ]
 BAND_MARGIN = 8   # SV_BAND_MARGIN: spare rows around a band-only input buffer
 COMM_ID_BYTES = 128
@@ -130,6 +131,8 @@ def _declare(lib):
         "sv_destroy": ([_vp], None),
         "sv_synchronize": ([_vp], _c_int),
         "sv_release_scratch": ([_vp], _c_int),
+        "sv_event_record": ([_vp, _c_int, _vp], _c_int),
+        "sv_stream_wait_event": ([_vp, _c_int, _vp], _c_int),
         "sv_stream": ([_vp], _vp),
         "sv_plan": ([_c_int, _c_int, _c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),
                      ctypes.POINTER(_c_int)], _c_int),
@@ -449,6 +452,14 @@ class Engine:
 
     def synchronize(self):
         _check("sv_synchronize", self.lib.sv_synchronize(self._h))
+
+    def event_record(self, slot: int, stream: int = 0):
+        """Mark the work enqueued on `stream` so far (event slot 0..15 of this context)."""
+        _check("sv_event_record", self.lib.sv_event_record(self._h, int(slot), stream or None))
+
+    def stream_wait_event(self, slot: int, stream: int = 0):
+        """Work enqueued on `stream` from now on waits for the mark in `slot`."""
+        _check("sv_stream_wait_event", self.lib.sv_stream_wait_event(self._h, int(slot), stream or None))
 
     def release_scratch(self):
         """Free the context's grow-only device scratch (e.g. after a large SGBM batch)."""

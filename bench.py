@@ -625,6 +625,19 @@ def main():
                 raise SystemExit(f"RCCL group over devices {devices} unavailable ({ex}); "
                                  "pass --allow-peer-copies to gather with peer copies")
             log(f"RCCL group unavailable ({ex}); gathering with peer copies")
+    # one process, N devices, gather: two lanes of contexts (own streams, scratch, RCCL
+    # group and root outputs each) that consecutive steps alternate over, so one step's
+    # gather overlaps the next step's kernels
+    glanes = None
+    if gather_all:
+        comms2 = None
+        if comms is not None:
+            comms2 = Communicator.init_all(devices)
+        engines2 = [Engine(d) for d in devices]
+        all_engines.extend(engines2)
+        glanes = [(engines, comms, depth[0], disp[0], norm[0]),
+                  (engines2, comms2, arenas[0].alloc(4 * n_px * out_frames), arenas[0].alloc(4 * n_px * out_frames),
+                   arenas[0].alloc(n_px * out_frames))]
     # launched frames mode with the gather: every step's disparity maps (f32, the reference's
     # returned disparity) go to rank 0 on a communication stream of their own, double-buffered,
     # so step i's gather overlaps step i+1's kernels; rank 0 receives them into one stack per
@@ -662,9 +675,10 @@ def main():
                                      depth[0], disp[0], norm[0], cost=args.cost)
             return
         if gather_all:     # one process, N devices, maps gathered on device 0
-            multi_gpu_depth_map_dev(engines, comms, [p + f * n_px for p in dL],
-                                    [p + f * n_px for p in dR], [B] * len(engines), H, W, W, n_px,
-                                    0, D, win, 0.3, 2.0, depth[0], disp[0], norm[0], cost=args.cost)
+            le, lc, ldep, ldis, lnor = glanes[i % 2]
+            multi_gpu_depth_map_dev(le, lc, [p + f * n_px for p in dL],
+                                    [p + f * n_px for p in dR], [B] * len(le), H, W, W, n_px,
+                                    0, D, win, 0.3, 2.0, ldep, ldis, lnor, cost=args.cost)
             return
         engs, depth_o, disp_o, norm_o = lanes[i % nstreams]
         if gathered is not None:   # double-buffered output sets; set s free once its gather ran
@@ -712,7 +726,7 @@ def main():
             sync_all()    # the time test sees device progress, not just enqueued steps
     sync_all()
     warm_s = time.perf_counter() - t_w
-    for pe in [eng] + ([ceng] if ceng is not None else []):
+    for pe in [eng] + ([ceng] if ceng is not None else []) + ([glanes[1][0][0]] if glanes else []):
         pe.profile(False)
         pe.profile_reset()
     gather_wall[0] = 0.0
@@ -722,7 +736,7 @@ def main():
         pg.barrier()
     sync_all()
     t0 = time.perf_counter()
-    prof_engs = [eng] + ([ceng] if ceng is not None else [])
+    prof_engs = [eng] + ([ceng] if ceng is not None else []) + ([glanes[1][0][0]] if glanes else [])
     for i in range(args.steps):
         for pe in prof_engs:
             if not args.no_profile and every > 1:
@@ -742,6 +756,9 @@ def main():
     remap_ms, remap_n = eng.profile_read("remap")
     harris_ms, harris_n = eng.profile_read("harris")
     gath_ms, gath_n = (ceng or eng).profile_read("gather")
+    if glanes:   # the second lane's root context times its own gathers
+        m2, n2 = glanes[1][0][0].profile_read("gather")
+        gath_ms, gath_n = gath_ms + m2, gath_n + n2
     scat_ms, scat_n = eng.profile_read("scatter")
     k_name = "sgbm pipeline (k_sgbm_*)" if args.cost == "sgbm" else "k_match"
     if pg is not None:
@@ -773,10 +790,11 @@ def main():
                 ver.frame("full frame gathered on device 0", hostL[0][0], hostR[0][0],
                           *fetch_maps(eng, depth[0], disp[0], norm[0], 0, n_px, H, W))
         elif gather_all:
+            _, _, ldep, ldis, lnor = glanes[last % 2]
             for k in range(len(engines)):
                 for z in zs:
                     ver.frame(f"device {k} frame {f0 + z} (gathered on device 0)", hostL[k][f0 + z],
-                              hostR[k][f0 + z], *fetch_maps(eng, depth[0], disp[0], norm[0], k * B + z,
+                              hostR[k][f0 + z], *fetch_maps(eng, ldep, ldis, lnor, k * B + z,
                                                             n_px, H, W))
         else:
             engs, depth_o, disp_o, norm_o = lanes[last % nstreams]
@@ -902,7 +920,8 @@ def main():
                         gathered_maps=("rows of depth f32 + disparity f32 + depth u8" if rowtile else
                                        "disparity f32 of every frame, overlapped with the next step "
                                        "(communication stream, double-buffered maps)" if launched else
-                                       "depth f32 + disparity f32 + depth u8 of every frame")
+                                       "depth f32 + disparity f32 + depth u8 of every frame, two "
+                                       "context lanes so a step's gather overlaps the next step")
                         if (gather_on or rowtile) else None)
     parallelism = (f"row-tiled x{ngpu}" + (" (band inputs scattered from GPU 0)" if band_inputs else "")
                    + " + band gather" if rowtile else
@@ -977,6 +996,9 @@ def main():
         a.free()
     if comms:
         for c in comms:
+            c.close()
+    if glanes and glanes[1][1]:
+        for c in glanes[1][1]:
             c.close()
     if pg is not None:
         pg.close()

@@ -117,6 +117,7 @@ struct sv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
+    DevBuf wctr;   // persistent matcher's work counters (zeroed once; the kernel resets them)
     DevBuf img[2], gray[2], d16, fa, fb, fc, u8, harris, hog[2], fin, lut, rmap1, rmap2, rdst[2], stats, sel,
         sg_hsum, sg_c, sg_l, sg_lt, sg_band, sg_rec, cc_parent, cc_size, hist_copies, cmap, bgr;
     uint8_t cmap_host[768] = {};   // BGR table currently in `cmap`
@@ -403,6 +404,8 @@ int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int 
     a.pad_key = (uint32_t)((sv::max_cost(win, cost) + 1) << plan.dbits);
     a.out = out;
     a.opitch = opitch;
+    SV_HIP(c->wctr.ensure_zeroed(256));
+    a.work_ctr = c->wctr.as<unsigned>();
     a.nf = nf < 1 ? 1 : nf;
     a.fs_in = fs_in;
     a.fs_out = fs_out;
@@ -702,7 +705,7 @@ void sv_destroy(sv_ctx* c) {
         (void)hipStreamSynchronize(c->stream);
         c->prof_drain();
         for (auto e : c->pool) (void)hipEventDestroy(e);
-        DevBuf* bufs[] = {&c->img[0], &c->img[1], &c->gray[0], &c->gray[1], &c->d16, &c->fa, &c->fb,
+        DevBuf* bufs[] = {&c->wctr, &c->img[0], &c->img[1], &c->gray[0], &c->gray[1], &c->d16, &c->fa, &c->fb,
                           &c->fc, &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->lut,
                           &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1], &c->stats, &c->sel,
                           &c->sg_hsum, &c->sg_c, &c->sg_l, &c->sg_lt, &c->sg_band, &c->cc_parent,

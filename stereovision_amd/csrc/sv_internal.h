@@ -54,6 +54,10 @@ struct MatchParams {
     long long fs_in, fs_out, fs_hist;
     uint32_t pad_key;      // (max_cost + 1) << dbits: key offset of padding disparities
     int segm;              // segment length in LPG units (set by launch_match)
+    // persistent kinds: the launching context's work counters (16 B, zero between launches;
+    // the kernel's last wave resets them), so concurrent launches on other contexts never
+    // share one
+    unsigned* work_ctr;
 };
 
 // Host-side launchers (return hipError_t as int).

@@ -34,6 +34,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
+#include <cstdio>
 #include <type_traits>
 
 namespace sv {
@@ -1219,6 +1221,14 @@ struct StreamParams {
     int nb;                    // bodies per row bundle
     int nq, nbund;             // row quads / bundles per frame
     long long total;           // bodies of the launch (nf * nbund * nb)
+    int dbg;                   // SV_STREAM_DBG ablations (timing only, results wrong): 1 no
+                               // producer, 4 no bursts, 8 no output stores
+    unsigned long long* trace; // SV_STREAM_TRACE (diagnostic): per wave {start, end, HW_ID, XCC}
+    // work: bodies [0, t_static) in equal contiguous shares, then segments of `seg` bodies of
+    // [t_static, total) handed out by ctr[0] (ctr[1] counts finished waves; the last resets)
+    long long t_static;
+    int seg;
+    unsigned* ctr;
 };
 
 template <int R, int LPG> struct StreamCfg {
@@ -1229,10 +1239,11 @@ template <int R, int LPG> struct StreamCfg {
     static constexpr int TPR = 5 * W2;                               // mirrored slots
     static constexpr int RSL = RPER + TPR;
     static constexpr int LL = (U + PRE + 3 + 3) & ~3;                // left ring positions
-    static constexpr int TL = U;
-    static constexpr int LSL = LL + TL;
+    static constexpr int LPER = LL + LL / 4;                         // ... slots (1 gap per 4)
+    static constexpr int TL = 5 * W2;                                // mirrored slots
+    static constexpr int LSL = LPER + TL;
     static constexpr int GROUP_BYTES = 24 * (RSL + LSL);
-    static constexpr int LDS_BYTES = G * GROUP_BYTES + 32;           // + one dummy slot pair
+    static constexpr int LDS_BYTES = G * GROUP_BYTES;
     static constexpr int NROW = 2 * R + 4;                          // image rows of a pack
 };
 
@@ -1247,26 +1258,29 @@ struct StreamUnit {
 // Loads of one unit: NROW dwords, rows clamp(yq - R + j), columns clamp(col, 0, W - 4) (the
 // edge bytes are replicated by stream_store's v_perm when the unit crosses an image border).
 // ONE load per row through one resource covering both images (per-lane image offset), so
-// the loaded registers are not touched until the transposes at the end of the body.
-// fast: rows of every producer group inside the image (uniform): row j = soffset j * pitch.
+// the loaded registers are not touched until the transposes at the end of the body.  One
+// code path for every row (clamped offsets, 2 VALU per row): a uniform fast/border branch
+// around the loads made the compiler's wait counters assume the other path's loads might
+// be in flight, and wait for every outstanding store (vmcnt(0)) at the top of each body.
 template <int R>
 __device__ __forceinline__ void stream_load(const StreamParams& p, __amdgpu_buffer_rsrc_t rs, const StreamUnit& u,
-                                            bool fast, uint32_t (&rw)[2 * R + 4]) {
+                                            uint32_t (&rw)[2 * R + 4]) {
     constexpr int NROW = 2 * R + 4;
     const int OOR = 0x7FFF0000;
-    const int io = u.right ? p.offR : p.offL;
-    const int cl = clampi(u.col, 0, p.W - 4);
-    if (fast) {
-        const int base = u.gg >= 0 ? io + (u.yq - R) * p.pitch + cl : OOR;
-#pragma unroll
-        for (int j = 0; j < NROW; ++j) rw[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, base, j * p.pitch, 0);
-        return;
-    }
+    const int io = (u.right ? p.offR : p.offL) + clampi(u.col, 0, p.W - 4);
+    // every offset first (plain selects, 24-bit multiplies), then the loads back to back: an
+    // offset computed into a register that an earlier load of the sequence still writes made
+    // the compiler wait for that load (a memory latency at the top of every body)
+    int off[NROW];
 #pragma unroll
     for (int j = 0; j < NROW; ++j) {
-        const int off = u.gg >= 0 ? io + clampi(u.yq - R + j, 0, p.H - 1) * p.pitch + cl : OOR;
-        rw[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+        const int o = io + __mul24(clampi(u.yq - R + j, 0, p.H - 1), p.pitch);
+        off[j] = u.gg >= 0 ? o : OOR;
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NROW; ++j) rw[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, off[j], 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // v_perm selector replicating the edge bytes of a unit that starts at column `col`
@@ -1279,7 +1293,7 @@ __device__ __forceinline__ uint32_t stream_edge_sel(int col, int W) {
 }
 
 // Ring slots of a unit's 4 packs (positions 4 m .. 4 m + 3 of its stream) and the writes,
-// mirrored slots included; idle lanes write the dummy slot.
+// mirrored slots included (idle lanes write nothing).
 template <int R, int LPG>
 __device__ __forceinline__ void stream_store(char* lds, const StreamUnit& u, int m, int c0, uint32_t (&rw)[2 * R + 4],
                                              bool edges, int W) {
@@ -1290,9 +1304,10 @@ __device__ __forceinline__ void stream_store(char* lds, const StreamUnit& u, int
 #pragma unroll
         for (int j = 0; j < 2 * R + 4; ++j) rw[j] = __builtin_amdgcn_perm(rw[j], rw[j], sel);
     }
-    // slot byte offsets of the 4 packs (main array; the common array is at +cofs, half the
-    // stride) and of their mirrors (the dummy slot when not mirrored / idle lane)
-    const int dummy = C::G * C::GROUP_BYTES;
+    // slot offsets of the 4 packs (main array; the common array at +cofs, half the stride)
+    // and of their mirrors (-1: not mirrored).  Both rings keep one empty slot per 4
+    // positions, so the 16 lanes of a b128 write pass (units 4 positions apart) land 5 slots
+    // = 80 B apart, on distinct banks; idle lanes and unmirrored slots do not write at all
     const int gb = u.gg * C::GROUP_BYTES;
     int s0[4], s1[4];
     const int cofs = u.right ? 16 * C::RSL : 16 * C::LSL;
@@ -1305,10 +1320,17 @@ __device__ __forceinline__ void stream_store(char* lds, const StreamUnit& u, int
             s1[k] = ph < C::TPR ? ph + C::RPER : -1;
         } else {
             const int q = (4 * m) % C::LL + k;
-            s0[k] = q;
-            s1[k] = q < C::TL ? q + C::LL : -1;
+            const int ph = q + (q >> 2);
+            s0[k] = ph;
+            s1[k] = ph < C::TL ? ph + C::LPER : -1;
         }
     }
+    const bool act = u.gg >= 0;
+    // every loaded row is consumed here on every path (the transposes below feed stores that
+    // idle lanes skip; sunk into those branches, a load left pending on the skip path made
+    // the compiler wait for it at the top of the next body)
+#pragma unroll
+    for (int j = 0; j < 2 * R + 4; ++j) asm volatile("" : "+v"(rw[j]));
     const int abase = gb + (u.right ? 0 : 24 * C::RSL);
     // common words first (rows 3 .. 2r), written before the custom words are formed: the
     // unit's live registers stay near NROW + 8 while the body's register rings are live
@@ -1324,10 +1346,8 @@ __device__ __forceinline__ void stream_store(char* lds, const StreamUnit& u, int
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint2 v = make_uint2(w[0][k], NC > 1 ? w[NC > 1 ? 1 : 0][k] : 0u);
-            const int a0 = u.gg < 0 ? dummy + 16 : abase + cofs + 8 * s0[k];
-            const int a1 = (u.gg < 0 || s1[k] < 0) ? dummy + 16 : abase + cofs + 8 * s1[k];
-            *reinterpret_cast<uint2*>(lds + a0) = v;
-            *reinterpret_cast<uint2*>(lds + a1) = v;
+            if (act) *reinterpret_cast<uint2*>(lds + abase + cofs + 8 * s0[k]) = v;
+            if (act && s1[k] >= 0) *reinterpret_cast<uint2*>(lds + abase + cofs + 8 * s1[k]) = v;
         }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -1346,10 +1366,8 @@ __device__ __forceinline__ void stream_store(char* lds, const StreamUnit& u, int
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint4 v = make_uint4(w[0][k], w[1][k], w[2][k], w[3][k]);
-            const int a0 = u.gg < 0 ? dummy : abase + 16 * s0[k];
-            const int a1 = (u.gg < 0 || s1[k] < 0) ? dummy : abase + 16 * s1[k];
-            *reinterpret_cast<uint4*>(lds + a0) = v;
-            *reinterpret_cast<uint4*>(lds + a1) = v;
+            if (act) *reinterpret_cast<uint4*>(lds + abase + 16 * s0[k]) = v;
+            if (act && s1[k] >= 0) *reinterpret_cast<uint4*>(lds + abase + 16 * s1[k]) = v;
         }
     }
 }
@@ -1367,9 +1385,13 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
     const int g = lane / LPG, l = lane & (LPG - 1);
     const int band = p.X1 - p.X0;
 
-    // this wave's share of the launch: bodies [b_lo, b_hi)
-    const long long b_lo = p.total * (long long)blockIdx.x / gridDim.x;
-    const long long b_hi = p.total * (long long)(blockIdx.x + 1) / gridDim.x;
+    const unsigned long long t_start = p.trace ? wall_clock64() : 0ull;
+    // this wave's static share: bodies [b_lo, b_hi) of [0, t_static); then dynamic segments
+    // of the rest (the two waves of a SIMD do not progress equally: oldest-first issue lets
+    // one finish ~30% before the other, whose tail then runs alone on the SIMD)
+    long long b_lo = p.t_static * (long long)blockIdx.x / gridDim.x;
+    long long b_hi = p.t_static * (long long)(blockIdx.x + 1) / gridDim.x;
+    const long long s_lo = b_lo, s_len = max(1ll, b_hi - b_lo);
 
     // per-lane constants of the step loop
     const int dl = p.delta - 4 * l;                      // right position offset of the lane
@@ -1394,9 +1416,18 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
     const int rmain = gbase, rcom = gbase + 16 * C::RSL;
     const int lmain = gbase + 24 * C::RSL, lcom = lmain + 16 * C::LSL;
 
+    Pk<NW> rn[RG_DPL], Lnext;
+    for (;;) {
+    if (b_lo >= b_hi) {   // next dynamic segment
+        unsigned k = 0;
+        if (lane == 0) k = atomicAdd(p.ctr, 1u);
+        k = __builtin_amdgcn_readfirstlane(k);
+        b_lo = p.t_static + (long long)k * p.seg;
+        if (b_lo >= p.total) break;
+        b_hi = min(p.total, b_lo + p.seg);
+    }
     long long b = b_lo;
     bool first_row = true;
-    Pk<NW> rn[RG_DPL], Lnext;
     while (b < b_hi) {
         // ---- row setup -------------------------------------------------------------------
         const long long bund = b / p.nb;
@@ -1409,9 +1440,6 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
         const auto rsI = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.img + frame * p.fs_in), 0, p.img_span,
                                                           0x00020000);
         const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(p.out + frame * p.fs_out, 0, 0x7FFFFFFF, 0x00020000);
-        // rows of every group inside the image (uniform): fast producer loads
-        const int ytop = p.row0 + bq * G * 4;
-        const bool rows_in = ytop - R >= 0 && ytop + 4 * G - 1 + R <= p.H - 1;
         // producer lane's unit rows
         const int p_yq = p.row0 + (bq * G + min(pg_, G - 1)) * 4;
         // emission: lane's output offset at step 0 and its column window
@@ -1439,18 +1467,25 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
             const int r_hi = (s_end + p.delta + 3) >> 2;
             const int l_lo = s_first >> 2, l_hi = (s_end + 3) >> 2;          // left units
             const int nr = r_hi - r_lo, nl = l_hi - l_lo, nug = nr + nl;
-            for (int i = lane; i < G * nug; i += 64) {
+            // at most 2 units per lane (G * nug <= 128), both loaded before either is used:
+            // one memory latency per burst
+            const int nall = (p.dbg & 4) ? 0 : G * nug;
+            StreamUnit u[2];
+            int um[2];
+            uint32_t rw[2][C::NROW];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int i = lane + 64 * t;
                 const int gg = i / nug, kk = i - gg * nug;
-                StreamUnit u;
-                u.gg = gg;
-                u.right = kk < nr ? 1 : 0;
-                const int m = u.right ? r_lo + kk : l_lo + (kk - nr);
-                u.col = (u.right ? p.xr0 : p.xl0) + 4 * m;
-                u.yq = p.row0 + (bq * G + gg) * 4;
-                uint32_t rw[C::NROW];
-                stream_load<R>(p, rsI, u, false, rw);
-                stream_store<R, LPG>(lds, u, m, p.c0, rw, true, p.W);
+                u[t].gg = i < nall ? gg : -1;
+                u[t].right = kk < nr ? 1 : 0;
+                um[t] = u[t].right ? r_lo + kk : l_lo + (kk - nr);
+                u[t].col = (u[t].right ? p.xr0 : p.xl0) + 4 * um[t];
+                u[t].yq = p.row0 + (bq * G + min(gg, G - 1)) * 4;
+                stream_load<R>(p, rsI, u[t], rw[t]);
             }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) stream_store<R, LPG>(lds, u[t], um[t], p.c0, rw[t], true, p.W);
         }
         __syncthreads();
         // running window state of the row, (re)started after the burst so the previous row's
@@ -1490,9 +1525,9 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
             const int ph = q + ((q + p.c0) >> 2);
             const PackPtr<COST_SAD4, R> rb{reinterpret_cast<const uint4*>(lds + rmain) + ph,
                                            reinterpret_cast<const typename P::CT*>(lds + rcom) + ph};
-            const int lq = s_first % C::LL;
-            const PackPtr<COST_SAD4, R> lb{reinterpret_cast<const uint4*>(lds + lmain) + lq,
-                                           reinterpret_cast<const typename P::CT*>(lds + lcom) + lq};
+            const int lq = s_first % C::LL, lph = lq + (lq >> 2);
+            const PackPtr<COST_SAD4, R> lb{reinterpret_cast<const uint4*>(lds + lmain) + lph,
+                                           reinterpret_cast<const typename P::CT*>(lds + lcom) + lph};
 #pragma unroll
             for (int c = 0; c < C::PRE / 4; ++c) {
                 const int ch = W2 - C::PRE / 4 + c;       // ring slots of the body's last chunks
@@ -1500,7 +1535,7 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
                 for (int u = 0; u < 4; ++u) {
                     const int slot = (4 * ch + u) % W2;
                     rn[u] = ld<COST_SAD4, R, true>(rb + (5 * c + u));
-                    const Pk<NW> Lc = ld<COST_SAD4, R, true>(lb + (4 * c + u));
+                    const Pk<NW> Lc = ld<COST_SAD4, R, true>(lb + (5 * c + u));
 #pragma unroll
                     for (int k = 0; k < RG_DPL; ++k)
 #pragma unroll
@@ -1527,9 +1562,18 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
         for (int jb = jb0; b < b_end; ++b, ++jb) {
             const int s_b = jb * U;
             const bool has_next = b + 1 < b_end;
+            if (p.dbg & 16) {
+                // wave priority from the static share's progress: behind -> higher priority,
+                // so oldest-first issue does not let the older waves of a SIMD run ahead
+                const int q = __builtin_amdgcn_readfirstlane((int)(min(4ll, (b - s_lo) * 4 / s_len)));
+                if (q == 0) __builtin_amdgcn_s_setprio(3);
+                else if (q == 1) __builtin_amdgcn_s_setprio(2);
+                else if (q == 2) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
             // producer unit of the next body: loads now, transposes + writes after the steps
             StreamUnit pu;
-            pu.gg = (prod && has_next) ? pg_ : -1;
+            pu.gg = (prod && has_next && !(p.dbg & 1)) ? pg_ : -1;
             pu.right = p_right;
             const int pm = p_right ? ((s_b + U + p.delta) >> 2) + p_k : ((s_b + U) >> 2) + p_k;
             pu.col = (p_right ? p.xr0 : p.xl0) + 4 * pm;
@@ -1543,8 +1587,12 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
             const int rc_lo = p.xr0 + 4 * ((s_b + U + p.delta) >> 2), rc_hi = rc_lo + 4 * NUR;
             const int lc_lo = p.xl0 + s_b + U, lc_hi = lc_lo + 4 * W2;
             const bool edges = rc_lo < 0 || rc_hi > p.W || lc_lo < 0 || lc_hi > p.W;
+            // unconditional (a body without a next one loads nothing: out-of-range offsets)
+            // so the wait counters see every load consumed in the same iteration; a load
+            // under a branch made the compiler wait for every store (vmcnt 0) at the next
+            // body's top
             uint32_t praw[C::NROW];
-            if (has_next) stream_load<R>(p, rsI, pu, rows_in, praw);
+            stream_load<R>(p, rsI, pu, praw);
 
             // ring bases of this body
             int q = (s_b % C::RL) + dl;
@@ -1552,13 +1600,13 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
             const int ph = q + ((q + p.c0) >> 2);
             const PackPtr<COST_SAD4, R> rb{reinterpret_cast<const uint4*>(lds + rmain) + ph,
                                            reinterpret_cast<const typename P::CT*>(lds + rcom) + ph};
-            const int lq = s_b % C::LL;
-            const PackPtr<COST_SAD4, R> lb{reinterpret_cast<const uint4*>(lds + lmain) + lq,
-                                           reinterpret_cast<const typename P::CT*>(lds + lcom) + lq};
+            const int lq = s_b % C::LL, lph = lq + (lq >> 2);
+            const PackPtr<COST_SAD4, R> lb{reinterpret_cast<const uint4*>(lds + lmain) + lph,
+                                           reinterpret_cast<const typename P::CT*>(lds + lcom) + lph};
             Lnext = ld<COST_SAD4, R, true>(lb);
             const int eb = el0 + s_b;
             const int ob = ooff0 + 2 * s_b;
-            const int emax = emit_lane ? band_l : 0;
+            const int emax = (emit_lane && !(p.dbg & 8)) ? band_l : 0;
 #pragma unroll
             for (int ch = 0; ch < W2; ++ch) {
                 // a uniform branch that never skips: one basic block per chunk (as in the ring
@@ -1572,7 +1620,7 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
                     const int slot = (4 * ch + u) % W2;
                     rn[u] = ld<COST_SAD4, R, true>(rb + (5 * ch + u));
                     const Pk<NW> Lc = Lnext;
-                    if (ch < W2 - 1 || u < 3) Lnext = ld<COST_SAD4, R, true>(lb + (4 * ch + u + 1));
+                    if (ch < W2 - 1 || u < 3) Lnext = ld<COST_SAD4, R, true>(lb + (5 * ch + u + 1 + (u == 3 ? 1 : 0)));
 #pragma unroll
                     for (int k = 0; k < RG_DPL; ++k)
 #pragma unroll
@@ -1616,12 +1664,31 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
                     }
                 }
             }
-            if (has_next) {
-                __builtin_amdgcn_sched_barrier(0);
-                stream_store<R, LPG>(lds, pu, pm, p.c0, praw, edges, p.W);
-            }
-            __syncthreads();
+            __builtin_amdgcn_sched_barrier(0);
+            stream_store<R, LPG>(lds, pu, pm, p.c0, praw, edges, p.W);
+            // the next body reads what this one wrote: LDS instructions of one wave execute
+            // in order, so only the compiler needs fencing (no s_barrier / lgkmcnt(0) wait)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_sched_barrier(0);
         }
+    }
+    b_lo = b_hi;   // range done
+    }
+    if (lane == 0) {   // the last wave out resets the counters for the next launch
+        if (atomicAdd(p.ctr + 1, 1u) == gridDim.x - 1) {
+            atomicExch(p.ctr, 0u);
+            atomicExch(p.ctr + 1, 0u);
+        }
+    }
+    if (p.trace && lane == 0) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        unsigned long long* t = p.trace + 4 * blockIdx.x;
+        t[0] = t_start;
+        t[1] = wall_clock64();
+        t[2] = hw;
+        t[3] = xcc;
     }
 }
 
@@ -1673,6 +1740,11 @@ int launch_stream_rl(const MatchParams& a, hipStream_t s) {
     p.row1 = a.row1;
     p.fs_in = a.fs_in;
     p.fs_out = a.fs_out;
+    static const int dbg = [] {
+        const char* e = std::getenv("SV_STREAM_DBG");
+        return e ? std::atoi(e) : 0;
+    }();
+    p.dbg = dbg;
     p.xl0 = (a.X0 - R) & ~3;                                   // floor to a multiple of 4
     p.xr0 = (p.xl0 - a.minD - 4 * (LPG - 1) - 3) & ~3;
     p.delta = p.xl0 - a.minD - p.xr0;
@@ -1684,9 +1756,50 @@ int launch_stream_rl(const MatchParams& a, hipStream_t s) {
     const int nf = a.nf > 1 ? a.nf : 1;
     p.total = (long long)nf * p.nbund * p.nb;
     const int per_cu = std::min(8, (160 * 1024) / C::LDS_BYTES);
-    const long long waves = std::min<long long>(p.total, (long long)per_cu * device_cus());
+    // SV_STREAM_BODIES=<k> (A/B): k bodies per wave, as many waves as that takes (the
+    // hardware schedules them), instead of one persistent wave per slot
+    static const int bodies = [] {
+        const char* e = std::getenv("SV_STREAM_BODIES");
+        return e ? std::atoi(e) : 0;
+    }();
+    long long waves = std::min<long long>(p.total, (long long)per_cu * device_cus());
+    if (bodies > 0) waves = (p.total + bodies - 1) / bodies;
+    // static share / dynamic tail split (SV_STREAM_DYN: percent of the bodies handed out
+    // dynamically, SV_STREAM_SEG: bodies per dynamic segment; A/B tuning)
+    static const int dyn_pct = [] {
+        const char* e = std::getenv("SV_STREAM_DYN");
+        const int v = e ? std::atoi(e) : 20;
+        return v < 0 ? 0 : v > 100 ? 100 : v;
+    }();
+    static const int seg = [] {
+        const char* e = std::getenv("SV_STREAM_SEG");
+        const int v = e ? std::atoi(e) : 2;
+        return v < 1 ? 1 : v;
+    }();
+    p.seg = seg;
+    p.t_static = (waves < 64 || bodies > 0) ? p.total : p.total - p.total * dyn_pct / 100;
+    p.ctr = a.work_ctr;
+    // SV_STREAM_TRACE=<file> (diagnostic): per-wave start / end clocks and hardware ids of
+    // every launch appended to <file> (the launch is waited for)
+    static const char* trace_path = std::getenv("SV_STREAM_TRACE");
+    static unsigned long long* trace_buf = nullptr;
+    if (trace_path && !trace_buf && hipMalloc(&trace_buf, 4 * 8 * 65536) != hipSuccess) trace_buf = nullptr;
+    p.trace = (trace_path && waves <= 65536) ? trace_buf : nullptr;
     hipLaunchKernelGGL((k_match_stream<R, LPG>), dim3((unsigned)waves), dim3(64), C::LDS_BYTES, s, p);
-    return (int)hipGetLastError();
+    const int e = (int)hipGetLastError();
+    if (!e && p.trace) {
+        std::vector<unsigned long long> h((size_t)4 * waves);
+        if (hipMemcpyAsync(h.data(), trace_buf, h.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess) {
+            if (FILE* f = std::fopen(trace_path, "ab")) {
+                const long long hdr[2] = {waves, p.total};
+                std::fwrite(hdr, sizeof(hdr), 1, f);
+                std::fwrite(h.data(), 8, h.size(), f);
+                std::fclose(f);
+            }
+        }
+    }
+    return e;
 }
 template <int R>
 int launch_stream_r(const MatchParams& a, hipStream_t s) {

@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import argparse
 import csv
+import faulthandler
 import glob
 import json
 import os
@@ -528,6 +529,9 @@ def parse_args(argv=None):
                     help="skip the bit-exact check of the timed steps' outputs")
     ap.add_argument("--no-live-pmc", action="store_true", help="skip the rocprofv3 PMC passes")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host_path measurement")
+    ap.add_argument("--hang-timeout", type=float, default=900.0,
+                    help="dump every thread's stack and exit non-zero when the run takes longer "
+                         "than this many seconds (a rank stuck in a collective fails loudly)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
     if args.pmc_child:
@@ -539,6 +543,8 @@ def parse_args(argv=None):
 
 def main():
     args = parse_args()
+    if args.hang_timeout > 0:
+        faulthandler.dump_traceback_later(args.hang_timeout, exit=True)
     launched = int(os.environ.get("WORLD_SIZE", "1")) > 1
     rowtile = args.mode == "rowtile"
     pg = None
@@ -719,11 +725,28 @@ def main():
 
     t_w = time.perf_counter()
     n_warm = 0
-    while n_warm < args.warmup or (time.perf_counter() - t_w < args.warmup_seconds and n_warm < 100000):
-        step(n_warm)
-        n_warm += 1
-        if n_warm >= args.warmup and n_warm % 8 == 0:
-            sync_all()    # the time test sees device progress, not just enqueued steps
+    if pg is None:
+        while n_warm < args.warmup or (time.perf_counter() - t_w < args.warmup_seconds and n_warm < 100000):
+            step(n_warm)
+            n_warm += 1
+            if n_warm >= args.warmup and n_warm % 8 == 0:
+                sync_all()    # the time test sees device progress, not just enqueued steps
+    else:
+        # launched: a step may hold a collective (the gather, the row-tile scatter), so every
+        # rank must run the same number of warm-up steps — the W steps, then the extra steps
+        # the slowest rank needs to fill --warmup-seconds (agreed through a max over ranks)
+        for _ in range(max(1, args.warmup)):
+            step(n_warm)
+            n_warm += 1
+        sync_all()
+        per = (time.perf_counter() - t_w) / n_warm
+        left = max(0.0, args.warmup_seconds - (time.perf_counter() - t_w))
+        extra = int(pg.allreduce_max(float(min(100000, int(left / max(per, 1e-6)) + 1) if left > 0 else 0)))
+        for _ in range(extra):
+            step(n_warm)
+            n_warm += 1
+            if n_warm % 8 == 0:
+                sync_all()
     sync_all()
     warm_s = time.perf_counter() - t_w
     for pe in [eng] + ([ceng] if ceng is not None else []) + ([glanes[1][0][0]] if glanes else []):

@@ -2355,12 +2355,14 @@ int sv_frame_stats(sv_ctx* c, const uint8_t* img0, const uint8_t* img1, int H, i
 // One select pass over the context stream (a batch of a.narr arrays): hist [narr][kMaxRanks]
 // [2048] and counts [narr][2] back on the host.
 static int select_pass(sv_ctx* c, sv::SelectArgs& a, uint32_t* hist_host, unsigned long long* counts_host) {
-    // device: [narr][copies][kMaxRanks][2048] accumulators | [narr] count slots | folded
-    // hist [narr][kMaxRanks][2048] | counts [narr][2]
+    // device: [kSelBatch][copies][kMaxRanks][2048] accumulators | [kSelBatch] count slots |
+    // folded hist [narr][kMaxRanks][2048] | counts [narr][2].  The accumulator regions are
+    // laid out for the largest batch whatever narr is: the folds leave them zeroed, and a
+    // smaller batch's outputs must never land where a larger batch accumulates
     const size_t na = (size_t)(a.narr > 0 ? a.narr : 1);
     const size_t hb = (size_t)sv::kMaxRanks * 2048 * sizeof(uint32_t);
-    const size_t ab = na * sv::kHistCopies * hb;
-    const size_t cb = na * sv::kCountSlots * 16 * sizeof(unsigned long long);
+    const size_t ab = (size_t)sv::kSelBatch * sv::kHistCopies * hb;
+    const size_t cb = (size_t)sv::kSelBatch * sv::kCountSlots * 16 * sizeof(unsigned long long);
     const size_t ob = na * hb + na * 16;
     SV_HIP(c->sel.ensure_zeroed(ab + cb + ob));
     uint8_t* base = c->sel.as<uint8_t>();

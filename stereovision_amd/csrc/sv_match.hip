@@ -1692,13 +1692,14 @@ __global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
     }
 }
 
-// Stream kind eligibility (SV_STREAM=0 disables it, for A/B runs): SAD with 5 <= win <= 9,
-// 65 <= D <= 256, 4-aligned images and widths (dword unit loads), 32-bit output offsets.
+// Stream kind eligibility (opt-in, SV_STREAM=1): SAD with 5 <= win <= 9, 65 <= D <= 256,
+// 4-aligned images and widths (dword unit loads), 32-bit output offsets.  Off by default:
+// measured at the metric config it issues the same VALU instructions as the ring kind
+// (325.3 M per 16-frame launch; the in-loop pack transposes cost what the warm-up saved)
+// at a lower issue rate (more LDS bank conflicts): 590 vs 547 us per launch (profiles/r03b).
 bool stream_kind(const MatchParams& a) {
-    static const bool on = [] {
-        const char* e = std::getenv("SV_STREAM");
-        return !(e && e[0] == '0');
-    }();
+    const char* e = std::getenv("SV_STREAM");   // read per launch: tests switch it in-process
+    const bool on = e && e[0] == '1';
     if (!on || a.win < 5 || a.win > 9 || a.D <= 64 || a.D > 256 || (a.W & 3) || (a.pitch & 3) || a.X1 - a.X0 < 4 ||
         ((reinterpret_cast<uintptr_t>(a.L) | reinterpret_cast<uintptr_t>(a.R)) & 3u))
         return false;

@@ -6,7 +6,8 @@ cover both lane-group widths (32: D <= 128, 64: D <= 256), every radius, shares 
 inside a row (prologue) or at a row start, bundles with a null group (odd row-quad counts),
 partial row quads, row bands, frame batches, non-zero / negative / odd minimum disparities
 (the right stream's gap phase), image borders on both sides, and A/B equality with the ring
-kind (SV_STREAM=0 in a child process).
+kind (SV_STREAM=0 in a child process).  The stream kind is opt-in (SV_STREAM=1, read per
+launch): every test here switches it on.
 """
 import os
 import subprocess
@@ -20,6 +21,11 @@ from stereovision_amd.synthetic import stereo_pair
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(autouse=True)
+def _stream_on(monkeypatch):
+    monkeypatch.setenv("SV_STREAM", "1")
 
 
 def _dev(engine, a):
@@ -77,7 +83,7 @@ def test_stream_row_bands(engine, row0, row1):
 
 
 def test_stream_and_ring_kinds_agree():
-    """The same maps from a child with SV_STREAM=0 (ring kind) and one with the default."""
+    """The same maps from a child with SV_STREAM=0 (ring kind) and one with SV_STREAM=1."""
     code = ("import sys, numpy as np; sys.path.insert(0, %r)\n"
             "from stereovision_amd.engine import get_engine\n"
             "from stereovision_amd.synthetic import stereo_pair\n"

@@ -285,8 +285,8 @@ def test_bench_under_torch_distributed_run_two_ranks(mode):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
            "--steps", "3", "--warmup", "1", "--height", "96", "--width", "400", "--num-disp", "64",
            "--frames", "2", "--batch", "2", "--mode", mode, "--no-live-pmc", "--no-aux",
-           "--no-host-path", "--no-cpu-baseline"]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+           "--no-host-path", "--no-cpu-baseline", "--hang-timeout", "90"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     import json
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]

@@ -14,9 +14,9 @@ step() {  # step <name> <seconds> <cmd...>
 }
 B="--no-host-path --no-cpu-baseline --no-aux"
 step pytest_stream 300 python -u -m pytest tests/test_gpu_stream.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
-step bench_stream 200 python bench.py --steps 200 --warmup 20 $B
+step bench_stream 200 env SV_STREAM=1 python bench.py --steps 200 --warmup 20 $B
 step bench_ring 200 env SV_STREAM=0 python bench.py --steps 200 --warmup 20 $B
-step d192_stream 120 python bench.py --steps 100 --warmup 10 --num-disp 192 $B --no-live-pmc
+step d192_stream 120 env SV_STREAM=1 python bench.py --steps 100 --warmup 10 --num-disp 192 $B --no-live-pmc
 step d192_ring 120 env SV_STREAM=0 python bench.py --steps 100 --warmup 10 --num-disp 192 $B --no-live-pmc
 for f in bench_stream bench_ring d192_stream d192_ring; do
   grep '^{' "$OUT/$f.log" | python -c "

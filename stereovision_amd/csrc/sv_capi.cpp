@@ -130,6 +130,10 @@ struct sv_ctx {
     std::vector<HostEnt> hl_ent;
     bool hl_valid = false;
     hipEvent_t cev[8] = {};
+    // host-buffer frame path: band k's outputs come back on `dstream` (after cev[k] on the
+    // compute stream), `dev_done[k]` marks their arrival
+    hipStream_t dstream = nullptr;
+    hipEvent_t dev_done[8] = {};
     hipEvent_t tmr[2] = {nullptr, nullptr};   // sv_timer_begin / sv_timer_end
     // SGBM: second stream + fork/join events for the vertical path beside the horizontal ones
     hipStream_t sg_aux = nullptr;
@@ -723,6 +727,12 @@ void sv_destroy(sv_ctx* c) {
         }
         for (auto e : c->cev)
             if (e) (void)hipEventDestroy(e);
+        for (auto e : c->dev_done)
+            if (e) (void)hipEventDestroy(e);
+        if (c->dstream) {
+            (void)hipStreamSynchronize(c->dstream);
+            (void)hipStreamDestroy(c->dstream);
+        }
         for (auto e : c->tmr)
             if (e) (void)hipEventDestroy(e);
         if (c->sg_aux) {
@@ -1697,50 +1707,26 @@ bool host_registered(const void* p, size_t bytes) {
 
 // Host memory -> pinned staging -> device, in chunks: the DMA of one chunk runs while the
 // host threads copy the next (one call per frame, as the reference calls the path).
-int stage_image_chunked(sv_ctx* c, const uint8_t* src, int H, size_t row, int stride, uint8_t* stage,
-                        void* dev) {
-    const int nchunk = H >= 64 ? 6 : 1;
+// Rows [y0, y1) of a host image -> the pinned staging buffer (host pool threads) -> the
+// device image (one async H2D per sub-chunk on the compute stream, so a sub-chunk's DMA
+// overlaps the next one's copy).
+int stage_rows(sv_ctx* c, const uint8_t* src, int y0, int y1, size_t row, int stride, uint8_t* stage, uint8_t* dev,
+               int nsub) {
     sv::HostPool& pool = sv::HostPool::get();
-    for (int k = 0; k < nchunk; ++k) {
-        const int y0 = (int)((long long)H * k / nchunk), y1 = (int)((long long)H * (k + 1) / nchunk);
-        if (y1 <= y0) continue;
+    for (int k = 0; k < nsub; ++k) {
+        const int a0 = y0 + (int)((long long)(y1 - y0) * k / nsub), a1 = y0 + (int)((long long)(y1 - y0) * (k + 1) / nsub);
+        if (a1 <= a0) continue;
         const int parts = pool.threads();
         pool.parallel_for(parts, [&](int p) {
-            const int a = y0 + (int)((long long)(y1 - y0) * p / parts), b = y0 + (int)((long long)(y1 - y0) * (p + 1) / parts);
+            const int a = a0 + (int)((long long)(a1 - a0) * p / parts), b = a0 + (int)((long long)(a1 - a0) * (p + 1) / parts);
             if (b <= a) return;
             if ((size_t)stride == row)
                 std::memcpy(stage + (size_t)a * row, src + (size_t)a * row, (size_t)(b - a) * row);
             else
                 for (int y = a; y < b; ++y) std::memcpy(stage + (size_t)y * row, src + (size_t)y * stride, row);
         });
-        SV_HIP(hipMemcpyAsync(static_cast<uint8_t*>(dev) + (size_t)y0 * row, stage + (size_t)y0 * row,
-                              (size_t)(y1 - y0) * row, hipMemcpyHostToDevice, c->stream));
-    }
-    return 0;
-}
-
-int stage_pair_chunked(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels, int stride) {
-    if (check_image(left, H, W) || check_image(right, H, W)) return SV_EINVAL;
-    if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
-    const size_t row = (size_t)W * channels;
-    if (stride < (int)row) return fail(SV_EINVAL, "stride smaller than a row");
-    const size_t n = row * H;
-    SV_HIP(c->hin.ensure(2 * n));
-    SV_HIP(c->gray[0].ensure((size_t)H * W));
-    SV_HIP(c->gray[1].ensure((size_t)H * W));
-    const uint8_t* src[2] = {left, right};
-    for (int k = 0; k < 2; ++k) {
-        uint8_t* stage = c->hin.as<uint8_t>() + k * n;
-        void* dst = channels == 1 ? c->gray[k].p : nullptr;
-        if (channels == 3) {
-            SV_HIP(c->img[k].ensure(n));
-            dst = c->img[k].p;
-        }
-        int rc = stage_image_chunked(c, src[k], H, row, stride, stage, dst);
-        if (rc) return rc;
-        if (channels == 3)
-            SV_LAUNCH(c, SV_K_GRAY, c->stream,
-                      sv::launch_gray(c->img[k].as<uint8_t>(), H, W, (int)row, c->gray[k].as<uint8_t>(), c->stream));
+        SV_HIP(hipMemcpyAsync(dev + (size_t)a0 * row, stage + (size_t)a0 * row, (size_t)(a1 - a0) * row,
+                              hipMemcpyHostToDevice, c->stream));
     }
     return 0;
 }
@@ -1845,104 +1831,102 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
     int rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
     if (rc) return rc;
     if ((long long)H * W >= (1LL << 30)) return fail(SV_EINVAL, "frame too large");
-    rc = stage_pair_chunked(c, left, right, H, W, channels, stride);
-    if (rc) return rc;
-    if (prof) { const double t = now_ms(); tm[0] = t - tp; tp = t; }
+    if (check_image(left, H, W) || check_image(right, H, W)) return SV_EINVAL;
+    if (channels != 1 && channels != 3) return fail(SV_EINVAL, "channels must be 1 or 3");
+    const size_t row = (size_t)W * channels;
+    if (stride < (int)row) return fail(SV_EINVAL, "stride smaller than a row");
     const size_t n = (size_t)H * W;
+    SV_HIP(c->hin.ensure(2 * row * H));
+    SV_HIP(c->gray[0].ensure(n));
+    SV_HIP(c->gray[1].ensure(n));
+    if (channels == 3) {
+        SV_HIP(c->img[0].ensure(row * H));
+        SV_HIP(c->img[1].ensure(row * H));
+    }
     SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
     SV_HIP(c->m16.ensure(n * sizeof(int16_t)));
     SV_HIP(c->hout.ensure(n * sizeof(int16_t)));
-    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp,
-                           win, cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
-    if (rc) return rc;
     rc = attach_lut(c, pp, c->stream);
     if (rc) return rc;
     if (pp.lut_n <= 0) return fail(SV_EINVAL, "no post-processing table for these parameters");
-    const bool scaled_mode = pp.mode == SV_POST_SCALED;
-    if (host_registered(o.a, n * 4) && host_registered(o.disp, n * 4) && (!o.u8 || host_registered(o.u8, n)) &&
-        (!scaled_mode || host_registered(o.b, n * 4)) && (!o.bgr || host_registered(o.bgr, 3 * n))) {
-        // registered outputs: the median kernel's epilogue writes every output on the device
-        // and they come back by DMA in row chunks (no host expansion)
+    const bool scaled = pp.mode == SV_POST_SCALED;
+    // registered outputs: the median kernel's epilogue writes every output on the device and
+    // they come back by DMA; otherwise only the int16 medians come back and the host expands
+    // them with the table the device built
+    const bool reg = host_registered(o.a, n * 4) && host_registered(o.disp, n * 4) &&
+                     (!o.u8 || host_registered(o.u8, n)) && (!scaled || host_registered(o.b, n * 4)) &&
+                     (!o.bgr || host_registered(o.bgr, 3 * n));
+    sv::PostParams mp = pp;
+    int m0 = 0, nl = 0;
+    const HostEnt* ent = nullptr;
+    const float* lb = nullptr;
+    if (reg) {
         SV_HIP(c->fa.ensure(n * 4));
         SV_HIP(c->fb.ensure(n * 4));
         SV_HIP(c->u8.ensure(n));
-        if (scaled_mode) SV_HIP(c->fc.ensure(n * 4));
+        if (scaled) SV_HIP(c->fc.ensure(n * 4));
         if (o.bgr) SV_HIP(c->bgr.ensure(3 * n));
-        sv::PostParams dp = pp;
-        dp.out_a = c->fa.as<float>();
-        dp.out_u8 = c->u8.as<uint8_t>();
-        dp.out_b = scaled_mode ? c->fc.as<float>() : nullptr;
-        rc = attach_cmap(c, dp, table, o.bgr ? c->bgr.as<uint8_t>() : nullptr, c->stream);
+        mp.out_a = c->fa.as<float>();
+        mp.out_u8 = c->u8.as<uint8_t>();
+        mp.out_b = scaled ? c->fc.as<float>() : nullptr;
+        rc = attach_cmap(c, mp, table, o.bgr ? c->bgr.as<uint8_t>() : nullptr, c->stream);
         if (rc) return rc;
-        SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
-                  sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, c->fb.as<float>(), dp, c->stream));
-        if (prof) { const double t = now_ms(); tm[1] = t - tp; tp = t; }
-        const int nck = H >= 64 ? 4 : 1;
-        for (int k = 0; k < nck; ++k) {
-            const size_t y0 = (size_t)H * k / nck, y1 = (size_t)H * (k + 1) / nck, i0 = y0 * W, m = (y1 - y0) * W;
-            SV_HIP(hipMemcpyAsync(o.disp + i0, c->fb.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, c->stream));
-            SV_HIP(hipMemcpyAsync(o.a + i0, c->fa.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, c->stream));
-            if (o.u8) SV_HIP(hipMemcpyAsync(o.u8 + i0, c->u8.as<uint8_t>() + i0, m, hipMemcpyDeviceToHost, c->stream));
-            if (scaled_mode)
-                SV_HIP(hipMemcpyAsync(o.b + i0, c->fc.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, c->stream));
-            if (o.bgr)
-                SV_HIP(hipMemcpyAsync(o.bgr + 3 * i0, c->bgr.as<uint8_t>() + 3 * i0, 3 * m, hipMemcpyDeviceToHost,
-                                      c->stream));
+    } else {
+        rc = host_lut(c, pp);
+        if (rc) return rc;
+        mp.mode = SV_POST_NONE;      // the median kernel writes only the int16 medians
+        mp.out_m16 = c->m16.as<int16_t>();
+        m0 = pp.lut_m0;
+        nl = pp.lut_n;
+        // one 8-byte entry per table index: the f32 output and (u8, B, G, R) packed, so a
+        // pixel costs one L1 load instead of the dependent u8 -> colormap lookups
+        try {
+            c->hl_ent.resize((size_t)nl);
+        } catch (...) {
+            return fail(SV_ENOMEM, "host table allocation failed");
         }
-        SV_HIP(hipStreamSynchronize(c->stream));
-        if (prof) {
-            const double t = now_ms();
-            tm[4] = t - tp;
-            tm[5] = t - t0;
-            host_prof().add(tm);
+        for (int i = 0; i < nl; ++i) {
+            const uint8_t u = c->hl_u8[i];
+            const uint32_t bgr = table ? (uint32_t)table[3 * u] | (uint32_t)table[3 * u + 1] << 8 |
+                                         (uint32_t)table[3 * u + 2] << 16 : 0u;
+            c->hl_ent[i] = HostEnt{c->hl_a[i], u | bgr << 8};
         }
-        return 0;
+        ent = c->hl_ent.data();
+        lb = c->hl_b.data();
     }
-    rc = host_lut(c, pp);
-    if (rc) return rc;
-    sv::PostParams mp = pp;      // the median kernel writes only the int16 medians
-    mp.mode = SV_POST_NONE;
-    mp.out_m16 = c->m16.as<int16_t>();
-    SV_LAUNCH(c, SV_K_MEDIAN, c->stream, sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, nullptr, mp, c->stream));
-    const int nchunk = H >= 64 ? 8 : 1;
-    for (int k = 0; k < nchunk; ++k) {
-        if (!c->cev[k]) SV_HIP(hipEventCreateWithFlags(&c->cev[k], hipEventDisableTiming));
-        const size_t y0 = (size_t)H * k / nchunk, y1 = (size_t)H * (k + 1) / nchunk;
-        SV_HIP(hipMemcpyAsync(c->hout.as<int16_t>() + y0 * W, c->m16.as<int16_t>() + y0 * W, (y1 - y0) * W * 2,
-                              hipMemcpyDeviceToHost, c->stream));
-        SV_HIP(hipEventRecord(c->cev[k], c->stream));
-    }
-    const int m0 = pp.lut_m0, nl = pp.lut_n;
-    // one 8-byte entry per table index: the f32 output and (u8, B, G, R) packed, so a pixel
-    // costs one L1 load instead of the dependent u8 -> colormap lookups
-    try {
-        c->hl_ent.resize((size_t)nl);
-    } catch (...) {
-        return fail(SV_ENOMEM, "host table allocation failed");
-    }
-    for (int i = 0; i < nl; ++i) {
-        const uint8_t u = c->hl_u8[i];
-        const uint32_t bgr = table ? (uint32_t)table[3 * u] | (uint32_t)table[3 * u + 1] << 8 |
-                                     (uint32_t)table[3 * u + 2] << 16 : 0u;
-        c->hl_ent[i] = HostEnt{c->hl_a[i], u | bgr << 8};
-    }
-    const HostEnt* ent = c->hl_ent.data();
-    const float* lb = c->hl_b.data();
-    const int16_t* med = c->hout.as<int16_t>();
-    const bool scaled = pp.mode == SV_POST_SCALED;
+    if (prof) { const double t = now_ms(); tm[0] = t - tp; tp = t; }
+
+    // Row bands, pipelined: band k's input rows are staged and uploaded, then every
+    // disparity row whose window lies in the rows uploaded so far, then every median row
+    // whose 5x5 neighbourhood is computed, and those output rows go back on the download
+    // stream while band k+1 is staged (the H2D and D2H directions overlap).  SGBM's top-down
+    // path spans the frame: one band.
+    const char* be = std::getenv("SV_HOST_BANDS");   // A/B (read per call): 1, 2 or 4 bands
+    const int bv = be ? std::atoi(be) : 1;
+    const int bands_env = bv == 2 || bv == 4 ? bv : 1;
+    const int nband = (cost != SV_COST_SGBM && H >= 64 * bands_env) ? bands_env : 1;
+    // one band: the outputs come back on the compute stream itself (no cross-stream wait)
+    const int npiece = 8 / nband;   // D2H pieces per band, each with its arrival event
+    if (nband > 1 && !c->dstream) SV_HIP(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
+    hipStream_t ds = nband > 1 ? c->dstream : c->stream;
+    const int below = win / 2 + 1;   // input rows below a disparity row (HOG: window + gradient)
+    int d_done = 0, m_done = 0;
+    int bands[8][2] = {};   // output rows of each D2H piece
     std::atomic<int> bad{0};
     sv::HostPool& pool = sv::HostPool::get();
-    for (int k = 0; k < nchunk; ++k) {
-        SV_HIP(hipEventSynchronize(c->cev[k]));
+    auto expand = [&](int k) -> int {   // host expansion of piece k's medians
+        const int y0 = bands[k][0], y1 = bands[k][1];
+        if (y1 <= y0) return 0;
+        SV_HIP(hipEventSynchronize(c->dev_done[k]));
         if (prof) { const double t = now_ms(); tm[k ? 4 : 2] += t - tp; tp = t; }
-        const size_t y0 = (size_t)H * k / nchunk, y1 = (size_t)H * (k + 1) / nchunk;
-        const size_t i0 = y0 * W, i1 = y1 * W;
+        const size_t i0 = (size_t)y0 * W, i1 = (size_t)y1 * W;
+        const int16_t* med = c->hout.as<int16_t>();
         const int parts = pool.threads();
         pool.parallel_for(parts, [&](int p) {
             const size_t a = i0 + (i1 - i0) * p / parts, b = i0 + (i1 - i0) * (p + 1) / parts;
-            const int nbad = (o.u8 ? 1 : 0) | (scaled ? 2 : 0) | (o.bgr ? 4 : 0);
+            const int sel = (o.u8 ? 1 : 0) | (scaled ? 2 : 0) | (o.bgr ? 4 : 0);
             int nb = 0;
-            switch (nbad) {   // the output set picks the instantiation (no per-pixel branches)
+            switch (sel) {   // the output set picks the instantiation (no per-pixel branches)
                 case 0: nb = expand_rows<false, false, false>(med, a, b, m0, nl, ent, lb, o); break;
                 case 1: nb = expand_rows<true, false, false>(med, a, b, m0, nl, ent, lb, o); break;
                 case 2: nb = expand_rows<false, true, false>(med, a, b, m0, nl, ent, lb, o); break;
@@ -1955,9 +1939,84 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
             if (nb) bad.fetch_add(nb);
         });
         if (prof) { const double t = now_ms(); tm[3] += t - tp; tp = t; }
+        return 0;
+    };
+    const uint8_t* src[2] = {left, right};
+    for (int k = 0; k < nband; ++k) {
+        const int y0 = (int)((long long)H * k / nband), y1 = (int)((long long)H * (k + 1) / nband);
+        const bool last = k == nband - 1;
+        for (int i = 0; i < 2; ++i) {
+            uint8_t* stage = c->hin.as<uint8_t>() + (size_t)i * row * H;
+            uint8_t* dst = channels == 1 ? c->gray[i].as<uint8_t>() : c->img[i].as<uint8_t>();
+            rc = stage_rows(c, src[i], y0, y1, row, stride, stage, dst, nband == 1 ? 6 : 2);
+            if (rc) return rc;
+            if (channels == 3)
+                SV_LAUNCH(c, SV_K_GRAY, c->stream,
+                          sv::launch_gray(c->img[i].as<uint8_t>() + (size_t)y0 * row, y1 - y0, W, (int)row,
+                                          c->gray[i].as<uint8_t>() + (size_t)y0 * W, c->stream));
+        }
+        const int d1 = last ? H : std::max(d_done, y1 - below);
+        if (d1 > d_done) {
+            rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp,
+                                   num_disp, win, cost, d_done, d1, c->d16.as<int16_t>(), W, c->stream);
+            if (rc) return rc;
+            d_done = d1;
+        }
+        const int m1 = last ? H : std::max(m_done, d_done - 2);
+        if (m1 > m_done) {
+            SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
+                      sv::launch_median_i16(c->d16.as<int16_t>(), H, W, m_done, m1, reg ? c->fb.as<float>() : nullptr,
+                                            mp, c->stream));
+            if (ds != c->stream) {
+                if (!c->cev[k]) SV_HIP(hipEventCreateWithFlags(&c->cev[k], hipEventDisableTiming));
+                SV_HIP(hipEventRecord(c->cev[k], c->stream));
+                SV_HIP(hipStreamWaitEvent(ds, c->cev[k], 0));
+            }
+            for (int j = 0; j < npiece; ++j) {
+                const int q = k * npiece + j;
+                const int p0 = m_done + (int)((long long)(m1 - m_done) * j / npiece);
+                const int p1 = m_done + (int)((long long)(m1 - m_done) * (j + 1) / npiece);
+                bands[q][0] = p0;
+                bands[q][1] = p1;
+                if (p1 <= p0) continue;
+                const size_t i0 = (size_t)p0 * W, m = (size_t)(p1 - p0) * W;
+                if (reg) {
+                    SV_HIP(hipMemcpyAsync(o.disp + i0, c->fb.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
+                    SV_HIP(hipMemcpyAsync(o.a + i0, c->fa.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
+                    if (o.u8) SV_HIP(hipMemcpyAsync(o.u8 + i0, c->u8.as<uint8_t>() + i0, m, hipMemcpyDeviceToHost, ds));
+                    if (scaled)
+                        SV_HIP(hipMemcpyAsync(o.b + i0, c->fc.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
+                    if (o.bgr)
+                        SV_HIP(hipMemcpyAsync(o.bgr + 3 * i0, c->bgr.as<uint8_t>() + 3 * i0, 3 * m,
+                                              hipMemcpyDeviceToHost, ds));
+                } else {
+                    SV_HIP(hipMemcpyAsync(c->hout.as<int16_t>() + i0, c->m16.as<int16_t>() + i0, m * 2,
+                                          hipMemcpyDeviceToHost, ds));
+                    if (!c->dev_done[q]) SV_HIP(hipEventCreateWithFlags(&c->dev_done[q], hipEventDisableTiming));
+                    SV_HIP(hipEventRecord(c->dev_done[q], ds));
+                }
+            }
+            m_done = m1;
+        }
+        if (prof && k == 0) { const double t = now_ms(); tm[1] = t - tp; tp = t; }
+        if (!reg && k > 0) {   // the previous band's expansion runs while this band is in flight
+            for (int j = 0; j < npiece; ++j) {
+                rc = expand((k - 1) * npiece + j);
+                if (rc) return rc;
+            }
+        }
     }
+    if (!reg) {
+        for (int j = 0; j < npiece; ++j) {
+            rc = expand((nband - 1) * npiece + j);
+            if (rc) return rc;
+        }
+    }
+    SV_HIP(hipStreamSynchronize(ds));
     if (prof) {
-        tm[5] = now_ms() - t0;
+        const double t = now_ms();
+        tm[4] += t - tp;
+        tm[5] = t - t0;
         host_prof().add(tm);
     }
     if (bad.load()) return fail(SV_EHIP, "median value outside the post-processing table");

@@ -604,3 +604,27 @@ def test_ring_kind_huge_out_pitch_falls_back_exactly(engine, win, D):
     finally:
         for p in (dL, dR, d16):
             engine.dev_free(p)
+
+
+@pytest.mark.parametrize("bands", ["1", "2", "4"])
+@pytest.mark.parametrize("H,W,D,win,cost", [(127, 200, 64, 9, "sad"), (256, 208, 64, 9, "sad"),
+                                            (257, 240, 96, 15, "sad"), (301, 256, 64, 11, "ssd"),
+                                            (260, 320, 64, 7, "hog"), (1080, 1920, 128, 9, "sad")])
+def test_host_path_row_bands_match_oracle(engine, monkeypatch, bands, H, W, D, win, cost):
+    """The host-buffer frame path can run a frame as pipelined row bands (SV_HOST_BANDS, read
+    per call; frames of >= 64 rows per band): each band's disparity rows start once their
+    window's input rows are uploaded, each band's outputs return on a download stream while
+    the next band uploads.  Every output, on both the fresh-array path (int16 medians + host
+    expansion in 8 pieces) and the registered-output path (device epilogue + DMA), equals the
+    whole-frame C oracle."""
+    monkeypatch.setenv("SV_HOST_BANDS", bands)
+    L, R, _ = stereo_pair(H, W, D, seed=H + W + win)
+    bl, br = to_bgr(L), to_bgr(R)
+    g0, g1 = C.gray(bl), C.gray(br)
+    e_depth, e_disp, e_norm = C.depth_map(g0, g1, 0, D, win, {"sad": 0, "ssd": 1, "hog": 2}[cost], 0.3, 2.0)
+    for it in range(4):        # fresh set, then recycled sets (registered from their reuse)
+        depth, disp, norm = engine.depth_map(bl, br, 0, D, win, 0.3, 2.0, cost=cost)
+        np.testing.assert_array_equal(disp, e_disp, err_msg=f"call {it}")
+        np.testing.assert_array_equal(depth, e_depth, err_msg=f"call {it}")
+        np.testing.assert_array_equal(norm, e_norm, err_msg=f"call {it}")
+        del depth, disp, norm

@@ -216,14 +216,18 @@ def hbm_entry(name, bytes_per_launch, ms, n):
             "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4), "launches": n}
 
 
-def aux_kernels(eng, H, W, B, med_ms, med_n, reps=20, blocker=None):
+def aux_kernels(eng, H, W, B, med_ms, med_n, reps=20, blocker=None, frames=None, maps=None):
     """HBM rooflines of the memory-bound kernels around k_match, measured after the timed
     region (not part of `value`): k_median_i16 from the timed steps, k_remap (the
     rectify+gray stage in front of the path) over a batch of B raw BGR frames, the occlusion
     statistics of a pair and one radix-select pass.  The small kernels are timed as a run of
     `reps` back-to-back calls between two stream events (sv_timer_*), enqueued behind a
     `blocker` (one step of the path) so they run back to back on the device: device time
-    per call, without host launch latency or per-launch event overhead."""
+    per call, without host launch latency or per-launch event overhead.  `frames` = (left,
+    right) device stacks of >= B gray frames and `maps` = a device stack of >= B f32 disparity
+    maps from the path: the occlusion statistics run on the camera frames and the selects on
+    the disparity maps, as the reference applies them (fused_depth_map.py:131-301,
+    1169-1257); without them, uniform random data."""
     out = {"k_median_i16": hbm_entry("k_median_i16", 11 * H * W * B, med_ms, med_n)}
     arena = DevArena(eng)
 
@@ -256,20 +260,24 @@ def aux_kernels(eng, H, W, B, med_ms, med_n, reps=20, blocker=None):
         # histogram fold runs in the same launch)
         nb = max(1, H // 48) * max(1, W // 48)
         st = arena.alloc(4 * 2 * (2 * nb + 256))
-        ms, n = timed(lambda: eng.frame_stats_dev(dst, dst + H * W, H, W, 1, W, st, st + 8 * nb,
-                                                  st + 16 * nb))
+        f0, f1 = frames if frames else (dst, dst + H * W)
+        ms, n = timed(lambda: eng.frame_stats_dev(f0, f1, H, W, 1, W, st, st + 8 * nb, st + 16 * nb))
         out["k_frame_stats"] = hbm_entry("k_frame_stats", 2 * H * W, ms, n)
         # the same statistics for a batch of B pairs in one launch + one fold
         # (sv_frame_stats_batch_dev): the queued-frames form
-        gpair = arena.upload(rng.integers(0, 256, (B, 2, H, W), dtype=np.uint8))
+        if frames:
+            g0, g1, gfs = frames[0], frames[1], H * W
+        else:
+            gpair = arena.upload(rng.integers(0, 256, (B, 2, H, W), dtype=np.uint8))
+            g0, g1, gfs = gpair, gpair + H * W, 2 * H * W
         stb = arena.alloc(4 * 2 * B * (2 * nb + 256))
-        ms, n = timed(lambda: eng.frame_stats_batch_dev(gpair, gpair + H * W, B, 2 * H * W, H, W, 1, W, stb,
-                                                        stb + 8 * B * nb, stb + 16 * B * nb))
+        ms, n = timed(lambda: eng.frame_stats_batch_dev(g0, g1, B, gfs, H, W, 1, W, stb, stb + 8 * B * nb,
+                                                        stb + 16 * B * nb))
         out["k_frame_stats_batch"] = hbm_entry(f"k_frame_stats ({B} pairs per launch)", 2 * H * W * B, ms, n)
         # one radix-select pass over a float32 disparity map (4 B/px).  select_count returns
         # its counts to the host (a synchronising call), so this one is timed per launch by
         # the context's kernel events
-        d = arena.upload(rng.random((H, W), dtype=np.float32))
+        d = maps if maps else arena.upload(rng.random((H, W), dtype=np.float32))
         eng.profile_reset()
         eng.profile(True)
         for _ in range(reps):
@@ -279,7 +287,7 @@ def aux_kernels(eng, H, W, B, med_ms, med_n, reps=20, blocker=None):
         out["k_select_hist"] = hbm_entry("k_select_hist", 4 * H * W, ms, n)
         # one pass over a batch of B maps per launch (sv_select_count_batch: grid.y = map)
         Bm = min(B, 16)
-        dm = arena.upload(rng.random((Bm, H, W), dtype=np.float32))
+        dm = maps if maps else arena.upload(rng.random((Bm, H, W), dtype=np.float32))
         eng.select_count_batch(dm, H * W, H * W, Bm, 1)
         eng.profile_reset()
         eng.profile(True)
@@ -993,7 +1001,10 @@ def main():
         rect.close()
     elif solo and not rowtile and not args.no_aux:
         try:
-            result["aux_kernels"] = aux_kernels(eng, H, W, B, med_ms, med_n, blocker=lambda: step(0))
+            result["aux_kernels"] = aux_kernels(eng, H, W, B, med_ms, med_n, blocker=lambda: step(0),
+                                                frames=(dL[0], dR[0]), maps=disp[0])
+            result["aux_kernels"]["inputs"] = ("occlusion statistics on the bench's gray frame pairs, "
+                                               "selects (mask disparity > 0) on the path's disparity maps")
         except Exception as e:  # reported, never required
             log(f"aux kernels failed: {e}")
     if harris and harris_n:     # 1 B/px gray read + 4 B/px f32 response written

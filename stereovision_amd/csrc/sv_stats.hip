@@ -56,6 +56,7 @@ __device__ __forceinline__ uint32_t gray_at(const uint8_t* p, int cn) {
     return cn == 3 ? (uint32_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14) : (uint32_t)p[0];
 }
 
+template <int AGG>
 __global__ __launch_bounds__(256) void k_frame_stats(FrameStatsArgs a) {
     __shared__ uint32_t hist[4][256];
     const int z = blockIdx.z;
@@ -84,12 +85,43 @@ __global__ __launch_bounds__(256) void k_frame_stats(FrameStatsArgs a) {
             for (int k = 0; k < kSlots; ++k) {
                 const int i = lane + 64 * k;
                 if (i < 576 && i / 12 < h) {
+                    if (AGG == 2) {
+                        // slot-level aggregation: a dword of 4 equal bytes adds 4 at once, and
+                        // when every active lane holds the same such dword one lane adds the
+                        // wave's total (flat regions: same-address LDS atomics serialise);
+                        // other dwords add byte by byte
+                        const uint32_t dk = d[k];
+                        const bool same4 = ((dk ^ (dk >> 8)) & 0xFFFFFFu) == 0u;
+                        const uint32_t b0 = dk & 0xffu;
+                        if (same4) {
+                            s += 4 * b0;
+                            q += 4 * b0 * b0;
+                            const unsigned long long act = __ballot(1);
+                            const uint32_t lead = (uint32_t)__builtin_amdgcn_readfirstlane((int)dk);
+                            const unsigned long long uni = __ballot(dk == lead) & act;
+                            if (uni == act) {
+                                if (__lane_id() == (unsigned)__builtin_ctzll(act))
+                                    atomicAdd(&hist[wv][b0], 4u * (uint32_t)__builtin_popcountll(act));
+                            } else {
+                                atomicAdd(&hist[wv][b0], 4u);
+                            }
+                        } else {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const uint32_t v = (d[k] >> (8 * j)) & 0xff;
-                        s += v;
-                        q += v * v;
-                        hist_add<1>(hist[wv], v);
+                            for (int j = 0; j < 4; ++j) {
+                                const uint32_t v = (dk >> (8 * j)) & 0xff;
+                                s += v;
+                                q += v * v;
+                                atomicAdd(&hist[wv][v], 1u);
+                            }
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const uint32_t v = (d[k] >> (8 * j)) & 0xff;
+                            s += v;
+                            q += v * v;
+                            hist_add<AGG>(hist[wv], v);
+                        }
                     }
                 }
             }
@@ -102,7 +134,7 @@ __global__ __launch_bounds__(256) void k_frame_stats(FrameStatsArgs a) {
                     const uint32_t v = gray_at(p + j * a.cn, a.cn);
                     s += v;
                     q += v * v;
-                    hist_add<1>(hist[wv], v);
+                    hist_add<AGG == 2 ? 1 : AGG>(hist[wv], v);
                 }
             }
         }
@@ -146,44 +178,61 @@ __device__ __forceinline__ uint32_t f32_key(float f) {
 // Pass 0 (shift = 21, all prefixes empty) also counts selected elements and NaNs.
 constexpr int kSelVec = 4;   // float4 loads per thread per iteration (16 elements)
 
-__device__ __forceinline__ void select_one(const SelectArgs& a, const uint32_t* prefix, uint32_t (*h)[2048], int nb,
-                                           float v, float m, uint32_t& cnt, uint32_t& nan) {
-    if (a.mask_mode == SEL_MASK_GT && !(m > a.thr)) return;   // confidence > 0.7
-    if (v != v) {                                               // NaN in the selection -> nan
-        nan += a.mask_mode != SEL_POSITIVE;
+// The pass's scalars, copied out of the kernel arguments once (the kernels never modify or
+// take the address of their SelectArgs: a by-value argument indexed by blockIdx.y, or
+// written to, is copied to scratch memory and every use becomes a scratch load).
+struct SelPass {
+    int mode, shift, bits, nranks, nb;
+    float thr;
+    uint32_t pre[kMaxRanks];
+};
+
+__device__ __forceinline__ void select_one(const SelPass& q, uint32_t* h, float v, float m, uint32_t& cnt,
+                                           uint32_t& nan) {
+    if (q.mode == SEL_MASK_GT && !(m > q.thr)) return;   // confidence > 0.7
+    if (v != v) {                                         // NaN in the selection -> nan
+        nan += q.mode != SEL_POSITIVE;
         return;
     }
-    if (a.mask_mode == SEL_POSITIVE && !(v > 0.f)) return;     // disparity > 0
+    if (q.mode == SEL_POSITIVE && !(v > 0.f)) return;    // disparity > 0
     ++cnt;
     const uint32_t k = f32_key(v);
-    const uint32_t d = (k >> a.shift) & (uint32_t)(nb - 1);
-    const uint32_t hi = a.shift + a.bits >= 32 ? 0u : (k >> (a.shift + a.bits));
-    for (int r = 0; r < a.nranks; ++r)
-        if (hi == prefix[r]) hist_add<4>(h[r], d);
+    const uint32_t d = (k >> q.shift) & (uint32_t)(q.nb - 1);
+    const uint32_t hi = q.shift + q.bits >= 32 ? 0u : (k >> (q.shift + q.bits));
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r)
+        if (r < q.nranks && hi == q.pre[r]) hist_add<4>(h + r * q.nb, d);
 }
 
 // Pass `shift` of the select: histogram of digit (key >> shift) & (nbins-1) over the
 // selected elements whose key agrees with prefix[r] above the digit, for each rank r.
 // Pass 0 (shift = 21, all prefixes empty) also counts selected elements and NaNs.
 // Each thread loads kSelVec float4s (and mask float4s) before using any of them.
-__global__ __launch_bounds__(256) void k_select_hist(SelectArgs a) {
-    __shared__ uint32_t h[kMaxRanks][2048];
+__global__ __launch_bounds__(256) void k_select_hist(const SelectArgs a) {
+    extern __shared__ uint32_t h[];   // [nranks][1 << bits]: sized per pass (occupancy)
     const int y = blockIdx.y;                   // array of a batch
-    const uint32_t* prefix = a.prefix[y];
-    a.x += y * a.xstride;
-    if (a.mask) a.mask += y * a.mstride;
-    a.ghist += (size_t)y * kHistCopies * kMaxRanks * 2048;
-    a.counts += (size_t)y * kCountSlots * 16;
-    const int nb = 1 << a.bits;
-    for (int r = 0; r < a.nranks; ++r)
-        for (int i = threadIdx.x; i < nb; i += 256) h[r][i] = 0;
+    SelPass q;
+    q.mode = a.mask_mode;
+    q.shift = a.shift;
+    q.bits = a.bits;
+    q.nranks = a.nranks;
+    q.nb = 1 << a.bits;
+    q.thr = a.thr;
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r) q.pre[r] = a.prefix[y][r];
+    const float* x = a.x + y * a.xstride;
+    const float* mk = a.mask ? a.mask + y * a.mstride : nullptr;
+    uint32_t* ghist = a.ghist + (size_t)y * kHistCopies * kMaxRanks * 2048;
+    unsigned long long* counts = a.counts + (size_t)y * kCountSlots * 16;
+    const size_t n = a.n;
+    for (int i = threadIdx.x; i < q.nranks * q.nb; i += 256) h[i] = 0;
     __syncthreads();
     uint32_t cnt = 0, nan = 0;
-    const bool vec = ((((uintptr_t)a.x) & 15) == 0) && (a.mask_mode != SEL_MASK_GT || ((((uintptr_t)a.mask) & 15) == 0));
-    const size_t n4 = vec ? a.n / 4 : 0;
-    const float4* x4 = reinterpret_cast<const float4*>(a.x);
-    const float4* m4 = reinterpret_cast<const float4*>(a.mask);
-    const bool use_mask = a.mask_mode == SEL_MASK_GT;
+    const bool use_mask = q.mode == SEL_MASK_GT;
+    const bool vec = ((((uintptr_t)x) & 15) == 0) && (!use_mask || ((((uintptr_t)mk) & 15) == 0));
+    const size_t n4 = vec ? n / 4 : 0;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const float4* m4 = reinterpret_cast<const float4*>(mk);
     const size_t step = (size_t)gridDim.x * 256 * kSelVec;
     for (size_t base = (size_t)blockIdx.x * 256 * kSelVec + threadIdx.x; base < n4; base += step) {
         float4 v[kSelVec], m[kSelVec];
@@ -197,20 +246,20 @@ __global__ __launch_bounds__(256) void k_select_hist(SelectArgs a) {
 #pragma unroll
         for (int k = 0; k < kSelVec; ++k) {
             if (base + (size_t)k * 256 < n4) {
-                select_one(a, prefix, h, nb, v[k].x, m[k].x, cnt, nan);
-                select_one(a, prefix, h, nb, v[k].y, m[k].y, cnt, nan);
-                select_one(a, prefix, h, nb, v[k].z, m[k].z, cnt, nan);
-                select_one(a, prefix, h, nb, v[k].w, m[k].w, cnt, nan);
+                select_one(q, h, v[k].x, m[k].x, cnt, nan);
+                select_one(q, h, v[k].y, m[k].y, cnt, nan);
+                select_one(q, h, v[k].z, m[k].z, cnt, nan);
+                select_one(q, h, v[k].w, m[k].w, cnt, nan);
             }
         }
     }
     // scalar elements: the tail after the float4s, or everything when unaligned
-    for (size_t i = 4 * n4 + (size_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (size_t)gridDim.x * 256)
-        select_one(a, prefix, h, nb, a.x[i], use_mask ? a.mask[i] : 0.f, cnt, nan);
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        select_one(q, h, x[i], use_mask ? mk[i] : 0.f, cnt, nan);
     __syncthreads();
-    for (int r = 0; r < a.nranks; ++r)
-        for (int i = threadIdx.x; i < nb; i += 256)
-            if (h[r][i]) atomicAdd(&a.ghist[((blockIdx.x % kHistCopies) * kMaxRanks + r) * 2048 + i], h[r][i]);
+    for (int r = 0; r < q.nranks; ++r)
+        for (int i = threadIdx.x; i < q.nb; i += 256)
+            if (h[r * q.nb + i]) atomicAdd(&ghist[((blockIdx.x % kHistCopies) * kMaxRanks + r) * 2048 + i], h[r * q.nb + i]);
     {   // one add per block, striped over slots (same-address atomics serialise at L2)
         __shared__ uint32_t part[2][4];
         cnt = wave_sum(cnt);
@@ -222,7 +271,7 @@ __global__ __launch_bounds__(256) void k_select_hist(SelectArgs a) {
         __syncthreads();
         if (threadIdx.x < 2) {
             const uint32_t* p = part[threadIdx.x];
-            atomicAdd(&a.counts[(blockIdx.x % kCountSlots) * 16 + threadIdx.x],
+            atomicAdd(&counts[(blockIdx.x % kCountSlots) * 16 + threadIdx.x],
                       (unsigned long long)p[0] + p[1] + p[2] + p[3]);
         }
     }
@@ -230,27 +279,27 @@ __global__ __launch_bounds__(256) void k_select_hist(SelectArgs a) {
 
 // hist_out = sum of the accumulator copies (nranks x 2048 bins, 8 blocks per rank), counts_out
 // = sum of the count slots; every accumulator read is zeroed for the next pass.
-__global__ __launch_bounds__(256) void k_select_fold(SelectArgs a) {
+__global__ __launch_bounds__(256) void k_select_fold(const SelectArgs a) {
     const int y = blockIdx.y;
-    a.ghist += (size_t)y * kHistCopies * kMaxRanks * 2048;
-    a.counts += (size_t)y * kCountSlots * 16;
-    a.hist_out += (size_t)y * kMaxRanks * 2048;
-    a.counts_out += (size_t)y * 2;
+    uint32_t* ghist = a.ghist + (size_t)y * kHistCopies * kMaxRanks * 2048;
+    unsigned long long* counts = a.counts + (size_t)y * kCountSlots * 16;
+    uint32_t* hist_out = a.hist_out + (size_t)y * kMaxRanks * 2048;
+    unsigned long long* counts_out = a.counts_out + (size_t)y * 2;
     const int i = blockIdx.x * 256 + threadIdx.x;   // < nranks * 2048
     uint32_t v = 0;
     for (int k = 0; k < kHistCopies; ++k) {
-        uint32_t* p = a.ghist + (size_t)k * kMaxRanks * 2048 + i;
+        uint32_t* p = ghist + (size_t)k * kMaxRanks * 2048 + i;
         v += *p;
         *p = 0;
     }
-    a.hist_out[i] = v;
+    hist_out[i] = v;
     if (blockIdx.x == 0 && threadIdx.x < 2) {
         unsigned long long c = 0;
         for (int k = 0; k < kCountSlots; ++k) {
-            c += a.counts[k * 16 + threadIdx.x];
-            a.counts[k * 16 + threadIdx.x] = 0;
+            c += counts[k * 16 + threadIdx.x];
+            counts[k * 16 + threadIdx.x] = 0;
         }
-        a.counts_out[threadIdx.x] = c;
+        counts_out[threadIdx.x] = c;
     }
 }
 
@@ -278,7 +327,16 @@ int launch_frame_stats(const FrameStatsArgs& a, int nimg, hipStream_t s) {
     const int tiles_x = (a.W + kTile - 1) / kTile;
     dim3 grid((tiles_x + 3) / 4, (a.H + kTile - 1) / kTile, nimg);
     const size_t nh = (size_t)nimg * 256;
-    hipLaunchKernelGGL(k_frame_stats, grid, dim3(256), 0, s, a);
+    // SV_STATS_AGG (A/B): 0 plain LDS atomics per byte, 1 a wave-aggregated add per byte,
+    // 2 (default) slot-level aggregation of flat dwords / flat waves
+    static const int agg = [] {
+        const char* e = std::getenv("SV_STATS_AGG");
+        const int v = e ? std::atoi(e) : 2;
+        return v >= 0 && v <= 2 ? v : 2;
+    }();
+    if (agg == 2) hipLaunchKernelGGL(k_frame_stats<2>, grid, dim3(256), 0, s, a);
+    else if (agg == 1) hipLaunchKernelGGL(k_frame_stats<1>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_frame_stats<0>, grid, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_fold_u32, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, s, a.hist_copies,
                        kHistCopies, nh, (int)nh, a.hist);
     return (int)hipGetLastError();
@@ -289,7 +347,8 @@ int launch_select_hist(const SelectArgs& a, hipStream_t s) {
     int blocks = (int)((a.n + 256 * 4 * kSelVec - 1) / (256 * 4 * kSelVec));
     if (blocks > 1024) blocks = 1024;
     const int narr = a.narr > 0 ? a.narr : 1;
-    if (a.n > 0) hipLaunchKernelGGL(k_select_hist, dim3(blocks, narr), dim3(256), 0, s, a);
+    const size_t lds = (size_t)(a.nranks > 0 ? a.nranks : 1) * ((size_t)1 << a.bits) * sizeof(uint32_t);
+    if (a.n > 0) hipLaunchKernelGGL(k_select_hist, dim3(blocks, narr), dim3(256), lds, s, a);
     // the fold runs for n = 0 too: it writes the (empty) result
     hipLaunchKernelGGL(k_select_fold, dim3(a.nranks * 8, narr), dim3(256), 0, s, a);
     return (int)hipGetLastError();

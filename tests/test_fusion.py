@@ -162,6 +162,41 @@ def test_gpu_frame_stats_exact(engine, shape, channels):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("agg", ["0", "1", "2"])
+def test_gpu_frame_stats_flat_and_mixed_regions(engine, agg):
+    """The histogram adds' aggregation branches (SV_STATS_AGG, read at the first launch of a
+    process: run in a child) on images built to hit each: flat tiles (one wave-uniform dword),
+    tiles of 4-equal-byte dwords that differ across lanes, noisy-flat tiles (few distinct
+    values), random tiles and ragged borders."""
+    import subprocess, sys, os
+    code = r"""
+import sys, numpy as np
+sys.path.insert(0, %r); sys.path.insert(0, %r)
+from stereovision_amd.engine import get_engine
+rng = np.random.default_rng(5)
+H, W = 250, 500
+a = np.zeros((H, W), np.uint8)
+a[:, :96] = 200                                            # flat tiles
+a[:, 96:192] = np.repeat(rng.integers(0, 256, (H, 24), dtype=np.uint8), 4, axis=1)   # 4-equal dwords
+a[:, 192:288] = 40 + rng.integers(0, 3, (H, 96), dtype=np.uint8)                     # noisy flat
+a[:, 288:] = rng.integers(0, 256, (H, W - 288), dtype=np.uint8)                      # random
+b = np.full((H, W), 7, np.uint8)
+b[100:, 300:] = rng.integers(0, 256, (H - 100, W - 300), dtype=np.uint8)
+bs, bq, hist = get_engine(0).frame_stats(a, b)
+for k, g in enumerate((a, b)):
+    assert np.array_equal(hist[k], np.bincount(g.ravel(), minlength=256)), k
+    for i in range(H // 48):
+        for j in range(W // 48):
+            blk = g[i * 48:(i + 1) * 48, j * 48:(j + 1) * 48].astype(np.int64)
+            assert bs[k, i, j] == blk.sum() and bq[k, i, j] == (blk * blk).sum(), (k, i, j)
+print("ok")
+""" % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, SV_STATS_AGG=agg, SV_WARMUP_AT_IMPORT="0"))
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nf,shape,channels,pair", [(8, (1080, 1920), 1, True), (3, (47, 61), 3, True),
                                                     (5, (480, 640), 1, False), (1, (96, 144), 1, True)])
 def test_gpu_frame_stats_batch_equals_per_frame(engine, nf, shape, channels, pair):

@@ -1005,9 +1005,18 @@ PathPlan hpath_plan(int D) { return hpath16_plan(D); }
 
 template <typename LT>
 int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
-    const PathPlan ph = hpath_plan(a.D), pv = vpath_plan(a.D), pw = pv;
     const bool fused = a.fused != 0;
-    const dim3 gh((a.H + 3) / 4, fused ? 1 : 2, nf), gv((a.Wb + 64 / pv.lpc - 1) / (64 / pv.lpc), 1, nf);
+    // single frames / small batches (unfused): the horizontal lines take the vertical path's
+    // 32-lane plan (half the disparities per lane: a shorter dependent chain per step, and
+    // twice the waves of the 16-lane plan on a machine the ~540 16-lane waves leave half
+    // idle); batches keep 16-lane lines (the fused R->L/WTA kernel is 16-lane).
+    // SV_SGBM_H32=0: 16-lane lines for every launch (A/B).
+    static const bool h32 = [] {
+        const char* e = std::getenv("SV_SGBM_H32");
+        return !(e && e[0] == '0');
+    }();
+    const PathPlan ph = (fused || !h32) ? hpath_plan(a.D) : vpath_plan(a.D), pv = vpath_plan(a.D), pw = pv;
+    const dim3 gh((a.H + 64 / ph.lpc - 1) / (64 / ph.lpc), fused ? 1 : 2, nf), gv((a.Wb + 64 / pv.lpc - 1) / (64 / pv.lpc), 1, nf);
     const size_t npx = (size_t)a.H * a.Wb;
     const dim3 gw((unsigned)((npx + 64 / pw.lpc - 1) / (64 / pw.lpc)), 1, nf);
     // vertical path on the second stream, beside the horizontal paths
@@ -1037,6 +1046,8 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
         SV_HPATH(16, 12, 8, 2) SV_HPATH(16, 16, 6, 2) SV_HPATH(16, 20, 4, 2) SV_HPATH(16, 24, 4, 2)
         SV_HPATH(16, 32, 4, 1)
     }
+    SV_HPATH(32, 2, 16, 2) SV_HPATH(32, 4, 12, 2) SV_HPATH(32, 6, 10, 2) SV_HPATH(32, 8, 8, 2)
+    SV_HPATH(32, 10, 6, 2) SV_HPATH(32, 12, 4, 2) SV_HPATH(32, 16, 3, 2)
     SV_HPATH(16, 1, 24, 1) SV_HPATH(16, 2, 24, 1) SV_HPATH(16, 4, 16, 1) SV_HPATH(16, 8, 16, 1)
     SV_HPATH(16, 12, 10, 1) SV_HPATH(16, 16, 8, 1) SV_HPATH(16, 20, 6, 1) SV_HPATH(16, 24, 6, 1)
     SV_HPATH(16, 32, 4, 1)

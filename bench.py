@@ -444,6 +444,18 @@ def fetch_maps(eng, d_depth, d_disp, d_norm, index, n_px, H, W):
             eng.to_host(d_norm + n_px * index, (H, W), np.uint8))
 
 
+def agreed_extra_warmup(pg, spent_s: float, steps_done: int, warmup_seconds: float) -> int:
+    """Warm-up steps every rank runs after its first W (one-process-per-GPU launches): each
+    rank estimates how many more steps fill --warmup-seconds at its own rate, and all take the
+    max over ranks, so ranks whose steps hold a collective stay in lock step (a rank that
+    decided on its own clock ran one warm-up step more than its peers and waited in a gather
+    the others never entered)."""
+    per = spent_s / max(1, steps_done)
+    left = max(0.0, warmup_seconds - spent_s)
+    mine = min(100000, int(left / max(per, 1e-6)) + 1) if left > 0 else 0
+    return int(pg.allreduce_max(float(mine)))
+
+
 def dist_summary(ngpu, launched, pg=None, comms=None, gather=False, rowtile=False,
                  gather_ms=0.0, gather_n=0, scatter_ms=0.0, scatter_n=0, gather_wall_s=0.0,
                  steps=0, gather_bytes=0, scatter_bytes=0, reason="", gathered_maps=None):
@@ -747,9 +759,7 @@ def main():
             step(n_warm)
             n_warm += 1
         sync_all()
-        per = (time.perf_counter() - t_w) / n_warm
-        left = max(0.0, args.warmup_seconds - (time.perf_counter() - t_w))
-        extra = int(pg.allreduce_max(float(min(100000, int(left / max(per, 1e-6)) + 1) if left > 0 else 0)))
+        extra = agreed_extra_warmup(pg, time.perf_counter() - t_w, n_warm, args.warmup_seconds)
         for _ in range(extra):
             step(n_warm)
             n_warm += 1

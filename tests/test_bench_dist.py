@@ -47,6 +47,33 @@ def _dist_worker(rank, world, path, q):
     pg.close()
 
 
+def _warm_worker(rank, world, path, q):
+    os.environ.update({"WORLD_SIZE": str(world), "RANK": str(rank), "LOCAL_RANK": str(rank),
+                       "SV_RDZV_DIR": path})
+    pg = SD.init_process_group(device=0, backend="auto", timeout=60, strict=True)
+    # rank k's steps take (k + 1) ms: alone they would pick different warm-up counts
+    n = bench.agreed_extra_warmup(pg, 0.005 * (rank + 1), 5, 1.0)
+    q.put((rank, n))
+    pg.close()
+
+
+def test_warmup_count_agreed_across_ranks():
+    """Launched runs: every rank runs the same number of warm-up steps (the max over ranks
+    of each rank's own estimate), whatever its step rate."""
+    path = tempfile.mkdtemp(prefix="sv_bench_warm_")
+    os.rmdir(path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_warm_worker, args=(k, 3, path, q)) for k in range(3)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(3))
+    for p in ps:
+        p.join(timeout=60)
+    assert len(set(res.values())) == 1, res
+    assert res[0] == int((1.0 - 0.005) / 0.001) + 1     # the fastest rank's (largest) count
+
+
 def test_dist_fields_under_the_file_store_rehearsal():
     path = tempfile.mkdtemp(prefix="sv_bench_dist_")
     os.rmdir(path)

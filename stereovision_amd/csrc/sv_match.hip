@@ -797,7 +797,11 @@ __device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
 }
 
-template <int R, int LPGT>
+// DEFER: a chunk's second step pair is not reduced at the chunk's end (where its DPP /
+// permlane chain ran alone before the next basic block) but in the next chunk's step 1,
+// beside that chunk's first pair: two independent reduce-scatter chains interleaved, +9
+// loop-carried VGPRs (off for r 5, which would spill).
+template <int R, int LPGT, bool DEFER>
 __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     using P = PackCfg<COST_SAD4, R>;
     constexpr int NW = P::NW, NC = P::NC, W2 = 2 * R + 1;
@@ -916,6 +920,41 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFFF, 0x00020000);
     const int emax = ((l & 1) == 0 && l < (join2 ? 32 : 16) && y + jq < a.row1) ? max(0, min(S, a.X1 - xs)) : 0;
 
+    // store of a reduced key for the chunk starting at step tt (join2) / of step tt
+    auto emit_key = [&](uint32_t key, int tt) {
+        // non-emitting lanes store past the buffer's range (dropped by the hardware bounds
+        // check, as in composable_kernel): no exec-mask branch
+        const int off = (unsigned)(tt + eb) < (unsigned)emax ? ooff + 2 * tt : (int)0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16), orsrc, off, 0, 0);
+    };
+    // join2: pair (0,1) in kA, pair (2,3) in kB: one swap joins both
+    auto join_pairs = [&](uint32_t kA_, uint32_t kB_) {
+        auto p = __builtin_amdgcn_permlane16_swap(kA_, kB_, false, false);
+        uint32_t key = min(p[0], p[1]);
+        if (LPG == 64) {   // rows 0 and 2 hold the same pair (1 and 3 the other)
+            p = __builtin_amdgcn_permlane32_swap(key, key, false, false);
+            key = min(p[0], p[1]);
+        }
+        return key;
+    };
+    auto join_rows = [&](uint32_t key) {   // !join2: a pair's key over the group's DPP rows
+        if (LPG >= 32) {   // rows 0,1 (and 2,3) of the wave: min with lane ^ 16
+            const auto p = __builtin_amdgcn_permlane16_swap(key, key, false, false);
+            key = min(p[0], p[1]);
+        }
+        if (LPG == 64) {   // halves: min with lane ^ 32
+            const auto p = __builtin_amdgcn_permlane32_swap(key, key, false, false);
+            key = min(p[0], p[1]);
+        }
+        return key;
+    };
+    // DEFER state: the previous chunk's second pair (8 keys), its first pair's reduced key
+    // and its first step (a first chunk has none: the sentinel step stores out of range)
+    uint32_t dv[8], kA = 0xFFFFFFFFu;
+    int tprev = -(1 << 24);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dv[i] = 0xFFFFFFFFu;
+
     // whole bodies of U = 4*W2 steps, no exits inside a body (an exit per chunk made LLVM
     // shuffle the rings); the first body skips its first e0 chunks by a uniform branch
     for (int it = 0, t0 = -4 * e0; it < nit; ++it) {
@@ -923,7 +962,6 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
         for (int ch = 0; ch < W2; ++ch, t0 += 4) {
             if (t0 < 0) continue;            // the first body's skipped chunks (uniform)
             uint32_t bk[4][2];
-            uint32_t kA;                     // join2: key of the chunk's first pair (set at u = 1)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int slot = (4 * ch + u) % W2;
@@ -982,48 +1020,44 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                 // too (their keys are not emitted): no branch, so a chunk is one basic block and
                 // the scheduler can interleave a reduction's DPP / permlane chain with the next
                 // step's independent cost work
-                if (u & 1) {
+                if (DEFER && u == 3) {   // the second pair waits for the next chunk
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) dv[i] = bk[i >> 1][i & 1];
+                } else if (DEFER && u == 1) {   // this chunk's first pair + the previous chunk's second
                     uint32_t v[8];
 #pragma unroll
                     for (int i = 0; i < 8; ++i) v[i] = bk[i >> 1][i & 1];
                     reduce_scatter8_bm(v, lane & 15);
-                    uint32_t key = v[0];
+                    reduce_scatter8_bm(dv, lane & 15);
                     if (join2) {
-                        if (u == 1) {
-                            kA = key;
-                        } else {   // pair (0,1) in kA, pair (2,3) in key: one swap joins both
-                            auto p = __builtin_amdgcn_permlane16_swap(kA, key, false, false);
-                            key = min(p[0], p[1]);
-                            if (LPG == 64) {   // rows 0 and 2 hold the same pair (1 and 3 the other)
-                                p = __builtin_amdgcn_permlane32_swap(key, key, false, false);
-                                key = min(p[0], p[1]);
-                            }
-                            const int tt = t0;
-                            // non-emitting lanes store past the buffer's range (dropped by the
-                            // hardware bounds check, as in composable_kernel): no exec-mask branch
-                            const int off = (unsigned)(tt + eb) < (unsigned)emax ? ooff + 2 * tt : (int)0x80000000u;
-                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16),
-                                                                  orsrc, off, 0, 0);
-                        }
+                        emit_key(join_pairs(kA, dv[0]), tprev);
+                        kA = v[0];
                     } else {
-                        if (LPG >= 32) {   // rows 0,1 (and 2,3) of the wave: min with lane ^ 16
-                            const auto p = __builtin_amdgcn_permlane16_swap(key, key, false, false);
-                            key = min(p[0], p[1]);
-                        }
-                        if (LPG == 64) {   // halves: min with lane ^ 32
-                            const auto p = __builtin_amdgcn_permlane32_swap(key, key, false, false);
-                            key = min(p[0], p[1]);
-                        }
-                        const int tt = t0 + u - 1;
-                        const int off = (unsigned)(tt + eb) < (unsigned)emax ? ooff + 2 * tt : (int)0x80000000u;
-                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16),
-                                                              orsrc, off, 0, 0);
+                        emit_key(join_rows(dv[0]), tprev + 2);
+                        emit_key(join_rows(v[0]), t0);
+                    }
+                    tprev = t0;
+                } else if (u & 1) {
+                    uint32_t v[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[i] = bk[i >> 1][i & 1];
+                    reduce_scatter8_bm(v, lane & 15);
+                    if (join2) {
+                        if (u == 1) kA = v[0];
+                        else emit_key(join_pairs(kA, v[0]), t0);
+                    } else {
+                        emit_key(join_rows(v[0]), t0 + u - 1);
                     }
                 }
             }
         }
         rb = rb + W2 * (RG_DPL + 1);
         lb = lb + U;
+    }
+    if (DEFER) {   // the last chunk's second pair
+        reduce_scatter8_bm(dv, lane & 15);
+        if (join2) emit_key(join_pairs(kA, dv[0]), tprev);
+        else emit_key(join_rows(dv[0]), tprev + 2);
     }
 }
 
@@ -1147,7 +1181,12 @@ size_t ring_lds_bytes(int lpg, int seg, int r) {
 
 template <int R, int LPG>
 int launch_ring_rl(const MatchParams& a, size_t lds, hipStream_t s) {
-    auto fn = k_match_ring<R, LPG>;
+    // SV_RING_DEFER=0 (A/B): every pair reduced inside its own chunk
+    static const bool defer = [] {
+        const char* e = std::getenv("SV_RING_DEFER");
+        return !(e && e[0] == '0');
+    }();
+    auto fn = (defer && R != 5) ? k_match_ring<R, LPG, R != 5> : k_match_ring<R, LPG, false>;
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return (int)e;

@@ -691,6 +691,72 @@ __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
         if (y0 + u < a.H) row(y0 + u, rc[u]);
 }
 
+// Top->bottom path fused with the winner-take-all (unfused launches, VWTA): the horizontal
+// paths run first (both directions stored), then each line walks its band column down the
+// rows like k_sgbm_vpath and at every row sums its fresh L_tb with L_lr and L_rl (prefetched
+// in register rings beside C) and runs wta_line on the sum: L_tb is never stored, so its
+// write and the WTA's read of it leave the pipeline, and the WTA launch goes.
+template <int DPL, int LPC, typename LT, int PF>
+__global__ __launch_bounds__(64, 2) void k_sgbm_vpath_wta(SgbmArgs a) {
+    if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
+    constexpr int NL = 64 / LPC;
+    const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
+    const int xb = blockIdx.x * NL + g;
+    const int D = a.D, Wb = a.Wb, dbase = j * DPL;
+    const size_t plane = (size_t)Wb * a.Dp;
+    const size_t col = (size_t)min(xb, Wb - 1) * a.Dp + (dbase < D ? dbase : 0);
+    const uint16_t* Cc = a.C + col;
+    const LT* Ac = static_cast<const LT*>(a.Llr) + col;
+    const LT* Bc = static_cast<const LT*>(a.Lrl) + col;
+    BandOut* bout = reinterpret_cast<BandOut*>(a.band) + min(xb, Wb - 1);
+    const bool emit = xb < Wb && j == 0;
+    __shared__ int lds_s[64 * DPL];
+    using CP = Pack<uint16_t, DPL>;
+    using LP = Pack<LT, DPL>;
+    CP rc[PF];
+    LP ra[PF], rb[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+        const size_t o = (size_t)min(p, a.H - 1) * plane;
+        rc[p] = *reinterpret_cast<const CP*>(Cc + o);
+        ra[p] = *reinterpret_cast<const LP*>(Ac + o);
+        rb[p] = *reinterpret_cast<const LP*>(Bc + o);
+    }
+    int prev[DPL], pad[DPL];
+    pad_init<DPL>(pad, dbase, D);
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) prev[k] = dbase + k < D ? 0 : kInf;
+    int mn = 0;
+    auto row = [&](int y, const CP& cp, const LP& lp, const LP& rp) {
+        int c[DPL];
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) c[k] = (int)cp.v[k];
+        path_step<DPL, LPC>(prev, c, mn, a.P1, a.P2, pad, j);
+        mn = line_min<LPC>(lane_min<DPL>(prev));
+        int sm[DPL];
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) sm[k] = prev[k] + (int)lp.v[k] + (int)rp.v[k];
+        const BandOut o = wta_line<DPL, LPC>(a, sm, dbase, lds_s + lane * DPL, lds_s + g * LPC * DPL);
+        if (emit) bout[(size_t)y * Wb] = o;
+    };
+    int y0 = 0;
+    for (; y0 + PF <= a.H; y0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const CP c = rc[u];
+            const LP la = ra[u], lb = rb[u];
+            const size_t o = (size_t)min(y0 + u + PF, a.H - 1) * plane;
+            rc[u] = *reinterpret_cast<const CP*>(Cc + o);
+            ra[u] = *reinterpret_cast<const LP*>(Ac + o);
+            rb[u] = *reinterpret_cast<const LP*>(Bc + o);
+            row(y0 + u, c, la, lb);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (y0 + u < a.H) row(y0 + u, rc[u], ra[u], rb[u]);
+}
+
 // S = L_lr + L_rl + L_tb and the winner-take-all, one pixel per line of LPC lanes: every
 // pixel is independent, so this runs with full occupancy (it was the issue-bound half of a
 // fused vertical-path kernel on ~900 waves).
@@ -1019,7 +1085,17 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
     const dim3 gh((a.H + 64 / ph.lpc - 1) / (64 / ph.lpc), fused ? 1 : 2, nf), gv((a.Wb + 64 / pv.lpc - 1) / (64 / pv.lpc), 1, nf);
     const size_t npx = (size_t)a.H * a.Wb;
     const dim3 gw((unsigned)((npx + 64 / pw.lpc - 1) / (64 / pw.lpc)), 1, nf);
-    // vertical path on the second stream, beside the horizontal paths
+    // unfused launches (SV_SGBM_VWTA=0: A/B): the horizontal paths first, then the vertical
+    // path fused with the WTA (L_tb never stored); otherwise the vertical path on the second
+    // stream beside the horizontal paths and a separate WTA
+    static const bool vwta_on = [] {
+        const char* e = std::getenv("SV_SGBM_VWTA");
+        return !(e && e[0] == '0');
+    }();
+    // (D <= 128 measured even: 703 vs 707 frames/s per call at D=128, so the concurrent form
+    // stays there; D=320: 337 -> 359 per call, 373 -> 416 at batch 4)
+    const bool vwta = !fused && vwta_on && pv.lpc == 32 && a.D > 128;
+    if (vwta) aux = nullptr;
     hipStream_t sv = aux ? aux : s;
     if (aux) {
         if (hipEventRecord(fork, s) != hipSuccess || hipStreamWaitEvent(aux, fork, 0) != hipSuccess)
@@ -1031,9 +1107,13 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
         hipLaunchKernelGGL((k_sgbm_vpath<N, L, LT, PF>), gv, dim3(64), 0, sv, a);   \
         v = true;                                                                    \
     }
-    SV_VPATH(16, 1, 16) SV_VPATH(16, 2, 16)
-    SV_VPATH(32, 2, 16) SV_VPATH(32, 4, 12) SV_VPATH(32, 6, 10) SV_VPATH(32, 8, 8) SV_VPATH(32, 10, 6)
-    SV_VPATH(32, 12, 4) SV_VPATH(32, 16, 3)
+    if (!vwta) {
+        SV_VPATH(16, 1, 16) SV_VPATH(16, 2, 16)
+        SV_VPATH(32, 2, 16) SV_VPATH(32, 4, 12) SV_VPATH(32, 6, 10) SV_VPATH(32, 8, 8) SV_VPATH(32, 10, 6)
+        SV_VPATH(32, 12, 4) SV_VPATH(32, 16, 3)
+    } else {
+        v = true;   // launched after the horizontal paths (below)
+    }
 #undef SV_VPATH
     if (aux && hipEventRecord(join, aux) != hipSuccess) return (int)hipErrorLaunchFailure;
 #define SV_HPATH(L, N, PF, WPE)                                                      \
@@ -1053,6 +1133,15 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
     SV_HPATH(16, 32, 4, 1)
 #undef SV_HPATH
     if (aux && hipStreamWaitEvent(s, join, 0) != hipSuccess) return (int)hipErrorLaunchFailure;
+    if (vwta) {
+#define SV_VWTA(N, PF)                                                                      \
+        if (!w && pv.dpl == N) {                                                            \
+            hipLaunchKernelGGL((k_sgbm_vpath_wta<N, 32, LT, PF>), gv, dim3(64), 0, s, a);   \
+            w = true;                                                                       \
+        }
+        SV_VWTA(2, 8) SV_VWTA(4, 6) SV_VWTA(6, 4) SV_VWTA(8, 3) SV_VWTA(10, 2) SV_VWTA(12, 2) SV_VWTA(16, 1)
+#undef SV_VWTA
+    }
     if (fused) {
         const dim3 gf((a.H + 3) / 4, 1, nf);
 #define SV_RLWTA(N, PF)                                                              \

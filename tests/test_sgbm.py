@@ -80,6 +80,9 @@ def test_gpu_sgbm_parameter_paths(engine, kw):
 def test_gpu_sgbm_int32_paths_window15(engine):
     L, R, _ = stereo_pair(40, 180, 32, seed=5)
     np.testing.assert_array_equal(engine.sgbm(L, R, 0, 32, 15), SG.sgbm(L, R, 0, 32, 15))
+    # D > 128: the vertical path fused with the WTA, on int32 path volumes
+    L, R, _ = stereo_pair(19, 330, 192, seed=6)
+    np.testing.assert_array_equal(engine.sgbm(L, R, 0, 192, 15), SG.sgbm(L, R, 0, 192, 15))
 
 
 @pytest.mark.gpu
@@ -198,6 +201,8 @@ def test_gpu_sgbm_tall_frames_row_bands(engine, H, W, D, win):
                                                 (9, 29, 133, 48, 15, -3),   # fused, int32 paths
                                                 (3, 29, 133, 48, 15, -3),   # unfused, int32
                                                 (2, 64, 200, 64, 9, 4),     # unfused
+                                                (3, 23, 430, 320, 7, 0),    # unfused, vertical path + WTA fused
+                                                (2, 17, 300, 160, 13, -2),  # unfused, vertical + WTA, int32
                                                 (8, 16, 380, 320, 7, 0),    # fused, DPL 20
                                                 (8, 12, 560, 512, 5, 0),    # fused, DPL 32
                                                 (8, 21, 90, 16, 3, 0),      # fused, DPL 1

@@ -319,7 +319,7 @@ int enqueue_sgbm(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int W, in
     const size_t kSgbmBudget = std::max(sgbm_budget(c->device) + held, per_frame);
     int chunk = (int)std::max<size_t>(1, std::min<size_t>({(size_t)nf, (size_t)kSgbmChunk,
                                                             kSgbmBudget / std::max<size_t>(per_frame, 1)}));
-    const bool fused = sv::sgbm_fused(chunk);
+    const bool fused = sv::sgbm_fused(chunk, num_disp);
     if (fused)   // no L_rl volume: a third more frames fit the budget
         chunk = (int)std::max<size_t>(1, std::min<size_t>({(size_t)nf, (size_t)kSgbmChunk,
                                                             kSgbmBudget / (per_frame - vol * lsz)}));

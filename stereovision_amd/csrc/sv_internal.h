@@ -192,11 +192,13 @@ struct SgbmArgs {
     }
 };
 int sgbm_dp(int D);   // per-pixel volume stride for D disparities, -1 if D > 512
-// Whether launches of nf frames fuse the R->L path with the WTA (k_sgbm_rl_wta, L_rl never
-// stored): batches of >= 8 frames, where the extra work per step hides behind other waves'
-// chains (one frame: both paths in k_sgbm_hpath, concurrent, then k_sgbm_wta).
-// SV_SGBM_FUSED=0 / 1 forces either form.
-bool sgbm_fused(int nf);
+// Whether launches of nf frames of D disparities fuse the R->L path with the WTA
+// (k_sgbm_rl_wta, L_rl never stored): batches of >= 8 frames with D <= 128, where the extra
+// work per step hides behind other waves' chains.  Otherwise both horizontal directions run
+// in k_sgbm_hpath, and for D > 128 the vertical path is fused with the WTA instead
+// (k_sgbm_vpath_wta, L_tb never stored; measured faster at every batch size there: D=320
+// 412 -> 459 frames/s at batch 8, 449 -> 491 at 16).  SV_SGBM_FUSED=0 / 1 forces either form.
+bool sgbm_fused(int nf, int D);
 // r <= 4: pixel cost and both window sums in one pass (k_sgbm_cost, no hsum
 // volume); SV_SGBM_COST=0 restores k_sgbm_hsum_tiled + k_sgbm_vsum8
 bool sgbm_cost_fused(int D, int r);

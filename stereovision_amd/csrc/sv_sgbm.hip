@@ -1177,12 +1177,10 @@ bool sgbm_cost_fused(int D, int r) {
     return !off && D >= 1 && D <= 512 && r <= 4;
 }
 
-bool sgbm_fused(int nf) {
-    static const int force = [] {
-        const char* e = std::getenv("SV_SGBM_FUSED");
-        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
-    }();
-    return force >= 0 ? force == 1 : nf >= 8;
+bool sgbm_fused(int nf, int D) {
+    const char* e = std::getenv("SV_SGBM_FUSED");   // read per call (tests switch it)
+    const int force = e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+    return force >= 0 ? force == 1 : (nf >= 8 && D <= 128);
 }
 
 int sgbm_dp(int D) {

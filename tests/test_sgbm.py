@@ -203,17 +203,21 @@ def test_gpu_sgbm_tall_frames_row_bands(engine, H, W, D, win):
                                                 (2, 64, 200, 64, 9, 4),     # unfused
                                                 (3, 23, 430, 320, 7, 0),    # unfused, vertical path + WTA fused
                                                 (2, 17, 300, 160, 13, -2),  # unfused, vertical + WTA, int32
-                                                (8, 16, 380, 320, 7, 0),    # fused, DPL 20
-                                                (8, 12, 560, 512, 5, 0),    # fused, DPL 32
+                                                (8, 16, 380, 320, 7, 0),    # DPL 20 (R->L fused when forced)
+                                                (8, 12, 560, 512, 5, 0),    # DPL 32 (forced)
                                                 (8, 21, 90, 16, 3, 0),      # fused, DPL 1
                                                 (8, 19, 230, 128, 9, -2),   # fused, DPL 8
-                                                (8, 14, 300, 192, 5, 0),    # fused, DPL 12
-                                                (8, 13, 330, 256, 7, 3),    # fused, DPL 16
-                                                (8, 11, 450, 384, 3, 0)])   # fused, DPL 24
-def test_gpu_sgbm_frame_batch(engine, nf, H, W, D, win, minD):
+                                                (8, 14, 300, 192, 5, 0),    # DPL 12 (forced)
+                                                (8, 13, 330, 256, 7, 3),    # DPL 16 (forced)
+                                                (8, 11, 450, 384, 3, 0)])   # DPL 24 (forced)
+@pytest.mark.parametrize("fused", ["auto", "1"])
+def test_gpu_sgbm_frame_batch(engine, monkeypatch, fused, nf, H, W, D, win, minD):
     """Frame batches (every SGBM stage and the speckle filter over grid.z; batches of >= 8
-    frames fuse the R->L path with the WTA): each frame of a pitched, strided stack bit-exact against the
-    oracle run on that frame alone."""
+    frames with D <= 128 fuse the R->L path with the WTA, D > 128 the vertical path; fused="1"
+    forces the R->L fusion, SV_SGBM_FUSED read per call): each frame of a pitched, strided
+    stack bit-exact against the oracle run on that frame alone."""
+    if fused != "auto":
+        monkeypatch.setenv("SV_SGBM_FUSED", fused)
     pitch, fs = W + 24, (H + 3) * (W + 24)
     Ls = np.zeros((nf, H + 3, pitch), np.uint8)
     Rs = np.zeros_like(Ls)

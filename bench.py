@@ -664,18 +664,21 @@ def main():
         glanes = [(engines, comms, depth[0], disp[0], norm[0]),
                   (engines2, comms2, arenas[0].alloc(4 * n_px * out_frames), arenas[0].alloc(4 * n_px * out_frames),
                    arenas[0].alloc(n_px * out_frames))]
-    # launched frames mode with the gather: every step's disparity maps (f32, the reference's
-    # returned disparity) go to rank 0 on a communication stream of their own, double-buffered,
-    # so step i's gather overlaps step i+1's kernels; rank 0 receives them into one stack per
-    # buffer (rank-major).  Event slots of `eng`: 2s = set s computed, 2s+1 = set s gathered.
+    # launched frames mode with the gather: every step's disparity maps go to rank 0 as int16
+    # x16 (OpenCV's fixed-point disparity, written by the median epilogue beside the f32 map,
+    # which is exactly it / 16: half the xGMI bytes of the f32 map) on a communication stream
+    # of their own, double-buffered, so step i's gather overlaps step i+1's kernels; rank 0
+    # receives them into one stack per buffer (rank-major).  Event slots of `eng`: 2s = set s
+    # computed, 2s+1 = set s gathered.
     gathered, ceng, cstream = None, None, 0
     if launched and gather_on:
         ceng = Engine(devices[0])
         cstream = ceng.stream
         all_engines.append(ceng)
-        gset = [(depth[0], disp[0], norm[0]),
-                (arenas[0].alloc(4 * n_px * B), arenas[0].alloc(4 * n_px * B), arenas[0].alloc(n_px * B))]
-        gathered = [arenas[0].alloc(4 * n_px * B * world) if rank == 0 else 0 for _ in range(2)]
+        gset = [(depth[0], disp[0], norm[0], arenas[0].alloc(2 * n_px * B)),
+                (arenas[0].alloc(4 * n_px * B), arenas[0].alloc(4 * n_px * B), arenas[0].alloc(n_px * B),
+                 arenas[0].alloc(2 * n_px * B))]
+        gathered = [arenas[0].alloc(2 * n_px * B * world) if rank == 0 else 0 for _ in range(2)]
     gather_wall = [0.0]
 
     def step(i):
@@ -707,11 +710,13 @@ def main():
                                     0, D, win, 0.3, 2.0, ldep, ldis, lnor, cost=args.cost)
             return
         engs, depth_o, disp_o, norm_o = lanes[i % nstreams]
+        med_o = 0
         if gathered is not None:   # double-buffered output sets; set s free once its gather ran
             gs = i % 2
             if i >= 2:
                 eng.stream_wait_event(2 * gs + 1, eng.stream)
             depth_o, disp_o, norm_o = [gset[gs][0]], [gset[gs][1]], [gset[gs][2]]
+            med_o = gset[gs][3]
         for k, e in enumerate(engs):
             if rectify:
                 for src, m1, m2, g in ((dL[k], m1l, m2l, gL), (dR[k], m1r, m2r, gR)):
@@ -720,12 +725,13 @@ def main():
                                 dst_frame_stride=n_px)
                 e.depth_map_batch_dev(gL, gR, B, H, W, W, n_px, 0, D, win, 0.3, 2.0, depth[k],
                                       disp[k], norm[k], cost=args.cost)
-            elif B == 1:
+            elif B == 1 and not med_o:
                 e.depth_map_dev(dL[k] + f * n_px, dR[k] + f * n_px, H, W, W, 0, D, win, 0.3, 2.0,
                                 depth_o[k], disp_o[k], norm_o[k], cost=args.cost)
             else:
                 e.depth_map_batch_dev(dL[k] + f * n_px, dR[k] + f * n_px, B, H, W, W, n_px, 0, D, win,
-                                      0.3, 2.0, depth_o[k], disp_o[k], norm_o[k], cost=args.cost)
+                                      0.3, 2.0, depth_o[k], disp_o[k], norm_o[k], cost=args.cost,
+                                      d_med16=med_o)
             if harris:      # one launch over the batch's left frames
                 e.harris_batch_dev(gL if rectify else dL[k] + f * n_px, B, H, W, W, n_px, hmaps[k])
         if gathered is not None:   # every rank's disparity maps -> rank 0 (RCCL over xGMI)
@@ -734,7 +740,7 @@ def main():
             eng.event_record(2 * gs, eng.stream)        # set gs computed
             eng.stream_wait_event(2 * gs, cstream)      # the gather follows it
             ceng.profile_region_begin("gather", cstream)
-            gather_frames(pg, gset[gs][1], B, gathered[gs], 4 * n_px, stream=cstream)
+            gather_frames(pg, gset[gs][3], B, gathered[gs], 2 * n_px, stream=cstream)
             ceng.profile_region_end(cstream)
             eng.event_record(2 * gs + 1, cstream)       # set gs free again
             gather_wall[0] += time.perf_counter() - t_g
@@ -864,9 +870,9 @@ def main():
                             Lz, Rz = hostL[0][f0 + z], hostR[0][f0 + z]
                         else:   # rank r's inputs, regenerated from its seed
                             Lz, Rz, _ = stereo_pair(H, W, D, seed=1000 * r + f0 + z)
+                        m16 = eng.to_host(gathered[last % 2] + 2 * n_px * (r * B + z), (H, W), np.int16)
                         ver.disparity(f"rank {r} frame {f0 + z} (gathered on rank 0)", Lz, Rz,
-                                      eng.to_host(gathered[last % 2] + 4 * n_px * (r * B + z), (H, W),
-                                                  np.float32))
+                                      m16.astype(np.float32) / np.float32(16.0))
         ok = ver.result()
         if pg is not None:
             ok = pg.allreduce_max(0.0 if ok else 1.0) == 0.0
@@ -952,14 +958,15 @@ def main():
                 gbytes += 9 * (b["r1"] - b["r0"]) * W
                 if band_inputs:
                     sbytes += 2 * (b["in1"] - b["in0"]) * W
-        elif gather_on:   # launched: the f32 disparity maps; one process: all three outputs
-            gbytes = (4 if launched else 9) * n_px * B * (ngpu - 1)
+        elif gather_on:   # launched: the int16 x16 disparity maps; one process: all three outputs
+            gbytes = (2 if launched else 9) * n_px * B * (ngpu - 1)
     dist = dist_summary(ngpu, launched, pg, comms, gather=gather_on, rowtile=rowtile,
                         gather_ms=gath_ms, gather_n=gath_n, scatter_ms=scat_ms, scatter_n=scat_n,
                         gather_wall_s=gather_wall[0], steps=args.steps, gather_bytes=gbytes,
                         scatter_bytes=sbytes, reason=comm_reason,
                         gathered_maps=("rows of depth f32 + disparity f32 + depth u8" if rowtile else
-                                       "disparity f32 of every frame, overlapped with the next step "
+                                       "disparity of every frame as int16 x16 (OpenCV's fixed point; the "
+                                       "f32 map is it / 16 exactly), overlapped with the next step "
                                        "(communication stream, double-buffered maps)" if launched else
                                        "depth f32 + disparity f32 + depth u8 of every frame, two "
                                        "context lanes so a step's gather overlaps the next step")

@@ -238,6 +238,16 @@ int sv_depth_map_batch_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_
                            int min_disp, int num_disp, int win, int cost, float min_depth,
                            float max_depth, float depth_range, float min_disp_global,
                            float* d_depth, float* d_disparity, uint8_t* d_norm, void* stream);
+/* sv_depth_map_batch_dev that also writes each frame's median map as int16 x16 (OpenCV's
+ * fixed-point disparity, the value the reference divides by 16 at depth_map.py:909, so
+ * d_disparity = d_med16 / 16 exactly) into d_med16 (dense per frame; NULL: not written) —
+ * half the bytes of the f32 map for a gather over xGMI. */
+int sv_depth_map_batch_m16_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
+                               int n_frames, int H, int W, int pitch, int64_t frame_stride,
+                               int min_disp, int num_disp, int win, int cost, float min_depth,
+                               float max_depth, float depth_range, float min_disp_global,
+                               float* d_depth, float* d_disparity, uint8_t* d_norm,
+                               int16_t* d_med16, void* stream);
 
 /* Frame-sharded batch over several devices from ONE host process:
  * replaces the reference's per-frame loop over create_depth_map (depth_map.py:837-946,

@@ -925,6 +925,16 @@ int sv_depth_map_batch_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_ri
                            int pitch, int64_t frame_stride, int min_disp, int num_disp, int win, int cost,
                            float min_depth, float max_depth, float depth_range, float min_disp_global,
                            float* d_depth, float* d_disparity, uint8_t* d_norm, void* stream) {
+    return sv_depth_map_batch_m16_dev(c, d_left, d_right, n_frames, H, W, pitch, frame_stride, min_disp, num_disp,
+                                      win, cost, min_depth, max_depth, depth_range, min_disp_global, d_depth,
+                                      d_disparity, d_norm, nullptr, stream);
+}
+
+int sv_depth_map_batch_m16_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, int n_frames, int H,
+                               int W, int pitch, int64_t frame_stride, int min_disp, int num_disp, int win,
+                               int cost, float min_depth, float max_depth, float depth_range,
+                               float min_disp_global, float* d_depth, float* d_disparity, uint8_t* d_norm,
+                               int16_t* d_med16, void* stream) {
     SV_ENTER(c);
     if (check_image(d_left, H, W) || check_image(d_right, H, W) || !d_depth || !d_disparity || !d_norm ||
         n_frames < 0)
@@ -943,6 +953,7 @@ int sv_depth_map_batch_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_ri
                                   num_disp, d_depth, d_norm, nullptr);
     rc = attach_lut(c, pp, s);
     if (rc) return rc;
+    pp.out_m16 = d_med16;   // nullable: the int16 x16 medians beside the f32 disparity
     SV_LAUNCH(c, SV_K_MEDIAN, s,
               sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, d_disparity, pp, s, n_frames, fs, fs));
     return 0;

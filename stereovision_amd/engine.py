@@ -36,7 +36,7 @@ EXPORTED = [
     "sv_depth_map_dev", "sv_harris_dev", "sv_hog_hist_dev", "sv_profile_enable",
     "sv_profile_read", "sv_profile_reset", "sv_disparity_rows", "sv_dev_alloc", "sv_dev_free",
     "sv_copy_to_device", "sv_copy_to_host", "sv_host_register", "sv_host_unregister", "sv_timer_begin", "sv_timer_end", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
-    "sv_depth_map_batch_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
+    "sv_depth_map_batch_dev", "sv_depth_map_batch_m16_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
     "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
     "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
     "sv_select_ranks", "sv_affine_f32_dev", "sv_sgbm", "sv_sgbm_dev", "sv_filter_speckles",
@@ -186,6 +186,10 @@ def _declare(lib):
         "sv_depth_map_batch_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
                                     ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
                                     _c_float, _c_float, _c_float, _vp, _vp, _vp, _vp], _c_int),
+        "sv_depth_map_batch_m16_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
+                                        ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                        _c_float, _c_float, _c_float, _vp, _vp, _vp, _vp, _vp],
+                                       _c_int),
         "sv_init_undistort_rectify_map": ([_vp, _f64p, _NullableF64, _c_int, _NullableF64,
                                            _NullableF64, _c_int, _c_int, _c_int, _i16p, _u16p],
                                           _c_int),
@@ -758,13 +762,18 @@ class Engine:
                             pitch: int, frame_stride: int, min_disp: int, num_disp: int,
                             win: int, min_depth: float, max_depth: float, d_depth: int,
                             d_disp: int, d_norm: int, cost="sad", min_disp_global=None,
-                            stream: int = 0):
+                            stream: int = 0, d_med16: int = 0):
+        """d_med16 (optional): also the int16 x16 median maps (d_disp = d_med16 / 16 exactly)."""
         mdg = min_disp if min_disp_global is None else min_disp_global
-        _check("sv_depth_map_batch_dev", self.lib.sv_depth_map_batch_dev(
-            self._h, d_left, d_right, int(n_frames), H, W, pitch, int(frame_stride),
-            int(min_disp), int(num_disp), int(win), _cost(cost), np.float32(min_depth),
-            np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
-            np.float32(mdg), d_depth, d_disp, d_norm, stream or None))
+        args = (self._h, d_left, d_right, int(n_frames), H, W, pitch, int(frame_stride),
+                int(min_disp), int(num_disp), int(win), _cost(cost), np.float32(min_depth),
+                np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
+                np.float32(mdg), d_depth, d_disp, d_norm)
+        if d_med16:
+            _check("sv_depth_map_batch_m16_dev",
+                   self.lib.sv_depth_map_batch_m16_dev(*args, d_med16, stream or None))
+        else:
+            _check("sv_depth_map_batch_dev", self.lib.sv_depth_map_batch_dev(*args, stream or None))
 
     def harris_batch_dev(self, d_gray: int, n_frames: int, H: int, W: int, pitch: int,
                          frame_stride: int, d_out: int, stream: int = 0):

@@ -628,3 +628,34 @@ def test_host_path_row_bands_match_oracle(engine, monkeypatch, bands, H, W, D, w
         np.testing.assert_array_equal(depth, e_depth, err_msg=f"call {it}")
         np.testing.assert_array_equal(norm, e_norm, err_msg=f"call {it}")
         del depth, disp, norm
+
+
+def test_depth_map_batch_int16_medians(engine):
+    """sv_depth_map_batch_m16_dev: the int16 x16 median maps beside the f32 outputs (the
+    multi-GPU bench gathers these): med16 / 16 == the f32 disparity, both == the oracle."""
+    nf, H, W, D = 3, 70, 300, 64
+    Ls, Rs = [], []
+    for z in range(nf):
+        L, R, _ = stereo_pair(H, W, D, seed=70 + z)
+        Ls.append(L)
+        Rs.append(R)
+    L, R = np.stack(Ls), np.stack(Rs)
+    n = H * W
+    dL, dR = engine.dev_alloc(L.nbytes), engine.dev_alloc(R.nbytes)
+    bufs = [engine.dev_alloc(4 * n * nf), engine.dev_alloc(4 * n * nf), engine.dev_alloc(n * nf),
+            engine.dev_alloc(2 * n * nf)]
+    try:
+        engine.to_device(dL, L)
+        engine.to_device(dR, R)
+        engine.depth_map_batch_dev(dL, dR, nf, H, W, W, n, 0, D, 9, 0.3, 2.0, bufs[0], bufs[1], bufs[2],
+                                   d_med16=bufs[3])
+        engine.synchronize()
+        disp = engine.to_host(bufs[1], (nf, H, W), np.float32)
+        med = engine.to_host(bufs[3], (nf, H, W), np.int16)
+        np.testing.assert_array_equal(med.astype(np.float32) / np.float32(16.0), disp)
+        for z in range(nf):
+            _, e_disp, _ = C.depth_map(L[z], R[z], 0, D, 9)
+            np.testing.assert_array_equal(disp[z], e_disp)
+    finally:
+        for p in [dL, dR] + bufs:
+            engine.dev_free(p)

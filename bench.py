@@ -913,7 +913,11 @@ def main():
         insts = pmc.get("SQ_INSTS_VALU")
         fetch = pmc.get("FETCH_SIZE")
         write = pmc.get("WRITE_SIZE")
-        traffic = round((fetch + write) * 1024) if fetch is not None and write is not None else None
+        # gfx950: FETCH_SIZE tallies 128-B fabric reads at 64 B (MI355X_MICROARCH.md, HBM /
+        # rocprofv3): x2.  Calibrated on k_match's own dword reads: with the XCD tile order
+        # every input byte is fetched once, and FETCH_SIZE reads 0.49 x the 66.4 MB of input
+        traffic = (round((2 * fetch + write) * 1024) if fetch is not None and write is not None
+                   else None)
         roofline = {
             # bound: what limits the kernel (VALU issue); achieved/peak/frac stay
             # the contract's HBM figures (algorithmic bytes by SURVEY.md §8(d)), the VALU
@@ -940,9 +944,11 @@ def main():
                      "cells_per_s": round(npx * D / k_avg_s)},
             "pmc": {"source": "rocprofv3 --pmc, 3 separate passes over a 6-step child run of this "
                               "script on this box (mean per k_match dispatch)",
-                    "traffic_note": "FETCH_SIZE + WRITE_SIZE (KiB x 1024), uncorrected: the gfx950 "
-                                    "x2 FETCH correction applies to 16-B/lane streaming reads; "
-                                    "k_match reads dwords",
+                    "traffic_note": "traffic = 2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024): the guide's "
+                                    "gfx950 x2 FETCH correction, calibrated on k_match's own reads "
+                                    "(XCD tile order: each input byte fetched once = 2 x FETCH_SIZE); "
+                                    "inputs stay resident in the 256 MB Infinity Cache, whose hits "
+                                    "the counter includes",
                     **{k: (round(v, 1) if isinstance(v, float) else v) for k, v in pmc.items()}},
             "median_post_avg_us": round(med_ms / med_n * 1e3, 2) if med_n else None,
         }

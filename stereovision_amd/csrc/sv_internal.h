@@ -58,6 +58,7 @@ struct MatchParams {
     // the kernel's last wave resets them), so concurrent launches on other contexts never
     // share one
     unsigned* work_ctr;
+    int xcd_map;           // ring kind: XCD-aware tile order (launch_ring_rl)
 };
 
 // Host-side launchers (return hipError_t as int).

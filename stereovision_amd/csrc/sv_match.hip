@@ -811,10 +811,30 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     constexpr bool PK = R >= 6;
     static_assert(P::SPLIT && (P::CW == 2) != PK, "ring kind expects split packs (24 B; 32 B for r 6..7)");
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    if (blockIdx.z) {   // frame batch
-        a.L += blockIdx.z * a.fs_in;
-        a.R += blockIdx.z * a.fs_in;
-        a.out += blockIdx.z * a.fs_out;
+    // XCD-aware tile order: workgroups are dealt to the 8 XCDs round-robin in dispatch order,
+    // so tile T = lin (row-major x, then row quad, then frame) put horizontal and vertical
+    // neighbours (which share 2r of their 2r+4 input rows and most right-image columns) on
+    // different L2s.  With a.xcd_map, XCD x takes the contiguous tile range [x*N/8, (x+1)*N/8):
+    // its co-resident waves are neighbours and their overlapping reads hit its L2.
+    int bx, by, bz;
+    {
+        const unsigned nx = gridDim.x, ny = gridDim.y;
+        const unsigned n = nx * ny * gridDim.z;
+        const unsigned lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+        unsigned t = lin;
+        if (a.xcd_map) {
+            const unsigned per = n >> 3, rem = n & 7u, xcd = lin & 7u, k = lin >> 3;
+            t = xcd * per + min(xcd, rem) + k;
+        }
+        // wave-uniform: keep every address derived from them in SGPRs
+        bx = __builtin_amdgcn_readfirstlane((int)(t % nx));
+        by = __builtin_amdgcn_readfirstlane((int)((t / nx) % ny));
+        bz = __builtin_amdgcn_readfirstlane((int)(t / (nx * ny)));
+    }
+    if (bz) {   // frame batch
+        a.L += bz * a.fs_in;
+        a.R += bz * a.fs_in;
+        a.out += bz * a.fs_out;
     }
     const int lane = threadIdx.x;
     constexpr int LPG = LPGT;                           // lanes per group (template: no
@@ -838,14 +858,14 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     const PackPtr<COST_SAD4, R> Lp{Lw.x, Lw.c};
     const PackPtr<COST_SAD4, R> Rp{Rw.x, Rw.c};
 
-    const int y = a.row0 + (int)blockIdx.y * 4;
+    const int y = a.row0 + by * 4;
     const int yc = min(y, a.row1 - 1);
-    const int xw = a.X0 + (int)blockIdx.x * WC;
+    const int xw = a.X0 + bx * WC;
     const int cL0 = xw - R;                             // L index i -> column cL0 + i
     const int cR0 = cL0 - a.minD - (4 * LPG - 1);       // R index i -> column cR0 + i
     build_all_packs<COST_SAD4, R, RG_DPL>(a, yc, cL0, NL, cR0, NRlog, c0, Lw, Rw, lane);
 
-    if (blockIdx.x == 0) {  // columns outside the matched band are invalid
+    if (bx == 0) {  // columns outside the matched band are invalid
         const int16_t inv = (int16_t)((a.minD - 1) * 16);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1193,7 +1213,14 @@ int launch_ring_rl(const MatchParams& a, size_t lds, hipStream_t s) {
     }
     const int wc = (64 / a.lpg) * a.segm;
     dim3 grid((a.X1 - a.X0 + wc - 1) / wc, (a.row1 - a.row0 + 3) / 4, a.nf > 1 ? a.nf : 1);
-    hipLaunchKernelGGL(fn, grid, dim3(64), lds, s, a);
+    // SV_XCD_MAP=0 (A/B): tiles in plain dispatch order
+    static const bool xcd = [] {
+        const char* e = std::getenv("SV_XCD_MAP");
+        return !(e && e[0] == '0');
+    }();
+    MatchParams b = a;
+    b.xcd_map = xcd ? 1 : 0;
+    hipLaunchKernelGGL(fn, grid, dim3(64), lds, s, b);
     return (int)hipGetLastError();
 }
 template <int R>

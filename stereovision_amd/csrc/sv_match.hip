@@ -31,6 +31,7 @@
 //   SSD   v_dot4_u32_u8: sum (L-R)^2 = sum L^2 + sum R^2 - 2 sum L*R (squares per pack);
 //   HOG   9-bin u16 window histograms as packs compared with v_sad_u16 (no running window).
 #include "sv_internal.h"
+#include "sv_xcd.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -811,26 +812,10 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     constexpr bool PK = R >= 6;
     static_assert(P::SPLIT && (P::CW == 2) != PK, "ring kind expects split packs (24 B; 32 B for r 6..7)");
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    // XCD-aware tile order: workgroups are dealt to the 8 XCDs round-robin in dispatch order,
-    // so tile T = lin (row-major x, then row quad, then frame) put horizontal and vertical
-    // neighbours (which share 2r of their 2r+4 input rows and most right-image columns) on
-    // different L2s.  With a.xcd_map, XCD x takes the contiguous tile range [x*N/8, (x+1)*N/8):
-    // its co-resident waves are neighbours and their overlapping reads hit its L2.
+    // XCD-aware tile order (sv_xcd.h): horizontal and vertical neighbours share 2r of their
+    // 2r+4 input rows and most right-image columns; each XCD takes a contiguous tile range
     int bx, by, bz;
-    {
-        const unsigned nx = gridDim.x, ny = gridDim.y;
-        const unsigned n = nx * ny * gridDim.z;
-        const unsigned lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
-        unsigned t = lin;
-        if (a.xcd_map) {
-            const unsigned per = n >> 3, rem = n & 7u, xcd = lin & 7u, k = lin >> 3;
-            t = xcd * per + min(xcd, rem) + k;
-        }
-        // wave-uniform: keep every address derived from them in SGPRs
-        bx = __builtin_amdgcn_readfirstlane((int)(t % nx));
-        by = __builtin_amdgcn_readfirstlane((int)((t / nx) % ny));
-        bz = __builtin_amdgcn_readfirstlane((int)(t / (nx * ny)));
-    }
+    xcd_tile(a.xcd_map != 0, bx, by, bz);
     if (bz) {   // frame batch
         a.L += bz * a.fs_in;
         a.R += bz * a.fs_in;

@@ -106,6 +106,88 @@ __global__ __launch_bounds__(256) void k_harris_lds(const uint8_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------
+// Harris, register/DPP form (the default for W, H >= 8): one wave = 64 consecutive columns
+// (lane j <-> column x0 - 2 + j, 60 outputs for lanes 2..61) walking down a band of HB output
+// rows (PF image rows prefetched); no LDS, no barriers.  Per product row a lane loads ONE image byte (its column of the
+// next row, reflect-101), its left/right neighbours come by wave_shr/wave_shl DPP: the Sobel
+// column sums and row smooths, the 3 gradient products, their vertical 3-row sums from a
+// register ring and the horizontal 3-sums by DPP again; coalesced f32 stores.  Reflect-101
+// of the PRODUCT images (cv2.cornerHarris box-filters the products with reflect-101) falls
+// out of computing every product from reflect-101 pixels, except the cross product's sign:
+// outside the image gx (row) or gy (column) flips, so gxy is negated once per dimension in
+// which the position lies outside (gxx, gyy are even).  Sums are exact integers; the float
+// epilogue is the LDS kernel's, so outputs are identical.
+template <int HB, int PF>
+__global__ __launch_bounds__(64) void k_harris_dpp(const uint8_t* __restrict__ g, int H, int W, int pitch,
+                                                   float* __restrict__ out, long long fs_in, long long fs_out) {
+    g += blockIdx.z * fs_in;
+    out += blockIdx.z * fs_out;
+    const int lane = threadIdx.x;
+    const int x0 = blockIdx.x * 60, y0 = blockIdx.y * HB;
+    const int c = x0 - 2 + lane;
+    const int cc = refl101(clampi(c, -2, W + 1), W);              // loaded column
+    const int csign = (c < 0 || c >= W) ? -1 : 1;                  // gxy sign outside the image
+    const bool emit = lane >= 2 && lane < 62 && c < W;
+    auto ldrow = [&](int r) -> int {   // image row r (reflect-101), this lane's column
+        return (int)g[(size_t)refl101(clampi(r, -2, H + 1), H) * pitch + cc];
+    };
+    // lane j-1 / j+1 through a plain v_mov_b32_dpp wave_shr/shl:1 kept unfolded: folded into
+    // an ALU op (v_subrev_u32_dpp ... wave_shr:1 bound_ctrl:1, what the compiler emits for
+    // old = 0) the wave shifts read 0 on every lane on gfx950 (tools/microbench/dpp_check)
+    auto shr1 = [](int v) {
+        int t = __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false);
+        asm volatile("" : "+v"(t));
+        return t;
+    };
+    auto shl1 = [](int v) {
+        int t = __builtin_amdgcn_update_dpp(v, v, 0x130, 0xF, 0xF, false);
+        asm volatile("" : "+v"(t));
+        return t;
+    };
+    auto rowsm = [&](int v) { return shr1(v) + 2 * v + shl1(v); };
+    const float s2 = (float)((1.0 / (4.0 * 3.0 * 255.0)) * (1.0 / (4.0 * 3.0 * 255.0)));
+    // product rows y0-1 .. y0+HB; image rows y0-2 .. y0+HB+1
+    // PF image rows in flight ahead of the one being used (the loads are one byte per lane:
+    // latency, not bandwidth, is what they cost)
+    int im = ldrow(y0 - 2), ic = ldrow(y0 - 1);
+    int pre[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) pre[k] = ldrow(y0 + k);
+    int rsm = rowsm(im), rsc = rowsm(ic);
+    int pxx[3] = {0, 0, 0}, pxy[3] = {0, 0, 0}, pyy[3] = {0, 0, 0};
+    const int rend = min(y0 + HB, H);                               // last output row + 1
+    for (int r = y0 - 1; r <= rend; ++r) {
+        const int ip = pre[0];
+#pragma unroll
+        for (int k = 0; k + 1 < PF; ++k) pre[k] = pre[k + 1];
+        pre[PF - 1] = ldrow(r + 1 + PF);
+        const int rsp = rowsm(ip);
+        const int col = im + 2 * ic + ip;
+        const int gx = shl1(col) - shr1(col);
+        const int gy = rsp - rsm;
+        const int rsign = (r < 0 || r >= H) ? -csign : csign;
+        pxx[0] = pxx[1]; pxx[1] = pxx[2]; pxx[2] = __mul24(gx, gx);
+        pyy[0] = pyy[1]; pyy[1] = pyy[2]; pyy[2] = __mul24(gy, gy);
+        pxy[0] = pxy[1]; pxy[1] = pxy[2]; pxy[2] = rsign * __mul24(gx, gy);
+        im = ic;
+        ic = ip;
+        rsm = rsc;
+        rsc = rsp;
+        if (r >= y0 + 1) {   // output row r - 1 from product rows r-2 .. r
+            const int vxx = pxx[0] + pxx[1] + pxx[2], vxy = pxy[0] + pxy[1] + pxy[2], vyy = pyy[0] + pyy[1] + pyy[2];
+            const int sxx = shr1(vxx) + vxx + shl1(vxx);
+            const int sxy = shr1(vxy) + vxy + shl1(vxy);
+            const int syy = shr1(vyy) + vyy + shl1(vyy);
+            const float a = (float)sxx * s2, b = (float)sxy * s2, cf = (float)syy * s2;
+            const float t1 = a * cf, t2 = b * b, t3 = a + cf, t4 = t3 * t3;
+            const float rr = t1 - t2;
+            const float kt = 0.04f * t4;
+            if (emit) out[(size_t)(r - 1) * W + c] = rr - kt;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // HOG window histograms: 64x16 output tile, window radius r <= 7.
 constexpr int GT_W = 64, GT_H = 16, GR_MAX = 7;
 constexpr int GX_MAX = GT_W + 2 * GR_MAX, GY_MAX = GT_H + 2 * GR_MAX;
@@ -677,6 +759,28 @@ int launch_gray(const uint8_t* bgr, int H, int W, int pitch, uint8_t* gray, hipS
 int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStream_t s, int nf,
                   long long fs_in, long long fs_out) {
     if (nf <= 0) return 0;
+    // SV_HARRIS=lds (A/B): the LDS-tile kernel everywhere; it also serves images under 8 px
+    static const bool lds = [] {
+        const char* e = std::getenv("SV_HARRIS");
+        return e && e[0] == 'l';
+    }();
+    if (!lds && W >= 8 && H >= 8) {
+        // SV_HARRIS_HB (A/B): output rows per wave
+        static const int hb = [] {
+            const char* e = std::getenv("SV_HARRIS_HB");
+            const int v = e ? std::atoi(e) : 8;
+            return v == 16 || v == 32 ? v : 8;
+        }();
+#define SV_HARRIS_L(HB, PF)                                                                                    \
+        hipLaunchKernelGGL((k_harris_dpp<HB, PF>), dim3((W + 59) / 60, (H + HB - 1) / HB, nf), dim3(64), 0, s, g, \
+                           H, W, pitch, out, fs_in, fs_out)
+        // 8 rows: C2 16.8 us per 16 VGA frames (16: 17.7, 32: 21.0; 1080p 99 / 98 / 105 us)
+        if (hb == 16) SV_HARRIS_L(16, 4);
+        else if (hb == 32) SV_HARRIS_L(32, 4);
+        else SV_HARRIS_L(8, 4);
+#undef SV_HARRIS_L
+        return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(k_harris_lds, dim3((W + HX2 - 1) / HX2, (H + HY2 - 1) / HY2, nf), dim3(256), 0, s, g,
                        H, W, pitch, out, fs_in, fs_out);
     return (int)hipGetLastError();

@@ -11,6 +11,7 @@
 // All are HBM-bound stencils: LDS tiles with halos, one read and one write per pixel.
 // Built with -ffp-contract=off so every f32 operation rounds exactly like NumPy's.
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include "sv_internal.h"
 #include "sv_median_net.h"
@@ -183,6 +184,138 @@ __global__ __launch_bounds__(64) void k_harris_dpp(const uint8_t* __restrict__ g
             const float rr = t1 - t2;
             const float kt = 0.04f * t4;
             if (emit) out[(size_t)(r - 1) * W + c] = rr - kt;
+        }
+    }
+}
+
+// Harris, 4 columns per lane (the default for W >= 1024; any W >= 256 works): lane j holds columns x0-4+4j ..
+// x0-1+4j as one dword per image row (interior waves: one aligned dword load per lane-row;
+// waves touching an image border or unaligned rows assemble it from 4 reflect-101 byte
+// loads), the lane's first/last neighbours come by wave_shr/shl:1 DPP; 248 output columns
+// per wave (lanes 1..62), f32x4 stores.  Same arithmetic, same reflect-101 product rule and
+// the same float epilogue as k_harris_dpp: bit-identical outputs.
+__device__ __forceinline__ int dpp_shr1_keep(int v) {   // lane j-1 (lane 0 keeps its own)
+    int t = __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false);
+    asm volatile("" : "+v"(t));
+    return t;
+}
+__device__ __forceinline__ int dpp_shl1_keep(int v) {   // lane j+1 (lane 63 keeps its own)
+    int t = __builtin_amdgcn_update_dpp(v, v, 0x130, 0xF, 0xF, false);
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
+template <int HB, int PF>
+__global__ __launch_bounds__(64) void k_harris_dpp4(const uint8_t* __restrict__ g, int H, int W, int pitch,
+                                                    float* __restrict__ out, long long fs_in, long long fs_out) {
+    g += blockIdx.z * fs_in;
+    out += blockIdx.z * fs_out;
+    const int lane = threadIdx.x;
+    const int x0 = blockIdx.x * 248, y0 = blockIdx.y * HB;
+    const int c0 = x0 - 4 + 4 * lane;                               // first column of the lane
+    // interior: every lane's 4 columns inside the image and dword-aligned rows (uniform)
+    const bool fast = x0 >= 4 && x0 + 252 <= W && ((pitch & 3) == 0) && ((((uintptr_t)g) & 3) == 0);
+    int cc[4], csg[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = c0 + i;
+        cc[i] = refl101(clampi(c, -2, W + 1), W);
+        csg[i] = (c < 0 || c >= W) ? -1 : 1;
+    }
+    auto ldrow = [&](int r) -> uint32_t {   // image row r (reflect-101), the lane's 4 columns
+        const uint8_t* row = g + (size_t)refl101(clampi(r, -2, H + 1), H) * pitch;
+        if (fast) return *reinterpret_cast<const uint32_t*>(row + c0);
+        return (uint32_t)row[cc[0]] | ((uint32_t)row[cc[1]] << 8) | ((uint32_t)row[cc[2]] << 16) |
+               ((uint32_t)row[cc[3]] << 24);
+    };
+    auto unpack = [](uint32_t w, int (&p)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p[i] = (int)((w >> (8 * i)) & 0xffu);
+    };
+    // row smooth p[i-1] + 2 p[i] + p[i+1] of the lane's 4 columns (neighbour bytes by DPP)
+    auto rowsm4 = [&](uint32_t w, int (&o)[4]) {
+        int p[4];
+        unpack(w, p);
+        const int lft = (int)(((uint32_t)dpp_shr1_keep((int)w)) >> 24);
+        const int rgt = (int)(((uint32_t)dpp_shl1_keep((int)w)) & 0xffu);
+        o[0] = lft + 2 * p[0] + p[1];
+        o[1] = p[0] + 2 * p[1] + p[2];
+        o[2] = p[1] + 2 * p[2] + p[3];
+        o[3] = p[2] + 2 * p[3] + rgt;
+    };
+    const float s2 = (float)((1.0 / (4.0 * 3.0 * 255.0)) * (1.0 / (4.0 * 3.0 * 255.0)));
+    int im[4], ic[4], rsm[4], rsc[4];
+    {
+        const uint32_t wm = ldrow(y0 - 2), wc = ldrow(y0 - 1);
+        unpack(wm, im);
+        unpack(wc, ic);
+        rowsm4(wm, rsm);
+        rowsm4(wc, rsc);
+    }
+    uint32_t pre[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) pre[k] = ldrow(y0 + k);
+    int pxx[3][4] = {}, pxy[3][4] = {}, pyy[3][4] = {};
+    const int rend = min(y0 + HB, H);
+    const bool emit_lane = lane >= 1 && lane < 63;
+    for (int r = y0 - 1; r <= rend; ++r) {
+        const uint32_t wp = pre[0];
+#pragma unroll
+        for (int k = 0; k + 1 < PF; ++k) pre[k] = pre[k + 1];
+        pre[PF - 1] = ldrow(r + 1 + PF);
+        int ip[4], rsp[4], col[4];
+        unpack(wp, ip);
+        rowsm4(wp, rsp);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) col[i] = im[i] + 2 * ic[i] + ip[i];
+        const int cl = dpp_shr1_keep(col[3]), cr = dpp_shl1_keep(col[0]);
+        const bool rout = r < 0 || r >= H;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int gx = (i < 3 ? col[i + 1] : cr) - (i > 0 ? col[i - 1] : cl);
+            const int gy = rsp[i] - rsm[i];
+            const int sg = rout ? -csg[i] : csg[i];
+            pxx[0][i] = pxx[1][i]; pxx[1][i] = pxx[2][i]; pxx[2][i] = __mul24(gx, gx);
+            pyy[0][i] = pyy[1][i]; pyy[1][i] = pyy[2][i]; pyy[2][i] = __mul24(gy, gy);
+            pxy[0][i] = pxy[1][i]; pxy[1][i] = pxy[2][i]; pxy[2][i] = sg * __mul24(gx, gy);
+            im[i] = ic[i];
+            ic[i] = ip[i];
+            rsm[i] = rsc[i];
+            rsc[i] = rsp[i];
+        }
+        if (r >= y0 + 1) {   // output row r - 1
+            int vxx[4], vxy[4], vyy[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                vxx[i] = pxx[0][i] + pxx[1][i] + pxx[2][i];
+                vxy[i] = pxy[0][i] + pxy[1][i] + pxy[2][i];
+                vyy[i] = pyy[0][i] + pyy[1][i] + pyy[2][i];
+            }
+            const int lxx = dpp_shr1_keep(vxx[3]), rxx = dpp_shl1_keep(vxx[0]);
+            const int lxy = dpp_shr1_keep(vxy[3]), rxy = dpp_shl1_keep(vxy[0]);
+            const int lyy = dpp_shr1_keep(vyy[3]), ryy = dpp_shl1_keep(vyy[0]);
+            float o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int sxx = (i > 0 ? vxx[i - 1] : lxx) + vxx[i] + (i < 3 ? vxx[i + 1] : rxx);
+                const int sxy = (i > 0 ? vxy[i - 1] : lxy) + vxy[i] + (i < 3 ? vxy[i + 1] : rxy);
+                const int syy = (i > 0 ? vyy[i - 1] : lyy) + vyy[i] + (i < 3 ? vyy[i + 1] : ryy);
+                const float a = (float)sxx * s2, b = (float)sxy * s2, cf = (float)syy * s2;
+                const float t1 = a * cf, t2 = b * b, t3 = a + cf, t4 = t3 * t3;
+                const float rr = t1 - t2;
+                const float kt = 0.04f * t4;
+                o[i] = rr - kt;
+            }
+            if (emit_lane) {
+                float* orow = out + (size_t)(r - 1) * W;
+                if (c0 + 3 < W && ((W & 3) == 0) && ((((uintptr_t)out) & 15) == 0)) {
+                    *reinterpret_cast<float4*>(orow + c0) = make_float4(o[0], o[1], o[2], o[3]);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (c0 + i >= 0 && c0 + i < W) orow[c0 + i] = o[i];
+                }
+            }
         }
     }
 }
@@ -775,6 +908,18 @@ int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStre
         hipLaunchKernelGGL((k_harris_dpp<HB, PF>), dim3((W + 59) / 60, (H + HB - 1) / HB, nf), dim3(64), 0, s, g, \
                            H, W, pitch, out, fs_in, fs_out)
         // 8 rows: C2 16.8 us per 16 VGA frames (16: 17.7, 32: 21.0; 1080p 99 / 98 / 105 us)
+        // SV_HARRIS=dpp1 (A/B): one column per lane everywhere
+        static const bool one = [] {
+            const char* e = std::getenv("SV_HARRIS");
+            return e && std::strcmp(e, "dpp1") == 0;
+        }();
+        // 4 columns per lane from 1024 columns (1080p: 91.6 vs 98.6 us per 16 frames); narrower
+        // frames keep 1 per lane (VGA: 16.7 vs 21.6 us — a quarter of the waves hides less latency)
+        if (!one && W >= 1024) {
+            hipLaunchKernelGGL((k_harris_dpp4<8, 4>), dim3((W + 247) / 248, (H + 7) / 8, nf), dim3(64), 0, s, g, H, W,
+                               pitch, out, fs_in, fs_out);
+            return (int)hipGetLastError();
+        }
         if (hb == 16) SV_HARRIS_L(16, 4);
         else if (hb == 32) SV_HARRIS_L(32, 4);
         else SV_HARRIS_L(8, 4);

@@ -662,14 +662,17 @@ def test_depth_map_batch_int16_medians(engine):
 
 
 def test_harris_dpp_kernel_equals_lds_kernel():
-    """k_harris_dpp (wave = 64 columns walking a 16-row band, DPP neighbours, reflect-101 of
-    the product images through the cross product's sign) gives the same bytes as the LDS-tile
-    kernel (SV_HARRIS=lds, in a child), at tile / band edges and tiny sizes, and both are
-    within the north_star tolerance of the oracle."""
+    """k_harris_dpp4 (4 columns per lane, W >= 1024) and k_harris_dpp (1 column per lane;
+    SV_HARRIS=dpp1) — waves walking row bands, DPP neighbours, reflect-101 of the product
+    images through the cross product's sign — give the same bytes as the LDS-tile kernel
+    (SV_HARRIS=lds), each in a child, at tile / band edges, unaligned widths and tiny sizes,
+    and all are within the north_star tolerance of the oracle."""
     import os
     import subprocess
     import sys
-    sizes = [(8, 8), (9, 61), (16, 60), (17, 120), (31, 121), (33, 179), (480, 640), (70, 333)]
+    sizes = [(8, 8), (9, 61), (16, 60), (17, 120), (31, 121), (33, 179), (480, 640), (70, 333),
+             (9, 256), (13, 258), (33, 500), (17, 1023), (20, 1024), (24, 1920), (11, 1030),
+             (19, 1027)]
     code = ("import sys, numpy as np; sys.path.insert(0, %r)\n"
             "from stereovision_amd.engine import get_engine\n"
             "e = get_engine(0)\n"
@@ -678,12 +681,12 @@ def test_harris_dpp_kernel_equals_lds_kernel():
             "    sys.stdout.buffer.write(e.harris(g).tobytes())\n") % (
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), sizes)
     outs = []
-    for flag in ("dpp", "lds"):
+    for flag in ("dpp", "dpp1", "lds"):   # 4 columns per lane (W >= 1024), 1 per lane, LDS tiles
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=120,
                            env=dict(os.environ, SV_HARRIS=flag, SV_WARMUP_AT_IMPORT="0"))
         assert r.returncode == 0, r.stderr.decode()[-2000:]
         outs.append(r.stdout)
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[2] and outs[1] == outs[2]
     off = 0
     for H, W in sizes:
         g = np.random.default_rng(H * 1000 + W).integers(0, 256, (H, W), dtype=np.uint8)

@@ -4,7 +4,7 @@ R="${GRAFT_REPO_ROOT:-/root/repo}"
 OUT="$R/gpurun_out/${1:-sgprof}"
 mkdir -p "$OUT"; cd "$R" || exit 2
 export TMPDIR=/tmp
-F="--cost sgbm --no-cpu-baseline --no-aux --no-live-pmc --no-host-path --steps 10 --warmup 2 --batch 1 --frames 4"
+F="--cost sgbm --no-cpu-baseline --no-aux --no-live-pmc --no-host-path --steps 10 --warmup 2 --batch ${SGB:-1} --frames ${SGB:-4}"
 for cfg in "d320 --num-disp 320 --win 7" "d128 --num-disp 128 --win 9"; do
   set -- $cfg; name=$1; shift
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o sg -- python3 bench.py $F "$@" > "$OUT/$name.log" 2>&1 || { echo "prof $name failed"; exit 1; }

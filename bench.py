@@ -533,10 +533,11 @@ def parse_args(argv=None):
     ap.add_argument("--rectify", action="store_true",
                     help="camera pipeline: raw BGR frames resident in HBM -> rectify+gray "
                          "(k_remap, calibrated CV_16SC2 maps) -> disparity -> median/post")
-    ap.add_argument("--streams", type=int, default=1,
+    ap.add_argument("--streams", type=int, default=0,
                     help="frames mode: contexts (HIP streams) per GPU that consecutive steps "
-                         "alternate over, so one step's median/post overlaps the next step's "
-                         "k_match (separate output buffers per stream)")
+                         "alternate over, so one step overlaps the next (separate output buffers "
+                         "per stream); 0 = auto: 3 for frames of <= 1 MP (a 16-frame VGA batch "
+                         "leaves most of the chip idle between its launches), else 1")
     ap.add_argument("--no-aux", action="store_true", help="skip the aux-kernel rooflines")
     ap.add_argument("--harris", action="store_true",
                     help="C2: also compute the Harris response of every left frame (k_harris)")
@@ -624,7 +625,8 @@ def main():
     disp = [a.alloc(4 * n_px * out_frames) for a in arenas]
     norm = [a.alloc(n_px * out_frames) for a in arenas]
     # --streams S: S-1 extra contexts per GPU (own stream, own outputs) that steps alternate over
-    nstreams = max(1, args.streams) if not (rowtile or args.rectify or gather_on or args.harris) else 1
+    req_streams = args.streams if args.streams > 0 else (3 if n_px <= 1_000_000 else 1)
+    nstreams = max(1, req_streams) if not (rowtile or args.rectify or gather_on) else 1
     lanes = [(engines, depth, disp, norm)]
     for _ in range(nstreams - 1):
         lanes.append(([Engine(d) for d in devices], [a.alloc(4 * n_px * out_frames) for a in arenas],
@@ -634,8 +636,9 @@ def main():
         rect = make_rectifier(eng, W, H)
         gL, gR = arenas[0].alloc(B * n_px), arenas[0].alloc(B * n_px)
         m1l, m2l, m1r, m2r, _, _ = rect.device_maps
-    if harris:
-        hmaps = [a.alloc(4 * n_px * B) for a in arenas]
+    if harris:   # per stream lane: its own Harris maps
+        hmaps_l = [[a.alloc(4 * n_px * B) for a in arenas] for _ in range(nstreams)]
+        hmaps = hmaps_l[0]
     tile = None
     if rowtile and launched:
         from stereovision_amd.distributed import RowTiledDepthMap
@@ -733,7 +736,8 @@ def main():
                                       0.3, 2.0, depth_o[k], disp_o[k], norm_o[k], cost=args.cost,
                                       d_med16=med_o)
             if harris:      # one launch over the batch's left frames
-                e.harris_batch_dev(gL if rectify else dL[k] + f * n_px, B, H, W, W, n_px, hmaps[k])
+                e.harris_batch_dev(gL if rectify else dL[k] + f * n_px, B, H, W, W, n_px,
+                                   hmaps_l[i % nstreams][k])
         if gathered is not None:   # every rank's disparity maps -> rank 0 (RCCL over xGMI)
             from stereovision_amd.distributed import gather_frames
             t_g = time.perf_counter()
@@ -861,7 +865,8 @@ def main():
                               *fetch_maps(e, depth_o[k], disp_o[k], norm_o[k], z, n_px, H, W))
                     if harris:
                         ver.harris(f"rank {rank} device {k} frame {f0 + z}", Lz,
-                                   e.to_host(hmaps[k] + 4 * n_px * z, (H, W), np.float32))
+                                   e.to_host(hmaps_l[last % nstreams][k] + 4 * n_px * z, (H, W),
+                                             np.float32))
             if gathered is not None and rank == 0:
                 from stereovision_amd.synthetic import stereo_pair
                 for r in range(world):
@@ -1000,6 +1005,7 @@ def main():
                    "height": H, "width": W, "num_disp": D, "win": win, "cost": args.cost,
                    "frames_resident_per_gpu": 1 if rowtile else F,
                    "frames_per_step_per_gpu": 1 if rowtile else B,
+                   "streams_per_gpu": nstreams,
                    "parallelism": parallelism},
         "verified": verified,
         "verify": verify_info,
@@ -1032,7 +1038,7 @@ def main():
             log(f"aux kernels failed: {e}")
     if harris and harris_n:     # 1 B/px gray read + 4 B/px f32 response written
         result["aux_kernels"] = dict(result["aux_kernels"] or {})
-        result["aux_kernels"]["k_harris"] = hbm_entry("k_harris_lds", 5 * n_px * B, harris_ms,
+        result["aux_kernels"]["k_harris"] = hbm_entry("k_harris_dpp", 5 * n_px * B, harris_ms,
                                                        harris_n)
     if solo and not args.no_host_path and args.cost != "sgbm" and not rectify:
         try:

@@ -49,8 +49,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from stereovision_amd.engine import (Communicator, Engine, device_count, depth_map_rows_multi,  # noqa: E402
-                                     depth_map_rows_scatter, get_engine, multi_gpu_depth_map_dev)
+from stereovision_amd.engine import (POST_DEPTH, Communicator, Engine, device_count,  # noqa: E402
+                                     depth_map_rows_multi, depth_map_rows_scatter, get_engine,
+                                     multi_gpu_depth_map_dev, multi_gpu_m16_dev)
 from stereovision_amd.synthetic import stereo_batch, stereo_pair, synthetic_calibration, to_bgr  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -458,7 +459,8 @@ def agreed_extra_warmup(pg, spent_s: float, steps_done: int, warmup_seconds: flo
 
 def dist_summary(ngpu, launched, pg=None, comms=None, gather=False, rowtile=False,
                  gather_ms=0.0, gather_n=0, scatter_ms=0.0, scatter_n=0, gather_wall_s=0.0,
-                 steps=0, gather_bytes=0, scatter_bytes=0, reason="", gathered_maps=None):
+                 steps=0, gather_bytes=0, scatter_bytes=0, reason="", gathered_maps=None,
+                 expand_ms=0.0, expand_n=0, root_outputs=None):
     """The multi-GPU fields of the bench line (None for one GPU): the backend the run used,
     how many ranks the RCCL communicator saw (0 + the reason when it fell back), and the
     gather / scatter time per step from HIP events on the root's stream (these include the
@@ -484,6 +486,9 @@ def dist_summary(ngpu, launched, pg=None, comms=None, gather=False, rowtile=Fals
                                        if (gather_wall_s and steps) else None)}
     if out["gather_us_per_step"] and gather_bytes:
         out["gather_GBps"] = round(gather_bytes / (gather_ms * 1e-3 / gather_n) / 1e9, 1)
+    out["root_outputs"] = root_outputs
+    # the root's k_post_m16 launches (peers' medians -> create_depth_map outputs), HIP events
+    out["root_expand_us_per_step"] = round(expand_ms * 1e3 / expand_n, 2) if expand_n else None
     if rowtile:
         out["scatter_us_per_step"] = round(scatter_ms * 1e3 / scatter_n, 2) if scatter_n else None
         out["scatter_bytes_per_step"] = scatter_bytes or None
@@ -530,6 +535,16 @@ def parse_args(argv=None):
     ap.add_argument("--allow-peer-copies", action="store_true",
                     help="one process, N devices: gather with peer copies if RCCL cannot start "
                          "(default: exit non-zero)")
+    ap.add_argument("--root-outputs", default="m16", choices=["m16", "full"],
+                    help="frames mode, N > 1: what GPU 0 holds after each step's gather — m16: "
+                         "every frame's disparity rows as int16 x16 (north_star's 'gather of the "
+                         "final disparity rows', 2 B/px over xGMI); full: also create_depth_map's "
+                         "depth f32 / disparity f32 / u8 for every frame, expanded on GPU 0 from "
+                         "the gathered medians (k_post_m16, 11 B/px of GPU 0's HBM per peer frame)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="one process: run --gpus N logical GPUs on the visible devices (logical "
+                         "GPU k on device k %% devices: own context, stream and buffers; gathers "
+                         "as device copies) — the 1-GPU rehearsal of the N-GPU one-process path")
     ap.add_argument("--rectify", action="store_true",
                     help="camera pipeline: raw BGR frames resident in HBM -> rectify+gray "
                          "(k_remap, calibrated CV_16SC2 maps) -> disparity -> median/post")
@@ -581,11 +596,14 @@ def main():
         rank, world = 0, 1
         n = max(1, args.gpus)
         nd = device_count()
-        if n > nd:
-            raise SystemExit(f"--gpus {n} but only {nd} device(s) are visible")
-        devices = list(range(n))
+        if n > nd and not args.rehearse:
+            raise SystemExit(f"--gpus {n} but only {nd} device(s) are visible (--rehearse runs "
+                             "them as contexts of the visible devices)")
+        devices = [k % max(1, nd) for k in range(n)] if args.rehearse else list(range(n))
     ngpu = world * len(devices)
-    engines = [get_engine(d) for d in devices]
+    # one context per logical GPU (the rehearsal puts several on one device)
+    engines = [get_engine(d) if k == devices.index(d) else Engine(d) for k, d in enumerate(devices)]
+    shared_devices = len(set(devices)) < len(devices)
     eng = engines[0]
 
     H, W, D, win = args.height, args.width, args.num_disp, args.win
@@ -619,8 +637,9 @@ def main():
             L, R = np.repeat(L[..., None], 3, axis=3), np.repeat(R[..., None], 3, axis=3)
         dL.append(a.upload(L))
         dR.append(a.upload(R))
-    gather_all = gather_on and not launched and len(engines) > 1
-    out_frames = (1 if rowtile else B) * (len(engines) if gather_all else 1)
+    gather_all = (gather_on or rowtile) and not launched and len(engines) > 1
+    root_full = args.root_outputs == "full"
+    out_frames = 1 if rowtile else B * (len(engines) if gather_all else 1)
     depth = [a.alloc(4 * n_px * out_frames) for a in arenas]
     disp = [a.alloc(4 * n_px * out_frames) for a in arenas]
     norm = [a.alloc(n_px * out_frames) for a in arenas]
@@ -639,13 +658,20 @@ def main():
     if harris:   # per stream lane: its own Harris maps
         hmaps_l = [[a.alloc(4 * n_px * B) for a in arenas] for _ in range(nstreams)]
         hmaps = hmaps_l[0]
-    tile = None
+    tile = tiles = None
+    rt = {"t": 0, "primed": False, "last": 0}
     if rowtile and launched:
         from stereovision_amd.distributed import RowTiledDepthMap
-        tile = RowTiledDepthMap(H, W, D, win, cost=args.cost, device=devices[0], rank=rank,
-                                world=world, engine=eng)
+        # two tiles (band inputs, medians, outputs each) alternate over consecutive frames, so
+        # the band scatter of frame i+1 and the gather of frame i run on a communication stream
+        # while frame i+1 computes
+        tiles = [RowTiledDepthMap(H, W, D, win, cost=args.cost, device=devices[0], rank=rank,
+                                  world=world, engine=eng) for _ in range(2 if world > 1 else 1)]
+        tile = tiles[0]
     comms, comm_reason = None, ""
-    if not launched and len(engines) > 1 and (gather_on or rowtile):
+    if shared_devices:
+        comm_reason = "rehearsal: logical GPUs share a device (device copies, no RCCL)"
+    elif not launched and len(engines) > 1 and (gather_on or rowtile):
         try:
             comms = Communicator.init_all(devices)
         except Exception as ex:
@@ -664,16 +690,16 @@ def main():
             comms2 = Communicator.init_all(devices)
         engines2 = [Engine(d) for d in devices]
         all_engines.extend(engines2)
-        glanes = [(engines, comms, depth[0], disp[0], norm[0]),
+        glanes = [(engines, comms, depth[0], disp[0], norm[0], arenas[0].alloc(2 * n_px * out_frames)),
                   (engines2, comms2, arenas[0].alloc(4 * n_px * out_frames), arenas[0].alloc(4 * n_px * out_frames),
-                   arenas[0].alloc(n_px * out_frames))]
+                   arenas[0].alloc(n_px * out_frames), arenas[0].alloc(2 * n_px * out_frames))]
     # launched frames mode with the gather: every step's disparity maps go to rank 0 as int16
     # x16 (OpenCV's fixed-point disparity, written by the median epilogue beside the f32 map,
     # which is exactly it / 16: half the xGMI bytes of the f32 map) on a communication stream
     # of their own, double-buffered, so step i's gather overlaps step i+1's kernels; rank 0
     # receives them into one stack per buffer (rank-major).  Event slots of `eng`: 2s = set s
     # computed, 2s+1 = set s gathered.
-    gathered, ceng, cstream = None, None, 0
+    gathered, ceng, cstream, expanded = None, None, 0, None
     if launched and gather_on:
         ceng = Engine(devices[0])
         cstream = ceng.stream
@@ -682,35 +708,73 @@ def main():
                 (arenas[0].alloc(4 * n_px * B), arenas[0].alloc(4 * n_px * B), arenas[0].alloc(n_px * B),
                  arenas[0].alloc(2 * n_px * B))]
         gathered = [arenas[0].alloc(2 * n_px * B * world) if rank == 0 else 0 for _ in range(2)]
+        # --root-outputs full: rank 0 expands the peers' gathered medians into create_depth_map's
+        # outputs (its own frames already have them), double-buffered like the gathers
+        nexp = n_px * B * (world - 1)
+        expanded = ([(arenas[0].alloc(4 * nexp), arenas[0].alloc(4 * nexp), arenas[0].alloc(nexp))
+                     for _ in range(2)] if (root_full and rank == 0) else None)
+    if tiles is not None and world > 1:
+        ceng = Engine(devices[0])
+        cstream = ceng.stream
+        all_engines.append(ceng)
     gather_wall = [0.0]
 
     def step(i):
         f = (i * B) % F
         if rowtile:
-            if launched:
-                if band_inputs and world > 1:
-                    eng.profile_region_begin("scatter", eng.stream)
-                    tile.scatter(pg, dL[0], dR[0])
-                    eng.profile_region_end(eng.stream)
-                    tile.compute()
+            if launched and world == 1:
+                tile.compute(dL[0], dR[0])
+            elif launched:
+                # pipelined over the two tiles (event slots of `eng`: 4+t = tile t's band inputs
+                # scattered, 6+t = tile t computed): compute(i) on the compute stream; on the
+                # communication stream the scatter of frame i+1's band inputs (into the other
+                # tile, whose previous compute the gather before it already waited for), then
+                # the gather of frame i's int16 x16 medians (+ the root's expansion)
+                t = rt["t"]
+                u = (t + 1) % len(tiles)
+                bo = "full" if rank == 0 else "m16"
+
+                def scatter_into(x):
+                    ceng.profile_region_begin("scatter", cstream)
+                    tiles[x].scatter(pg, dL[0], dR[0], stream=cstream)
+                    ceng.profile_region_end(cstream)
+                    eng.event_record(4 + x, cstream)
+                if band_inputs:
+                    if not rt["primed"]:
+                        scatter_into(t)
+                        rt["primed"] = True
+                    eng.stream_wait_event(4 + t, eng.stream)
+                    tiles[t].compute(band_outputs=bo)
                 else:
-                    tile.compute(dL[0], dR[0])
-                if world > 1:
-                    eng.profile_region_begin("gather", eng.stream)
-                    tile.gather(pg, stream=eng.stream)
-                    eng.profile_region_end(eng.stream)
-            elif band_inputs:
-                depth_map_rows_scatter(engines, comms, dL[0], dR[0], H, W, W, 0, D, win, 0.3, 2.0,
-                                       depth[0], disp[0], norm[0], cost=args.cost)
-            else:
-                depth_map_rows_multi(engines, comms, dL, dR, H, W, W, 0, D, win, 0.3, 2.0,
-                                     depth[0], disp[0], norm[0], cost=args.cost)
+                    tiles[t].compute(dL[0], dR[0], band_outputs=bo)
+                eng.event_record(6 + t, eng.stream)
+                if band_inputs:
+                    scatter_into(u)
+                eng.stream_wait_event(6 + t, cstream)
+                ceng.profile_region_begin("gather", cstream)
+                tiles[t].gather(pg, stream=cstream)
+                ceng.profile_region_end(cstream)
+                rt["last"], rt["t"] = t, u
+            else:   # one process: two lanes of contexts alternate, so frame i+1's scatter and
+                    # kernels overlap frame i's gather and expansion
+                le, lc, ldep, ldis, lnor, _ = glanes[i % 2]
+                if band_inputs:
+                    depth_map_rows_scatter(le, lc, dL[0], dR[0], H, W, W, 0, D, win, 0.3, 2.0,
+                                           ldep, ldis, lnor, cost=args.cost)
+                else:
+                    depth_map_rows_multi(le, lc, dL, dR, H, W, W, 0, D, win, 0.3, 2.0,
+                                         ldep, ldis, lnor, cost=args.cost)
+                rt["last"] = i % 2
             return
-        if gather_all:     # one process, N devices, maps gathered on device 0
-            le, lc, ldep, ldis, lnor = glanes[i % 2]
-            multi_gpu_depth_map_dev(le, lc, [p + f * n_px for p in dL],
-                                    [p + f * n_px for p in dR], [B] * len(le), H, W, W, n_px,
-                                    0, D, win, 0.3, 2.0, ldep, ldis, lnor, cost=args.cost)
+        if gather_all:     # one process, N devices, maps gathered on device 0 (2 B/px)
+            le, lc, ldep, ldis, lnor, lm16 = glanes[i % 2]
+            if root_full:
+                multi_gpu_depth_map_dev(le, lc, [p + f * n_px for p in dL],
+                                        [p + f * n_px for p in dR], [B] * len(le), H, W, W, n_px,
+                                        0, D, win, 0.3, 2.0, ldep, ldis, lnor, cost=args.cost)
+            else:
+                multi_gpu_m16_dev(le, lc, [p + f * n_px for p in dL], [p + f * n_px for p in dR],
+                                  [B] * len(le), H, W, W, n_px, 0, D, win, lm16, cost=args.cost)
             return
         engs, depth_o, disp_o, norm_o = lanes[i % nstreams]
         med_o = 0
@@ -746,6 +810,11 @@ def main():
             ceng.profile_region_begin("gather", cstream)
             gather_frames(pg, gset[gs][3], B, gathered[gs], 2 * n_px, stream=cstream)
             ceng.profile_region_end(cstream)
+            if expanded is not None:   # the peers' frames, after the gather on the same stream
+                xd, xp, xu = expanded[gs]
+                ceng.post_m16_dev(gathered[gs] + 2 * n_px * B, nexp, POST_DEPTH, d_disparity=xp,
+                                  d_out_a=xd, d_out_u8=xu, min_depth=0.3, max_depth=2.0,
+                                  min_disp_global=0, min_disp=0, num_disp=D, stream=cstream)
             eng.event_record(2 * gs + 1, cstream)       # set gs free again
             gather_wall[0] += time.perf_counter() - t_g
 
@@ -810,7 +879,14 @@ def main():
     if glanes:   # the second lane's root context times its own gathers
         m2, n2 = glanes[1][0][0].profile_read("gather")
         gath_ms, gath_n = gath_ms + m2, gath_n + n2
-    scat_ms, scat_n = eng.profile_read("scatter")
+    scat_ms, scat_n = (ceng or eng).profile_read("scatter")
+    if glanes:
+        m2, n2 = glanes[1][0][0].profile_read("scatter")
+        scat_ms, scat_n = scat_ms + m2, scat_n + n2
+    exp_ms, exp_n = (ceng or eng).profile_read("post")
+    if glanes:
+        m2, n2 = glanes[1][0][0].profile_read("post")
+        exp_ms, exp_n = exp_ms + m2, exp_n + n2
     k_name = "sgbm pipeline (k_sgbm_*)" if args.cost == "sgbm" else "k_match"
     if pg is not None:
         elapsed = pg.allreduce_max(elapsed)
@@ -833,20 +909,27 @@ def main():
         if rowtile:
             if launched:
                 if rank == 0:
+                    tl = tiles[rt["last"]]
                     ver.frame("full frame gathered on rank 0", hostL[0][0], hostR[0][0],
-                              eng.to_host(tile.out_a, (H, W), np.float32),
-                              eng.to_host(tile.disp, (H, W), np.float32),
-                              eng.to_host(tile.out_u8, (H, W), np.uint8))
+                              eng.to_host(tl.out_a, (H, W), np.float32),
+                              eng.to_host(tl.disp, (H, W), np.float32),
+                              eng.to_host(tl.out_u8, (H, W), np.uint8))
             else:
+                od, op, on = (glanes[rt["last"]][2:5] if glanes else (depth[0], disp[0], norm[0]))
                 ver.frame("full frame gathered on device 0", hostL[0][0], hostR[0][0],
-                          *fetch_maps(eng, depth[0], disp[0], norm[0], 0, n_px, H, W))
+                          *fetch_maps(eng, od, op, on, 0, n_px, H, W))
         elif gather_all:
-            _, _, ldep, ldis, lnor = glanes[last % 2]
+            _, _, ldep, ldis, lnor, lm16 = glanes[last % 2]
             for k in range(len(engines)):
                 for z in zs:
-                    ver.frame(f"device {k} frame {f0 + z} (gathered on device 0)", hostL[k][f0 + z],
-                              hostR[k][f0 + z], *fetch_maps(eng, ldep, ldis, lnor, k * B + z,
-                                                            n_px, H, W))
+                    tag = f"device {k} frame {f0 + z} (gathered on device 0)"
+                    if root_full:
+                        ver.frame(tag, hostL[k][f0 + z], hostR[k][f0 + z],
+                                  *fetch_maps(eng, ldep, ldis, lnor, k * B + z, n_px, H, W))
+                    else:
+                        m16 = eng.to_host(lm16 + 2 * n_px * (k * B + z), (H, W), np.int16)
+                        ver.disparity(tag + " int16 x16", hostL[k][f0 + z], hostR[k][f0 + z],
+                                      m16.astype(np.float32) / np.float32(16.0))
         else:
             engs, depth_o, disp_o, norm_o = lanes[last % nstreams]
             if gathered is not None:
@@ -878,6 +961,10 @@ def main():
                         m16 = eng.to_host(gathered[last % 2] + 2 * n_px * (r * B + z), (H, W), np.int16)
                         ver.disparity(f"rank {r} frame {f0 + z} (gathered on rank 0)", Lz, Rz,
                                       m16.astype(np.float32) / np.float32(16.0))
+                        if expanded is not None and r > 0:
+                            xd, xp, xu = expanded[last % 2]
+                            ver.frame(f"rank {r} frame {f0 + z} (expanded on rank 0)", Lz, Rz,
+                                      *fetch_maps(eng, xd, xp, xu, (r - 1) * B + z, n_px, H, W))
         ok = ver.result()
         if pg is not None:
             ok = pg.allreduce_max(0.0 if ok else 1.0) == 0.0
@@ -891,6 +978,10 @@ def main():
     elif args.cost == "sgbm":
         verify_info = {"skipped": "SGBM mode: the NumPy SGBM-3WAY oracle takes ~15 s per 1080p "
                                   "frame; tests/test_sgbm.py checks the kernels bit-exactly"}
+    # the collectives are over: from here on every phase (rocprofv3 passes, host path, CPU
+    # baseline) has its own time limit, so the whole-run hang guard stands down
+    if args.hang_timeout > 0:
+        faulthandler.cancel_dump_traceback_later()
 
     # pixels of one k_match launch: the batch (frames) or this GPU's band + median halo
     npx = n_px * B
@@ -966,21 +1057,26 @@ def main():
             from stereovision_amd.distributed import band_layout
             for k in range(1, ngpu):
                 b = band_layout(H, k, ngpu, win)
-                gbytes += 9 * (b["r1"] - b["r0"]) * W
+                gbytes += 2 * (b["r1"] - b["r0"]) * W    # int16 x16 median rows
                 if band_inputs:
                     sbytes += 2 * (b["in1"] - b["in0"]) * W
         elif gather_on:   # launched: the int16 x16 disparity maps; one process: all three outputs
-            gbytes = (2 if launched else 9) * n_px * B * (ngpu - 1)
+            gbytes = 2 * n_px * B * (ngpu - 1)   # int16 x16 medians (both process models)
     dist = dist_summary(ngpu, launched, pg, comms, gather=gather_on, rowtile=rowtile,
                         gather_ms=gath_ms, gather_n=gath_n, scatter_ms=scat_ms, scatter_n=scat_n,
                         gather_wall_s=gather_wall[0], steps=args.steps, gather_bytes=gbytes,
-                        scatter_bytes=sbytes, reason=comm_reason,
-                        gathered_maps=("rows of depth f32 + disparity f32 + depth u8" if rowtile else
+                        scatter_bytes=sbytes, reason=comm_reason, expand_ms=exp_ms, expand_n=exp_n,
+                        root_outputs=(("full" if (rowtile or root_full) else "m16") if (gather_on or rowtile)
+                                      else None),
+                        gathered_maps=("row bands as int16 x16 medians, expanded on GPU 0 into depth f32 + "
+                                       "disparity f32 + depth u8" if rowtile else
                                        "disparity of every frame as int16 x16 (OpenCV's fixed point; the "
-                                       "f32 map is it / 16 exactly), overlapped with the next step "
-                                       "(communication stream, double-buffered maps)" if launched else
-                                       "depth f32 + disparity f32 + depth u8 of every frame, two "
-                                       "context lanes so a step's gather overlaps the next step")
+                                       "f32 map is it / 16 exactly)"
+                                       + (", expanded on GPU 0 into depth f32 + disparity f32 + depth u8"
+                                          if root_full else "")
+                                       + (", overlapped with the next step (communication stream, "
+                                          "double-buffered maps)" if launched else
+                                          ", two context lanes so a step's gather overlaps the next step"))
                         if (gather_on or rowtile) else None)
     parallelism = (f"row-tiled x{ngpu}" + (" (band inputs scattered from GPU 0)" if band_inputs else "")
                    + " + band gather" if rowtile else
@@ -1053,8 +1149,8 @@ def main():
             log(f"cpu baseline failed: {e}")
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if tile is not None:
-        tile.close()
+    for tl in tiles or []:
+        tl.close()
     for a in arenas:
         a.free()
     if comms:

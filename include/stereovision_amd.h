@@ -206,6 +206,22 @@ int sv_median_post_color_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W,
                              const uint8_t* cmap_bgr, float* d_disparity, float* d_out_a,
                              uint8_t* d_out_u8, float* d_out_b, uint8_t* d_bgr, void* stream);
 
+/* sv_median_post_dev with an optional int16 x16 median map d_med16 (rows [row0, row1) at
+ * their full-frame offsets) beside the outputs; d_disparity may then be NULL, and mode =
+ * SV_POST_NONE writes only d_med16 (a row band's medians before a gather). */
+int sv_median_post_m16_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W, int row0, int row1,
+                           int mode, float min_depth, float max_depth, float depth_range,
+                           float min_disp_global, int min_disp, int num_disp, float* d_disparity,
+                           float* d_out_a, uint8_t* d_out_u8, float* d_out_b, int16_t* d_med16,
+                           void* stream);
+/* The post-processing of n median values d_med16 (int16 x16, e.g. maps gathered over xGMI):
+ * d_disparity = m / 16 (nullable), and mode's outputs element-wise, exactly as the median
+ * kernel's epilogue writes them (depth_map.py:915-936 / fused_depth_map.py:1010-1024). */
+int sv_post_m16_dev(sv_ctx* ctx, const int16_t* d_med16, int64_t n, int mode, float min_depth,
+                    float max_depth, float depth_range, float min_disp_global, int min_disp,
+                    int num_disp, float* d_disparity, float* d_out_a, uint8_t* d_out_u8,
+                    float* d_out_b, void* stream);
+
 /* Whole app-1 device path on gray device images: disparity -> median -> depth post. */
 int sv_depth_map_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int H, int W,
                      int pitch, int min_disp, int num_disp, int win, int cost, float min_depth,
@@ -301,9 +317,11 @@ int sv_comm_synchronize(sv_comm* comm);
 /* C4 on device-resident frames, one process driving ndev contexts: context k computes
  * create_depth_map (disparity -> median -> depth post, one launch per kernel over its
  * frames) for n_frames[k] gray pairs at d_left[k]/d_right[k] (+ z*frame_stride bytes, on
- * its own device), and the three outputs of every frame are gathered into d_depth /
- * d_disparity / d_norm on ctxs[0]'s device, dense, in context order (frame z of context k
- * at index sum(n_frames[:k]) + z).  comms (nullable; else comms[k] must be on ctxs[k]'s
+ * its own device), and the three outputs of every frame end up in d_depth / d_disparity /
+ * d_norm on ctxs[0]'s device, dense, in context order (frame z of context k at index
+ * sum(n_frames[:k]) + z).  Only the peers' int16 x16 medians cross xGMI (2 B/px instead of
+ * the outputs' 9); the root expands them with the post-processing table (k_post_m16,
+ * profiled as SV_K_POST) after the gather.  comms (nullable; else comms[k] must be on ctxs[k]'s
  * device with rank k): the gather runs as RCCL send/recv over xGMI; NULL: hipMemcpyPeerAsync
  * (a plain device copy when two contexts share a device).  Returns after enqueueing: the
  * outputs are complete once ctxs[0]'s stream is (sv_synchronize(ctxs[0])). */
@@ -314,11 +332,22 @@ int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int n
                                float max_depth, float depth_range, float min_disp_global,
                                float* d_depth, float* d_disparity, uint8_t* d_norm);
 
+/* C4 as north_star states it ("a trivial RCCL gather of the final disparity rows"): as
+ * sv_multi_gpu_depth_map_dev, but every context's median kernel writes only the int16 x16
+ * median maps (OpenCV's fixed-point disparity after medianBlur, depth_map.py:909-912) and
+ * those are gathered into d_med16 on ctxs[0]'s device (dense, context order): 2 B/px over
+ * xGMI.  sv_post_m16_dev turns any of them into create_depth_map's outputs. */
+int sv_multi_gpu_m16_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
+                         const uint8_t* const* d_left, const uint8_t* const* d_right,
+                         const int* n_frames, int H, int W, int pitch, int64_t frame_stride,
+                         int min_disp, int num_disp, int win, int cost, int16_t* d_med16);
+
 /* C5: ONE frame row-tiled over ndev contexts.  Every context holds the full gray frame
  * (d_left[k]/d_right[k] on its device; the window and median halos are read locally, so the
  * bands reassemble bit-exactly); context k computes output rows [H*k/ndev, H*(k+1)/ndev)
- * of create_depth_map and the bands are gathered into the full H x W d_depth / d_disparity
- * / d_norm on ctxs[0]'s device.  comms / completion as sv_multi_gpu_depth_map_dev. */
+ * of create_depth_map and the bands end up in the full H x W d_depth / d_disparity /
+ * d_norm on ctxs[0]'s device (the peers' bands cross xGMI as int16 x16 medians and are
+ * expanded on the root).  comms / completion as sv_multi_gpu_depth_map_dev. */
 int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
                             const uint8_t* const* d_left, const uint8_t* const* d_right, int H,
                             int W, int pitch, int min_disp, int num_disp, int win, int cost,

@@ -125,6 +125,9 @@ struct sv_ctx {
     // host-buffer frame path: int16 medians come back over PCIe and are expanded on the
     // host with a host copy of the post-processing table (hl_*, valid for hl_key)
     DevBuf m16;
+    // multi-device entry points: int16 x16 medians a context sends to the root (peers) or
+    // receives from the peers (root), 2 B/px over xGMI
+    DevBuf gm16;
     std::vector<float> hl_a, hl_b;
     std::vector<uint8_t> hl_u8;
     std::vector<HostEnt> hl_ent;
@@ -840,6 +843,51 @@ int sv_median_post_dev(sv_ctx* c, const int16_t* d_disp16, int H, int W, int row
     return 0;
 }
 
+int sv_median_post_m16_dev(sv_ctx* c, const int16_t* d_disp16, int H, int W, int row0, int row1, int mode,
+                           float min_depth, float max_depth, float depth_range, float min_disp_global,
+                           int min_disp, int num_disp, float* d_disparity, float* d_out_a, uint8_t* d_out_u8,
+                           float* d_out_b, int16_t* d_med16, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_disp16, H, W) || (!d_disparity && !d_med16)) return fail(SV_EINVAL, "bad median arguments");
+    if (mode != SV_POST_NONE && mode != SV_POST_DEPTH && mode != SV_POST_SCALED) return fail(SV_EINVAL, "bad mode");
+    if (mode == SV_POST_DEPTH && (!d_out_a || !d_out_u8)) return fail(SV_EINVAL, "depth post outputs missing");
+    if (mode == SV_POST_SCALED && (!d_out_a || !d_out_u8 || !d_out_b || num_disp <= 0))
+        return fail(SV_EINVAL, "scaled post outputs missing");
+    if ((long long)H * W >= (1LL << 30)) return fail(SV_EINVAL, "frame too large for the median kernel");
+    if (row0 < 0) row0 = 0;
+    if (row1 > H) row1 = H;
+    hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
+    sv::PostParams pp = make_post(mode, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
+                                  d_out_a, d_out_u8, d_out_b);
+    int lrc = attach_lut(c, pp, s);
+    if (lrc) return lrc;
+    pp.out_m16 = d_med16;
+    SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(d_disp16, H, W, row0, row1, d_disparity, pp, s));
+    return 0;
+}
+
+int sv_post_m16_dev(sv_ctx* c, const int16_t* d_med16, int64_t n, int mode, float min_depth, float max_depth,
+                    float depth_range, float min_disp_global, int min_disp, int num_disp, float* d_disparity,
+                    float* d_out_a, uint8_t* d_out_u8, float* d_out_b, void* stream) {
+    SV_ENTER(c);
+    if (n < 0 || (n > 0 && !d_med16)) return fail(SV_EINVAL, "bad median map");
+    if (mode != SV_POST_NONE && mode != SV_POST_DEPTH && mode != SV_POST_SCALED) return fail(SV_EINVAL, "bad mode");
+    if (mode == SV_POST_NONE && !d_disparity) return fail(SV_EINVAL, "no outputs");
+    if (mode == SV_POST_DEPTH && (!d_out_a || !d_out_u8)) return fail(SV_EINVAL, "depth post outputs missing");
+    if (mode == SV_POST_SCALED && (!d_out_a || !d_out_u8 || !d_out_b || num_disp <= 0))
+        return fail(SV_EINVAL, "scaled post outputs missing");
+    if (n == 0) return 0;
+    hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
+    sv::PostParams pp = make_post(mode, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
+                                  d_out_a, d_out_u8, d_out_b);
+    int rc = attach_lut(c, pp, s);
+    if (rc) return rc;
+    SV_LAUNCH(c, SV_K_POST, s, sv::launch_post_m16(d_med16, (long long)n, d_disparity, pp, s));
+    return 0;
+}
+
 int sv_median_post_color_dev(sv_ctx* c, const int16_t* d_disp16, int H, int W, int row0, int row1, int mode,
                              float min_depth, float max_depth, float depth_range, float min_disp_global,
                              int min_disp, int num_disp, const uint8_t* cmap_bgr, float* d_disparity,
@@ -1222,6 +1270,46 @@ int gather_blocks_impl(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
     return 0;
 }
 
+// The root's expansion of the peers' gathered int16 x16 medians (n pixels at root->gm16 +
+// in_off) into the create_depth_map outputs at element offset `off` (k_post_m16 on the root
+// stream, after the gather), timed as SV_K_POST.
+int expand_on_root(sv_ctx* root, size_t n, size_t in_off, size_t off, float min_depth, float max_depth, float depth_range,
+                   float min_disp_global, int min_disp, int num_disp, float* d_depth, float* d_disparity,
+                   uint8_t* d_norm) {
+    if (!n) return 0;
+    SV_HIP(hipSetDevice(root->device));
+    sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                                  num_disp, d_depth + off, d_norm + off, nullptr);
+    int rc = attach_lut(root, pp, root->stream);
+    if (rc) return rc;
+    SV_LAUNCH(root, SV_K_POST, root->stream,
+              sv::launch_post_m16(root->gm16.as<int16_t>() + in_off, (long long)n, d_disparity + off, pp,
+                                  root->stream));
+    return scratch_mark(root, root->stream);
+}
+
+// Median (+ post) of output rows [r0, r1) of context k's disparity band: the root writes the
+// create_depth_map outputs in place, a peer only its int16 x16 medians (c->gm16, full-frame
+// layout) for the gather.
+int band_median(sv_ctx* c, int k, int H, int W, int r0, int r1, float min_depth, float max_depth, float depth_range,
+                float min_disp_global, int min_disp, int num_disp, float* d_depth, float* d_disparity,
+                uint8_t* d_norm, hipStream_t s) {
+    sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                                  num_disp, d_depth, d_norm, nullptr);
+    float* o_disp = d_disparity;
+    if (k > 0) {
+        SV_HIP(c->gm16.ensure((size_t)H * W * sizeof(int16_t)));
+        pp = make_post(SV_POST_NONE, 0.f, 0.f, 0.f, 0.f, 0, 0, nullptr, nullptr, nullptr);
+        pp.out_m16 = c->gm16.as<int16_t>();
+        o_disp = nullptr;
+    } else {
+        int rc = attach_lut(c, pp, s);
+        if (rc) return rc;
+    }
+    SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(c->d16.as<int16_t>(), H, W, r0, r1, o_disp, pp, s));
+    return 0;
+}
+
 int multi_prologue(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev) {
     int rc = check_contexts(ctxs, ndev);
     if (rc) return rc;
@@ -1237,12 +1325,14 @@ int multi_prologue(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev) {
 
 }  // namespace
 
-int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
-                               const uint8_t* const* d_right, const int* n_frames, int H, int W, int pitch,
-                               int64_t frame_stride, int min_disp, int num_disp, int win, int cost, float min_depth,
-                               float max_depth, float depth_range, float min_disp_global, float* d_depth,
-                               float* d_disparity, uint8_t* d_norm) {
-    if (!d_left || !d_right || !n_frames || !d_depth || !d_disparity || !d_norm) return fail(SV_EINVAL, "null arguments");
+namespace {
+// C4 over ndev contexts.  d_med16 == nullptr: create_depth_map outputs on the root (its own
+// frames written by its median epilogue, the peers' from their gathered int16 x16 medians);
+// else only the int16 x16 medians of every frame, gathered into d_med16.
+int multi_frames(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
+                 const uint8_t* const* d_right, const int* n_frames, int H, int W, int pitch, int64_t frame_stride,
+                 int min_disp, int num_disp, int win, int cost, float min_depth, float max_depth, float depth_range,
+                 float min_disp_global, float* d_depth, float* d_disparity, uint8_t* d_norm, int16_t* d_med16) {
     int rc = multi_prologue(ctxs, comms, ndev);
     if (rc) return rc;
     sv::MatchPlan plan;
@@ -1266,6 +1356,16 @@ int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int n
     } catch (...) {
         return fail(SV_ENOMEM, "allocation failed");
     }
+    sv_ctx* root = ctxs[0];
+    size_t total = 0;
+    for (int k = 0; k < ndev; ++k) total += (size_t)n_frames[k];
+    const size_t n0 = (size_t)n_frames[0];   // the root's own frames come first
+    // the peers' int16 x16 medians land in the root's gm16 (frames n0 .. total-1, dense)
+    SV_HIP(hipSetDevice(root->device));
+    rc = scratch_wait(root, root->stream);
+    if (rc) return rc;
+    if (total > n0 && !d_med16) SV_HIP(root->gm16.ensure((total - n0) * n * sizeof(int16_t)));
+    int16_t* recv = d_med16 ? d_med16 + n0 * n : root->gm16.as<int16_t>();   // peers' medians
     size_t f_off = 0;
     for (int k = 0; k < ndev; ++k) {
         sv_ctx* c = ctxs[k];
@@ -1278,34 +1378,53 @@ int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int n
         rc = scratch_wait(c, s);
         if (rc) return rc;
         SV_HIP(c->d16.ensure((size_t)nf * n * sizeof(int16_t)));
-        float* o_depth = d_depth + off * n;
-        float* o_disp = d_disparity + off * n;
-        uint8_t* o_norm = d_norm + off * n;
-        if (k > 0) {   // results stay in this context's scratch until gathered
-            SV_HIP(c->fa.ensure((size_t)nf * n * sizeof(float)));
-            SV_HIP(c->fb.ensure((size_t)nf * n * sizeof(float)));
-            SV_HIP(c->u8.ensure((size_t)nf * n));
-            o_depth = c->fb.as<float>();
-            o_disp = c->fa.as<float>();
-            o_norm = c->u8.as<uint8_t>();
-        }
         rc = enqueue_disparity(c, d_left[k], d_right[k], H, W, pitch, min_disp, num_disp, win, cost, 0, H,
                                c->d16.as<int16_t>(), W, s, nf, frame_stride, (long long)n);
         if (rc) return rc;
-        sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
-                                      num_disp, o_depth, o_norm, nullptr);
-        rc = attach_lut(c, pp, s);
-        if (rc) return rc;
+        sv::PostParams pp = make_post(SV_POST_NONE, 0.f, 0.f, 0.f, 0.f, 0, 0, nullptr, nullptr, nullptr);
+        float* o_disp = nullptr;
+        if (k > 0) {   // peers: only the int16 x16 medians (2 B/px), sent to the root
+            SV_HIP(c->gm16.ensure((size_t)nf * n * sizeof(int16_t)));
+            pp.out_m16 = c->gm16.as<int16_t>();
+        } else if (d_med16) {
+            pp.out_m16 = d_med16;
+        } else {       // the root's own frames: create_depth_map's outputs in place
+            pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
+                           d_depth + off * n, d_norm + off * n, nullptr);
+            o_disp = d_disparity + off * n;
+            rc = attach_lut(c, pp, s);
+            if (rc) return rc;
+        }
         SV_LAUNCH(c, SV_K_MEDIAN, s,
                   sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, o_disp, pp, s, nf, (long long)n,
                                         (long long)n));
         active.push_back(k);
-        if (k > 0)
-            blocks[k] = {{d_depth + off * n, o_depth, (size_t)nf * n * sizeof(float)},
-                         {d_disparity + off * n, o_disp, (size_t)nf * n * sizeof(float)},
-                         {d_norm + off * n, o_norm, (size_t)nf * n}};
+        if (k > 0) blocks[k] = {{recv + (off - n0) * n, c->gm16.p, (size_t)nf * n * sizeof(int16_t)}};
     }
-    return gather_blocks(ctxs, comms, ndev, blocks, active);
+    rc = gather_blocks(ctxs, comms, ndev, blocks, active);
+    if (rc || d_med16) return rc;
+    return expand_on_root(root, (total - n0) * n, 0, n0 * n, min_depth, max_depth, depth_range, min_disp_global,
+                          min_disp, num_disp, d_depth, d_disparity, d_norm);
+}
+}  // namespace
+
+int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
+                               const uint8_t* const* d_right, const int* n_frames, int H, int W, int pitch,
+                               int64_t frame_stride, int min_disp, int num_disp, int win, int cost, float min_depth,
+                               float max_depth, float depth_range, float min_disp_global, float* d_depth,
+                               float* d_disparity, uint8_t* d_norm) {
+    if (!d_left || !d_right || !n_frames || !d_depth || !d_disparity || !d_norm) return fail(SV_EINVAL, "null arguments");
+    return multi_frames(ctxs, comms, ndev, d_left, d_right, n_frames, H, W, pitch, frame_stride, min_disp, num_disp,
+                        win, cost, min_depth, max_depth, depth_range, min_disp_global, d_depth, d_disparity, d_norm,
+                        nullptr);
+}
+
+int sv_multi_gpu_m16_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
+                         const uint8_t* const* d_right, const int* n_frames, int H, int W, int pitch,
+                         int64_t frame_stride, int min_disp, int num_disp, int win, int cost, int16_t* d_med16) {
+    if (!d_left || !d_right || !n_frames || !d_med16) return fail(SV_EINVAL, "null arguments");
+    return multi_frames(ctxs, comms, ndev, d_left, d_right, n_frames, H, W, pitch, frame_stride, min_disp, num_disp,
+                        win, cost, 0.f, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, d_med16);
 }
 
 int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
@@ -1333,6 +1452,11 @@ int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev
     } catch (...) {
         return fail(SV_ENOMEM, "allocation failed");
     }
+    sv_ctx* root = ctxs[0];
+    SV_HIP(hipSetDevice(root->device));
+    rc = scratch_wait(root, root->stream);
+    if (rc) return rc;
+    SV_HIP(root->gm16.ensure(n * sizeof(int16_t)));
     for (int k = 0; k < ndev; ++k) {
         sv_ctx* c = ctxs[k];
         const int r0 = (int)((long long)H * k / ndev), r1 = (int)((long long)H * (k + 1) / ndev);
@@ -1343,34 +1467,23 @@ int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev
         rc = scratch_wait(c, s);
         if (rc) return rc;
         SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
-        float* o_depth = d_depth;
-        float* o_disp = d_disparity;
-        uint8_t* o_norm = d_norm;
-        if (k > 0) {
-            SV_HIP(c->fa.ensure(n * sizeof(float)));
-            SV_HIP(c->fb.ensure(n * sizeof(float)));
-            SV_HIP(c->u8.ensure(n));
-            o_depth = c->fb.as<float>();
-            o_disp = c->fa.as<float>();
-            o_norm = c->u8.as<uint8_t>();
-        }
         rc = enqueue_disparity(c, d_left[k], d_right[k], H, W, pitch, min_disp, num_disp, win, cost, h0, h1,
                                c->d16.as<int16_t>(), W, s);
         if (rc) return rc;
-        sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
-                                      num_disp, o_depth, o_norm, nullptr);
-        rc = attach_lut(c, pp, s);
+        rc = band_median(c, k, H, W, r0, r1, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
+                         d_depth, d_disparity, d_norm, s);
         if (rc) return rc;
-        SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(c->d16.as<int16_t>(), H, W, r0, r1, o_disp, pp, s));
         active.push_back(k);
         if (k > 0) {
             const size_t o = (size_t)r0 * W, m = (size_t)(r1 - r0) * W;
-            blocks[k] = {{d_depth + o, o_depth + o, m * sizeof(float)},
-                         {d_disparity + o, o_disp + o, m * sizeof(float)},
-                         {d_norm + o, o_norm + o, m}};
+            blocks[k] = {{root->gm16.as<int16_t>() + o, c->gm16.as<int16_t>() + o, m * sizeof(int16_t)}};
         }
     }
-    return gather_blocks(ctxs, comms, ndev, blocks, active);
+    rc = gather_blocks(ctxs, comms, ndev, blocks, active);
+    if (rc) return rc;
+    const size_t rr1 = (size_t)((long long)H / ndev) * W;   // the root's band ends at row H / ndev
+    return expand_on_root(root, n - rr1, rr1, rr1, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                          num_disp, d_depth, d_disparity, d_norm);
 }
 
 int sv_depth_map_rows_scatter(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* d_left,
@@ -1400,6 +1513,10 @@ int sv_depth_map_rows_scatter(sv_ctx* const* ctxs, sv_comm* const* comms, int nd
     }
     sv_ctx* root = ctxs[0];
     for (int k = 0; k < ndev; ++k) band_rows_of(H, k, ndev, win, rows[k]);
+    SV_HIP(hipSetDevice(root->device));
+    rc = scratch_wait(root, root->stream);
+    if (rc) return rc;
+    SV_HIP(root->gm16.ensure(n * sizeof(int16_t)));
     // 1. scatter: context k > 0 receives input rows [in0, in1) of both images into its scratch
     //    (img[0], img[1]: SV_BAND_MARGIN spare rows above and below, never read as data)
     for (int k = 1; k < ndev; ++k) {
@@ -1467,35 +1584,24 @@ int sv_depth_map_rows_scatter(sv_ctx* const* ctxs, sv_comm* const* comms, int nd
         const uint8_t* L = k ? c->img[0].as<uint8_t>() + shift : d_left;
         const uint8_t* R = k ? c->img[1].as<uint8_t>() + shift : d_right;
         SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
-        float* o_depth = d_depth;
-        float* o_disp = d_disparity;
-        uint8_t* o_norm = d_norm;
-        if (k > 0) {
-            SV_HIP(c->fa.ensure(n * sizeof(float)));
-            SV_HIP(c->fb.ensure(n * sizeof(float)));
-            SV_HIP(c->u8.ensure(n));
-            o_depth = c->fb.as<float>();
-            o_disp = c->fa.as<float>();
-            o_norm = c->u8.as<uint8_t>();
-        }
         rc = enqueue_disparity(c, L, R, H, W, pitch, min_disp, num_disp, win, cost, b.h0, b.h1,
                                c->d16.as<int16_t>(), W, s);
         if (rc) return rc;
-        sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
-                                      num_disp, o_depth, o_norm, nullptr);
-        rc = attach_lut(c, pp, s);
+        rc = band_median(c, k, H, W, b.r0, b.r1, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                         num_disp, d_depth, d_disparity, d_norm, s);
         if (rc) return rc;
-        SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(c->d16.as<int16_t>(), H, W, b.r0, b.r1, o_disp, pp, s));
         active.push_back(k);
         if (k > 0) {
             const size_t o = (size_t)b.r0 * W, m = (size_t)(b.r1 - b.r0) * W;
-            blocks[k] = {{d_depth + o, o_depth + o, m * sizeof(float)},
-                         {d_disparity + o, o_disp + o, m * sizeof(float)},
-                         {d_norm + o, o_norm + o, m}};
+            blocks[k] = {{root->gm16.as<int16_t>() + o, c->gm16.as<int16_t>() + o, m * sizeof(int16_t)}};
         }
     }
-    // 3. bands -> the root's full-frame outputs
-    return gather_blocks(ctxs, comms, ndev, blocks, active);
+    // 3. the peers' int16 x16 median bands -> the root (2 B/px), expanded there
+    rc = gather_blocks(ctxs, comms, ndev, blocks, active);
+    if (rc) return rc;
+    const size_t rr1 = (size_t)rows[0].r1 * W;
+    return expand_on_root(root, n - rr1, rr1, rr1, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                          num_disp, d_depth, d_disparity, d_norm);
 }
 
 int sv_band_rows_in(int H, int rank, int world, int win, int cost, int* out6) {

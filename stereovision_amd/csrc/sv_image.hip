@@ -346,9 +346,13 @@ __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g,
     // columns x0-r-1 .. x0+GT_W+r, clamped; every pixel the gradients below read (the
     // replicate-clamped window positions and their reflect-101 neighbours) lies inside
     const int sy0 = y0 - r - 1, sx0 = x0 - r - 1;
+    // rows below row1 + r feed only outputs at or past row1 (never stored): clamp the staging
+    // there too, so a band-only input buffer (rows [row0 - r - 1, row1 + r] + SV_BAND_MARGIN)
+    // is never read past its end when row1 - row0 is not a multiple of the tile height
+    const int ylast = min(H - 1, row1 + r);
     for (int i = threadIdx.x; i < (ny + 2) * (nx + 2); i += 256) {
         const int ty = i / (nx + 2), tx = i - ty * (nx + 2);
-        simg[ty][tx] = g[(size_t)clampi(sy0 + ty, 0, H - 1) * pitch + clampi(sx0 + tx, 0, W - 1)];
+        simg[ty][tx] = g[(size_t)clampi(sy0 + ty, 0, ylast) * pitch + clampi(sx0 + tx, 0, W - 1)];
     }
     __syncthreads();
     for (int i = threadIdx.x; i < nx * ny; i += 256) {
@@ -677,6 +681,62 @@ __device__ __forceinline__ PostVals post_median(const PostParams& pp, int mv) {
     return post_vals(pp, (float)mv / 16.0f);
 }
 
+// Post-processing of an int16 x16 median map (the value OpenCV's fixed-point disparity holds
+// after medianBlur, depth_map.py:909-912) into create_depth_map's outputs (depth_map.py:
+// 915-936) or the scaled app's (fused_depth_map.py:1010-1024): the median kernel's epilogue
+// as a pass of its own, for maps that crossed xGMI as 2 B/px (multi-GPU gathers).  8 pixels
+// per thread: one 16-B load, 2 x 16-B f32 stores per output, one 8-B u8 store; table lookup
+// as in the median epilogue (bit-identical).  Algorithmic bytes: 2 in + 9 out (DEPTH).
+__global__ __launch_bounds__(256) void k_post_m16(const int16_t* __restrict__ in, long long n,
+                                                  float* __restrict__ disp, PostParams pp) {
+    const long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
+    if (i0 >= n) return;
+    const bool vec = i0 + 8 <= n && ((((uintptr_t)in) & 15) | (((uintptr_t)disp | (uintptr_t)pp.out_a |
+                                                                  (uintptr_t)pp.out_b) & 15) |
+                                     ((uintptr_t)pp.out_u8 & 7)) == 0;
+    if (vec) {
+        const uint4 raw = *reinterpret_cast<const uint4*>(in + i0);
+        const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+        int mv[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            mv[2 * q] = (int)(int16_t)(w[q] & 0xFFFFu);
+            mv[2 * q + 1] = (int)(int16_t)(w[q] >> 16);
+        }
+        if (disp) {
+            float4* d = reinterpret_cast<float4*>(disp + i0);
+            d[0] = make_float4((float)mv[0] / 16.0f, (float)mv[1] / 16.0f, (float)mv[2] / 16.0f, (float)mv[3] / 16.0f);
+            d[1] = make_float4((float)mv[4] / 16.0f, (float)mv[5] / 16.0f, (float)mv[6] / 16.0f, (float)mv[7] / 16.0f);
+        }
+        if (pp.mode == POST_NONE) return;
+        PostVals o[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = post_median(pp, mv[q]);
+        float4* a = reinterpret_cast<float4*>(pp.out_a + i0);
+        a[0] = make_float4(o[0].a, o[1].a, o[2].a, o[3].a);
+        a[1] = make_float4(o[4].a, o[5].a, o[6].a, o[7].a);
+        uint32_t u[2] = {0u, 0u};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) u[q >> 2] |= (uint32_t)o[q].u << (8 * (q & 3));
+        *reinterpret_cast<uint2*>(pp.out_u8 + i0) = make_uint2(u[0], u[1]);
+        if (pp.mode == POST_SCALED) {
+            float4* b = reinterpret_cast<float4*>(pp.out_b + i0);
+            b[0] = make_float4(o[0].b, o[1].b, o[2].b, o[3].b);
+            b[1] = make_float4(o[4].b, o[5].b, o[6].b, o[7].b);
+        }
+        return;
+    }
+    for (long long i = i0; i < i0 + 8 && i < n; ++i) {
+        const int mv = (int)in[i];
+        if (disp) disp[i] = (float)mv / 16.0f;
+        if (pp.mode == POST_NONE) continue;
+        const PostVals o = post_median(pp, mv);
+        pp.out_a[i] = o.a;
+        pp.out_u8[i] = o.u;
+        if (pp.mode == POST_SCALED) pp.out_b[i] = o.b;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ in, int H, int W,
                                                     int row0, int row1, float* __restrict__ disp,
                                                     PostParams pp, long long fs_in, long long fs_out) {
@@ -687,7 +747,7 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
     if (blockIdx.z) {   // frame batch
         in += blockIdx.z * fs_in;
         const long long o = blockIdx.z * fs_out;
-        disp += o;
+        if (disp) disp += o;   // nullable (an int16-only median pass): keep it null
         if (pp.out_a) pp.out_a += o;
         if (pp.out_u8) pp.out_u8 += o;
         if (pp.out_b) pp.out_b += o;
@@ -1001,6 +1061,14 @@ int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float
     if ((long long)H * W >= (1LL << 30)) return (int)hipErrorInvalidValue;   // 32-bit offsets
     hipLaunchKernelGGL(k_median_i16, dim3((W + MQ_W - 1) / MQ_W, (row1 - row0 + MQ_H - 1) / MQ_H, nf),
                        dim3(256), 0, s, in, H, W, row0, row1, disp, pp, fs_in, fs_out);
+    return (int)hipGetLastError();
+}
+
+int launch_post_m16(const int16_t* in, long long n, float* disp, const PostParams& pp, hipStream_t s) {
+    if (n <= 0) return 0;
+    const long long blocks = (n + 8 * 256 - 1) / (8 * 256);
+    if (blocks > 0x7FFFFFFFLL) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_post_m16, dim3((unsigned)blocks), dim3(256), 0, s, in, n, disp, pp);
     return (int)hipGetLastError();
 }
 

@@ -242,6 +242,9 @@ int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float
                       const PostParams& pp, hipStream_t s, int nf = 1, long long fs_in = 0,
                       long long fs_out = 0);
 int launch_median_f32(const float* in, int H, int W, float* out, hipStream_t s);
+// The median kernel's post-processing epilogue over an int16 x16 median map of n pixels
+// (disp = m / 16 and the pp outputs, element-wise; the table must be attached).
+int launch_post_m16(const int16_t* in, long long n, float* disp, const PostParams& pp, hipStream_t s);
 int launch_post(const float* disp, int n, const PostParams& pp, hipStream_t s);
 // Evaluates the post-processing of pp.mode for m = m0 .. m0+n-1 (d = m/16) into the tables.
 int launch_post_lut(const PostParams& pp, int m0, int n, float* lut_a, uint8_t* lut_u8,

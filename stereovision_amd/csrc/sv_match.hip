@@ -798,6 +798,12 @@ __device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
 }
 
+// v_sad_u32 = |a - b| + c (unsigned).  No clang builtin, and the umax - umin + c pattern is
+// split into four ops inside the ring kernel's body, so inline asm (no hazards: plain VOP3).
+__device__ __forceinline__ void sad_u32_acc(uint32_t& a, uint32_t b, uint32_t c) {   // a = |a - b| + c
+    asm("v_sad_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+}
+
 // DEFER: a chunk's second step pair is not reduced at the chunk's end (where its DPP /
 // permlane chain ran alone before the next basic block) but in the next chunk's step 1,
 // beside that chunk's first pair: two independent reduce-scatter chains interleaved, +9
@@ -826,7 +832,15 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                                                         // branches between the steps)
     const int S = a.segm;                               // segment width per group (multiple of 4)
     const int WC = (64 / LPG) * S;
-    constexpr int U = 4 * W2;                           // steps per unrolled body
+    // SADU (r <= 4): the window update is ONE v_sad_u32 (key - leaving + entering), which
+    // reads the leaving column's cost after the entering one is computed, so the two cannot
+    // share a register: the cost ring gets M = W2 + 1 slots (the entering cost goes to the
+    // slot whose value left the window one step earlier) and keeps static register names.
+    // r 5 keeps the sub/add form (16 more ring VGPRs would spill), r 6..7 the packed form.
+    constexpr bool SADU = !PK && R <= 4;
+    constexpr int M = SADU ? W2 + 1 : W2;               // cost ring slots
+    constexpr int U = M % 4 == 0 ? M : M % 2 == 0 ? 2 * M : 4 * M;   // lcm(4, M) steps per body
+    constexpr int NCH = U / 4;                          // chunks per body
     // steps per segment: S outputs + 2r warm-up, in chunks of 4; whole bodies of U steps,
     // the first body entered at chunk e0 (its first e0 chunks skipped)
     const int Tn = (S + 2 * R + 3) & ~3;
@@ -883,9 +897,9 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
 #pragma unroll
         for (int q = 0; q < RQ; ++q) h[k][q] = base;
     }
-    uint32_t ring[W2][RG_DPL][RQ];
+    uint32_t ring[M][RG_DPL][RQ];
 #pragma unroll
-    for (int s = 0; s < W2; ++s)
+    for (int s = 0; s < M; ++s)
 #pragma unroll
         for (int k = 0; k < RG_DPL; ++k)
 #pragma unroll
@@ -964,23 +978,27 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     // shuffle the rings); the first body skips its first e0 chunks by a uniform branch
     for (int it = 0, t0 = -4 * e0; it < nit; ++it) {
 #pragma unroll
-        for (int ch = 0; ch < W2; ++ch, t0 += 4) {
+        for (int ch = 0; ch < NCH; ++ch, t0 += 4) {
             if (t0 < 0) continue;            // the first body's skipped chunks (uniform)
             uint32_t bk[4][2];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int slot = (4 * ch + u) % W2;
+                // the entering cost goes to `slot`, the leaving one (entered W2 steps ago)
+                // is read from `oslot`
+                const int slot = (4 * ch + u) % M, oslot = (4 * ch + u + 1) % M;
                 // this step's packs: L (every k) and the entering right column (k = 0 only)
                 rn[u] = ld<COST_SAD4, R, true>(rb + (ch * (RG_DPL + 1) + u));
                 const Pk<NW> Lc = Lnext;                 // loaded one step ahead
                 Lnext = ld<COST_SAD4, R, true>(lb + (4 * ch + u + 1));
-                // the leaving column's costs need no LDS data: subtract them while the loads
-                // are in flight; k = 0 (the fresh right pack) last
+                // !SADU: the leaving column's costs need no LDS data: subtract them while the
+                // loads are in flight; k = 0 (the fresh right pack) last
+                if constexpr (!SADU) {
 #pragma unroll
-                for (int k = 0; k < RG_DPL; ++k)
+                    for (int k = 0; k < RG_DPL; ++k)
 #pragma unroll
-                    for (int q = 0; q < RQ; ++q)
-                        h[k][q] = PK ? pk_sub16(h[k][q], ring[slot][k][q]) : h[k][q] - ring[slot][k][q];
+                        for (int q = 0; q < RQ; ++q)
+                            h[k][q] = PK ? pk_sub16(h[k][q], ring[slot][k][q]) : h[k][q] - ring[slot][k][q];
+                }
 #pragma unroll
                 for (int kk = 0; kk < RG_DPL; ++kk) {
                     const int k = RG_DPL - 1 - kk;
@@ -1007,7 +1025,12 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
                             const uint32_t c = __builtin_amdgcn_sad_hi_u8(Lc.w[NC + q], Rk.w[NC + q], cn);
-                            h[k][q] += c;
+                            // SADU: key - leaving + entering as ONE v_sad_u32 (|key - leaving|
+                            // + entering): the key holds the leaving column's cost as one of
+                            // its summands, so key >= leaving and the absolute value is the
+                            // plain difference (one VOP3 instead of a VOP2 sub + add)
+                            if constexpr (SADU) sad_u32_acc(h[k][q], ring[oslot][k][q], c);
+                            else h[k][q] += c;
                             ring[slot][k][q] = c;
                         }
                     }
@@ -1056,7 +1079,7 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                 }
             }
         }
-        rb = rb + W2 * (RG_DPL + 1);
+        rb = rb + NCH * (RG_DPL + 1);
         lb = lb + U;
     }
     if (DEFER) {   // the last chunk's second pair

@@ -37,7 +37,7 @@ import time
 
 import numpy as np
 
-from .engine import BAND_MARGIN, POST_DEPTH, POST_SCALED, Communicator, get_engine
+from .engine import BAND_MARGIN, POST_DEPTH, POST_NONE, POST_SCALED, Communicator, get_engine
 
 
 # ---- partition arithmetic -----------------------------------------------------------------
@@ -383,10 +383,14 @@ class RowTiledDepthMap:
     band-only (:meth:`scatter` from the root's full frame: rank k receives just the input rows
     [in0, in1) its band reads into :attr:`band_left` / :attr:`band_right`, then
     :meth:`compute` without arguments).  Each rank computes disparity for its band plus the
-    median halo (sv_disparity_dev), then median + post for the band (sv_median_post_dev);
-    :meth:`gather` moves the bands into rank 0's buffers.  Every operation is enqueued on
-    the engine's stream unless a stream is passed, so scatter -> compute -> gather are ordered
-    on one stream (the RCCL calls included).
+    median halo (sv_disparity_dev), then the median of the band (sv_median_post_m16_dev): its
+    int16 x16 medians (:attr:`m16`, full-frame row offsets) and, unless ``band_outputs="m16"``,
+    the post outputs too.  :meth:`gather` moves the bands' int16 x16 medians into the root's
+    :attr:`m16` (2 B/px over xGMI instead of the outputs' 9) and the root expands the other
+    ranks' rows into its full-frame outputs (sv_post_m16_dev).  Every operation is enqueued
+    on the engine's stream unless a stream is passed, so scatter -> compute -> gather are
+    ordered on one stream (the RCCL calls included); two instances on a communication stream
+    pipeline consecutive frames (bench.py --mode rowtile).
     """
 
     def __init__(self, H: int, W: int, num_disp: int, win: int, min_disp: int = 0,
@@ -404,7 +408,9 @@ class RowTiledDepthMap:
         self.out_a = e.dev_alloc(4 * n)
         self.out_b = e.dev_alloc(4 * n)
         self.out_u8 = e.dev_alloc(n)
+        self.m16 = e.dev_alloc(2 * n)
         self.rows = self.r1 - self.r0
+        self._post = None   # the post parameters of the last compute (the root's expansion)
         # band-only inputs: input rows [in0, in1) with BAND_MARGIN spare rows either side
         self.band_bytes = (self.in1 - self.in0) * W
         nb = self.band_bytes + 2 * BAND_MARGIN * W
@@ -424,10 +430,11 @@ class RowTiledDepthMap:
             pg.scatterv(full, offs, sizes, band, self.band_bytes, root=root, stream=s)
 
     def compute(self, d_left: int = 0, d_right: int = 0, mode: int = POST_DEPTH, min_depth: float = 0.3,
-                max_depth: float = 2.0, min_disp_global=None, stream: int = 0):
-        """Enqueue this rank's band; outputs at their full-frame row offsets of self.disp /
-        self.out_a / self.out_u8 (/ self.out_b for POST_SCALED).  d_left/d_right: full-frame
-        gray images, or 0 for the band buffers filled by :meth:`scatter`."""
+                max_depth: float = 2.0, min_disp_global=None, stream: int = 0, band_outputs: str = "full"):
+        """Enqueue this rank's band: int16 x16 medians at their full-frame row offsets of
+        self.m16 and (band_outputs="full") the outputs in self.disp / self.out_a / self.out_u8
+        (/ self.out_b for POST_SCALED).  d_left/d_right: full-frame gray images, or 0 for the
+        band buffers filled by :meth:`scatter`."""
         e, H, W = self.engine, self.H, self.W
         s = self._stream(stream)
         if not d_left:   # band buffer addressed as a full frame (row y at base + y * W)
@@ -436,23 +443,41 @@ class RowTiledDepthMap:
         e.disparity_dev(d_left, d_right, H, W, W, self.min_disp, self.num_disp, self.win, self.cost,
                         self.h0, self.h1, self.d16, W, stream=s)
         mdg = self.min_disp if min_disp_global is None else min_disp_global
-        e.median_post_dev(self.d16, H, W, self.r0, self.r1, mode, self.disp, self.out_a,
-                          self.out_u8, self.out_b if mode == POST_SCALED else 0,
-                          min_depth=min_depth, max_depth=max_depth, min_disp_global=mdg,
-                          min_disp=self.min_disp, num_disp=self.num_disp, stream=s)
+        self._post = dict(min_depth=min_depth, max_depth=max_depth, min_disp_global=mdg,
+                          min_disp=self.min_disp, num_disp=self.num_disp)
+        self._mode = mode
+        if band_outputs == "m16":
+            e.median_post_m16_dev(self.d16, H, W, self.r0, self.r1, POST_NONE, d_med16=self.m16, stream=s)
+        else:
+            e.median_post_m16_dev(self.d16, H, W, self.r0, self.r1, mode, d_disparity=self.disp,
+                                  d_out_a=self.out_a, d_out_u8=self.out_u8,
+                                  d_out_b=self.out_b if mode == POST_SCALED else 0, d_med16=self.m16,
+                                  stream=s, **self._post)
 
-    def gather(self, pg: "ProcessGroup", root: int = 0, stream: int = 0,
-               outputs=("disp", "out_a", "out_u8")):
-        """Bands of every rank into the root's full-frame buffers (in place), on the engine
-        stream unless `stream` is given (never the communicator's own stream: ADVICE r02)."""
+    def gather(self, pg: "ProcessGroup", root: int = 0, stream: int = 0, expand: bool = True):
+        """Every rank's band of int16 x16 medians into the root's self.m16 (in place, 2 B/px),
+        then (expand) the root turns the other ranks' rows into its full-frame outputs; on the
+        engine stream unless `stream` is given (never the communicator's own stream: ADVICE
+        r02).  The root's own band must have been computed with band_outputs="full"."""
         s = self._stream(stream)
-        for name in outputs:
-            elem = 1 if name == "out_u8" else 4
-            gather_rows(pg, getattr(self, name), self.H, self.W * elem, root=root, stream=s)
+        gather_rows(pg, self.m16, self.H, self.W * 2, root=root, stream=s)
+        if not expand or pg.rank != root or self._post is None:
+            return
+        e, W, mode = self.engine, self.W, self._mode
+        mr0, mr1 = band_rows(self.H, root, pg.world)
+        # the other ranks' bands are the rows above and below the root's own: <= 2 launches
+        for r0, r1 in ((0, mr0), (mr1, self.H)):
+            if r1 <= r0:
+                continue
+            o = r0 * W
+            e.post_m16_dev(self.m16 + 2 * o, (r1 - r0) * W, mode, d_disparity=self.disp + 4 * o,
+                           d_out_a=self.out_a + 4 * o, d_out_u8=self.out_u8 + o,
+                           d_out_b=(self.out_b + 4 * o) if mode == POST_SCALED else 0, stream=s,
+                           **self._post)
 
     def close(self):
-        for p in (self.d16, self.disp, self.out_a, self.out_b, self.out_u8, *self._band):
+        for p in (self.d16, self.disp, self.out_a, self.out_b, self.out_u8, self.m16, *self._band):
             if p:
                 self.engine.dev_free(p)
-        self.d16 = self.disp = self.out_a = self.out_b = self.out_u8 = 0
+        self.d16 = self.disp = self.out_a = self.out_b = self.out_u8 = self.m16 = 0
         self._band = []

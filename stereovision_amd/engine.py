@@ -48,7 +48,7 @@ EXPORTED = [
     "sv_median_post_color_dev", "sv_profile_region_begin", "sv_profile_region_end",
     "sv_comm_scatterv", "sv_depth_map_rows_scatter", "sv_band_rows_in", "sv_release_scratch",
     "sv_frame_stats_batch_dev", "sv_select_count_batch", "sv_select_ranks_batch", "sv_event_record",
-    "sv_stream_wait_event",
+    "sv_stream_wait_event", "sv_median_post_m16_dev", "sv_post_m16_dev", "sv_multi_gpu_m16_dev",
 ]
 BAND_MARGIN = 8   # SV_BAND_MARGIN: spare rows around a band-only input buffer
 COMM_ID_BYTES = 128
@@ -251,6 +251,15 @@ def _declare(lib):
                                         ctypes.POINTER(_c_int), _c_int, _c_int, _c_int,
                                         ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
                                         _c_float, _c_float, _c_float, _vp, _vp, _vp], _c_int),
+        "sv_median_post_m16_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                    _c_float, _c_float, _c_float, _c_int, _c_int, _vp, _vp, _vp,
+                                    _vp, _vp, _vp], _c_int),
+        "sv_post_m16_dev": ([_vp, _vp, ctypes.c_int64, _c_int, _c_float, _c_float, _c_float,
+                             _c_float, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp], _c_int),
+        "sv_multi_gpu_m16_dev": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
+                                  ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                  ctypes.POINTER(_c_int), _c_int, _c_int, _c_int,
+                                  ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _vp], _c_int),
         "sv_depth_map_rows_multi": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
                                      ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int, _c_int, _c_int,
                                      _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float,
@@ -716,6 +725,28 @@ class Engine:
             np.float32(min_disp_global), int(min_disp), int(num_disp), d_disparity,
             d_out_a or None, d_out_u8 or None, d_out_b or None, stream or None))
 
+    def median_post_m16_dev(self, d_disp16: int, H: int, W: int, row0: int, row1: int, mode: int,
+                            d_disparity: int = 0, d_out_a: int = 0, d_out_u8: int = 0,
+                            d_out_b: int = 0, d_med16: int = 0, min_depth=0.0, max_depth=0.0,
+                            min_disp_global=0.0, min_disp=0, num_disp=0, stream: int = 0):
+        """sv_median_post_m16_dev: median of rows [row0, row1) plus (mode) the post outputs
+        and/or the int16 x16 medians d_med16 (full-frame offsets)."""
+        _check("sv_median_post_m16_dev", self.lib.sv_median_post_m16_dev(
+            self._h, d_disp16, H, W, int(row0), int(row1), int(mode), np.float32(min_depth),
+            np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
+            np.float32(min_disp_global), int(min_disp), int(num_disp), d_disparity or None,
+            d_out_a or None, d_out_u8 or None, d_out_b or None, d_med16 or None, stream or None))
+
+    def post_m16_dev(self, d_med16: int, n: int, mode: int, d_disparity: int = 0, d_out_a: int = 0,
+                     d_out_u8: int = 0, d_out_b: int = 0, min_depth=0.0, max_depth=0.0,
+                     min_disp_global=0.0, min_disp=0, num_disp=0, stream: int = 0):
+        """sv_post_m16_dev: n int16 x16 medians -> disparity (m / 16) and mode's outputs."""
+        _check("sv_post_m16_dev", self.lib.sv_post_m16_dev(
+            self._h, d_med16, int(n), int(mode), np.float32(min_depth), np.float32(max_depth),
+            np.float32(float(max_depth) - float(min_depth)), np.float32(min_disp_global),
+            int(min_disp), int(num_disp), d_disparity or None, d_out_a or None, d_out_u8 or None,
+            d_out_b or None, stream or None))
+
     def median_post_color_dev(self, d_disp16: int, H: int, W: int, row0: int, row1: int, mode: int,
                               cmap_bgr: np.ndarray, d_disparity: int, d_out_a: int, d_out_u8: int,
                               d_bgr: int, d_out_b: int = 0, min_depth=0.0, max_depth=0.0,
@@ -1048,8 +1079,9 @@ def multi_gpu_depth_map_dev(engines, comms, d_left, d_right, n_frames, H: int, W
                             d_norm: int, cost="sad", min_disp_global=None):
     """C4 on device-resident frames from ONE process (sv_multi_gpu_depth_map_dev): engine k
     runs create_depth_map over its n_frames[k] frames (its own device), and every output
-    frame is gathered to engines[0]'s device (d_depth/d_disp/d_norm, context order) over
-    RCCL (`comms`: Communicator list, rank k on engines[k]'s device) or peer copies (None).
+    frame ends up on engines[0]'s device (d_depth/d_disp/d_norm, context order): the peers'
+    int16 x16 medians cross over RCCL (`comms`: Communicator list, rank k on engines[k]'s
+    device) or peer copies (None), 2 B/px, and engines[0] expands them.
     Enqueue only: synchronize engines[0] before reading the outputs."""
     engines = list(engines)
     nd = len(engines)
@@ -1060,6 +1092,22 @@ def multi_gpu_depth_map_dev(engines, comms, d_left, d_right, n_frames, H: int, W
         _handles(engines), ch, nd, _ptrs(d_left), _ptrs(d_right), nf, H, W, pitch,
         int(frame_stride), int(min_disp), int(num_disp), int(win), _cost(cost),
         *_depth_args(min_depth, max_depth, min_disp, min_disp_global), d_depth, d_disp, d_norm))
+
+
+def multi_gpu_m16_dev(engines, comms, d_left, d_right, n_frames, H: int, W: int, pitch: int,
+                      frame_stride: int, min_disp: int, num_disp: int, win: int, d_med16: int,
+                      cost="sad"):
+    """C4 as north_star states it (sv_multi_gpu_m16_dev): engine k computes disparity +
+    median over its n_frames[k] frames, and only the int16 x16 median maps (2 B/px) are
+    gathered into d_med16 on engines[0]'s device (context order).  Enqueue only."""
+    engines = list(engines)
+    nd = len(engines)
+    lib = engines[0].lib
+    ch = None if comms is None else _handles([c.handle for c in comms])
+    nf = (_c_int * nd)(*[int(v) for v in n_frames])
+    _check("sv_multi_gpu_m16_dev", lib.sv_multi_gpu_m16_dev(
+        _handles(engines), ch, nd, _ptrs(d_left), _ptrs(d_right), nf, H, W, pitch,
+        int(frame_stride), int(min_disp), int(num_disp), int(win), _cost(cost), d_med16))
 
 
 def depth_map_rows_multi(engines, comms, d_left, d_right, H: int, W: int, pitch: int, min_disp: int,

@@ -24,8 +24,9 @@ import numpy as np
 import pytest
 
 import sv_oracle_c as C
-from stereovision_amd.engine import (Communicator, Engine, device_count, depth_map_rows_multi,
-                                     multi_gpu_depth_map_dev)
+from stereovision_amd.engine import (POST_DEPTH, POST_NONE, POST_SCALED, Communicator, Engine,
+                                     device_count, depth_map_rows_multi, multi_gpu_depth_map_dev,
+                                     multi_gpu_m16_dev)
 from stereovision_amd.synthetic import stereo_pair
 
 pytestmark = pytest.mark.gpu
@@ -92,6 +93,79 @@ def test_multi_gpu_depth_map_dev_gathers_every_frame(ctxs, ndev, counts, cost, w
             e.dev_free(b)
         for p in (o_depth, o_disp, o_norm):
             root.dev_free(p)
+
+
+@pytest.mark.parametrize("ndev,counts", [(8, [2, 1, 0, 3, 1, 1, 2, 1]), (3, [0, 2, 1]), (1, [2])])
+def test_multi_gpu_m16_dev_gathers_int16_medians(ctxs, ndev, counts):
+    """sv_multi_gpu_m16_dev: only the int16 x16 medians cross (2 B/px); they equal the C
+    oracle's median map x 16 frame by frame, in context order."""
+    H, W, D, win = 37, 300, 64, 9
+    es = ctxs[:ndev]
+    total = sum(counts)
+    frames = [stereo_pair(H, W, D, seed=900 + f)[:2] for f in range(total)]
+    dLs, dRs, f0 = [], [], 0
+    for e, n in zip(es, counts):
+        Ls = np.stack([frames[f0 + z][0] for z in range(n)]) if n else np.zeros((1, H, W), np.uint8)
+        Rs = np.stack([frames[f0 + z][1] for z in range(n)]) if n else np.zeros((1, H, W), np.uint8)
+        dLs.append(_upload(e, Ls))
+        dRs.append(_upload(e, Rs))
+        f0 += n
+    root = es[0]
+    d_m16 = root.dev_alloc(2 * H * W * total)
+    try:
+        for _ in range(2):
+            multi_gpu_m16_dev(es, None, dLs, dRs, counts, H, W, W, H * W, 0, D, win, d_m16)
+            root.synchronize()
+        m16 = root.to_host(d_m16, (total, H, W), np.int16)
+        for f, (L, R) in enumerate(frames):
+            e_disp = _oracle(L, R, D, win)[0]
+            np.testing.assert_array_equal(m16[f], (e_disp * 16).astype(np.int16), err_msg=f"frame {f}")
+    finally:
+        for e, a, b in zip(es, dLs, dRs):
+            e.dev_free(a)
+            e.dev_free(b)
+        root.dev_free(d_m16)
+
+
+@pytest.mark.parametrize("mode", [POST_DEPTH, POST_SCALED, POST_NONE])
+def test_post_m16_dev_equals_median_epilogue(engine, mode):
+    """sv_post_m16_dev over the int16 x16 medians reproduces the median kernel's own
+    epilogue byte for byte (the root's expansion of gathered maps), including a ragged
+    pixel count and an output offset that defeats the 16-byte vector path."""
+    H, W, D, win, md = 41, 203, 48, 7, -3
+    L, R, _ = stereo_pair(H, W, D, seed=77)
+    e, n = engine, H * W
+    dL, dR = _upload(e, L), _upload(e, R)
+    bufs = [e.dev_alloc(4 * n + 64) for _ in range(6)] + [e.dev_alloc(n + 64), e.dev_alloc(n + 64),
+                                                          e.dev_alloc(2 * n + 64), e.dev_alloc(2 * n)]
+    disp_a, a_a, b_a, disp_b, a_b, b_b, u_a, u_b, m16, d16 = bufs
+    try:
+        e.disparity_dev(dL, dR, H, W, W, md, D, win, "sad", 0, H, d16, W)
+        kw = dict(min_depth=0.3, max_depth=2.0, min_disp_global=md, min_disp=md, num_disp=D)
+        scaled = mode == POST_SCALED
+        e.median_post_m16_dev(d16, H, W, 0, H, mode, d_disparity=disp_a,
+                              d_out_a=a_a if mode else 0, d_out_u8=u_a if mode else 0,
+                              d_out_b=b_a if scaled else 0, d_med16=m16, **kw)
+        for off in (0, 4):   # element offset 4: 16-B f32 stores misaligned -> scalar path
+            e.post_m16_dev(m16 + 2 * off, n - off, mode, d_disparity=disp_b + 4 * off,
+                           d_out_a=(a_b + 4 * off) if mode else 0, d_out_u8=(u_b + off) if mode else 0,
+                           d_out_b=(b_b + 4 * off) if scaled else 0, **kw)
+            e.synchronize()
+            got = e.to_host(disp_b, (n,), np.float32)[off:]
+            np.testing.assert_array_equal(got, e.to_host(disp_a, (n,), np.float32)[off:])
+            if mode:
+                np.testing.assert_array_equal(e.to_host(a_b, (n,), np.float32)[off:],
+                                              e.to_host(a_a, (n,), np.float32)[off:])
+                np.testing.assert_array_equal(e.to_host(u_b, (n,), np.uint8)[off:],
+                                              e.to_host(u_a, (n,), np.uint8)[off:])
+            if scaled:
+                np.testing.assert_array_equal(e.to_host(b_b, (n,), np.float32)[off:],
+                                              e.to_host(b_a, (n,), np.float32)[off:])
+        np.testing.assert_array_equal(e.to_host(m16, (n,), np.int16).astype(np.float32) / np.float32(16),
+                                      e.to_host(disp_a, (n,), np.float32))
+    finally:
+        for p in (dL, dR, *bufs):
+            e.dev_free(p)
 
 
 def _rows_multi(es, comms, L, R, D, win, cost="sad"):
@@ -274,8 +348,8 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("mode", ["frames", "rowtile"])
-def test_bench_under_torch_distributed_run_two_ranks(mode):
+@pytest.mark.parametrize("mode,root_outputs", [("frames", "m16"), ("frames", "full"), ("rowtile", "m16")])
+def test_bench_under_torch_distributed_run_two_ranks(mode, root_outputs):
     """The driver's N>1 launch: torch.distributed.run starts 2 bench.py workers (torch-free).
     On a 1-GPU box both ranks share the GPU, so the group falls back to the file store (RCCL
     refuses two ranks on one device); on a multi-GPU box it is RCCL.  The gather is on by
@@ -285,7 +359,7 @@ def test_bench_under_torch_distributed_run_two_ranks(mode):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
            "--steps", "3", "--warmup", "1", "--height", "96", "--width", "400", "--num-disp", "64",
            "--frames", "2", "--batch", "2", "--mode", mode, "--no-live-pmc", "--no-aux",
-           "--no-host-path", "--no-cpu-baseline", "--hang-timeout", "90"]
+           "--no-host-path", "--no-cpu-baseline", "--hang-timeout", "90", "--root-outputs", root_outputs]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     import json
@@ -303,8 +377,44 @@ def test_bench_under_torch_distributed_run_two_ranks(mode):
     checked = res["verify"]["checked"]
     if mode == "frames":     # both ranks' first and last frame, from rank 0's gathered stacks
         assert sum("gathered on rank 0" in c for c in checked) == 4, checked
+        assert d["gather_bytes_per_step"] == 2 * 96 * 400 * 2 * 1     # 2 B/px, B frames, 1 peer
+        full = root_outputs == "full"
+        assert d["root_outputs"] == root_outputs
+        assert sum("expanded on rank 0" in c for c in checked) == (2 if full else 0), checked
+        assert (d["root_expand_us_per_step"] is not None) == full
     else:
         assert checked == ["full frame gathered on rank 0"]
+
+
+@pytest.mark.parametrize("ngpu,mode,root_outputs", [(2, "frames", "m16"), (3, "frames", "full"),
+                                                    (4, "rowtile", "m16")])
+def test_bench_one_process_rehearsal(ngpu, mode, root_outputs):
+    """`bench.py --gpus N` without a launcher (ONE process drives N GPUs: the gather lanes, two
+    context sets, sv_multi_gpu_m16_dev / sv_multi_gpu_depth_map_dev / sv_depth_map_rows_scatter)
+    on N logical GPUs of this box (--rehearse: contexts of the visible devices, gathers as
+    device copies): runs end to end and every gathered map of the last step is bit-exact
+    against the C oracle; the line reports 2 B/px of gather traffic."""
+    H, W, B = 96, 400, 2
+    cmd = [sys.executable, "bench.py", "--gpus", str(ngpu), "--rehearse", "--steps", "3",
+           "--warmup", "1", "--height", str(H), "--width", str(W), "--num-disp", "64",
+           "--frames", "4", "--batch", str(B), "--mode", mode, "--root-outputs", root_outputs,
+           "--no-live-pmc", "--no-aux", "--no-host-path", "--no-cpu-baseline", "--hang-timeout", "90"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    import json
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["n_gpus"] == ngpu and res["verified"] is True, res["verify"]
+    d = res["distributed"]
+    assert d["process_model"] == "one process, all devices" and d["gather"] is True
+    checked = res["verify"]["checked"]
+    if mode == "frames":
+        assert len(checked) == 2 * ngpu, checked
+        assert d["gather_bytes_per_step"] == 2 * H * W * B * (ngpu - 1)
+        assert d["root_outputs"] == root_outputs
+        assert (d["root_expand_us_per_step"] is not None) == (root_outputs == "full")
+    else:
+        assert checked == ["full frame gathered on device 0"]
+        assert d["root_outputs"] == "full" and d["root_expand_us_per_step"] is not None
 
 
 def test_bench_single_gpu_verifies_its_timed_outputs():

@@ -5,7 +5,7 @@
 // HOG winner-take-all engine specified in DESIGN.md ("Semantics").  Output: int16 = d*16,
 // invalid = (minD-1)*16 outside the matched band [X0, X1).
 //
-// Work decomposition (one wave = ROWS output rows (1 or 2), one run of output columns):
+// Work decomposition (one wave = ROWS output rows (1 or 4), one run of output columns):
 //   * the wave is split into G = 64/LPG groups of LPG lanes; group g walks its segment of
 //     S columns left to right;
 //   * lane l of a group owns the DPL consecutive disparities d = minD + l*DPL + k, so the
@@ -25,9 +25,9 @@
 //     before one coalesced store per lane.
 // Cost kinds:
 //   SAD   1 row/wave, pack = ceil(win/4) byte dwords, ceil(win/4) v_sad_u8 per column cell;
-//   SAD2  2 rows/wave (rows y, y+1) for 5 <= win <= 9: a pack holds the 2r shared middle
-//         rows + row y-r and row y+r+1 as single-byte dwords, so the two cells of a column
-//         cost ceil(2r/4) + 2 v_sad_u8 instead of 2*ceil(win/4) (win 9: 4 instead of 6);
+//   SAD4  4 rows/wave for win >= 5: packs of the 2r-2 rows the four windows share + one
+//         word per row for its 3 others; the metric configs run the ring kind below
+//         (k_match_ring: a register ring of entering-column costs, v_sad_u32 updates);
 //   SSD   v_dot4_u32_u8: sum (L-R)^2 = sum L^2 + sum R^2 - 2 sum L*R (squares per pack);
 //   HOG   9-bin u16 window histograms as packs compared with v_sad_u16 (no running window).
 #include "sv_internal.h"
@@ -42,7 +42,6 @@
 namespace sv {
 namespace {
 
-constexpr int COST_SAD2 = 3;          // internal kind: SAD, two output rows per wave
 constexpr int COST_SAD4 = 4;          // internal kind: SAD, four output rows per wave
 
 // Segment width per lane group: 4*LPG columns rounded up to a multiple of DPL so that
@@ -67,15 +66,14 @@ int seg_mult(int kind, int r) {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
 
-// A column pack holds NW live dwords inside a 16*Q-byte LDS slot.  ND is the kind's width
-// parameter: byte dwords (SAD, SSD), shared dwords (SAD2), unused (HOG).
+// A column pack holds NW live dwords inside a 16*Q-byte LDS slot.
 template <int COST, int ND> struct PackCfg {
-    // ND is the kind's width parameter: byte dwords (SAD, SSD), shared dwords (SAD2), the
-    // window radius r (SAD4: ceil((2r-2)/4) common dwords + 4 per-row dwords)
-    static constexpr int NW = COST == COST_SAD ? ND : COST == COST_SSD ? ND + 1 : COST == COST_SAD2 ? ND + 2
+    // ND is the kind's width parameter: byte dwords (SAD, SSD), unused (HOG), the window
+    // radius r (SAD4: ceil((2r-2)/4) common dwords + 4 per-row dwords)
+    static constexpr int NW = COST == COST_SAD ? ND : COST == COST_SSD ? ND + 1
                             : COST == COST_SAD4 ? (2 * ND - 2 + 3) / 4 + 4 : 5;
     static constexpr int Q = (NW + 3) / 4;
-    static constexpr int ROWS = COST == COST_SAD2 ? 2 : COST == COST_SAD4 ? 4 : 1;
+    static constexpr int ROWS = COST == COST_SAD4 ? 4 : 1;
     // waves per block: the 4-row kind's packs are large, one wave per block lets the LDS
     // hold as many waves as the register file does
     static constexpr int WPB = COST == COST_SAD4 ? 1 : 4;
@@ -157,7 +155,7 @@ __device__ __forceinline__ void put(PackOut<COST, ND> p, const uint32_t (&w)[8])
     }
 }
 
-// Column cost(s) of one (left pack, right pack) pair: v[0] (and v[1] = row y+1 for SAD2).
+// Column cost(s) of one (left pack, right pack) pair: v[0] (v[0..3]: the four rows of SAD4).
 template <int COST, int ND, int NW>
 __device__ __forceinline__ void ccol(const Pk<NW>& l, const Pk<NW>& r, uint32_t* v) {
     if constexpr (COST == COST_SAD) {
@@ -165,12 +163,6 @@ __device__ __forceinline__ void ccol(const Pk<NW>& l, const Pk<NW>& r, uint32_t*
 #pragma unroll
         for (int i = 0; i < ND; ++i) a = __builtin_amdgcn_sad_u8(l.w[i], r.w[i], a);
         v[0] = a;
-    } else if constexpr (COST == COST_SAD2) {
-        uint32_t s = 0u;
-#pragma unroll
-        for (int i = 0; i < ND; ++i) s = __builtin_amdgcn_sad_u8(l.w[i], r.w[i], s);
-        v[0] = __builtin_amdgcn_sad_u8(l.w[ND], r.w[ND], s);
-        v[1] = __builtin_amdgcn_sad_u8(l.w[ND + 1], r.w[ND + 1], s);
     } else if constexpr (COST == COST_SAD4) {
         constexpr int NC = NW - 4;
         uint32_t s = 0u;
@@ -207,23 +199,6 @@ __device__ __forceinline__ void build_pack(const MatchParams& a, const uint8_t* 
         const uint32_t* src = reinterpret_cast<const uint32_t*>(hist + ((size_t)y * a.W + cc) * 10);
         const uint32_t w[8] = {src[0], src[1], src[2], src[3], src[4], 0u, 0u, 0u};
         put<COST, ND>(dst, w);
-    } else if constexpr (COST == COST_SAD2) {
-        // rows y-r .. y+r+1: j = 0 -> word ND (row y only), j = 2r+1 -> word ND+1 (row y+1
-        // only), j in [1, 2r] -> shared word (j-1)/4
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        const int last = 2 * a.r + 1;
-        for (int j = 0; j <= last; ++j) {
-            const int yy = clampi(y - a.r + j, 0, a.H - 1);
-            const uint32_t v = img[(size_t)yy * a.pitch + cc];
-            const int q = j == 0 ? ND : j == last ? ND + 1 : (j - 1) >> 2;
-            const uint32_t sh = (j == 0 || j == last) ? v : v << (8 * ((j - 1) & 3));
-            w[0] |= q == 0 ? sh : 0u;
-            w[1] |= q == 1 ? sh : 0u;
-            w[2] |= q == 2 ? sh : 0u;
-            w[3] |= q == 3 ? sh : 0u;
-        }
-        const uint32_t o[8] = {w[0], w[1], w[2], w[3], 0u, 0u, 0u, 0u};
-        put<COST, ND>(dst, o);
     } else if constexpr (COST == COST_SAD4) {
         // rows y-r .. y+r+3 (j = 0 .. 2r+3): j in [3, 2r] -> common word (j-3)/4; the 3
         // rows of output q outside the common block -> byte positions of word ND+q
@@ -318,23 +293,15 @@ __device__ __forceinline__ void build_group(const MatchParams& a, const uint8_t*
         }
         return;
     }
-    constexpr int J0 = COST == COST_SAD2 ? 1 : 0;            // first shared row
-    const int nsh = COST == COST_SAD2 ? 2 * r : a.win;       // shared (transposed) rows
+    const int nsh = a.win;                                   // transposed rows
 #pragma unroll
     for (int q = 0; q < ND; ++q) {
         uint32_t d[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) d[t] = (4 * q + t < nsh) ? row(J0 + 4 * q + t) : 0u;
+        for (int t = 0; t < 4; ++t) d[t] = (4 * q + t < nsh) ? row(4 * q + t) : 0u;
         transpose4(d[0], d[1], d[2], d[3], w[q]);
     }
-    if constexpr (COST == COST_SAD2) {
-        const uint32_t s0 = row(0), s1 = row(2 * r + 1);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            w[ND][k] = (s0 >> (8 * k)) & 0xFFu;
-            w[ND + 1][k] = (s1 >> (8 * k)) & 0xFFu;
-        }
-    } else if constexpr (COST == COST_SSD) {
+    if constexpr (COST == COST_SSD) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             uint32_t sq = 0u;
@@ -586,7 +553,7 @@ __device__ __forceinline__ void reduce_scatter8_bm(uint32_t (&v)[8], int l) {
 // Occupancy target: LDS admits ~3 blocks/CU for the common configs (D <= 128, win <= 11),
 // so cap registers at 3 waves/SIMD (<= 168 VGPRs); the widest packs get 2 waves/SIMD.
 template <int COST, int ND> struct Occ {
-    static constexpr int W = COST == COST_SAD4 ? 2 : (COST == COST_SAD || COST == COST_SAD2 || ND <= 3) ? 3 : 2;
+    static constexpr int W = COST == COST_SAD4 ? 2 : (COST == COST_SAD || ND <= 3) ? 3 : 2;
 };
 
 template <int COST, int ND, int DPL>
@@ -782,8 +749,9 @@ __global__ __launch_bounds__((64 * PackCfg<COST, ND>::WPB), (Occ<COST, ND>::W)) 
 // 4 cells).  Here each lane owns RG_DPL = 4 consecutive disparities and keeps the entering
 // column's four row costs (hi-shifted, as in the key) in a register ring of W2 = 2r+1 steps,
 // so the leaving column's costs are read back instead of recomputed: a step costs 6 v_sad_hi
-// + 4 v_sub + 4 v_add per 4 cells.  Both rings (the W2-step cost ring and the 4-deep right
-// pack ring) have static register indices inside a body of lcm(4, W2) = 4*W2 unrolled steps.
+// + 4 v_sad_u32 per 4 cells (key = |key - leaving| + entering; r 5 on 16/64-lane groups: 4
+// v_sub + 4 v_add).  Both rings (the M-slot cost ring and the 4-deep right pack ring) have
+// static register indices inside a body of lcm(4, M) unrolled steps.
 // The first 2r steps of a segment fill the window (ring starts at zero) and emit nothing.
 // Keys are (cost << 16) | idx; padding disparities (idx >= D)
 // start at cost 0x8000, above every real window cost (<= 121*255 = 30855 for win 11).
@@ -836,8 +804,11 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     // reads the leaving column's cost after the entering one is computed, so the two cannot
     // share a register: the cost ring gets M = W2 + 1 slots (the entering cost goes to the
     // slot whose value left the window one step earlier) and keeps static register names.
-    // r 5 keeps the sub/add form (16 more ring VGPRs would spill), r 6..7 the packed form.
-    constexpr bool SADU = !PK && R <= 4;
+    // r 5: 16 more ring VGPRs spill 4-9 VGPRs, which still pays for 32-lane groups (1080p
+    // D=128 win 11: 572 -> 555 us per 16 frames) but not for 16-lane ones (VGA D=64 win 11:
+    // 122 -> 139 us), so those and the unmeasured 64-lane groups keep the sub/add form;
+    // r 6..7 the packed form.
+    constexpr bool SADU = !PK && (R <= 4 || (R == 5 && LPGT == 32));
     constexpr int M = SADU ? W2 + 1 : W2;               // cost ring slots
     constexpr int U = M % 4 == 0 ? M : M % 2 == 0 ? 2 * M : 4 * M;   // lcm(4, M) steps per body
     constexpr int NCH = U / 4;                          // chunks per body
@@ -1124,12 +1095,6 @@ template <int COST>
 int launch_nd(const MatchParams& a, const MatchPlan& p, size_t lds, hipStream_t s) {
     if constexpr (COST == COST_HOG) {
         return launch_dpl<COST, 5>(a, p, lds, s);
-    } else if constexpr (COST == COST_SAD2) {
-        switch (p.ndw) {
-            case 1: return launch_dpl<COST, 1>(a, p, lds, s);
-            case 2: return launch_dpl<COST, 2>(a, p, lds, s);
-        }
-        return (int)hipErrorInvalidValue;
     } else if constexpr (COST == COST_SAD4) {
         switch (p.ndw) {   // = r
             case 2: return launch_dpl<COST, 2>(a, p, lds, s);
@@ -1151,17 +1116,8 @@ int launch_nd(const MatchParams& a, const MatchPlan& p, size_t lds, hipStream_t 
     }
 }
 
-// Kind actually launched for a public cost: SAD with win >= 5 runs four rows per wave
-// (SV_SAD_ROWS=2 / 1 select the two-row kind for 5 <= win <= 9 / the one-row kind, for A/B
-// measurements).
+// Kind actually launched for a public cost: SAD with win >= 5 runs four rows per wave.
 int kind_of(int cost, int win) {
-    static const int rows = [] {
-        const char* e = std::getenv("SV_SAD_ROWS");
-        const int v = e ? std::atoi(e) : 4;
-        return v == 1 || v == 2 ? v : 4;
-    }();
-    if (cost == COST_SAD && rows == 1) return COST_SAD;
-    if (cost == COST_SAD && win >= 5 && win <= 9 && rows == 2) return COST_SAD2;
     if (cost == COST_SAD && win >= 5) return COST_SAD4;
     return cost;
 }
@@ -1261,633 +1217,6 @@ int launch_ring(const MatchParams& a0, hipStream_t s) {
 }
 
 
-// ---- stream kind: persistent waves walking whole rows (SAD, win 5..9, 65 <= D <= 256) -------
-// The ring kind above spends 2r warm-up steps per segment of S = 128 columns (6% of its steps
-// at the metric config) because a segment's right packs (S + D + 2r of them) must fit in LDS
-// at once, and its 30k waves per 16-frame launch leave a partly filled last round.  Here a
-// launch is exactly as many waves as the chip holds (8 per CU) and each wave takes an equal
-// contiguous share of the launch's work, measured in bodies of U = 4*W2 steps of a row bundle
-// (G = 64/LPG vertically adjacent row quads, one per lane group, walking the same columns in
-// lockstep).  Packs live in per-group LDS rings that are refilled one body ahead:
-//   * at the top of a body every producer lane issues the global loads of one 4-column unit
-//     of the NEXT body's packs (2r+4 dword rows; right units of group gg, then left units);
-//   * the body's U steps run exactly as in the ring kind (static register rings, one basic
-//     block);
-//   * at the bottom the units are transposed into packs and written to the rings.
-// A row starts with a burst build of the packs its first body needs (the right stream needs
-// D + 3 packs of history per lane group); the running window sums need no reset (a window
-// sum is exactly the sum of its ring entries), only the first 2r steps of a row emit nothing.
-// A wave whose share starts inside a row first runs a prologue of the 2r (rounded to 4)
-// steps before it, without reductions or stores.  Rows are padded to whole bodies.
-// Right ring: position p <-> column xR0 + p of the bundle's row, slot phys(p mod RL) with one
-// empty slot per 4 (phase c0: every lane's chunk reads 4 consecutive slots, 16 lanes of a
-// group on distinct banks), the first TPR slots mirrored after the period so a body's reads
-// never wrap.  Left ring: position s <-> column xL0 + s, broadcast reads, TL slots mirrored.
-struct StreamParams {
-    const uint8_t* img;        // min(L, R): one buffer resource covers both images
-    int offL, offR;            // byte offsets of L and R from img (host-checked < 2^31)
-    int img_span;              // bytes from img through the end of the later image
-    int16_t* out;
-    int H, W, pitch, opitch;
-    int minD, D, X0, X1, row0, row1;
-    long long fs_in, fs_out;
-    int xl0, xr0, delta, c0;   // stream origins (4-aligned), right read offset, gap phase
-    int nb;                    // bodies per row bundle
-    int nq, nbund;             // row quads / bundles per frame
-    long long total;           // bodies of the launch (nf * nbund * nb)
-    int dbg;                   // SV_STREAM_DBG ablations (timing only, results wrong): 1 no
-                               // producer, 4 no bursts, 8 no output stores
-    unsigned long long* trace; // SV_STREAM_TRACE (diagnostic): per wave {start, end, HW_ID, XCC}
-    // work: bodies [0, t_static) in equal contiguous shares, then segments of `seg` bodies of
-    // [t_static, total) handed out by ctr[0] (ctr[1] counts finished waves; the last resets)
-    long long t_static;
-    int seg;
-    unsigned* ctr;
-};
-
-template <int R, int LPG> struct StreamCfg {
-    static constexpr int W2 = 2 * R + 1, U = 4 * W2, G = 64 / LPG;
-    static constexpr int PRE = (2 * R + 3) / 4 * 4;                 // prologue steps
-    static constexpr int RL = (4 * (LPG - 1) + U + PRE + 9 + 3) & ~3;   // right ring positions
-    static constexpr int RPER = RL + RL / 4;                         // ... slots per period
-    static constexpr int TPR = 5 * W2;                               // mirrored slots
-    static constexpr int RSL = RPER + TPR;
-    static constexpr int LL = (U + PRE + 3 + 3) & ~3;                // left ring positions
-    static constexpr int LPER = LL + LL / 4;                         // ... slots (1 gap per 4)
-    static constexpr int TL = 5 * W2;                                // mirrored slots
-    static constexpr int LSL = LPER + TL;
-    static constexpr int GROUP_BYTES = 24 * (RSL + LSL);
-    static constexpr int LDS_BYTES = G * GROUP_BYTES;
-    static constexpr int NROW = 2 * R + 4;                          // image rows of a pack
-};
-
-// Unit geometry of a producer lane: which group's ring, which image, which unit column.
-struct StreamUnit {
-    int gg;        // group whose ring receives the unit (-1: idle lane)
-    int right;     // 1: right image / ring
-    int col;       // first image column of the unit (4-aligned, may lie outside [0, W))
-    int yq;        // top output row of the group's row quad
-};
-
-// Loads of one unit: NROW dwords, rows clamp(yq - R + j), columns clamp(col, 0, W - 4) (the
-// edge bytes are replicated by stream_store's v_perm when the unit crosses an image border).
-// ONE load per row through one resource covering both images (per-lane image offset), so
-// the loaded registers are not touched until the transposes at the end of the body.  One
-// code path for every row (clamped offsets, 2 VALU per row): a uniform fast/border branch
-// around the loads made the compiler's wait counters assume the other path's loads might
-// be in flight, and wait for every outstanding store (vmcnt(0)) at the top of each body.
-template <int R>
-__device__ __forceinline__ void stream_load(const StreamParams& p, __amdgpu_buffer_rsrc_t rs, const StreamUnit& u,
-                                            uint32_t (&rw)[2 * R + 4]) {
-    constexpr int NROW = 2 * R + 4;
-    const int OOR = 0x7FFF0000;
-    const int io = (u.right ? p.offR : p.offL) + clampi(u.col, 0, p.W - 4);
-    // every offset first (plain selects, 24-bit multiplies), then the loads back to back: an
-    // offset computed into a register that an earlier load of the sequence still writes made
-    // the compiler wait for that load (a memory latency at the top of every body)
-    int off[NROW];
-#pragma unroll
-    for (int j = 0; j < NROW; ++j) {
-        const int o = io + __mul24(clampi(u.yq - R + j, 0, p.H - 1), p.pitch);
-        off[j] = u.gg >= 0 ? o : OOR;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NROW; ++j) rw[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, off[j], 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-// v_perm selector replicating the edge bytes of a unit that starts at column `col`
-__device__ __forceinline__ uint32_t stream_edge_sel(int col, int W) {
-    const int cl = clampi(col, 0, W - 4);
-    uint32_t sel = 0u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) sel |= (uint32_t)(clampi(col + i, 0, W - 1) - cl) << (8 * i);
-    return sel;
-}
-
-// Ring slots of a unit's 4 packs (positions 4 m .. 4 m + 3 of its stream) and the writes,
-// mirrored slots included (idle lanes write nothing).
-template <int R, int LPG>
-__device__ __forceinline__ void stream_store(char* lds, const StreamUnit& u, int m, int c0, uint32_t (&rw)[2 * R + 4],
-                                             bool edges, int W) {
-    using C = StreamCfg<R, LPG>;
-    constexpr int NC = PackCfg<COST_SAD4, R>::NC, NCR = 2 * R - 2;
-    if (edges) {   // a unit of this batch may cross an image border (uniform)
-        const uint32_t sel = stream_edge_sel(u.col, W);
-#pragma unroll
-        for (int j = 0; j < 2 * R + 4; ++j) rw[j] = __builtin_amdgcn_perm(rw[j], rw[j], sel);
-    }
-    // slot offsets of the 4 packs (main array; the common array at +cofs, half the stride)
-    // and of their mirrors (-1: not mirrored).  Both rings keep one empty slot per 4
-    // positions, so the 16 lanes of a b128 write pass (units 4 positions apart) land 5 slots
-    // = 80 B apart, on distinct banks; idle lanes and unmirrored slots do not write at all
-    const int gb = u.gg * C::GROUP_BYTES;
-    int s0[4], s1[4];
-    const int cofs = u.right ? 16 * C::RSL : 16 * C::LSL;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (u.right) {
-            const int q = (4 * m) % C::RL + k;
-            const int ph = q + ((q + c0) >> 2);
-            s0[k] = ph;
-            s1[k] = ph < C::TPR ? ph + C::RPER : -1;
-        } else {
-            const int q = (4 * m) % C::LL + k;
-            const int ph = q + (q >> 2);
-            s0[k] = ph;
-            s1[k] = ph < C::TL ? ph + C::LPER : -1;
-        }
-    }
-    const bool act = u.gg >= 0;
-    // every loaded row is consumed here on every path (the transposes below feed stores that
-    // idle lanes skip; sunk into those branches, a load left pending on the skip path made
-    // the compiler wait for it at the top of the next body)
-#pragma unroll
-    for (int j = 0; j < 2 * R + 4; ++j) asm volatile("" : "+v"(rw[j]));
-    const int abase = gb + (u.right ? 0 : 24 * C::RSL);
-    // common words first (rows 3 .. 2r), written before the custom words are formed: the
-    // unit's live registers stay near NROW + 8 while the body's register rings are live
-    {
-        uint32_t w[NC][4];
-#pragma unroll
-        for (int mm = 0; mm < NC; ++mm) {
-            uint32_t d[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) d[t] = 4 * mm + t < NCR ? rw[3 + 4 * mm + t] : 0u;
-            transpose4(d[0], d[1], d[2], d[3], w[mm]);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint2 v = make_uint2(w[0][k], NC > 1 ? w[NC > 1 ? 1 : 0][k] : 0u);
-            if (act) *reinterpret_cast<uint2*>(lds + abase + cofs + 8 * s0[k]) = v;
-            if (act && s1[k] >= 0) *reinterpret_cast<uint2*>(lds + abase + cofs + 8 * s1[k]) = v;
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    {
-        uint32_t w[4][4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t d[3];
-            int n = 0;
-#pragma unroll
-            for (int j = q; j <= 2; ++j) d[n++] = rw[j];
-#pragma unroll
-            for (int j = 2 * R + 1; j <= 2 * R + q; ++j) d[n++] = rw[j];
-            transpose4(d[0], d[1], d[2], 0u, w[q]);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint4 v = make_uint4(w[0][k], w[1][k], w[2][k], w[3][k]);
-            if (act) *reinterpret_cast<uint4*>(lds + abase + 16 * s0[k]) = v;
-            if (act && s1[k] >= 0) *reinterpret_cast<uint4*>(lds + abase + 16 * s1[k]) = v;
-        }
-    }
-}
-
-template <int R, int LPG>
-__global__ __launch_bounds__(64, 2) void k_match_stream(StreamParams p) {
-    using P = PackCfg<COST_SAD4, R>;
-    using C = StreamCfg<R, LPG>;
-    constexpr int NW = P::NW, NC = P::NC, W2 = C::W2, U = C::U, G = C::G;
-    constexpr int RQ = 4;
-    static_assert(LPG >= 32 && R >= 2 && R <= 4, "stream kind: LPG 32/64, r 2..4");
-    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    char* lds = reinterpret_cast<char*>(smem);
-    const int lane = threadIdx.x;
-    const int g = lane / LPG, l = lane & (LPG - 1);
-    const int band = p.X1 - p.X0;
-
-    const unsigned long long t_start = p.trace ? wall_clock64() : 0ull;
-    // this wave's static share: bodies [b_lo, b_hi) of [0, t_static); then dynamic segments
-    // of the rest (the two waves of a SIMD do not progress equally: oldest-first issue lets
-    // one finish ~30% before the other, whose tail then runs alone on the SIMD)
-    long long b_lo = p.t_static * (long long)blockIdx.x / gridDim.x;
-    long long b_hi = p.t_static * (long long)(blockIdx.x + 1) / gridDim.x;
-    const long long s_lo = b_lo, s_len = max(1ll, b_hi - b_lo);
-
-    // per-lane constants of the step loop
-    const int dl = p.delta - 4 * l;                      // right position offset of the lane
-    uint32_t h[RG_DPL][RQ], ring[W2][RG_DPL][RQ];
-    const int jq = (lane >> 2) & 3, ju = (lane >> 1) & 1;
-    int pofs;
-    {
-        const auto pp = __builtin_amdgcn_permlane16_swap((uint32_t)lane, (uint32_t)lane + 64u, false, false);
-        pofs = (max(pp[0], pp[1]) < 64u) ? 0 : 2;
-    }
-    const int el0 = p.xl0 + ju + pofs - R - p.X0;        // + step: column - X0 of the lane's pair
-    const bool emit_lane = (l & 1) == 0 && l < 32;   // LPG 64: rows 0, 1 of the group
-    // producer lane roles (fixed): unit kk of group gg, right units first
-    const int NUR = W2 + ((p.delta & 3) ? 1 : 0);
-    const int per_g = NUR + W2;
-    const int pg_ = lane / per_g, pk_ = lane % per_g;
-    const bool prod = pg_ < G;
-    const int p_right = pk_ < NUR ? 1 : 0;
-    const int p_k = p_right ? pk_ : pk_ - NUR;
-
-    const int gbase = g * C::GROUP_BYTES;
-    const int rmain = gbase, rcom = gbase + 16 * C::RSL;
-    const int lmain = gbase + 24 * C::RSL, lcom = lmain + 16 * C::LSL;
-
-    Pk<NW> rn[RG_DPL], Lnext;
-    for (;;) {
-    if (b_lo >= b_hi) {   // next dynamic segment
-        unsigned k = 0;
-        if (lane == 0) k = atomicAdd(p.ctr, 1u);
-        k = __builtin_amdgcn_readfirstlane(k);
-        b_lo = p.t_static + (long long)k * p.seg;
-        if (b_lo >= p.total) break;
-        b_hi = min(p.total, b_lo + p.seg);
-    }
-    long long b = b_lo;
-    bool first_row = true;
-    while (b < b_hi) {
-        // ---- row setup -------------------------------------------------------------------
-        const long long bund = b / p.nb;
-        const int jb0 = (int)(b - bund * p.nb);
-        const long long b_end = min(b_hi, (bund + 1) * (long long)p.nb);
-        const int frame = (int)(bund / p.nbund);
-        const int bq = (int)(bund - (long long)frame * p.nbund);
-        const int yq = p.row0 + (bq * G + g) * 4;            // this lane's group row quad
-        const bool gvalid = bq * G + g < p.nq;
-        const auto rsI = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.img + frame * p.fs_in), 0, p.img_span,
-                                                          0x00020000);
-        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(p.out + frame * p.fs_out, 0, 0x7FFFFFFF, 0x00020000);
-        // producer lane's unit rows
-        const int p_yq = p.row0 + (bq * G + min(pg_, G - 1)) * 4;
-        // emission: lane's output offset at step 0 and its column window
-        const int band_l = (gvalid && yq + jq < p.row1) ? band : 0;
-        const int ooff0 = 2 * ((yq + jq) * p.opitch + p.xl0 + ju + pofs - R);
-
-        __syncthreads();   // the previous row's reads are done before its rings are rebuilt
-        if (jb0 == 0) {     // invalid columns outside the matched band, rows of every group
-            const int ninv = p.X0 + (p.W - p.X1);
-            const int16_t inv = (int16_t)((p.minD - 1) * 16);
-            for (int i = lane; i < G * 4 * ninv; i += 64) {
-                const int gq = i / ninv, c = i - gq * ninv;
-                const int x = c < p.X0 ? c : p.X1 + (c - p.X0);
-                const int y = p.row0 + (bq * G + gq / 4) * 4 + (gq & 3);
-                if (bq * G + gq / 4 < p.nq && y < p.row1)
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)inv, orsrc, 2 * (y * p.opitch + x), 0, 0);
-            }
-        }
-        // ---- burst: the packs of the first (partial) body --------------------------------
-        const int pre = (jb0 > 0 && first_row) ? C::PRE : 0;
-        const int s_first = jb0 * U - pre;                 // first step this wave runs in the row
-        const int s_end = jb0 * U + U;                     // ... through the end of its first body
-        {
-            const int r_lo = (s_first + p.delta - 4 * (LPG - 1) - 3) >> 2;   // right units
-            const int r_hi = (s_end + p.delta + 3) >> 2;
-            const int l_lo = s_first >> 2, l_hi = (s_end + 3) >> 2;          // left units
-            const int nr = r_hi - r_lo, nl = l_hi - l_lo, nug = nr + nl;
-            // at most 2 units per lane (G * nug <= 128), both loaded before either is used:
-            // one memory latency per burst
-            const int nall = (p.dbg & 4) ? 0 : G * nug;
-            StreamUnit u[2];
-            int um[2];
-            uint32_t rw[2][C::NROW];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int i = lane + 64 * t;
-                const int gg = i / nug, kk = i - gg * nug;
-                u[t].gg = i < nall ? gg : -1;
-                u[t].right = kk < nr ? 1 : 0;
-                um[t] = u[t].right ? r_lo + kk : l_lo + (kk - nr);
-                u[t].col = (u[t].right ? p.xr0 : p.xl0) + 4 * um[t];
-                u[t].yq = p.row0 + (bq * G + min(gg, G - 1)) * 4;
-                stream_load<R>(p, rsI, u[t], rw[t]);
-            }
-#pragma unroll
-            for (int t = 0; t < 2; ++t) stream_store<R, LPG>(lds, u[t], um[t], p.c0, rw[t], true, p.W);
-        }
-        __syncthreads();
-        // running window state of the row, (re)started after the burst so the previous row's
-        // state is dead while the burst holds its unit registers (a window sum is the sum of
-        // its ring entries: keys idx + 0, padding disparities idx + 0x8000 << 16)
-#pragma unroll
-        for (int k = 0; k < RG_DPL; ++k) {
-            const int idx = 4 * l + k;
-            const uint32_t base = idx < p.D ? (uint32_t)idx : (0x8000u << 16) | (uint32_t)idx;
-#pragma unroll
-            for (int q = 0; q < RQ; ++q) h[k][q] = base;
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < W2; ++s2)
-#pragma unroll
-            for (int k = 0; k < RG_DPL; ++k)
-#pragma unroll
-                for (int q = 0; q < RQ; ++q) ring[s2][k][q] = 0u;
-        // register rings of the first step: rn[4 - k] = right pack of step s_first - k
-        {
-            int q = (s_first % C::RL) + dl;
-            q = q >= C::RL ? q - C::RL : q;
-            const int ph = q + ((q + p.c0) >> 2);
-#pragma unroll
-            for (int k = 1; k < RG_DPL; ++k) {
-                int a = ph - k - 1;
-                a = a < 0 ? a + C::RPER : a;
-                const PackPtr<COST_SAD4, R> rp{reinterpret_cast<const uint4*>(lds + rmain) + a,
-                                               reinterpret_cast<const typename P::CT*>(lds + rcom) + a};
-                rn[RG_DPL - k] = ld<COST_SAD4, R, true>(rp);
-            }
-        }
-        // ---- prologue: the window's 2r steps before a share that starts inside a row -----
-        if (pre) {
-            int q = (s_first % C::RL) + dl;
-            q = q >= C::RL ? q - C::RL : q;
-            const int ph = q + ((q + p.c0) >> 2);
-            const PackPtr<COST_SAD4, R> rb{reinterpret_cast<const uint4*>(lds + rmain) + ph,
-                                           reinterpret_cast<const typename P::CT*>(lds + rcom) + ph};
-            const int lq = s_first % C::LL, lph = lq + (lq >> 2);
-            const PackPtr<COST_SAD4, R> lb{reinterpret_cast<const uint4*>(lds + lmain) + lph,
-                                           reinterpret_cast<const typename P::CT*>(lds + lcom) + lph};
-#pragma unroll
-            for (int c = 0; c < C::PRE / 4; ++c) {
-                const int ch = W2 - C::PRE / 4 + c;       // ring slots of the body's last chunks
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int slot = (4 * ch + u) % W2;
-                    rn[u] = ld<COST_SAD4, R, true>(rb + (5 * c + u));
-                    const Pk<NW> Lc = ld<COST_SAD4, R, true>(lb + (5 * c + u));
-#pragma unroll
-                    for (int k = 0; k < RG_DPL; ++k)
-#pragma unroll
-                        for (int q2 = 0; q2 < RQ; ++q2) h[k][q2] -= ring[slot][k][q2];
-#pragma unroll
-                    for (int k = 0; k < RG_DPL; ++k) {
-                        const Pk<NW>& Rk = rn[(u - k) & 3];
-                        uint32_t cn = 0u;
-#pragma unroll
-                        for (int i = 0; i < NC; ++i) cn = __builtin_amdgcn_sad_hi_u8(Lc.w[i], Rk.w[i], cn);
-#pragma unroll
-                        for (int q2 = 0; q2 < 4; ++q2) {
-                            const uint32_t cc = __builtin_amdgcn_sad_hi_u8(Lc.w[NC + q2], Rk.w[NC + q2], cn);
-                            h[k][q2] += cc;
-                            ring[slot][k][q2] = cc;
-                        }
-                    }
-                }
-            }
-        }
-        first_row = false;
-
-        // ---- bodies ----------------------------------------------------------------------
-        for (int jb = jb0; b < b_end; ++b, ++jb) {
-            const int s_b = jb * U;
-            const bool has_next = b + 1 < b_end;
-            if (p.dbg & 16) {
-                // wave priority from the static share's progress: behind -> higher priority,
-                // so oldest-first issue does not let the older waves of a SIMD run ahead
-                const int q = __builtin_amdgcn_readfirstlane((int)(min(4ll, (b - s_lo) * 4 / s_len)));
-                if (q == 0) __builtin_amdgcn_s_setprio(3);
-                else if (q == 1) __builtin_amdgcn_s_setprio(2);
-                else if (q == 2) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
-            // producer unit of the next body: loads now, transposes + writes after the steps
-            StreamUnit pu;
-            pu.gg = (prod && has_next && !(p.dbg & 1)) ? pg_ : -1;
-            pu.right = p_right;
-            const int pm = p_right ? ((s_b + U + p.delta) >> 2) + p_k : ((s_b + U) >> 2) + p_k;
-            pu.col = (p_right ? p.xr0 : p.xl0) + 4 * pm;
-            // laundered per body: the border path's 2r+4 clamped row offsets must not be
-            // hoisted out of the body loop (they would hold 2r+4 VGPRs for the whole row)
-            int pyq = p_yq;
-            asm volatile("" : "+v"(pyq));
-            pu.yq = pyq;
-            // units of this batch crossing an image border (uniform): their edge bytes are
-            // replicated in stream_store
-            const int rc_lo = p.xr0 + 4 * ((s_b + U + p.delta) >> 2), rc_hi = rc_lo + 4 * NUR;
-            const int lc_lo = p.xl0 + s_b + U, lc_hi = lc_lo + 4 * W2;
-            const bool edges = rc_lo < 0 || rc_hi > p.W || lc_lo < 0 || lc_hi > p.W;
-            // unconditional (a body without a next one loads nothing: out-of-range offsets)
-            // so the wait counters see every load consumed in the same iteration; a load
-            // under a branch made the compiler wait for every store (vmcnt 0) at the next
-            // body's top
-            uint32_t praw[C::NROW];
-            stream_load<R>(p, rsI, pu, praw);
-
-            // ring bases of this body
-            int q = (s_b % C::RL) + dl;
-            q = q >= C::RL ? q - C::RL : q;
-            const int ph = q + ((q + p.c0) >> 2);
-            const PackPtr<COST_SAD4, R> rb{reinterpret_cast<const uint4*>(lds + rmain) + ph,
-                                           reinterpret_cast<const typename P::CT*>(lds + rcom) + ph};
-            const int lq = s_b % C::LL, lph = lq + (lq >> 2);
-            const PackPtr<COST_SAD4, R> lb{reinterpret_cast<const uint4*>(lds + lmain) + lph,
-                                           reinterpret_cast<const typename P::CT*>(lds + lcom) + lph};
-            Lnext = ld<COST_SAD4, R, true>(lb);
-            const int eb = el0 + s_b;
-            const int ob = ooff0 + 2 * s_b;
-            const int emax = (emit_lane && !(p.dbg & 8)) ? band_l : 0;
-#pragma unroll
-            for (int ch = 0; ch < W2; ++ch) {
-                // a uniform branch that never skips: one basic block per chunk (as in the ring
-                // kind) lets the register allocator keep r = 4 at ~225 VGPRs; the whole body
-                // as one block needed > 256
-                if (s_b + 4 * ch < 0) continue;
-                uint32_t bk[4][2];
-                uint32_t kA = 0u;
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int slot = (4 * ch + u) % W2;
-                    rn[u] = ld<COST_SAD4, R, true>(rb + (5 * ch + u));
-                    const Pk<NW> Lc = Lnext;
-                    if (ch < W2 - 1 || u < 3) Lnext = ld<COST_SAD4, R, true>(lb + (5 * ch + u + 1 + (u == 3 ? 1 : 0)));
-#pragma unroll
-                    for (int k = 0; k < RG_DPL; ++k)
-#pragma unroll
-                        for (int q2 = 0; q2 < RQ; ++q2) h[k][q2] -= ring[slot][k][q2];
-#pragma unroll
-                    for (int kk = 0; kk < RG_DPL; ++kk) {
-                        const int k = RG_DPL - 1 - kk;
-                        const Pk<NW>& Rk = rn[(u - k) & 3];
-                        uint32_t cn = 0u;
-#pragma unroll
-                        for (int i = 0; i < NC; ++i) cn = __builtin_amdgcn_sad_hi_u8(Lc.w[i], Rk.w[i], cn);
-#pragma unroll
-                        for (int q2 = 0; q2 < 4; ++q2) {
-                            const uint32_t cc = __builtin_amdgcn_sad_hi_u8(Lc.w[NC + q2], Rk.w[NC + q2], cn);
-                            h[k][q2] += cc;
-                            ring[slot][k][q2] = cc;
-                        }
-                    }
-#pragma unroll
-                    for (int q2 = 0; q2 < 4; ++q2) bk[q2][u & 1] = min(min(h[0][q2], h[1][q2]), min(h[2][q2], h[3][q2]));
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (u & 1) {
-                        uint32_t v[8];
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) v[i] = bk[i >> 1][i & 1];
-                        reduce_scatter8_bm(v, lane & 15);
-                        if (u == 1) {
-                            kA = v[0];
-                        } else {   // pair (0,1) in kA, pair (2,3) in v[0]: one swap joins both
-                            auto pr = __builtin_amdgcn_permlane16_swap(kA, v[0], false, false);
-                            uint32_t key = min(pr[0], pr[1]);
-                            if (LPG == 64) {
-                                pr = __builtin_amdgcn_permlane32_swap(key, key, false, false);
-                                key = min(pr[0], pr[1]);
-                            }
-                            const int tt = 4 * ch;
-                            const int off = (unsigned)(eb + tt) < (unsigned)emax ? ob + 2 * tt : (int)0x80000000u;
-                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + p.minD) * 16),
-                                                                  orsrc, off, 0, 0);
-                        }
-                    }
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            stream_store<R, LPG>(lds, pu, pm, p.c0, praw, edges, p.W);
-            // the next body reads what this one wrote: LDS instructions of one wave execute
-            // in order, so only the compiler needs fencing (no s_barrier / lgkmcnt(0) wait)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    b_lo = b_hi;   // range done
-    }
-    if (lane == 0) {   // the last wave out resets the counters for the next launch
-        if (atomicAdd(p.ctr + 1, 1u) == gridDim.x - 1) {
-            atomicExch(p.ctr, 0u);
-            atomicExch(p.ctr + 1, 0u);
-        }
-    }
-    if (p.trace && lane == 0) {
-        unsigned hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        unsigned long long* t = p.trace + 4 * blockIdx.x;
-        t[0] = t_start;
-        t[1] = wall_clock64();
-        t[2] = hw;
-        t[3] = xcc;
-    }
-}
-
-// Stream kind eligibility (opt-in, SV_STREAM=1): SAD with 5 <= win <= 9, 65 <= D <= 256,
-// 4-aligned images and widths (dword unit loads), 32-bit output offsets.  Off by default:
-// measured at the metric config it issues the same VALU instructions as the ring kind
-// (325.3 M per 16-frame launch; the in-loop pack transposes cost what the warm-up saved)
-// at a lower issue rate (more LDS bank conflicts): 590 vs 547 us per launch (profiles/r03b).
-bool stream_kind(const MatchParams& a) {
-    const char* e = std::getenv("SV_STREAM");   // read per launch: tests switch it in-process
-    const bool on = e && e[0] == '1';
-    if (!on || a.win < 5 || a.win > 9 || a.D <= 64 || a.D > 256 || (a.W & 3) || (a.pitch & 3) || a.X1 - a.X0 < 4 ||
-        ((reinterpret_cast<uintptr_t>(a.L) | reinterpret_cast<uintptr_t>(a.R)) & 3u))
-        return false;
-    // one 32-bit buffer resource spans both images of every frame of the batch
-    const long long gap = a.L < a.R ? (long long)(a.R - a.L) : (long long)(a.L - a.R);
-    const long long span = gap + (long long)(a.H - 1) * a.pitch + a.W + (long long)((a.nf > 1 ? a.nf : 1) - 1) * a.fs_in;
-    return span < 0x7FFF0000LL;
-}
-
-int device_cus() {
-    static const int n = [] {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) != hipSuccess) return 256;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) return 256;
-        return v;
-    }();
-    return n;
-}
-
-template <int R, int LPG>
-int launch_stream_rl(const MatchParams& a, hipStream_t s) {
-    using C = StreamCfg<R, LPG>;
-    StreamParams p{};
-    const uint8_t* lo = a.L < a.R ? a.L : a.R;
-    p.img = lo;
-    p.offL = (int)(a.L - lo);
-    p.offR = (int)(a.R - lo);
-    p.img_span = (int)(std::max(p.offL, p.offR) + (long long)(a.H - 1) * a.pitch + a.W);
-    p.out = a.out;
-    p.H = a.H;
-    p.W = a.W;
-    p.pitch = a.pitch;
-    p.opitch = a.opitch;
-    p.minD = a.minD;
-    p.D = a.D;
-    p.X0 = a.X0;
-    p.X1 = a.X1;
-    p.row0 = a.row0;
-    p.row1 = a.row1;
-    p.fs_in = a.fs_in;
-    p.fs_out = a.fs_out;
-    static const int dbg = [] {
-        const char* e = std::getenv("SV_STREAM_DBG");
-        return e ? std::atoi(e) : 0;
-    }();
-    p.dbg = dbg;
-    p.xl0 = (a.X0 - R) & ~3;                                   // floor to a multiple of 4
-    p.xr0 = (p.xl0 - a.minD - 4 * (LPG - 1) - 3) & ~3;
-    p.delta = p.xl0 - a.minD - p.xr0;
-    p.c0 = (4 - (p.delta & 3)) & 3;
-    const int ns = a.X1 + R - p.xl0;                           // steps through the last output
-    p.nb = (ns + C::U - 1) / C::U;
-    p.nq = (a.row1 - a.row0 + 3) / 4;
-    p.nbund = (p.nq + C::G - 1) / C::G;
-    const int nf = a.nf > 1 ? a.nf : 1;
-    p.total = (long long)nf * p.nbund * p.nb;
-    const int per_cu = std::min(8, (160 * 1024) / C::LDS_BYTES);
-    // SV_STREAM_BODIES=<k> (A/B): k bodies per wave, as many waves as that takes (the
-    // hardware schedules them), instead of one persistent wave per slot
-    static const int bodies = [] {
-        const char* e = std::getenv("SV_STREAM_BODIES");
-        return e ? std::atoi(e) : 0;
-    }();
-    long long waves = std::min<long long>(p.total, (long long)per_cu * device_cus());
-    if (bodies > 0) waves = (p.total + bodies - 1) / bodies;
-    // static share / dynamic tail split (SV_STREAM_DYN: percent of the bodies handed out
-    // dynamically, SV_STREAM_SEG: bodies per dynamic segment; A/B tuning)
-    static const int dyn_pct = [] {
-        const char* e = std::getenv("SV_STREAM_DYN");
-        const int v = e ? std::atoi(e) : 20;
-        return v < 0 ? 0 : v > 100 ? 100 : v;
-    }();
-    static const int seg = [] {
-        const char* e = std::getenv("SV_STREAM_SEG");
-        const int v = e ? std::atoi(e) : 2;
-        return v < 1 ? 1 : v;
-    }();
-    p.seg = seg;
-    p.t_static = (waves < 64 || bodies > 0) ? p.total : p.total - p.total * dyn_pct / 100;
-    p.ctr = a.work_ctr;
-    // SV_STREAM_TRACE=<file> (diagnostic): per-wave start / end clocks and hardware ids of
-    // every launch appended to <file> (the launch is waited for)
-    static const char* trace_path = std::getenv("SV_STREAM_TRACE");
-    static unsigned long long* trace_buf = nullptr;
-    if (trace_path && !trace_buf && hipMalloc(&trace_buf, 4 * 8 * 65536) != hipSuccess) trace_buf = nullptr;
-    p.trace = (trace_path && waves <= 65536) ? trace_buf : nullptr;
-    hipLaunchKernelGGL((k_match_stream<R, LPG>), dim3((unsigned)waves), dim3(64), C::LDS_BYTES, s, p);
-    const int e = (int)hipGetLastError();
-    if (!e && p.trace) {
-        std::vector<unsigned long long> h((size_t)4 * waves);
-        if (hipMemcpyAsync(h.data(), trace_buf, h.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
-            hipStreamSynchronize(s) == hipSuccess) {
-            if (FILE* f = std::fopen(trace_path, "ab")) {
-                const long long hdr[2] = {waves, p.total};
-                std::fwrite(hdr, sizeof(hdr), 1, f);
-                std::fwrite(h.data(), 8, h.size(), f);
-                std::fclose(f);
-            }
-        }
-    }
-    return e;
-}
-template <int R>
-int launch_stream_r(const MatchParams& a, hipStream_t s) {
-    return a.D <= 128 ? launch_stream_rl<R, 32>(a, s) : launch_stream_rl<R, 64>(a, s);
-}
-int launch_stream(const MatchParams& a, hipStream_t s) {
-    switch (a.r) {
-        case 2: return launch_stream_r<2>(a, s);
-        case 3: return launch_stream_r<3>(a, s);
-        case 4: return launch_stream_r<4>(a, s);
-    }
-    return (int)hipErrorInvalidValue;
-}
 }  // namespace
 
 uint64_t max_cost(int win, int cost) {
@@ -1907,7 +1236,7 @@ int plan_match(int num_disp, int win, int cost, MatchPlan* plan) {
     plan->dpl = menu[i][0];
     plan->lpg = menu[i][1];
     const int kind = kind_of(cost, win);
-    plan->ndw = kind == COST_HOG ? 5 : kind == COST_SAD2 ? (win - 1 + 3) / 4 : kind == COST_SAD4 ? win / 2
+    plan->ndw = kind == COST_HOG ? 5 : kind == COST_SAD4 ? win / 2
               : (win + 3) / 4;
     int n = plan->dpl * plan->lpg - 1, bits = 0;
     while (n > 0) { ++bits; n >>= 1; }
@@ -1923,7 +1252,7 @@ int plan_match(int num_disp, int win, int cost, MatchPlan* plan) {
 
 size_t match_lds_bytes(const MatchPlan& p, int r, int cost) {
     const int kind = kind_of(cost, 2 * r + 1);
-    const int nw = kind == COST_SAD ? p.ndw : kind == COST_SSD ? p.ndw + 1 : kind == COST_SAD2 ? p.ndw + 2
+    const int nw = kind == COST_SAD ? p.ndw : kind == COST_SSD ? p.ndw + 1
                  : kind == COST_SAD4 ? (2 * p.ndw - 2 + 3) / 4 + 4 : 5;
     const int wpb = kind == COST_SAD4 ? 1 : 4;
     const bool split = (kind == COST_SAD4 && nw - 4 <= 3) || kind == COST_HOG || (kind == COST_SSD && nw == 5);
@@ -1957,7 +1286,6 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
     // (2 * (row * out_pitch + x) per frame); maps whose last row lies past 2^31 bytes take
     // the size_t-addressed four-row kind instead
     const bool ring_fits = 2LL * ((long long)(a.row1 + 3) * a.opitch + a.W + 64) < 0x7FFFFFFFLL;
-    if (ring_kind(cost, a.win, a.D) && ring_fits && stream_kind(a)) return launch_stream(a, s);
     if (ring_kind(cost, a.win, a.D) && ring_fits) return launch_ring(a, s);
     const size_t lds = match_lds_bytes(p, a.r, cost);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
@@ -1965,7 +1293,6 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
     b.segm = seg_mult(kind_of(cost, a.win), a.r);
     switch (kind_of(cost, a.win)) {
         case COST_SAD: return launch_nd<COST_SAD>(b, p, lds, s);
-        case COST_SAD2: return launch_nd<COST_SAD2>(b, p, lds, s);
         case COST_SAD4: return launch_nd<COST_SAD4>(b, p, lds, s);
         case COST_SSD: return launch_nd<COST_SSD>(b, p, lds, s);
         case COST_HOG: return launch_nd<COST_HOG>(b, p, lds, s);

@@ -67,7 +67,7 @@ struct RemapArgs {
     size_t src_bytes;         // bytes of one source frame: (sH-1)*spitch + sW*CN
     bool aligned;             // source frames start on a dword: dword-span fast path allowed
     bool vec;                 // W % 4 == 0 and 16/8-byte aligned maps: vector map loads
-    bool xcd_map;             // XCD-aware row order (sv_xcd.h; opt-in SV_XCD_REMAP=1)
+    bool xcd_map;             // XCD-aware row order (sv_xcd.h); off (see launch_remap)
 };
 
 // Bytes [p, p+n) of a row as a little-endian 64-bit value, from dword loads (n <= 6 needs
@@ -312,13 +312,10 @@ int launch_remap(const uint8_t* src, int sH, int sW, int channels, int spitch, l
     a.src_bytes = (size_t)(sH - 1) * spitch + (size_t)sW * channels;
     a.aligned = (((uintptr_t)src | (uintptr_t)sfs) & 3) == 0;
     a.vec = (W & 3) == 0 && ((uintptr_t)map1 & 15) == 0 && ((uintptr_t)map2 & 7) == 0;
-    // opt-in (SV_XCD_REMAP=1): measured 82-83 vs 85 us per 16-frame BGR->gray batch, but 51.4
-    // vs 49.0 us per 8-frame batch inside the two-camera pipeline (gpurun_out/remap1)
-    static const bool xcd = [] {
-        const char* e = std::getenv("SV_XCD_REMAP");
-        return e && e[0] == '1';
-    }();
-    a.xcd_map = xcd;
+    // plain dispatch order: an XCD-aware row order measured 82-83 vs 85 us per 16-frame
+    // BGR->gray batch alone but 51.4 vs 49.0 us per 8-frame batch inside the two-camera
+    // pipeline (round 3, gpurun_out/remap1), so it was dropped
+    a.xcd_map = false;
     dim3 grid((W + 4 * 256 - 1) / (4 * 256), H, nf);
     if (channels == 1)
         hipLaunchKernelGGL((k_remap<1, false>), grid, dim3(256), 0, s, a);

@@ -795,11 +795,15 @@ def main():
             elif B == 1 and not med_o:
                 e.depth_map_dev(dL[k] + f * n_px, dR[k] + f * n_px, H, W, W, 0, D, win, 0.3, 2.0,
                                 depth_o[k], disp_o[k], norm_o[k], cost=args.cost)
+            elif harris and not rectify and not med_o:   # Harris blocks inside the median launch
+                e.depth_map_batch_dev(dL[k] + f * n_px, dR[k] + f * n_px, B, H, W, W, n_px, 0, D, win,
+                                      0.3, 2.0, depth_o[k], disp_o[k], norm_o[k], cost=args.cost,
+                                      d_harris=hmaps_l[i % nstreams][k])
             else:
                 e.depth_map_batch_dev(dL[k] + f * n_px, dR[k] + f * n_px, B, H, W, W, n_px, 0, D, win,
                                       0.3, 2.0, depth_o[k], disp_o[k], norm_o[k], cost=args.cost,
                                       d_med16=med_o)
-            if harris:      # one launch over the batch's left frames
+            if harris and (rectify or med_o or B == 1):   # one launch over the batch's left frames
                 e.harris_batch_dev(gL if rectify else dL[k] + f * n_px, B, H, W, W, n_px,
                                    hmaps_l[i % nstreams][k])
         if gathered is not None:   # every rank's disparity maps -> rank 0 (RCCL over xGMI)
@@ -1136,6 +1140,11 @@ def main():
         result["aux_kernels"] = dict(result["aux_kernels"] or {})
         result["aux_kernels"]["k_harris"] = hbm_entry("k_harris_dpp", 5 * n_px * B, harris_ms,
                                                        harris_n)
+    elif harris:
+        result["aux_kernels"] = dict(result["aux_kernels"] or {})
+        result["aux_kernels"]["k_harris"] = {
+            "fused": "Harris blocks inside the k_median_i16 launch (sv_depth_map_harris_batch_dev): "
+                     "median_post_avg_us includes them"}
     if solo and not args.no_host_path and args.cost != "sgbm" and not rectify:
         try:
             result["host_path"] = host_path(H, W, D, win)

@@ -265,6 +265,18 @@ int sv_depth_map_batch_m16_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t
                                float* d_depth, float* d_disparity, uint8_t* d_norm,
                                int16_t* d_med16, void* stream);
 
+/* C2 (BASELINE.json: "Harris+disparity"): sv_depth_map_batch_dev plus the Harris response
+ * (cornerHarris(3, 3, 0.04) convention) of every LEFT frame into d_harris
+ * (dense f32 per frame).  The response is computed by extra blocks of the median launch (the
+ * register/DPP Harris form), so the path is two launches, not three; frames under 8 px a side
+ * take a separate Harris launch. */
+int sv_depth_map_harris_batch_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
+                                  int n_frames, int H, int W, int pitch, int64_t frame_stride,
+                                  int min_disp, int num_disp, int win, int cost, float min_depth,
+                                  float max_depth, float depth_range, float min_disp_global,
+                                  float* d_depth, float* d_disparity, uint8_t* d_norm,
+                                  float* d_harris, void* stream);
+
 /* Frame-sharded batch over several devices from ONE host process:
  * replaces the reference's per-frame loop over create_depth_map (depth_map.py:837-946,
  * called once per captured frame; fused_depth_map.py:2591-2598 submits frames to a worker

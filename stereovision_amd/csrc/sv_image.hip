@@ -118,13 +118,10 @@ __global__ __launch_bounds__(256) void k_harris_lds(const uint8_t* __restrict__ 
 // outside the image gx (row) or gy (column) flips, so gxy is negated once per dimension in
 // which the position lies outside (gxx, gyy are even).  Sums are exact integers; the float
 // epilogue is the LDS kernel's, so outputs are identical.
+// One wave's band: output columns x0 .. x0+59, rows y0 .. y0+HB-1 of one frame.
 template <int HB, int PF>
-__global__ __launch_bounds__(64) void k_harris_dpp(const uint8_t* __restrict__ g, int H, int W, int pitch,
-                                                   float* __restrict__ out, long long fs_in, long long fs_out) {
-    g += blockIdx.z * fs_in;
-    out += blockIdx.z * fs_out;
-    const int lane = threadIdx.x;
-    const int x0 = blockIdx.x * 60, y0 = blockIdx.y * HB;
+__device__ __forceinline__ void harris_wave(const uint8_t* __restrict__ g, int H, int W, int pitch,
+                                            float* __restrict__ out, int x0, int y0, int lane) {
     const int c = x0 - 2 + lane;
     const int cc = refl101(clampi(c, -2, W + 1), W);              // loaded column
     const int csign = (c < 0 || c >= W) ? -1 : 1;                  // gxy sign outside the image
@@ -186,6 +183,13 @@ __global__ __launch_bounds__(64) void k_harris_dpp(const uint8_t* __restrict__ g
             if (emit) out[(size_t)(r - 1) * W + c] = rr - kt;
         }
     }
+}
+
+template <int HB, int PF>
+__global__ __launch_bounds__(64) void k_harris_dpp(const uint8_t* __restrict__ g, int H, int W, int pitch,
+                                                   float* __restrict__ out, long long fs_in, long long fs_out) {
+    harris_wave<HB, PF>(g + blockIdx.z * fs_in, H, W, pitch, out + blockIdx.z * fs_out, blockIdx.x * 60,
+                        blockIdx.y * HB, threadIdx.x);
 }
 
 // Harris, 4 columns per lane (the default for W >= 1024; any W >= 256 works): lane j holds columns x0-4+4j ..
@@ -600,6 +604,147 @@ __global__ __launch_bounds__(64) void k_hog_hist_strip(const uint8_t* __restrict
     }
 }
 
+// HOG window histograms, vertical-first strip form (round 4, the default): as
+// k_hog_hist_strip, but each lane first keeps the VERTICAL window sum V of its own column
+// (5 packed dwords) over a register ring of the last 2r+1 pixel CODES (bin << 8 | magnitude,
+// one VGPR each instead of 5 dwords of row sums: 127 -> ~60 VGPRs, twice the waves per SIMD
+// for a kernel that is latency-bound), and the horizontal window sum of V is taken across the
+// wave only for rows that emit (prefix by DPP, P(j + r) - P(j - r - 1) by two ds_bpermute), so
+// the 2r warm-up rows of a strip skip the scan.  Same sums, same records: bit-identical.
+__device__ __forceinline__ void hog_onehot(uint32_t code, uint32_t (&o)[5]) {
+    const uint32_t b = code >> 8;
+    const uint32_t w = (code & 0xFFu) << ((b & 1u) << 4);
+    const uint32_t sel = 1u << (b >> 1);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = w & (uint32_t)(((int)(sel << (31 - k))) >> 31);
+}
+
+template <int r, int RP>
+__global__ __launch_bounds__(64, RP == 1 ? 8 : 5) void k_hog_hist_vf(const uint8_t* __restrict__ g, int H, int W, int pitch,
+                                                       int row0, int row1, uint16_t* __restrict__ hist, int hs_rows,
+                                                       const uint8_t* __restrict__ g1, uint16_t* __restrict__ hist1,
+                                                       long long fs_in, long long fs_hist) {
+    if (blockIdx.z) {   // image pairs: z = 2 * frame + (0 left, 1 right)
+        const int f = blockIdx.z >> 1;
+        if (blockIdx.z & 1) {
+            g = g1;
+            hist = hist1;
+        }
+        g += f * fs_in;
+        hist += f * fs_hist;
+    }
+    constexpr int W2 = 2 * r + 1, NOUT = 64 - 2 * r;
+    const int lane = threadIdx.x;
+    const int x0 = blockIdx.x * NOUT;
+    const int ys = row0 + blockIdx.y * hs_rows;
+    const int ye = min(ys + hs_rows, row1);
+    const int xx = clampi(x0 - r + lane, 0, W - 1);
+    const int xm = refl101(xx - 1, W), xp = refl101(xx + 1, W);
+    const int src_hi = (lane + r) << 2, src_lo = (lane - r - 1) << 2;
+    const uint32_t lo_mask = lane >= r + 1 ? ~0u : 0u;
+    const int xo = x0 + lane - r;
+    const bool out_lane = lane >= r && lane < 64 - r && xo < W;
+    const auto hdst = __builtin_amdgcn_make_buffer_rsrc(hist, 0, 0x7FFFFFFF, 0x00020000);
+    const int nbytes = 20 * min(NOUT, W - x0);
+    __shared__ __attribute__((aligned(16))) uint32_t stage[64 * 5 + 4];
+    const auto gsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(g), 0, 0x7FFFFFFF, 0x00020000);
+
+    uint32_t ring[W2], V[5];
+#pragma unroll
+    for (int s2 = 0; s2 < W2; ++s2) ring[s2] = 0u;   // code 0 = bin 0, magnitude 0: adds nothing
+#pragma unroll
+    for (int k = 0; k < 5; ++k) V[k] = 0u;
+
+    const int nsteps = ye - ys + 2 * r;
+    auto load_step = [&](int t, int (&n)[8]) {
+        const int c = clampi(ys - r + t, 0, H - 1);
+        const int om = refl101(c - 1, H) * pitch, oc = c * pitch, op = refl101(c + 1, H) * pitch;
+        auto ldb = [&](int col, int row) { return (int)__builtin_amdgcn_raw_buffer_load_b8(gsrc, col, row, 0); };
+        n[0] = ldb(xm, om); n[1] = ldb(xx, om); n[2] = ldb(xp, om);
+        n[3] = ldb(xm, oc); n[4] = ldb(xp, oc);
+        n[5] = ldb(xm, op); n[6] = ldb(xx, op); n[7] = ldb(xp, op);
+    };
+    int nb[RP][8];
+#pragma unroll
+    for (int rr = 0; rr < RP; ++rr) load_step(rr, nb[rr]);
+    for (int t0 = 0; t0 < nsteps; t0 += RP * W2) {
+#pragma unroll
+        for (int j = 0; j < W2; ++j) {
+            const int tb = t0 + RP * j;
+            if (tb >= nsteps) break;
+            uint32_t code[RP];
+#pragma unroll
+            for (int rr = 0; rr < RP; ++rr) {
+                const int a00 = nb[rr][0], a01 = nb[rr][1], a02 = nb[rr][2], a10 = nb[rr][3], a12 = nb[rr][4];
+                const int a20 = nb[rr][5], a21 = nb[rr][6], a22 = nb[rr][7];
+                load_step(tb + RP + rr, nb[rr]);
+                int gx = (a02 + 2 * a12 + a22) - (a00 + 2 * a10 + a20);
+                int gy = (a20 + 2 * a21 + a22) - (a00 + 2 * a01 + a02);
+                const uint32_t m = (uint32_t)(abs(gx) + abs(gy)) >> 3;
+                if (gy < 0 || (gy == 0 && gx < 0)) { gx = -gx; gy = -gy; }
+                int b = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int cy = kHogCos[k] * gy, sx = kHogSin[k] * gx;
+                    b += (cy >= sx) + (-cy >= sx);
+                }
+                code[rr] = ((uint32_t)b << 8) | m;
+            }
+#pragma unroll
+            for (int rr = 0; rr < RP; ++rr) {
+                const int t = tb + rr;
+                if (t >= nsteps) break;
+                const int slot = (RP * j + rr) % W2;      // = t mod W2 (t0 is a multiple of W2)
+                uint32_t on[5], of[5];
+                hog_onehot(code[rr], on);
+                hog_onehot(ring[slot], of);
+                ring[slot] = code[rr];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) V[k] = V[k] + on[k] - of[k];
+                if (t < 2 * r) continue;   // uniform: warm-up rows only fill the vertical window
+                // horizontal window of V across the wave: inclusive prefix (row_shr 1, 2, 4, 8,
+                // row_bcast 15 / 31), then P(j + r) - P(j - r - 1)
+                uint32_t pf[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) pf[k] = V[k];
+#define SV_HOG_SCAN(F) _Pragma("unroll") for (int k = 0; k < 5; ++k) pf[k] = F(pf[k]);
+                SV_HOG_SCAN(dpp_add<0x111>)
+                SV_HOG_SCAN(dpp_add<0x112>)
+                SV_HOG_SCAN(dpp_add<0x114>)
+                SV_HOG_SCAN(dpp_add<0x118>)
+                SV_HOG_SCAN((dpp_add_rm<0x142, 0xA>))
+                SV_HOG_SCAN((dpp_add_rm<0x143, 0xC>))
+#undef SV_HOG_SCAN
+                uint32_t hv[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_hi, (int)pf[k]);
+                    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lo, (int)pf[k]);
+                    hv[k] = hi - (lo & lo_mask);
+                }
+                const int rs = (ys + t - 2 * r) * W * 20 + x0 * 20;
+                const int ra = rs & 15, ro = rs - ra;
+                if (out_lane)
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) stage[(ra >> 2) + (lane - r) * 5 + k] = hv[k];
+                __syncthreads();   // (one wave: orders the staging, fences the compiler)
+                const int e = ra + nbytes;
+                for (int b0 = 16 * lane; b0 < e; b0 += 16 * 64) {
+                    const int b1 = b0 + 16;
+                    if (b0 >= ra && b1 <= e) {
+                        const v4u q = *reinterpret_cast<const v4u*>(stage + (b0 >> 2));
+                        __builtin_amdgcn_raw_buffer_store_b128(q, hdst, b0, ro, 0);
+                    } else if (b1 > ra) {
+                        for (int o = max(b0, ra); o < min(b1, e); o += 4)
+                            __builtin_amdgcn_raw_buffer_store_b32(stage[o >> 2], hdst, o, ro, 0);
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // Post-processing of one f32 disparity value (shared by the median kernels and k_post).
 struct PostVals { float a, b; uint8_t u; };
@@ -739,7 +884,19 @@ __global__ __launch_bounds__(256) void k_post_m16(const int16_t* __restrict__ in
 
 __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ in, int H, int W,
                                                     int row0, int row1, float* __restrict__ disp,
-                                                    PostParams pp, long long fs_in, long long fs_out) {
+                                                    PostParams pp, long long fs_in, long long fs_out,
+                                                    HarrisParams hp) {
+    // Harris blocks (hp.g != nullptr): blockIdx.x >= hp.mbx; each wave one DPP band of 60
+    // columns x 16 rows of the frame's left image (harris_wave, the k_harris_dpp form), so
+    // C2's Harris response rides in the median launch instead of a launch of its own
+    if ((int)blockIdx.x >= hp.mbx) {
+        const int w = (int)(blockIdx.x - hp.mbx) * 4 + (int)(threadIdx.x >> 6);
+        const int x0 = w * 60, y0 = row0 + (int)blockIdx.y * MQ_H;
+        if (x0 < W && y0 < row1)
+            harris_wave<MQ_H, 4>(hp.g + blockIdx.z * hp.fs_in, H, W, hp.pitch, hp.out + blockIdx.z * hp.fs_out, x0,
+                                 y0, threadIdx.x & 63);
+        return;
+    }
     // t2[r][c] = (tile row r, tile row r+2) of column x0-2+c; tile row r = image row y0-2+r
     __shared__ uint32_t t2[MQ_H + 2][MQ_W + 4];
     // srt[g][i][c]: rank i of column c over the shared pair rows 4g+1..4g+4 of t2
@@ -991,6 +1148,17 @@ int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStre
     return (int)hipGetLastError();
 }
 
+// SV_HOG_VF (A/B, round 4): 0 = the row-sum ring kernel, 1 / 2 = the vertical-first kernel
+// with 1 / 2 rows per step
+int hog_vf() {
+    static const int v = [] {
+        const char* e = std::getenv("SV_HOG_VF");
+        const int x = e ? std::atoi(e) : 1;
+        return x >= 0 && x <= 2 ? x : 1;
+    }();
+    return v;
+}
+
 int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0, int row1,
                     uint16_t* hist, hipStream_t s) {
     const int r = win / 2;
@@ -1010,7 +1178,12 @@ int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0
             return v >= 8 && v <= 4096 ? v : HS_ROWS;
         }();
         const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + hs_rows - 1) / hs_rows);
-        switch (r) {
+        const int vf = hog_vf();
+        switch (vf ? -1 - r - 8 * (vf - 1) : r) {
+#define SV_HOG_V(R) case -1 - R: hipLaunchKernelGGL((k_hog_hist_vf<R, 1>), grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows, g, hist, 0LL, 0LL); break; \
+                    case -9 - R: hipLaunchKernelGGL((k_hog_hist_vf<R, 2>), grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows, g, hist, 0LL, 0LL); break;
+            SV_HOG_V(0) SV_HOG_V(1) SV_HOG_V(2) SV_HOG_V(3) SV_HOG_V(4) SV_HOG_V(5) SV_HOG_V(6) SV_HOG_V(7)
+#undef SV_HOG_V
 #define SV_HOG_S(R) case R: hipLaunchKernelGGL(k_hog_hist_strip<R>, grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows, g, hist, 0LL, 0LL); break;
             SV_HOG_S(0) SV_HOG_S(1) SV_HOG_S(2) SV_HOG_S(3) SV_HOG_S(4) SV_HOG_S(5) SV_HOG_S(6) SV_HOG_S(7)
 #undef SV_HOG_S
@@ -1047,7 +1220,12 @@ int launch_hog_hist_pairs(const uint8_t* g0, const uint8_t* g1, int H, int W, in
         return 0;
     }
     const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + HS_ROWS - 1) / HS_ROWS, 2 * nf);
-    switch (r) {
+    const int vf = hog_vf();
+    switch (vf ? -1 - r - 8 * (vf - 1) : r) {
+#define SV_HOG_V(R) case -1 - R: hipLaunchKernelGGL((k_hog_hist_vf<R, 1>), grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0, HS_ROWS, g1, h1, fs_in, fs_hist); break; \
+                    case -9 - R: hipLaunchKernelGGL((k_hog_hist_vf<R, 2>), grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0, HS_ROWS, g1, h1, fs_in, fs_hist); break;
+        SV_HOG_V(0) SV_HOG_V(1) SV_HOG_V(2) SV_HOG_V(3) SV_HOG_V(4) SV_HOG_V(5) SV_HOG_V(6) SV_HOG_V(7)
+#undef SV_HOG_V
 #define SV_HOG_P(R) case R: hipLaunchKernelGGL(k_hog_hist_strip<R>, grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0, HS_ROWS, g1, h1, fs_in, fs_hist); break;
         SV_HOG_P(0) SV_HOG_P(1) SV_HOG_P(2) SV_HOG_P(3) SV_HOG_P(4) SV_HOG_P(5) SV_HOG_P(6) SV_HOG_P(7)
 #undef SV_HOG_P
@@ -1056,11 +1234,20 @@ int launch_hog_hist_pairs(const uint8_t* g0, const uint8_t* g1, int H, int W, in
 }
 
 int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float* disp,
-                      const PostParams& pp, hipStream_t s, int nf, long long fs_in, long long fs_out) {
+                      const PostParams& pp, hipStream_t s, int nf, long long fs_in, long long fs_out,
+                      const HarrisParams* harris) {
     if (row1 <= row0 || nf <= 0) return 0;
     if ((long long)H * W >= (1LL << 30)) return (int)hipErrorInvalidValue;   // 32-bit offsets
-    hipLaunchKernelGGL(k_median_i16, dim3((W + MQ_W - 1) / MQ_W, (row1 - row0 + MQ_H - 1) / MQ_H, nf),
-                       dim3(256), 0, s, in, H, W, row0, row1, disp, pp, fs_in, fs_out);
+    HarrisParams hp{};
+    hp.mbx = (W + MQ_W - 1) / MQ_W;
+    int hbx = 0;
+    if (harris && harris->g) {   // Harris of rows [row0, row1): 4 waves of 60 columns per block
+        hp = *harris;
+        hp.mbx = (W + MQ_W - 1) / MQ_W;
+        hbx = ((W + 59) / 60 + 3) / 4;
+    }
+    hipLaunchKernelGGL(k_median_i16, dim3(hp.mbx + hbx, (row1 - row0 + MQ_H - 1) / MQ_H, nf),
+                       dim3(256), 0, s, in, H, W, row0, row1, disp, pp, fs_in, fs_out, hp);
     return (int)hipGetLastError();
 }
 

@@ -237,10 +237,22 @@ struct PostParams {
     const float* lut_b;
     int lut_m0, lut_n;
 };
+// Harris response computed by extra blocks of the median launch (C2): the left gray frames
+// at g (+ z*fs_in bytes, row pitch `pitch`), f32 responses at out (+ z*fs_out floats, row
+// pitch W).  Needs W, H >= 8 (the DPP form).  mbx is set by the launcher.
+struct HarrisParams {
+    const uint8_t* g;
+    int pitch;
+    long long fs_in;
+    float* out;
+    long long fs_out;
+    int mbx;
+};
 // nf frames (grid.z): frame z reads in + z*fs_in and writes disp/out_* + z*fs_out elements.
+// harris (nullable): also the Harris response of rows [row0, row1) of each frame.
 int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float* disp,
                       const PostParams& pp, hipStream_t s, int nf = 1, long long fs_in = 0,
-                      long long fs_out = 0);
+                      long long fs_out = 0, const HarrisParams* harris = nullptr);
 int launch_median_f32(const float* in, int H, int W, float* out, hipStream_t s);
 // The median kernel's post-processing epilogue over an int16 x16 median map of n pixels
 // (disp = m / 16 and the pp outputs, element-wise; the table must be attached).

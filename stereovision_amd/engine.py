@@ -49,6 +49,7 @@ EXPORTED = [
     "sv_comm_scatterv", "sv_depth_map_rows_scatter", "sv_band_rows_in", "sv_release_scratch",
     "sv_frame_stats_batch_dev", "sv_select_count_batch", "sv_select_ranks_batch", "sv_event_record",
     "sv_stream_wait_event", "sv_median_post_m16_dev", "sv_post_m16_dev", "sv_multi_gpu_m16_dev",
+    "sv_depth_map_harris_batch_dev",
 ]
 BAND_MARGIN = 8   # SV_BAND_MARGIN: spare rows around a band-only input buffer
 COMM_ID_BYTES = 128
@@ -251,6 +252,10 @@ def _declare(lib):
                                         ctypes.POINTER(_c_int), _c_int, _c_int, _c_int,
                                         ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
                                         _c_float, _c_float, _c_float, _vp, _vp, _vp], _c_int),
+        "sv_depth_map_harris_batch_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
+                                           ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                           _c_float, _c_float, _c_float, _vp, _vp, _vp, _vp, _vp],
+                                          _c_int),
         "sv_median_post_m16_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float,
                                     _c_float, _c_float, _c_float, _c_int, _c_int, _vp, _vp, _vp,
                                     _vp, _vp, _vp], _c_int),
@@ -793,14 +798,21 @@ class Engine:
                             pitch: int, frame_stride: int, min_disp: int, num_disp: int,
                             win: int, min_depth: float, max_depth: float, d_depth: int,
                             d_disp: int, d_norm: int, cost="sad", min_disp_global=None,
-                            stream: int = 0, d_med16: int = 0):
-        """d_med16 (optional): also the int16 x16 median maps (d_disp = d_med16 / 16 exactly)."""
+                            stream: int = 0, d_med16: int = 0, d_harris: int = 0):
+        """d_med16 (optional): also the int16 x16 median maps (d_disp = d_med16 / 16 exactly).
+        d_harris (optional): also the Harris response of every left frame, computed inside the
+        median launch (sv_depth_map_harris_batch_dev; not combinable with d_med16)."""
         mdg = min_disp if min_disp_global is None else min_disp_global
         args = (self._h, d_left, d_right, int(n_frames), H, W, pitch, int(frame_stride),
                 int(min_disp), int(num_disp), int(win), _cost(cost), np.float32(min_depth),
                 np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
                 np.float32(mdg), d_depth, d_disp, d_norm)
-        if d_med16:
+        if d_harris:
+            if d_med16:
+                raise ValueError("d_harris and d_med16 are separate entry points")
+            _check("sv_depth_map_harris_batch_dev",
+                   self.lib.sv_depth_map_harris_batch_dev(*args, d_harris, stream or None))
+        elif d_med16:
             _check("sv_depth_map_batch_m16_dev",
                    self.lib.sv_depth_map_batch_m16_dev(*args, d_med16, stream or None))
         else:

@@ -483,6 +483,45 @@ def test_row_tiled_module_and_single_hip_runtime(engine):
     assert "torch" not in sys.modules
 
 
+@pytest.mark.parametrize("H,W,nf", [(45, 150, 3), (16, 64, 2), (33, 301, 3), (7, 70, 2), (120, 640, 4), (9, 8, 1)])
+def test_depth_map_harris_batch_dev_fused(engine, H, W, nf):
+    """sv_depth_map_harris_batch_dev (C2: Harris blocks inside the median launch) == the C
+    oracle frame by frame: the create_depth_map outputs bit-exact and the Harris response of
+    each left frame within 1e-4 (north_star; observed exact), with a row pitch wider than the
+    frame; frames under 8 px take the separate Harris launch."""
+    D, win, pitch = 32, 7, W + 3
+    rng = np.random.default_rng(H * W + nf)
+    L = np.zeros((nf, H, pitch), np.uint8)
+    R = np.zeros((nf, H, pitch), np.uint8)
+    for z in range(nf):
+        a, b = _pair(H, W, D, seed=40 + z)
+        L[z, :, :W], R[z, :, :W] = a, b
+        L[z, :, W:] = rng.integers(0, 256, (H, pitch - W))   # never read as data
+    n = H * W
+    dL, dR = engine.dev_alloc(L.nbytes), engine.dev_alloc(R.nbytes)
+    outs = [engine.dev_alloc(4 * n * nf), engine.dev_alloc(4 * n * nf), engine.dev_alloc(n * nf),
+            engine.dev_alloc(4 * n * nf)]
+    try:
+        engine.to_device(dL, L)
+        engine.to_device(dR, R)
+        engine.depth_map_batch_dev(dL, dR, nf, H, W, pitch, H * pitch, 0, D, win, 0.3, 2.0, outs[0],
+                                   outs[1], outs[2], d_harris=outs[3])
+        depth = engine.to_host(outs[0], (nf, H, W), np.float32)
+        disp = engine.to_host(outs[1], (nf, H, W), np.float32)
+        norm = engine.to_host(outs[2], (nf, H, W), np.uint8)
+        har = engine.to_host(outs[3], (nf, H, W), np.float32)
+        for z in range(nf):
+            Lz, Rz = np.ascontiguousarray(L[z, :, :W]), np.ascontiguousarray(R[z, :, :W])
+            e_depth, e_disp, e_norm = C.depth_map(Lz, Rz, 0, D, win)
+            np.testing.assert_array_equal(disp[z], e_disp, err_msg=f"frame {z}")
+            np.testing.assert_array_equal(depth[z], e_depth, err_msg=f"frame {z}")
+            np.testing.assert_array_equal(norm[z], e_norm, err_msg=f"frame {z}")
+            np.testing.assert_allclose(har[z], C.harris(Lz), rtol=0, atol=1e-4, err_msg=f"frame {z}")
+    finally:
+        for p_ in (dL, dR, *outs):
+            engine.dev_free(p_)
+
+
 @pytest.mark.parametrize("H,W", [(45, 150), (16, 64), (33, 130), (2, 70), (17, 3)])
 def test_harris_batch_dev_per_frame(engine, H, W):
     """sv_harris_batch_dev (one launch over grid.z, LDS-staged tiles) == the oracle's Harris

@@ -440,13 +440,13 @@ __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g,
 
 // ---------------------------------------------------------------------------------------
 // HOG window histograms, strip form: one wave = 64 consecutive (clamped) columns walking down
-// HS rows; lane j outputs column x0 + j - r for j in [r, 63 - r].  Per row step each lane
-// codes its pixel (bin, magnitude), the row's one-hot records are prefix-summed across the
-// wave by DPP (packed u16 halves: a row prefix is <= 64 * 255, so 32-bit adds never carry
-// between halves), the horizontal window sum is P(j + r) - P(j - r - 1) (two ds_bpermute),
-// and the vertical window sum runs over a register ring of the last 2r+1 row sums (<= 57,375
-// per bin).  No LDS tiles; a row's 50..64 records (contiguous in HBM) are staged in 1.3 KB of
-// LDS and leave as 16-byte stores.  4K, r = 7: 122 us (64x16 LDS tiles) -> 94 us per image.
+// HS rows; lane j outputs column x0 + j - r for j in [r, 63 - r]; no LDS tiles; a row's 50..64
+// records (contiguous in HBM) are staged in 1.3 KB of LDS and leave as 16-byte stores.
+// Packed u16 halves stay exact: a window sum is <= 57,375 per bin, and the 32-bit prefix
+// sums across the wave may carry between halves (or wrap) only in values whose difference
+// P(j + r) - P(j - r - 1) is exact modulo 2^32 and below 2^32.  (4K, r = 7: 122 us per image
+// with 64x16 LDS tiles; 94 -> 87 -> 69 us in 2-frame batches with a ring of the last 2r+1 row
+// sums; 65 -> 60.5 us with the vertical-first form below, which holds 49 VGPRs instead of 127.)
 constexpr int HS_ROWS = 64;
 
 template <int CTRL>
@@ -460,152 +460,7 @@ __device__ __forceinline__ uint32_t dpp_add_rm(uint32_t v) {
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-template <int r>
-__global__ __launch_bounds__(64) void k_hog_hist_strip(const uint8_t* __restrict__ g, int H, int W, int pitch,
-                                                       int row0, int row1, uint16_t* __restrict__ hist, int hs_rows,
-                                                       const uint8_t* __restrict__ g1, uint16_t* __restrict__ hist1,
-                                                       long long fs_in, long long fs_hist) {
-    if (blockIdx.z) {   // image pairs: z = 2 * frame + (0 left, 1 right)
-        const int f = blockIdx.z >> 1;
-        if (blockIdx.z & 1) {
-            g = g1;
-            hist = hist1;
-        }
-        g += f * fs_in;
-        hist += f * fs_hist;
-    }
-    constexpr int W2 = 2 * r + 1, NOUT = 64 - 2 * r;
-    const int lane = threadIdx.x;
-    const int x0 = blockIdx.x * NOUT;                    // first output column of the strip
-    const int ys = row0 + blockIdx.y * hs_rows;          // first output row
-    const int ye = min(ys + hs_rows, row1);
-    const int xx = clampi(x0 - r + lane, 0, W - 1);      // this lane's (clamped) window column
-    const int xm = refl101(xx - 1, W), xp = refl101(xx + 1, W);
-    const int src_hi = (lane + r) << 2, src_lo = (lane - r - 1) << 2;   // bpermute byte addresses
-    const uint32_t lo_mask = lane >= r + 1 ? ~0u : 0u;    // P(j - r - 1) = 0 left of the wave
-    const int xo = x0 + lane - r;
-    const bool out_lane = lane >= r && lane < 64 - r && xo < W;
-    const auto hdst = __builtin_amdgcn_make_buffer_rsrc(hist, 0, 0x7FFFFFFF, 0x00020000);
-    const int nbytes = 20 * min(NOUT, W - x0);           // the strip's record bytes per row
-    __shared__ __attribute__((aligned(16))) uint32_t stage[64 * 5 + 4];
-    // byte loads through one descriptor: uniform row offset + per-lane column (no 64-bit
-    // per-lane address arithmetic)
-    const auto gsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(g), 0, 0x7FFFFFFF, 0x00020000);
-
-    uint32_t ring[W2][5], V[5];
-#pragma unroll
-    for (int s = 0; s < W2; ++s)
-#pragma unroll
-        for (int k = 0; k < 5; ++k) ring[s][k] = 0u;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) V[k] = 0u;
-
-    // row t codes image row ys - r + t (clamped) and, from t = 2r on, emits output row
-    // ys + t - 2r; its 8 neighbourhood bytes are loaded one step ahead (3 steps ahead measured
-    // slower; loading 3 bytes instead of 8 gained 2 us: the DPP/LDS chain sets the pace)
-    const int nsteps = ye - ys + 2 * r;
-    auto load_step = [&](int t, int (&n)[8]) {
-        const int c = clampi(ys - r + t, 0, H - 1);
-        const int om = refl101(c - 1, H) * pitch, oc = c * pitch, op = refl101(c + 1, H) * pitch;
-        auto ldb = [&](int col, int row) { return (int)__builtin_amdgcn_raw_buffer_load_b8(gsrc, col, row, 0); };
-        n[0] = ldb(xm, om); n[1] = ldb(xx, om); n[2] = ldb(xp, om);
-        n[3] = ldb(xm, oc); n[4] = ldb(xp, oc);
-        n[5] = ldb(xm, op); n[6] = ldb(xx, op); n[7] = ldb(xp, op);
-    };
-    // two rows per step: their code / scan / bpermute chains are independent, so one wave
-    // keeps two in flight (the kernel is latency-bound at ~2.5 waves per SIMD)
-    constexpr int RP = 2;
-    int nb[RP][8];
-#pragma unroll
-    for (int rr = 0; rr < RP; ++rr) load_step(rr, nb[rr]);
-    for (int t0 = 0; t0 < nsteps; t0 += RP * W2) {
-#pragma unroll
-        for (int j = 0; j < W2; ++j) {
-            const int tb = t0 + RP * j;
-            if (tb >= nsteps) break;
-            uint32_t p[RP][5];
-#pragma unroll
-            for (int rr = 0; rr < RP; ++rr) {
-                const int a00 = nb[rr][0], a01 = nb[rr][1], a02 = nb[rr][2], a10 = nb[rr][3], a12 = nb[rr][4];
-                const int a20 = nb[rr][5], a21 = nb[rr][6], a22 = nb[rr][7];
-                load_step(tb + RP + rr, nb[rr]);          // the next pair's bytes
-                int gx = (a02 + 2 * a12 + a22) - (a00 + 2 * a10 + a20);
-                int gy = (a20 + 2 * a21 + a22) - (a00 + 2 * a01 + a02);
-                const uint32_t m = (uint32_t)(abs(gx) + abs(gy)) >> 3;
-                if (gy < 0 || (gy == 0 && gx < 0)) { gx = -gx; gy = -gy; }
-                int b = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int cy = kHogCos[k] * gy, sx = kHogSin[k] * gx;
-                    b += (cy >= sx) + (-cy >= sx);
-                }
-                const uint32_t w = m << ((b & 1) << 4);
-                const uint32_t sel = 1u << (b >> 1);      // dword of the bin, one-hot
-#pragma unroll
-                for (int k = 0; k < 5; ++k) p[rr][k] = w & (uint32_t)(((int)(sel << (31 - k))) >> 31);
-            }
-            // inclusive prefix over the wave: row_shr 1, 2, 4, 8, then row_bcast 15 / 31 (the
-            // ten dwords interleaved: no DPP read right after its VALU write)
-#define SV_HOG_SCAN(F)                                                                         \
-    _Pragma("unroll") for (int rr = 0; rr < RP; ++rr) _Pragma("unroll") for (int k = 0; k < 5; ++k) p[rr][k] = F(p[rr][k]);
-            SV_HOG_SCAN(dpp_add<0x111>)
-            SV_HOG_SCAN(dpp_add<0x112>)
-            SV_HOG_SCAN(dpp_add<0x114>)
-            SV_HOG_SCAN(dpp_add<0x118>)
-            SV_HOG_SCAN((dpp_add_rm<0x142, 0xA>))
-            SV_HOG_SCAN((dpp_add_rm<0x143, 0xC>))
-#undef SV_HOG_SCAN
-            uint32_t hr[RP][5];
-#pragma unroll
-            for (int rr = 0; rr < RP; ++rr)
-#pragma unroll
-                for (int k = 0; k < 5; ++k) {
-                    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_hi, (int)p[rr][k]);
-                    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lo, (int)p[rr][k]);
-                    hr[rr][k] = hi - (lo & lo_mask);
-                }
-#pragma unroll
-            for (int rr = 0; rr < RP; ++rr) {
-                const int t = tb + rr;
-                if (t >= nsteps) break;
-                const int slot = (RP * j + rr) % W2;      // = t mod W2 (t0 is a multiple of W2)
-#pragma unroll
-                for (int k = 0; k < 5; ++k) {
-                    V[k] += hr[rr][k] - ring[slot][k];
-                    ring[slot][k] = hr[rr][k];
-                }
-                if (t >= 2 * r) {
-                    // the strip's records are contiguous in the row: stage them in LDS and
-                    // leave as 16-byte stores (20-byte-strided dword stores: 5 partial-line
-                    // writes each).  16-byte stores must be 16-byte aligned: the staging
-                    // starts at the row start's alignment ra, lane j stores absolute-aligned
-                    // bytes [16j, 16j+16) of the staged run, edge lanes dword by dword.
-                    const int rs = (ys + t - 2 * r) * W * 20 + x0 * 20;
-                    const int ra = rs & 15, ro = rs - ra;
-                    if (out_lane)
-#pragma unroll
-                        for (int k = 0; k < 5; ++k) stage[(ra >> 2) + (lane - r) * 5 + k] = V[k];
-                    __syncthreads();   // (one wave: orders the staging, fences the compiler)
-                    const int e = ra + nbytes;              // <= 12 + 64 * 20: up to 81 chunks
-                    for (int b0 = 16 * lane; b0 < e; b0 += 16 * 64) {
-                        const int b1 = b0 + 16;
-                        if (b0 >= ra && b1 <= e) {
-                            const v4u q = *reinterpret_cast<const v4u*>(stage + (b0 >> 2));
-                            __builtin_amdgcn_raw_buffer_store_b128(q, hdst, b0, ro, 0);
-                        } else if (b1 > ra) {
-                            for (int o = max(b0, ra); o < min(b1, e); o += 4)
-                                __builtin_amdgcn_raw_buffer_store_b32(stage[o >> 2], hdst, o, ro, 0);
-                        }
-                    }
-                    __syncthreads();
-                }
-            }
-        }
-    }
-}
-
-// HOG window histograms, vertical-first strip form (round 4, the default): as
-// k_hog_hist_strip, but each lane first keeps the VERTICAL window sum V of its own column
+// Vertical-first (round 4): each lane first keeps the VERTICAL window sum V of its own column
 // (5 packed dwords) over a register ring of the last 2r+1 pixel CODES (bin << 8 | magnitude,
 // one VGPR each instead of 5 dwords of row sums: 127 -> ~60 VGPRs, twice the waves per SIMD
 // for a kernel that is latency-bound), and the horizontal window sum of V is taken across the
@@ -1148,17 +1003,6 @@ int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStre
     return (int)hipGetLastError();
 }
 
-// SV_HOG_VF (A/B, round 4): 0 = the row-sum ring kernel, 1 / 2 = the vertical-first kernel
-// with 1 / 2 rows per step
-int hog_vf() {
-    static const int v = [] {
-        const char* e = std::getenv("SV_HOG_VF");
-        const int x = e ? std::atoi(e) : 1;
-        return x >= 0 && x <= 2 ? x : 1;
-    }();
-    return v;
-}
-
 int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0, int row1,
                     uint16_t* hist, hipStream_t s) {
     const int r = win / 2;
@@ -1178,13 +1022,8 @@ int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0
             return v >= 8 && v <= 4096 ? v : HS_ROWS;
         }();
         const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + hs_rows - 1) / hs_rows);
-        const int vf = hog_vf();
-        switch (vf ? -1 - r - 8 * (vf - 1) : r) {
-#define SV_HOG_V(R) case -1 - R: hipLaunchKernelGGL((k_hog_hist_vf<R, 1>), grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows, g, hist, 0LL, 0LL); break; \
-                    case -9 - R: hipLaunchKernelGGL((k_hog_hist_vf<R, 2>), grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows, g, hist, 0LL, 0LL); break;
-            SV_HOG_V(0) SV_HOG_V(1) SV_HOG_V(2) SV_HOG_V(3) SV_HOG_V(4) SV_HOG_V(5) SV_HOG_V(6) SV_HOG_V(7)
-#undef SV_HOG_V
-#define SV_HOG_S(R) case R: hipLaunchKernelGGL(k_hog_hist_strip<R>, grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows, g, hist, 0LL, 0LL); break;
+        switch (r) {
+#define SV_HOG_S(R) case R: hipLaunchKernelGGL((k_hog_hist_vf<R, 1>), grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows, g, hist, 0LL, 0LL); break;
             SV_HOG_S(0) SV_HOG_S(1) SV_HOG_S(2) SV_HOG_S(3) SV_HOG_S(4) SV_HOG_S(5) SV_HOG_S(6) SV_HOG_S(7)
 #undef SV_HOG_S
         }
@@ -1220,13 +1059,8 @@ int launch_hog_hist_pairs(const uint8_t* g0, const uint8_t* g1, int H, int W, in
         return 0;
     }
     const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + HS_ROWS - 1) / HS_ROWS, 2 * nf);
-    const int vf = hog_vf();
-    switch (vf ? -1 - r - 8 * (vf - 1) : r) {
-#define SV_HOG_V(R) case -1 - R: hipLaunchKernelGGL((k_hog_hist_vf<R, 1>), grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0, HS_ROWS, g1, h1, fs_in, fs_hist); break; \
-                    case -9 - R: hipLaunchKernelGGL((k_hog_hist_vf<R, 2>), grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0, HS_ROWS, g1, h1, fs_in, fs_hist); break;
-        SV_HOG_V(0) SV_HOG_V(1) SV_HOG_V(2) SV_HOG_V(3) SV_HOG_V(4) SV_HOG_V(5) SV_HOG_V(6) SV_HOG_V(7)
-#undef SV_HOG_V
-#define SV_HOG_P(R) case R: hipLaunchKernelGGL(k_hog_hist_strip<R>, grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0, HS_ROWS, g1, h1, fs_in, fs_hist); break;
+    switch (r) {
+#define SV_HOG_P(R) case R: hipLaunchKernelGGL((k_hog_hist_vf<R, 1>), grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0, HS_ROWS, g1, h1, fs_in, fs_hist); break;
         SV_HOG_P(0) SV_HOG_P(1) SV_HOG_P(2) SV_HOG_P(3) SV_HOG_P(4) SV_HOG_P(5) SV_HOG_P(6) SV_HOG_P(7)
 #undef SV_HOG_P
     }

@@ -1031,6 +1031,11 @@ def main():
             "kernel_bytes_per_launch": k_bytes_kernel,
             "frac_kernel_bytes": round(k_bytes_kernel / k_avg_s / 1e9 / HBM_PEAK_GBS, 5),
             "avg_launch_us": round(k_avg_s * 1e6, 2), "launches": match_n,
+            # with S > 1 streams (frames <= 1 MP) lane 0's launches share the device
+            # with the other lanes' kernels, so these launch times are contended ones
+            "launch_concurrency": (f"{nstreams} streams: lane 0's launches timed while the other "
+                                   f"{nstreams - 1} lanes' kernels share the device (not comparable "
+                                   "with single-stream launch times)" if nstreams > 1 else "one stream"),
             # what actually bounds k_match: VALU issue.  SQ_INSTS_VALU per
             # launch from the live rocprofv3 pass over the live launch time, against the
             # full-rate issue peak (1 wave64 instruction / 2 cycles / SIMD); v_sad_u8 and the

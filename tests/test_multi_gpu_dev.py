@@ -461,3 +461,48 @@ def test_two_parameter_sets_alternating_on_two_streams(engine):
         engine.dev_free(dR)
     finally:
         other.close()
+
+
+def test_hog_band_only_inputs_both_histogram_kernels():
+    """band-only inputs with cost=HOG through both histogram kernels (the strip
+    form and the 64x16 tile form, SV_HOG_STRIP=0, each in a child): a band buffer holds only
+    the input rows [in0, in1) plus SV_BAND_MARGIN poisoned rows either side, the band's last
+    16-row tile starts at its last disparity row ((h1 - h0 - 1) % 16 == 0 for rank 1), and the
+    band's disparity rows equal the full-frame oracle's."""
+    from stereovision_amd.distributed import band_layout
+    H, W, D, win, world = 87, 300, 48, 7, 3
+    assert (band_layout(H, 1, world, win)["h1"] - band_layout(H, 1, world, win)["h0"] - 1) % 16 == 0
+    code = ("import sys, numpy as np; sys.path.insert(0, %r)\n"
+            "from stereovision_amd.engine import get_engine, BAND_MARGIN\n"
+            "from stereovision_amd.distributed import band_layout\n"
+            "from stereovision_amd.synthetic import stereo_pair\n"
+            "e = get_engine(0)\n"
+            "H, W, D, win, world = %d, %d, %d, %d, %d\n"
+            "L, R, _ = stereo_pair(H, W, D, seed=515)\n"
+            "for k in range(world):\n"
+            "    b = band_layout(H, k, world, win)\n"
+            "    rows = b['in1'] - b['in0']\n"
+            "    bufs, ptrs = [], []\n"
+            "    for img in (L, R):\n"
+            "        band = np.full((rows + 2 * BAND_MARGIN, W), 255, np.uint8)\n"
+            "        band[BAND_MARGIN:BAND_MARGIN + rows] = img[b['in0']:b['in1']]\n"
+            "        p = e.dev_alloc(band.nbytes); e.to_device(p, band); bufs.append(p)\n"
+            "        ptrs.append(p + (BAND_MARGIN - b['in0']) * W)\n"
+            "    out = e.dev_alloc(2 * H * W)\n"
+            "    e.disparity_dev(ptrs[0], ptrs[1], H, W, W, 0, D, win, 'hog', b['h0'], b['h1'], out, W)\n"
+            "    d = e.to_host(out, (H, W), np.int16)[b['h0']:b['h1']]\n"
+            "    sys.stdout.buffer.write(d.tobytes())\n"
+            "    for p in bufs + [out]: e.dev_free(p)\n") % (ROOT, H, W, D, win, world)
+    L, R, _ = stereo_pair(H, W, D, seed=515)
+    exp = C.disparity16(L, R, 0, D, win, 2)
+    for strip in ("1", "0"):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=120,
+                           env=dict(os.environ, SV_HOG_STRIP=strip, SV_WARMUP_AT_IMPORT="0"))
+        assert r.returncode == 0, r.stderr.decode()[-2000:]
+        off = 0
+        for k in range(world):
+            b = band_layout(H, k, world, win)
+            n = (b["h1"] - b["h0"]) * W * 2
+            got = np.frombuffer(r.stdout[off:off + n], np.int16).reshape(-1, W)
+            off += n
+            np.testing.assert_array_equal(got, exp[b["h0"]:b["h1"]], err_msg=f"strip={strip} rank {k}")

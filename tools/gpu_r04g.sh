@@ -6,3 +6,5 @@ rc=$?; tail -n 2 gpurun_out/r04g_pytest.log; [ $rc -ne 0 ] && exit $rc
 bash tools/prof_kernels.sh sg320b1 --cost sgbm --num-disp 320 --win 7 --batch 1 --steps 30 --warmup 5 || exit $?
 bash tools/prof_kernels.sh sg320b8 --cost sgbm --num-disp 320 --win 7 --batch 8 --frames 8 --steps 6 --warmup 2 || exit $?
 bash tools/prof_kernels.sh sg128b1 --cost sgbm --num-disp 128 --win 9 --batch 1 --steps 30 --warmup 5 || exit $?
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+timeout -k 10 300 python tools/pmc_ab.py --kernel k_median_i16 - > gpurun_out/r04g_median_pmc.txt 2>&1; tail -n 20 gpurun_out/r04g_median_pmc.txt

@@ -732,3 +732,65 @@ def test_harris_dpp_kernel_equals_lds_kernel():
         got = np.frombuffer(outs[0][off:off + 4 * H * W], np.float32).reshape(H, W)
         off += 4 * H * W
         assert np.abs(got - O.harris(g)).max() <= HARRIS_TOL, (H, W)
+
+
+class _LocalGather:
+    """A process group standing in for `world` ranks of one process: gatherv at the root copies
+    every other rank's block (from that rank's RowTiledDepthMap buffer) into the root's."""
+
+    def __init__(self, engine, tiles, rank):
+        self.engine, self.tiles, self.rank, self.world = engine, tiles, rank, len(tiles)
+
+    def gatherv(self, d_send, send_bytes, d_recv, offsets, sizes, root=0, stream=0):
+        if self.rank != root:
+            return
+        self.engine.synchronize()
+        for k, t in enumerate(self.tiles):
+            if k != root and sizes[k]:
+                blk = self.engine.to_host(t.m16 + offsets[k], (sizes[k],), np.uint8)
+                self.engine.to_device(d_recv + offsets[k], blk)
+
+
+@pytest.mark.parametrize("mode", ["depth", "scaled"])
+def test_row_tiled_int16_gather_and_root_expansion(engine, mode):
+    """RowTiledDepthMap since round 4: ranks other than the root compute only their bands'
+    int16 x16 medians (band_outputs="m16"), gather() moves those rows into the root's m16
+    buffer and the root expands them (sv_post_m16_dev) into its full-frame outputs — equal to
+    the whole-frame oracle for create_depth_map's post (DEPTH) and the scaled app's (SCALED),
+    with the root in the middle of the tiling."""
+    from stereovision_amd.distributed import RowTiledDepthMap
+    from stereovision_amd.engine import POST_DEPTH, POST_SCALED
+    H, W, D, win, md, world, root = 71, 260, 48, 7, -2, 3, 1
+    L, R = _pair(H, W, D, seed=61, min_disp=md)
+    dL, dR = engine.dev_alloc(H * W), engine.dev_alloc(H * W)
+    engine.to_device(dL, L)
+    engine.to_device(dR, R)
+    pm = POST_DEPTH if mode == "depth" else POST_SCALED
+    tiles = [RowTiledDepthMap(H, W, D, win, min_disp=md, rank=k, world=world, engine=engine)
+             for k in range(world)]
+    try:
+        for k, t in enumerate(tiles):
+            t.compute(dL, dR, mode=pm, min_disp_global=md, band_outputs="full" if k == root else "m16")
+        engine.synchronize()
+        tiles[root].gather(_LocalGather(engine, tiles, root), root=root)
+        engine.synchronize()
+        rt = tiles[root]
+        disp = engine.to_host(rt.disp, (H, W), np.float32)
+        e_disp = C.median5_f32(C.disparity16(L, R, md, D, win, 0))
+        np.testing.assert_array_equal(disp, e_disp)
+        a = engine.to_host(rt.out_a, (H, W), np.float32)
+        u = engine.to_host(rt.out_u8, (H, W), np.uint8)
+        if pm == POST_DEPTH:
+            e_a, e_u = C.depth_post(e_disp, 0.3, 2.0, md)
+            np.testing.assert_array_equal(a, e_a)
+            np.testing.assert_array_equal(u, e_u)
+        else:
+            e_a, e_u, e_b = C.scaled_post(e_disp, md, D)
+            np.testing.assert_array_equal(a, e_a)
+            np.testing.assert_array_equal(u, e_u)
+            np.testing.assert_array_equal(engine.to_host(rt.out_b, (H, W), np.float32), e_b)
+    finally:
+        for t in tiles:
+            t.close()
+        engine.dev_free(dL)
+        engine.dev_free(dR)

@@ -50,7 +50,7 @@ def main():
     a = np.random.default_rng(1).integers(0, 256, 6 * H * W, dtype=np.uint8)
     b = np.empty_like(a)
     out["host memcpy 12.4MB warm"] = rate(lambda i: np.copyto(b, a), n=30)
-    for depth in (2, 3, 4):
+    for depth in (1, 2, 3, 4, 6):
         pipe = DepthMapPipeline(D, win, depth=depth)
         try:
             for i in range(4):

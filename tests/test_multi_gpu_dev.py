@@ -95,11 +95,13 @@ def test_multi_gpu_depth_map_dev_gathers_every_frame(ctxs, ndev, counts, cost, w
             root.dev_free(p)
 
 
-@pytest.mark.parametrize("ndev,counts", [(8, [2, 1, 0, 3, 1, 1, 2, 1]), (3, [0, 2, 1]), (1, [2])])
-def test_multi_gpu_m16_dev_gathers_int16_medians(ctxs, ndev, counts):
+@pytest.mark.parametrize("ndev,counts,cost,win", [(8, [2, 1, 0, 3, 1, 1, 2, 1], "sad", 9),
+                                                   (3, [0, 2, 1], "hog", 7), (2, [1, 2], "ssd", 5),
+                                                   (1, [2], "sad", 11)])
+def test_multi_gpu_m16_dev_gathers_int16_medians(ctxs, ndev, counts, cost, win):
     """sv_multi_gpu_m16_dev: only the int16 x16 medians cross (2 B/px); they equal the C
     oracle's median map x 16 frame by frame, in context order."""
-    H, W, D, win = 37, 300, 64, 9
+    H, W, D = 37, 300, 64
     es = ctxs[:ndev]
     total = sum(counts)
     frames = [stereo_pair(H, W, D, seed=900 + f)[:2] for f in range(total)]
@@ -114,11 +116,11 @@ def test_multi_gpu_m16_dev_gathers_int16_medians(ctxs, ndev, counts):
     d_m16 = root.dev_alloc(2 * H * W * total)
     try:
         for _ in range(2):
-            multi_gpu_m16_dev(es, None, dLs, dRs, counts, H, W, W, H * W, 0, D, win, d_m16)
+            multi_gpu_m16_dev(es, None, dLs, dRs, counts, H, W, W, H * W, 0, D, win, d_m16, cost=cost)
             root.synchronize()
         m16 = root.to_host(d_m16, (total, H, W), np.int16)
         for f, (L, R) in enumerate(frames):
-            e_disp = _oracle(L, R, D, win)[0]
+            e_disp = _oracle(L, R, D, win, cost)[0]
             np.testing.assert_array_equal(m16[f], (e_disp * 16).astype(np.int16), err_msg=f"frame {f}")
     finally:
         for e, a, b in zip(es, dLs, dRs):

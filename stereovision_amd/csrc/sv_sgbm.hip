@@ -298,8 +298,12 @@ __global__ __launch_bounds__(256) void k_sgbm_records(SgbmArgs a) {
     a.recs[((size_t)img * a.H + y) * a.W + x] = bt_record(a, img ? a.R : a.L, y, x);
 }
 
+// columns per lane (ring: (2R+1)*CL/2 VGPRs).  A chunk re-costs its 2R halo columns; wider
+// chunks for r 3 (24: 256 VGPRs, no spills) measured slower (D=320 w7: 362 -> 355 frames/s per
+// call, 460-470 -> 447-456 at batch 8, round 4), r 4 with 24+ spills or lands in scratch
+__host__ __device__ constexpr int cost_cl(int r) { return r <= 2 ? 32 : 16; }
 template <int R> struct CostCfg {
-    static constexpr int CL = R <= 2 ? 32 : 16;           // columns per lane (ring: (2R+1)*CL/2 VGPRs)
+    static constexpr int CL = cost_cl(R);
     static constexpr int NREC = 2 * (CL + 2 * R) + 63;    // records per row of a wave
     static constexpr int NRT = (NREC + 63) / 64;          // per lane
 };
@@ -1202,7 +1206,7 @@ int launch_sgbm(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hipEv
         if (a.r > kMaxR) return (int)hipErrorInvalidValue;
         // pixel cost + window sums in one pass (k_sgbm_cost): one wave per (CL-column chunk,
         // 64 disparities, row band, frame); bands of >= 32 rows (the ring warm-up is 2r+1 rows)
-        const int cl = a.r <= 2 ? 32 : 16;                  // CostCfg<R>::CL
+        const int cl = cost_cl(a.r);                        // CostCfg<R>::CL
         const int chunks = (a.Wb + cl - 1) / cl, ndg = (a.D + 63) / 64;
         const long long per_band = (long long)chunks * ndg * nf;
         const int nb = (int)std::max<long long>(1, std::min<long long>(a.H / 32, (16384 + per_band - 1) / per_band));

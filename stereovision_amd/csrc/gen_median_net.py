@@ -11,6 +11,7 @@ Usage: python gen_median_net.py  (rewrites sv_median_net.h next to this file)
 """
 from __future__ import annotations
 
+import itertools
 import os
 import random
 
@@ -255,6 +256,79 @@ def build_sel20s(ranks, seeds=range(8)):
     return best[1], outs, best[0]
 
 
+def greedy_prune(net0, outs, w0, exp, seeds=range(16)):
+    """Drop comparators of `net0` greedily (seeded orders) while every output wire still
+    equals its expected bit-sliced 0-1 word; the cheapest seed after liveness pruning wins."""
+    def ok(net):
+        v = list(w0)
+        for a, b in net:
+            v[a], v[b] = v[a] & v[b], v[a] | v[b]
+        return all(v[o] == e for o, e in zip(outs, exp))
+
+    def liveness(net):
+        live, kept, ops = set(outs), [], 0
+        for a, b in reversed(net):
+            na, nb = a in live, b in live
+            if na or nb:
+                kept.append((a, b, int(na) | (int(nb) << 1)))
+                ops += 2 if na and nb else 1
+                live.update((a, b))
+        kept.reverse()
+        return ops, kept
+
+    assert ok(net0)
+    best = None
+    for seed in seeds:
+        rng = random.Random(seed)
+        order = list(range(len(net0)))
+        rng.shuffle(order)
+        drop = set()
+        for i in order:
+            if ok([c for k, c in enumerate(net0) if k not in drop and k != i]):
+                drop.add(i)
+        ops, kept = liveness([c for k, c in enumerate(net0) if k not in drop])
+        if best is None or ops < best[0]:
+            best = (ops, kept)
+    assert ok([(a, b) for a, b, _ in best[1]])
+    return best[1], best[0]
+
+
+def build_sel16h():
+    """Horizontal sharing (two adjacent windows x, x+1 of a row pair): their 20 shared values
+    hold 4 common sorted columns (16 values).  The 13th of 25 has common rank 3..12 (9 values
+    are outside the common 16), so the pair first takes sorted ranks 3..12 of the 16 (v[c*4+i],
+    column c, rank i), once."""
+    ranks = list(range(3, 13))
+    base, outs = build_sel(16, 16, 0, ranks)
+    cases = list(itertools.product(range(5), repeat=4))
+    w0 = [0] * 16
+    for t, ks in enumerate(cases):
+        for c, k in enumerate(ks):
+            for i in range(4 - k, 4):
+                w0[c * 4 + i] |= 1 << t
+    exp = [sum(1 << t for t, ks in enumerate(cases) if 16 - sum(ks) <= k) for k in ranks]
+    net, ops = greedy_prune([(a, b) for a, b, _ in base], outs, w0, exp)
+    return net, outs, ops
+
+
+def build_merge10_4():
+    """Per window: merge the pair's sorted ranks 3..12 (wires 0..9) with the window's own
+    sorted column (wires 10..13) -> sorted ranks 4..9 of the 14 (the 5 unique-row values
+    remain), i.e. the same 6 candidates SEL20S yields."""
+    ranks = list(range(4, 10))
+    base, outs = build_sel(14, 16, 0, ranks)
+    cases = [(ka, kc) for ka in range(11) for kc in range(5)]
+    w0 = [0] * 14
+    for t, (ka, kc) in enumerate(cases):
+        for i in range(10 - ka, 10):
+            w0[i] |= 1 << t
+        for i in range(4 - kc, 4):
+            w0[10 + i] |= 1 << t
+    exp = [sum(1 << t for t, (ka, kc) in enumerate(cases) if 14 - ka - kc <= k) for k in ranks]
+    net, ops = greedy_prune([(a, b) for a, b, _ in base], outs, w0, exp)
+    return net, outs, ops
+
+
 # optimal 9-comparator sorting network for 5 inputs (Knuth, TAOCP 5.3.4)
 SORT5 = [(0, 1), (3, 4), (2, 4), (2, 3), (1, 4), (0, 3), (0, 2), (1, 3), (1, 2)]
 
@@ -291,6 +365,19 @@ def main(check: bool = True):
         cols = [sorted(vals[j::5]) for j in range(5)]
         srt = [cols[j][i] for i in range(4) for j in range(5)]
         assert run_sel(sels, sels_out, srt) == sorted(vals)[7:13]
+    # horizontal pair form: SEL16H once per pair of windows + MERGE10_4 per window
+    selh, selh_out, selh_ops = build_sel16h()
+    mrg, mrg_out, mrg_ops = build_merge10_4()
+    for _ in range(4000):
+        vals = [rng.randint(-40, 40) for _ in range(25)]   # window: rows 0..4, columns 0..4
+        grid = [vals[5 * i:5 * i + 5] for i in range(5)]
+        shared = [sorted(grid[i][j] for i in range(1, 5)) for j in range(5)]   # 4 shared rows
+        common = [shared[j][i] for j in range(1, 5) for i in range(4)]
+        a = run_sel(selh, selh_out, common)
+        c = run_sel(mrg, mrg_out, a + shared[0])
+        u = sorted(grid[0])
+        r = min([c[5]] + [max(c[i], u[4 - i]) for i in range(5)])
+        assert r == sorted(vals)[12]
     here = os.path.dirname(os.path.abspath(__file__))
     lines = [
         "// Generated by gen_median_net.py — do not edit.",
@@ -333,6 +420,30 @@ def main(check: bool = True):
     for a, b, u in sels:
         lines.append(f"  {{{a}, {b}, {u}}},")
     lines.append("};")
+    lines += [
+        "",
+        "// Horizontal pair form (two adjacent windows share 4 sorted columns): sorted ranks 3..12",
+        f"// of the 16 common values v[c*4+i] (column c, rank i): {len(selh)} comparators ({selh_ops} ops),",
+        "// Batcher on 16 wires greedily pruned, verified over every sorted-column 0-1 input.",
+        f"#define SV_SEL16H_NCMP {len(selh)}",
+        "static constexpr unsigned char SV_SEL16H_OUT[10] = {" + ", ".join(map(str, selh_out)) + "};",
+        "static constexpr unsigned char SV_SEL16H_NET[SV_SEL16H_NCMP][3] = {",
+    ]
+    for a, b, u in selh:
+        lines.append(f"  {{{a}, {b}, {u}}},")
+    lines.append("};")
+    lines += [
+        "",
+        "// Per window: sorted ranks 4..9 of (SEL16H's 10 on wires 0..9 + the window's own sorted",
+        f"// column on wires 10..13): {len(mrg)} comparators ({mrg_ops} ops), verified over every sorted",
+        "// 0-1 input pair; the window's median is then min(C5, min_i max(C_i, U_(4-i))) as for SEL20S.",
+        f"#define SV_MRG14_NCMP {len(mrg)}",
+        "static constexpr unsigned char SV_MRG14_OUT[6] = {" + ", ".join(map(str, mrg_out)) + "};",
+        "static constexpr unsigned char SV_MRG14_NET[SV_MRG14_NCMP][3] = {",
+    ]
+    for a, b, u in mrg:
+        lines.append(f"  {{{a}, {b}, {u}}},")
+    lines.append("};")
     lines += ["", "// optimal 5-comparator sort of 4 values",
               "static constexpr unsigned char SV_SORT4_NET[5][2] = {" +
               ", ".join(f"{{{a}, {b}}}" for a, b in SORT4) + "};"]
@@ -342,7 +453,8 @@ def main(check: bool = True):
     with open(os.path.join(here, "sv_median_net.h"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print(f"{len(net)} comparators, output wire {out_slot}; SEL20 {len(sel)} comparators; "
-          f"SEL20S {len(sels)} comparators ({sels_ops} ops)")
+          f"SEL20S {len(sels)} comparators ({sels_ops} ops); SEL16H {len(selh)} ({selh_ops} ops); "
+          f"MRG14 {len(mrg)} ({mrg_ops} ops)")
 
 
 if __name__ == "__main__":

@@ -446,8 +446,10 @@ __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g,
 // sums across the wave may carry between halves (or wrap) only in values whose difference
 // P(j + r) - P(j - r - 1) is exact modulo 2^32 and below 2^32.  (4K, r = 7: 122 us per image
 // with 64x16 LDS tiles; 94 -> 87 -> 69 us in 2-frame batches with a ring of the last 2r+1 row
-// sums; 65 -> 60.5 us with the vertical-first form below, which holds 49 VGPRs instead of 127.)
-constexpr int HS_ROWS = 64;
+// sums; 65 -> 60.5 us with the vertical-first form below, which holds 49 VGPRs instead of 127;
+// round 4 rows per wave, C5 HOG 2-frame batches, per launch of 4 images: 32 252, 48 249,
+// 64 261, 96 265, 128 268 us.)
+constexpr int HS_ROWS = 48;
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_add(uint32_t v) {   // v + (lane shifted by CTRL, else 0)
@@ -474,7 +476,10 @@ __device__ __forceinline__ void hog_onehot(uint32_t code, uint32_t (&o)[5]) {
     for (int k = 0; k < 5; ++k) o[k] = w & (uint32_t)(((int)(sel << (31 - k))) >> 31);
 }
 
-template <int r, int RP>
+#ifndef SV_HOG_LV
+#define SV_HOG_LV 1
+#endif
+template <int r, int RP, bool LV = SV_HOG_LV>
 __global__ __launch_bounds__(64, RP == 1 ? 8 : 5) void k_hog_hist_vf(const uint8_t* __restrict__ g, int H, int W, int pitch,
                                                        int row0, int row1, uint16_t* __restrict__ hist, int hs_rows,
                                                        const uint8_t* __restrict__ g1, uint16_t* __restrict__ hist1,
@@ -509,6 +514,13 @@ __global__ __launch_bounds__(64, RP == 1 ? 8 : 5) void k_hog_hist_vf(const uint8
     for (int s2 = 0; s2 < W2; ++s2) ring[s2] = 0u;   // code 0 = bin 0, magnitude 0: adds nothing
 #pragma unroll
     for (int k = 0; k < 5; ++k) V[k] = 0u;
+    // LV: the lane's 5 vertical sums live in LDS ([bin pair][lane]) and each code lands as ONE
+    // ds_add_u32 / ds_sub_u32 at its bin pair instead of a 5-dword one-hot add in VALU.
+    __shared__ uint32_t vsum[LV ? 5 * 64 : 1];
+    if constexpr (LV) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) vsum[k * 64 + lane] = 0u;
+    }
 
     const int nsteps = ye - ys + 2 * r;
     auto load_step = [&](int t, int (&n)[8]) {
@@ -550,13 +562,26 @@ __global__ __launch_bounds__(64, RP == 1 ? 8 : 5) void k_hog_hist_vf(const uint8
                 const int t = tb + rr;
                 if (t >= nsteps) break;
                 const int slot = (RP * j + rr) % W2;      // = t mod W2 (t0 is a multiple of W2)
-                uint32_t on[5], of[5];
-                hog_onehot(code[rr], on);
-                hog_onehot(ring[slot], of);
-                ring[slot] = code[rr];
+                if constexpr (LV) {
+                    // code = bin << 8 | m: bin pair = code >> 9, half = bit 8 -> shift 16
+                    const uint32_t cn = code[rr], co = ring[slot];
+                    ring[slot] = cn;
+                    __hip_atomic_fetch_add(&vsum[(cn >> 9) * 64 + lane], (cn & 0xFFu) << ((cn >> 4) & 16u),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    __hip_atomic_fetch_sub(&vsum[(co >> 9) * 64 + lane], (co & 0xFFu) << ((co >> 4) & 16u),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    if (t < 2 * r) continue;
 #pragma unroll
-                for (int k = 0; k < 5; ++k) V[k] = V[k] + on[k] - of[k];
-                if (t < 2 * r) continue;   // uniform: warm-up rows only fill the vertical window
+                    for (int k = 0; k < 5; ++k) V[k] = vsum[k * 64 + lane];
+                } else {
+                    uint32_t on[5], of[5];
+                    hog_onehot(code[rr], on);
+                    hog_onehot(ring[slot], of);
+                    ring[slot] = code[rr];
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) V[k] = V[k] + on[k] - of[k];
+                    if (t < 2 * r) continue;   // uniform: warm-up rows only fill the vertical window
+                }
                 // horizontal window of V across the wave: inclusive prefix (row_shr 1, 2, 4, 8,
                 // row_bcast 15 / 31), then P(j + r) - P(j - r - 1)
                 uint32_t pf[5];
@@ -643,20 +668,23 @@ __device__ __forceinline__ void post_one(const PostParams& pp, size_t i, float d
     if (pp.mode == POST_SCALED) pp.out_b[i] = o.b;
 }
 
-// Median-of-25 for the int16 map, 4 output rows per lane.
+// Median-of-25 for the int16 map, 2 columns x 4 rows per lane.
 // Two vertically adjacent 5x5 windows (rows y, y+1) share 20 of their 25 values (rows
-// y-1..y+2).  The 13th smallest of a window lies in ranks 7..12 of the shared 20 or among
-// its 5 unique values.  The shared 20 are 5 columns of 4, and each column is read by 5
-// horizontally adjacent windows, so every column is sorted once (5 comparators, in LDS),
-// and SEL20S (59 comparators, 104 ops; 164 for the unsorted SEL20) takes ranks 7..12 of
-// the 5 sorted columns once per row pair; each window sorts its unique row (9 comparators),
-// and the median is the 6th smallest of (6 sorted + 5 sorted) = min_i max(C_i, U_{6-i})
-// (10 ops).  Each lane packs two row pairs (rows y,y+1 | y+2,y+3) into short2 halves, so
-// one v_pk_min/max_i16 serves both: ~43 ops per output (55 without the column sorts, 113
-// for the plain 25-input network).
+// y-1..y+2): 5 columns of 4, each read by 5 horizontally adjacent windows, so every column
+// is sorted once (5 comparators, in LDS).  Two horizontally adjacent windows (x, x+1) then
+// share 4 of those sorted columns: the 13th of 25 has rank 3..12 among the common 16 (9
+// values lie outside them), so SEL16H (41 comparators, 76 ops) takes the sorted ranks 3..12
+// once per column pair and each window merges its own column in (MRG14: 20 comparators, 32
+// ops) to the sorted ranks 4..9 of its 14 — the same 6 candidates C as SEL20S's ranks 7..12
+// of 20 (59 comparators, 104 ops per window, the round-3 form).  Each window's unique row is
+// sorted with its neighbour's (4 shared values sorted once, 1 inserted each), and the median
+// is the 6th smallest of (6 sorted + 5 sorted) = min_i max(C_i, U_{4-i}) (10 ops).  Each
+// lane packs two row pairs (rows y,y+1 | y+2,y+3) into short2 halves, so one
+// v_pk_min/max_i16 serves both: ~34 network ops per output (46 for the SEL20S form, 113 for
+// the plain 25-input network); round 4: 77 -> 68 us per 16 1080p frames.
 typedef short s2 __attribute__((ext_vector_type(2)));
 constexpr int MT_W = 64, MT_H = 8;        // k_median_f32 tile
-constexpr int MQ_W = 64, MQ_H = 16;       // k_median_i16: 64 columns x 16 rows per block
+constexpr int MQ_W = 128, MQ_H = 16;      // k_median_i16: 128 columns x 16 rows per block
 
 __device__ __forceinline__ s2 as_s2(uint32_t u) { return __builtin_bit_cast(s2, u); }
 
@@ -753,9 +781,10 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
         return;
     }
     // t2[r][c] = (tile row r, tile row r+2) of column x0-2+c; tile row r = image row y0-2+r
-    __shared__ uint32_t t2[MQ_H + 2][MQ_W + 4];
+    constexpr int TC = MQ_W + 4, TR = MQ_H + 2;
+    __shared__ uint32_t t2[TR][TC];
     // srt[g][i][c]: rank i of column c over the shared pair rows 4g+1..4g+4 of t2
-    __shared__ uint32_t srt[MQ_H / 4][4][MQ_W + 4];
+    __shared__ __attribute__((aligned(8))) uint32_t srt[MQ_H / 4][4][TC];
     if (blockIdx.z) {   // frame batch
         in += blockIdx.z * fs_in;
         const long long o = blockIdx.z * fs_out;
@@ -767,40 +796,47 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
         if (pp.out_m16) pp.out_m16 += o;
     }
     const int x0 = blockIdx.x * MQ_W, y0 = row0 + blockIdx.y * MQ_H;
-    {   // thread -> one tile column (clamped once), rows g, g+3, ...: 204 of 256 threads load
-        constexpr int TC = MQ_W + 4, TR = MQ_H + 2, G = 256 / TC;   // 68 columns, 3 row groups
-        const int c = threadIdx.x % TC, g = threadIdx.x / TC;
+    {   // thread -> tile column t % 128 (clamped once), rows t / 128, +2, ...; the 4 columns
+        // past 128 (72 entries) go to the first 72 threads
+        const int c = (int)(threadIdx.x & (MQ_W - 1)), g = (int)(threadIdx.x / MQ_W);
+        constexpr int G = 256 / MQ_W;
         static_assert(TR % G == 0, "row groups must tile the pair rows");
-        if (g < G) {
-            const uint32_t cx = (uint32_t)clampi(x0 - 2 + c, 0, W - 1);
-            if (y0 >= 2 && y0 + TR - 1 <= H - 1) {   // interior rows (uniform): no row clamps
-                uint32_t off = (uint32_t)(y0 - 2 + g) * W + cx;
-                const uint32_t two = 2u * (uint32_t)W, step = (uint32_t)G * W;
+        const uint32_t cx = (uint32_t)clampi(x0 - 2 + c, 0, W - 1);
+        if (y0 >= 2 && y0 + TR - 1 <= H - 1) {   // interior rows (uniform): no row clamps
+            uint32_t off = (uint32_t)(y0 - 2 + g) * W + cx;
+            const uint32_t two = 2u * (uint32_t)W, step = (uint32_t)G * W;
 #pragma unroll
-                for (int k = 0; k < TR / G; ++k) {
-                    const uint16_t a = (uint16_t)at(in, off);
-                    const uint16_t b = (uint16_t)at(in, off + two);
-                    t2[g + G * k][c] = (uint32_t)a | ((uint32_t)b << 16);
-                    off += step;
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < TR / G; ++k) {
-                    const int r = g + G * k;
-                    const uint16_t a = (uint16_t)at(in, (uint32_t)clampi(y0 - 2 + r, 0, H - 1) * W + cx);
-                    const uint16_t b = (uint16_t)at(in, (uint32_t)clampi(y0 + r, 0, H - 1) * W + cx);
-                    t2[r][c] = (uint32_t)a | ((uint32_t)b << 16);
-                }
+            for (int k = 0; k < TR / G; ++k) {
+                const uint16_t a = (uint16_t)at(in, off);
+                const uint16_t b = (uint16_t)at(in, off + two);
+                t2[g + G * k][c] = (uint32_t)a | ((uint32_t)b << 16);
+                off += step;
             }
+        } else {
+#pragma unroll
+            for (int k = 0; k < TR / G; ++k) {
+                const int r = g + G * k;
+                const uint16_t a = (uint16_t)at(in, (uint32_t)clampi(y0 - 2 + r, 0, H - 1) * W + cx);
+                const uint16_t b = (uint16_t)at(in, (uint32_t)clampi(y0 + r, 0, H - 1) * W + cx);
+                t2[r][c] = (uint32_t)a | ((uint32_t)b << 16);
+            }
+        }
+        if (threadIdx.x < 4 * TR) {
+            const int r = (int)(threadIdx.x >> 2), ce = MQ_W + (int)(threadIdx.x & 3);
+            const uint32_t cxe = (uint32_t)clampi(x0 - 2 + ce, 0, W - 1);
+            const uint16_t a = (uint16_t)at(in, (uint32_t)clampi(y0 - 2 + r, 0, H - 1) * W + cxe);
+            const uint16_t b = (uint16_t)at(in, (uint32_t)clampi(y0 + r, 0, H - 1) * W + cxe);
+            t2[r][ce] = (uint32_t)a | ((uint32_t)b << 16);
         }
     }
     __syncthreads();
     // every thread computes (the tile is clamped, so columns/rows past the edge read valid
-    // data); only in-range pixels are written, after the LDS transpose below
-    const int tx = threadIdx.x % MQ_W, tb = 4 * (threadIdx.x / MQ_W);
+    // data); only in-range pixels are written, after the LDS transpose below.  Thread (tb, tx)
+    // owns output columns tx, tx+1 (tile columns tx .. tx+5) of rows tb .. tb+3.
+    const int tx = 2 * (int)(threadIdx.x & 63), tb = 4 * (int)(threadIdx.x >> 6);
     {   // sort each column of the 4 shared pair rows once (5 comparators); the 5 windows
-        // that read a column share the sort.  Thread (tb, tx) sorts column tx of its row
-        // group; the 4 columns past 64 of each group go to the first 16 lanes of wave 0
+        // that read a column share the sort.  The 4 columns past 128 of each row group go to
+        // the first 16 lanes of wave 0
         auto sort_col = [&](int g4, int c) {
             s2 w[4];
 #pragma unroll
@@ -816,101 +852,155 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
             for (int i = 0; i < 4; ++i) srt[g4 >> 2][i][c] = __builtin_bit_cast(uint32_t, w[i]);
         };
         sort_col(tb, tx);
+        sort_col(tb, tx + 1);
         if (threadIdx.x < 16) sort_col(4 * (threadIdx.x >> 2), MQ_W + (threadIdx.x & 3));
     }
     __syncthreads();
 
-    s2 v[20];
+    // the two windows share tile columns tx+1 .. tx+4: SEL16H once (their sorted ranks 3..12),
+    // then each window merges its own column (MRG14) -> the 6 candidates C of SEL20S
+    s2 cm[16], own[2][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 5; ++j) v[i * 5 + j] = as_s2(srt[tb >> 2][i][tx + j]);
-#pragma unroll
-    for (int c = 0; c < SV_SEL20S_NCMP; ++c) {
-        const int a = SV_SEL20S_NET[c][0], b = SV_SEL20S_NET[c][1], use = SV_SEL20S_NET[c][2];
-        const s2 lo = __builtin_elementwise_min(v[a], v[b]);
-        const s2 hi = __builtin_elementwise_max(v[a], v[b]);
-        if (use & 1) v[a] = lo;
-        if (use & 2) v[b] = hi;
+    for (int i = 0; i < 4; ++i) {
+        const uint2 p0 = *reinterpret_cast<const uint2*>(&srt[tb >> 2][i][tx]);
+        const uint2 p1 = *reinterpret_cast<const uint2*>(&srt[tb >> 2][i][tx + 2]);
+        const uint2 p2 = *reinterpret_cast<const uint2*>(&srt[tb >> 2][i][tx + 4]);
+        own[0][i] = as_s2(p0.x);
+        cm[0 * 4 + i] = as_s2(p0.y);
+        cm[1 * 4 + i] = as_s2(p1.x);
+        cm[2 * 4 + i] = as_s2(p1.y);
+        cm[3 * 4 + i] = as_s2(p2.x);
+        own[1][i] = as_s2(p2.y);
     }
-    s2 m[2];
+#pragma unroll
+    for (int c = 0; c < SV_SEL16H_NCMP; ++c) {
+        const int a = SV_SEL16H_NET[c][0], b = SV_SEL16H_NET[c][1], use = SV_SEL16H_NET[c][2];
+        const s2 lo = __builtin_elementwise_min(cm[a], cm[b]);
+        const s2 hi = __builtin_elementwise_max(cm[a], cm[b]);
+        if (use & 1) cm[a] = lo;
+        if (use & 2) cm[b] = hi;
+    }
+    s2 cw[2][6];
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+        s2 z[14];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) z[k] = cm[SV_SEL16H_OUT[k]];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z[10 + k] = own[w][k];
+#pragma unroll
+        for (int c = 0; c < SV_MRG14_NCMP; ++c) {
+            const int a = SV_MRG14_NET[c][0], b = SV_MRG14_NET[c][1], use = SV_MRG14_NET[c][2];
+            const s2 lo = __builtin_elementwise_min(z[a], z[b]);
+            const s2 hi = __builtin_elementwise_max(z[a], z[b]);
+            if (use & 1) z[a] = lo;
+            if (use & 2) z[b] = hi;
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) cw[w][k] = z[SV_MRG14_OUT[k]];
+    }
+    // unique rows (tile rows tb, tb+5): the two windows share 4 of their 5 values, sorted once
+    // (5 comparators), each inserts its own (4); median = 6th of (C: 6 sorted, U: 5 sorted)
+    uint32_t mp[4];   // (column tx | column tx+1) of rows tb, tb+1, tb+2, tb+3
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        s2 u[5];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) u[j] = as_s2(t2[tb + 5 * h][tx + j]);
-#pragma unroll
-        for (int c = 0; c < 9; ++c) {
-            const int a = SV_SORT5_NET[c][0], b = SV_SORT5_NET[c][1];
-            const s2 lo = __builtin_elementwise_min(u[a], u[b]);
-            u[b] = __builtin_elementwise_max(u[a], u[b]);
-            u[a] = lo;
+        s2 q[6];
+        {
+            const uint2 p0 = *reinterpret_cast<const uint2*>(&t2[tb + 5 * h][tx]);
+            const uint2 p1 = *reinterpret_cast<const uint2*>(&t2[tb + 5 * h][tx + 2]);
+            const uint2 p2 = *reinterpret_cast<const uint2*>(&t2[tb + 5 * h][tx + 4]);
+            q[0] = as_s2(p0.x); q[1] = as_s2(p0.y); q[2] = as_s2(p1.x);
+            q[3] = as_s2(p1.y); q[4] = as_s2(p2.x); q[5] = as_s2(p2.y);
         }
-        s2 r = v[SV_SEL20S_OUT[5]];
+        s2 sc[4] = {q[1], q[2], q[3], q[4]};
 #pragma unroll
-        for (int i = 0; i < 5; ++i)
-            r = __builtin_elementwise_min(r, __builtin_elementwise_max(v[SV_SEL20S_OUT[i]], u[4 - i]));
-        m[h] = r;
+        for (int k = 0; k < 5; ++k) {
+            const int a = SV_SORT4_NET[k][0], b = SV_SORT4_NET[k][1];
+            const s2 lo = __builtin_elementwise_min(sc[a], sc[b]);
+            sc[b] = __builtin_elementwise_max(sc[a], sc[b]);
+            sc[a] = lo;
+        }
+        s2 m[2];
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+            s2 u[5] = {sc[0], sc[1], sc[2], sc[3], w ? q[5] : q[0]};
+#pragma unroll
+            for (int k = 3; k >= 0; --k) {   // insertion of u[4]
+                const s2 lo = __builtin_elementwise_min(u[k], u[k + 1]);
+                u[k + 1] = __builtin_elementwise_max(u[k], u[k + 1]);
+                u[k] = lo;
+            }
+            s2 r = cw[w][5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) r = __builtin_elementwise_min(r, __builtin_elementwise_max(cw[w][i], u[4 - i]));
+            m[w] = r;
+        }
+        // h = 0: (row tb, row tb+2), h = 1: (row tb+1, row tb+3); halves x = rows, w = columns
+        const uint32_t a0 = __builtin_bit_cast(uint32_t, m[0]), a1 = __builtin_bit_cast(uint32_t, m[1]);
+        mp[h] = (a0 & 0xFFFFu) | (a1 << 16);
+        mp[h + 2] = (a0 >> 16) | (a1 & 0xFFFF0000u);
     }
-    // m[0] = (row y, row y+2), m[1] = (row y+1, row y+3): park the four medians in LDS, then
-    // re-read them as 4 consecutive columns of one row per thread so the outputs leave as
-    // 16-byte (f32) and 4-byte (u8) stores instead of 4-byte / 1-byte ones
-    __shared__ int16_t med[MQ_H][MQ_W];
-    med[tb][tx] = m[0].x;
-    med[tb + 1][tx] = m[1].x;
-    med[tb + 2][tx] = m[0].y;
-    med[tb + 3][tx] = m[1].y;
+    // park the medians in LDS, then re-read them as 4 consecutive columns of one row per
+    // thread so the outputs leave as 16-byte (f32) and 4-byte (u8) stores
+    __shared__ __attribute__((aligned(8))) uint32_t med[MQ_H][MQ_W / 2];
+    med[tb][tx >> 1] = mp[0];
+    med[tb + 1][tx >> 1] = mp[1];
+    med[tb + 2][tx >> 1] = mp[2];
+    med[tb + 3][tx >> 1] = mp[3];
     __syncthreads();
-    const int r = threadIdx.x >> 4, c4 = (threadIdx.x & 15) * 4;
-    const int y = y0 + r, x = x0 + c4;
-    if (y >= row1 || x >= W) return;
-    const uint2 raw = *reinterpret_cast<const uint2*>(&med[r][c4]);
-    const int mv[4] = {(int)(int16_t)(raw.x & 0xFFFF), (int)(int16_t)(raw.x >> 16),
-                       (int)(int16_t)(raw.y & 0xFFFF), (int)(int16_t)(raw.y >> 16)};
-    const uint32_t i = (uint32_t)y * W + x;
-    const bool vec = x + 3 < W && (W & 3) == 0 &&
-                     (((uintptr_t)disp | (uintptr_t)pp.out_a | (uintptr_t)pp.out_b) & 15) == 0 &&
-                     (((uintptr_t)pp.out_u8 | (uintptr_t)pp.out_bgr) & 3) == 0 && ((uintptr_t)pp.out_m16 & 7) == 0;
-    if (vec) {
-        if (disp)
-            at(reinterpret_cast<float4*>(disp), i >> 2) =
-                make_float4((float)mv[0] / 16.0f, (float)mv[1] / 16.0f, (float)mv[2] / 16.0f, (float)mv[3] / 16.0f);
-        if (pp.out_m16) at(reinterpret_cast<uint2*>(pp.out_m16), i >> 2) = raw;
-        if (pp.mode == POST_NONE) return;
-        PostVals o[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = post_median(pp, mv[q]);
-        at(reinterpret_cast<float4*>(pp.out_a), i >> 2) = make_float4(o[0].a, o[1].a, o[2].a, o[3].a);
-        at(reinterpret_cast<uint32_t*>(pp.out_u8), i >> 2) =
-            (uint32_t)o[0].u | ((uint32_t)o[1].u << 8) | ((uint32_t)o[2].u << 16) | ((uint32_t)o[3].u << 24);
-        if (pp.mode == POST_SCALED)
-            at(reinterpret_cast<float4*>(pp.out_b), i >> 2) = make_float4(o[0].b, o[1].b, o[2].b, o[3].b);
-        if (pp.out_bgr) {   // 4 pixels = 12 bytes = 3 dwords (byte offset 3i, i % 4 == 0)
-            const uint32_t c0 = pp.cmap[o[0].u], c1 = pp.cmap[o[1].u], c2 = pp.cmap[o[2].u],
-                           c3 = pp.cmap[o[3].u];
-            uint32_t* d = &at(reinterpret_cast<uint32_t*>(pp.out_bgr), 3 * (i >> 2));
-            d[0] = c0 | (c1 << 24);
-            d[1] = (c1 >> 8) | (c2 << 16);
-            d[2] = (c2 >> 16) | (c3 << 8);
+    for (int pass = 0; pass < 2; ++pass) {
+        const int r = (int)(threadIdx.x >> 5) + 8 * pass, c4 = (int)(threadIdx.x & 31) * 4;
+        const int y = y0 + r, x = x0 + c4;
+        if (y >= row1 || x >= W) continue;
+        const uint2 raw = *reinterpret_cast<const uint2*>(&med[r][c4 >> 1]);
+        const int mv[4] = {(int)(int16_t)(raw.x & 0xFFFF), (int)(int16_t)(raw.x >> 16),
+                           (int)(int16_t)(raw.y & 0xFFFF), (int)(int16_t)(raw.y >> 16)};
+        const uint32_t i = (uint32_t)y * W + x;
+        const bool vec = x + 3 < W && (W & 3) == 0 &&
+                         (((uintptr_t)disp | (uintptr_t)pp.out_a | (uintptr_t)pp.out_b) & 15) == 0 &&
+                         (((uintptr_t)pp.out_u8 | (uintptr_t)pp.out_bgr) & 3) == 0 && ((uintptr_t)pp.out_m16 & 7) == 0;
+        if (vec) {
+            if (disp)
+                at(reinterpret_cast<float4*>(disp), i >> 2) =
+                    make_float4((float)mv[0] / 16.0f, (float)mv[1] / 16.0f, (float)mv[2] / 16.0f, (float)mv[3] / 16.0f);
+            if (pp.out_m16) at(reinterpret_cast<uint2*>(pp.out_m16), i >> 2) = raw;
+            if (pp.mode == POST_NONE) continue;
+            PostVals o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = post_median(pp, mv[q]);
+            at(reinterpret_cast<float4*>(pp.out_a), i >> 2) = make_float4(o[0].a, o[1].a, o[2].a, o[3].a);
+            at(reinterpret_cast<uint32_t*>(pp.out_u8), i >> 2) =
+                (uint32_t)o[0].u | ((uint32_t)o[1].u << 8) | ((uint32_t)o[2].u << 16) | ((uint32_t)o[3].u << 24);
+            if (pp.mode == POST_SCALED)
+                at(reinterpret_cast<float4*>(pp.out_b), i >> 2) = make_float4(o[0].b, o[1].b, o[2].b, o[3].b);
+            if (pp.out_bgr) {   // 4 pixels = 12 bytes = 3 dwords (byte offset 3i, i % 4 == 0)
+                const uint32_t c0 = pp.cmap[o[0].u], c1 = pp.cmap[o[1].u], c2 = pp.cmap[o[2].u],
+                               c3 = pp.cmap[o[3].u];
+                uint32_t* d = &at(reinterpret_cast<uint32_t*>(pp.out_bgr), 3 * (i >> 2));
+                d[0] = c0 | (c1 << 24);
+                d[1] = (c1 >> 8) | (c2 << 16);
+                d[2] = (c2 >> 16) | (c3 << 8);
+            }
+            continue;
         }
-        return;
-    }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if (x + q >= W) break;
-        if (disp) at(disp, i + q) = (float)mv[q] / 16.0f;
-        if (pp.out_m16) at(pp.out_m16, i + q) = (int16_t)mv[q];
-        if (pp.mode == POST_NONE) continue;
-        const PostVals o = post_median(pp, mv[q]);
-        at(pp.out_a, i + q) = o.a;
-        at(pp.out_u8, i + q) = o.u;
-        if (pp.mode == POST_SCALED) at(pp.out_b, i + q) = o.b;
-        if (pp.out_bgr) {
-            const uint32_t c = pp.cmap[o.u];
-            uint8_t* d = &at(pp.out_bgr, 3 * (i + q));
-            d[0] = (uint8_t)c;
-            d[1] = (uint8_t)(c >> 8);
-            d[2] = (uint8_t)(c >> 16);
+        for (int q = 0; q < 4; ++q) {
+            if (x + q >= W) break;
+            if (disp) at(disp, i + q) = (float)mv[q] / 16.0f;
+            if (pp.out_m16) at(pp.out_m16, i + q) = (int16_t)mv[q];
+            if (pp.mode == POST_NONE) continue;
+            const PostVals o = post_median(pp, mv[q]);
+            at(pp.out_a, i + q) = o.a;
+            at(pp.out_u8, i + q) = o.u;
+            if (pp.mode == POST_SCALED) at(pp.out_b, i + q) = o.b;
+            if (pp.out_bgr) {
+                const uint32_t c = pp.cmap[o.u];
+                uint8_t* d = &at(pp.out_bgr, 3 * (i + q));
+                d[0] = (uint8_t)c;
+                d[1] = (uint8_t)(c >> 8);
+                d[2] = (uint8_t)(c >> 16);
+            }
         }
     }
 }
@@ -1003,6 +1093,16 @@ int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStre
     return (int)hipGetLastError();
 }
 
+// rows per strip wave (SV_HOG_ROWS: A/B)
+static int hog_strip_rows() {
+    static const int v = [] {
+        const char* e = std::getenv("SV_HOG_ROWS");
+        const int x = e ? std::atoi(e) : 0;
+        return x >= 8 && x <= 4096 ? x : HS_ROWS;
+    }();
+    return v;
+}
+
 int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0, int row1,
                     uint16_t* hist, hipStream_t s) {
     const int r = win / 2;
@@ -1016,11 +1116,7 @@ int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0
     }();
     // (the strip kernel addresses through 32-bit buffer offsets)
     if (strip && (long long)H * W * 20 < (1LL << 31) && (long long)H * pitch < (1LL << 31)) {
-        static const int hs_rows = [] {
-            const char* e = std::getenv("SV_HOG_ROWS");
-            const int v = e ? std::atoi(e) : 0;
-            return v >= 8 && v <= 4096 ? v : HS_ROWS;
-        }();
+        const int hs_rows = hog_strip_rows();
         const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + hs_rows - 1) / hs_rows);
         switch (r) {
 #define SV_HOG_S(R) case R: hipLaunchKernelGGL((k_hog_hist_vf<R, 1>), grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows, g, hist, 0LL, 0LL); break;
@@ -1058,9 +1154,10 @@ int launch_hog_hist_pairs(const uint8_t* g0, const uint8_t* g1, int H, int W, in
         }
         return 0;
     }
-    const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + HS_ROWS - 1) / HS_ROWS, 2 * nf);
+    const int hs_rows = hog_strip_rows();
+    const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + hs_rows - 1) / hs_rows, 2 * nf);
     switch (r) {
-#define SV_HOG_P(R) case R: hipLaunchKernelGGL((k_hog_hist_vf<R, 1>), grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0, HS_ROWS, g1, h1, fs_in, fs_hist); break;
+#define SV_HOG_P(R) case R: hipLaunchKernelGGL((k_hog_hist_vf<R, 1>), grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0, hs_rows, g1, h1, fs_in, fs_hist); break;
         SV_HOG_P(0) SV_HOG_P(1) SV_HOG_P(2) SV_HOG_P(3) SV_HOG_P(4) SV_HOG_P(5) SV_HOG_P(6) SV_HOG_P(7)
 #undef SV_HOG_P
     }

@@ -700,8 +700,8 @@ __global__ __launch_bounds__(64) void k_sgbm_vpath(SgbmArgs a) {
 // rows like k_sgbm_vpath and at every row sums its fresh L_tb with L_lr and L_rl (prefetched
 // in register rings beside C) and runs wta_line on the sum: L_tb is never stored, so its
 // write and the WTA's read of it leave the pipeline, and the WTA launch goes.
-template <int DPL, int LPC, typename LT, int PF>
-__global__ __launch_bounds__(64, 2) void k_sgbm_vpath_wta(SgbmArgs a) {
+template <int DPL, int LPC, typename LT, int PF, int WPE>
+__global__ __launch_bounds__(64, WPE) void k_sgbm_vpath_wta(SgbmArgs a) {
     if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
     constexpr int NL = 64 / LPC;
     const int lane = threadIdx.x, g = lane / LPC, j = lane & (LPC - 1);
@@ -1099,6 +1099,17 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
     // (D <= 128 measured even: 703 vs 707 frames/s per call at D=128, so the concurrent form
     // stays there; D=320: 337 -> 359 per call, 373 -> 416 at batch 4)
     const bool vwta = !fused && vwta_on && pv.lpc == 32 && a.D > 128;
+    // deep: the vertical path + WTA of a launch this small (at most ~1 wave per SIMD: one
+    // 1080p frame is ~800 waves) takes the variant with one wave per SIMD and a 3x deeper
+    // prefetch ring of its three volumes (Little's law: the bytes in flight set the bandwidth):
+    // D=320 w7 952 -> 855-863 us, 362 -> 374 frames/s per call.  SV_SGBM_DEEP=0: the 2-wave
+    // variant everywhere (A/B)
+    static const bool deep_on = [] {
+        const char* e = std::getenv("SV_SGBM_DEEP");
+        return !(e && e[0] == '0');
+    }();
+    const long long hwaves = (long long)gh.x * gh.y * gh.z, vwaves = (long long)gv.x * gv.y * gv.z;
+    const bool deep = deep_on && !fused && hwaves <= 1280 && vwaves <= 1280;
     if (vwta) aux = nullptr;
     hipStream_t sv = aux ? aux : s;
     if (aux) {
@@ -1130,6 +1141,8 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
         SV_HPATH(16, 12, 8, 2) SV_HPATH(16, 16, 6, 2) SV_HPATH(16, 20, 4, 2) SV_HPATH(16, 24, 4, 2)
         SV_HPATH(16, 32, 4, 1)
     }
+    // (deeper prefetch did not pay for the horizontal lines of a single D=320 frame: one wave
+    // per SIMD with 16 steps ahead 1,105 -> 1,355 us, two waves with 9 steps ahead 1,119 us)
     SV_HPATH(32, 2, 16, 2) SV_HPATH(32, 4, 12, 2) SV_HPATH(32, 6, 10, 2) SV_HPATH(32, 8, 8, 2)
     SV_HPATH(32, 10, 6, 2) SV_HPATH(32, 12, 4, 2) SV_HPATH(32, 16, 3, 2)
     SV_HPATH(16, 1, 24, 1) SV_HPATH(16, 2, 24, 1) SV_HPATH(16, 4, 16, 1) SV_HPATH(16, 8, 16, 1)
@@ -1138,12 +1151,16 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
 #undef SV_HPATH
     if (aux && hipStreamWaitEvent(s, join, 0) != hipSuccess) return (int)hipErrorLaunchFailure;
     if (vwta) {
-#define SV_VWTA(N, PF)                                                                      \
-        if (!w && pv.dpl == N) {                                                            \
-            hipLaunchKernelGGL((k_sgbm_vpath_wta<N, 32, LT, PF>), gv, dim3(64), 0, s, a);   \
-            w = true;                                                                       \
+#define SV_VWTA(N, PF, WPE)                                                                      \
+        if (!w && pv.dpl == N) {                                                                 \
+            hipLaunchKernelGGL((k_sgbm_vpath_wta<N, 32, LT, PF, WPE>), gv, dim3(64), 0, s, a);   \
+            w = true;                                                                            \
         }
-        SV_VWTA(2, 8) SV_VWTA(4, 6) SV_VWTA(6, 4) SV_VWTA(8, 3) SV_VWTA(10, 2) SV_VWTA(12, 2) SV_VWTA(16, 1)
+        if (deep) {   // <= ~1 wave per SIMD: the whole register file for a deeper prefetch
+            SV_VWTA(6, 8, 1) SV_VWTA(8, 6, 1) SV_VWTA(10, 6, 1) SV_VWTA(12, 4, 1) SV_VWTA(16, 3, 1)
+        }
+        SV_VWTA(2, 8, 2) SV_VWTA(4, 6, 2) SV_VWTA(6, 4, 2) SV_VWTA(8, 3, 2) SV_VWTA(10, 2, 2) SV_VWTA(12, 2, 2)
+        SV_VWTA(16, 1, 2)
 #undef SV_VWTA
     }
     if (fused) {
@@ -1209,7 +1226,14 @@ int launch_sgbm(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hipEv
         const int cl = cost_cl(a.r);                        // CostCfg<R>::CL
         const int chunks = (a.Wb + cl - 1) / cl, ndg = (a.D + 63) / 64;
         const long long per_band = (long long)chunks * ndg * nf;
-        const int nb = (int)std::max<long long>(1, std::min<long long>(a.H / 32, (16384 + per_band - 1) / per_band));
+        // SV_SGBM_CWAVES (A/B): target waves of the cost launch (more bands = more waves, but
+        // each band re-costs its 2r-row warm-up)
+        static const long long cwaves = [] {
+            const char* e = std::getenv("SV_SGBM_CWAVES");
+            const long long v = e ? std::atoll(e) : 0;
+            return v >= 256 && v <= (1 << 20) ? v : 16384LL;
+        }();
+        const int nb = (int)std::max<long long>(1, std::min<long long>(a.H / 32, (cwaves + per_band - 1) / per_band));
         const int vb = (a.H + nb - 1) / nb;
         const dim3 grid((unsigned)chunks, (unsigned)(ndg * ((a.H + vb - 1) / vb)), (unsigned)nf);
         hipLaunchKernelGGL(k_sgbm_records, dim3((a.W + 255) / 256, 2 * a.H, nf), dim3(256), 0, s, a);

@@ -1226,14 +1226,9 @@ int launch_sgbm(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hipEv
         const int cl = cost_cl(a.r);                        // CostCfg<R>::CL
         const int chunks = (a.Wb + cl - 1) / cl, ndg = (a.D + 63) / 64;
         const long long per_band = (long long)chunks * ndg * nf;
-        // SV_SGBM_CWAVES (A/B): target waves of the cost launch (more bands = more waves, but
-        // each band re-costs its 2r-row warm-up)
-        static const long long cwaves = [] {
-            const char* e = std::getenv("SV_SGBM_CWAVES");
-            const long long v = e ? std::atoll(e) : 0;
-            return v >= 256 && v <= (1 << 20) ? v : 16384LL;
-        }();
-        const int nb = (int)std::max<long long>(1, std::min<long long>(a.H / 32, (cwaves + per_band - 1) / per_band));
+        // ~16k waves (D=320 w7 1080p: 33-row bands; 8k / 4k waves measured 598 / slower us,
+        // round 4: the bands' 2r-row warm-up is not what bounds the kernel)
+        const int nb = (int)std::max<long long>(1, std::min<long long>(a.H / 32, (16384 + per_band - 1) / per_band));
         const int vb = (a.H + nb - 1) / nb;
         const dim3 grid((unsigned)chunks, (unsigned)(ndg * ((a.H + vb - 1) / vb)), (unsigned)nf);
         hipLaunchKernelGGL(k_sgbm_records, dim3((a.W + 255) / 256, 2 * a.H, nf), dim3(256), 0, s, a);

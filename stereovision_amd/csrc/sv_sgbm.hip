@@ -1102,14 +1102,15 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
     // deep: the vertical path + WTA of a launch this small (at most ~1 wave per SIMD: one
     // 1080p frame is ~800 waves) takes the variant with one wave per SIMD and a 3x deeper
     // prefetch ring of its three volumes (Little's law: the bytes in flight set the bandwidth):
-    // D=320 w7 952 -> 855-863 us, 362 -> 374 frames/s per call.  SV_SGBM_DEEP=0: the 2-wave
-    // variant everywhere (A/B)
-    static const bool deep_on = [] {
+    // D=320 w7 952 -> 855-863 us, 362 -> 374 frames/s per call.  Batches keep the 2-wave form
+    // (every launch deep: batch 8 459-468 -> 453, batch 4 438 -> 416 frames/s).
+    // SV_SGBM_DEEP=0 / 2: the 2-wave / the deep variant everywhere (A/B)
+    static const int deep_mode = [] {   // 0 off, 1 small launches, 2 every launch (A/B)
         const char* e = std::getenv("SV_SGBM_DEEP");
-        return !(e && e[0] == '0');
+        return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
     }();
-    const long long hwaves = (long long)gh.x * gh.y * gh.z, vwaves = (long long)gv.x * gv.y * gv.z;
-    const bool deep = deep_on && !fused && hwaves <= 1280 && vwaves <= 1280;
+    const long long vwaves = (long long)gv.x * gv.y * gv.z;
+    const bool deep = !fused && (deep_mode == 2 || (deep_mode == 1 && vwaves <= 1280));
     if (vwta) aux = nullptr;
     hipStream_t sv = aux ? aux : s;
     if (aux) {

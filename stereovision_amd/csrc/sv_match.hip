@@ -807,8 +807,12 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     // r 5: 16 more ring VGPRs spill 4-9 VGPRs, which still pays for 32-lane groups (1080p
     // D=128 win 11: 572 -> 555 us per 16 frames) but not for 16-lane ones (VGA D=64 win 11:
     // 122 -> 139 us), so those and the unmeasured 64-lane groups keep the sub/add form;
-    // r 6..7 the packed form.
-    constexpr bool SADU = !PK && (R <= 4 || (R == 5 && LPGT == 32));
+    // r 6..7 (packed halves) take it too: 16 / 14 slots of 8 words.
+    // PK: the two u16 halves of a cost word update as ONE 32-bit v_sad_u32 as well: each half
+    // of the key holds its leaving cost as a summand, so key >= leaving as 32-bit integers with
+    // no borrow between the halves, and key - leaving + entering stays below 2^16 per half (no
+    // carry): the packed result is exact.
+    constexpr bool SADU = PK || R <= 4 || (R == 5 && LPGT == 32);
     constexpr int M = SADU ? W2 + 1 : W2;               // cost ring slots
     constexpr int U = M % 4 == 0 ? M : M % 2 == 0 ? 2 * M : 4 * M;   // lcm(4, M) steps per body
     constexpr int NCH = U / 4;                          // chunks per body
@@ -986,7 +990,8 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                             const uint32_t c = __builtin_amdgcn_sad_hi_u8(
                                 Lc.w[NC + 2 * j + 1], Rk.w[NC + 2 * j + 1],
                                 __builtin_amdgcn_sad_u8(Lc.w[NC + 2 * j], Rk.w[NC + 2 * j], cn));
-                            h[k][j] = pk_add16(h[k][j], c);
+                            if constexpr (SADU) sad_u32_acc(h[k][j], ring[oslot][k][j], c);
+                            else h[k][j] = pk_add16(h[k][j], c);
                             ring[slot][k][j] = c;
                         }
                     } else {

@@ -1105,10 +1105,8 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
     // D=320 w7 952 -> 855-863 us, 362 -> 374 frames/s per call.  Batches keep the 2-wave form
     // (every launch deep: batch 8 459-468 -> 453, batch 4 438 -> 416 frames/s).
     // SV_SGBM_DEEP=0 / 2: the 2-wave / the deep variant everywhere (A/B)
-    static const int deep_mode = [] {   // 0 off, 1 small launches, 2 every launch (A/B)
-        const char* e = std::getenv("SV_SGBM_DEEP");
-        return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
-    }();
+    const char* de = std::getenv("SV_SGBM_DEEP");   // read per call (tests switch it)
+    const int deep_mode = de && (de[0] == '0' || de[0] == '2') ? de[0] - '0' : 1;
     const long long vwaves = (long long)gv.x * gv.y * gv.z;
     const bool deep = !fused && (deep_mode == 2 || (deep_mode == 1 && vwaves <= 1280));
     if (vwta) aux = nullptr;

@@ -127,10 +127,15 @@ def test_gpu_sgbm_1080p_properties(engine):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("deep", [None, "0", "2"])
 @pytest.mark.parametrize("D,win", [(160, 5), (256, 7), (320, 7), (384, 3), (512, 5)])
-def test_gpu_sgbm_wide_disparity_ranges(engine, D, win):
+def test_gpu_sgbm_wide_disparity_ranges(engine, monkeypatch, D, win, deep):
     """Every lane plan of the path kernels (DPL 12..32), incl. the reference's default
-    NUM_DISP = 16*20 = 320 with WINDOW_SIZE = 7 (depth_map.py:31-33)."""
+    NUM_DISP = 16*20 = 320 with WINDOW_SIZE = 7 (depth_map.py:31-33); both forms of the
+    vertical path + WTA (SV_SGBM_DEEP, read per call: 0 = two waves per SIMD, 2 = one wave
+    with the deeper prefetch; default = deep for small launches like these)."""
+    if deep is not None:
+        monkeypatch.setenv("SV_SGBM_DEEP", deep)
     L, R, _ = stereo_pair(21, D + 90, D, seed=D)
     np.testing.assert_array_equal(engine.sgbm(L, R, 0, D, win), SG.sgbm(L, R, 0, D, win))
 

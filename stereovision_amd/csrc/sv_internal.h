@@ -10,6 +10,15 @@ struct sv_comm;
 
 namespace sv {
 
+// v_sad_u32: a = |a - b| + c (unsigned) — a running window sum's update `sum - leaving +
+// entering` in ONE VOP3 whenever sum >= leaving (the sum holds the leaving term as a summand);
+// also exact on two u16 halves per word when each half's sum holds its own leaving term and
+// stays below 2^16 (no borrow, no carry).  No clang builtin, and the umax - umin + c pattern
+// is split into several ops inside large bodies, so inline asm (plain VOP3: no hazards).
+__device__ __forceinline__ void sad_u32_acc(uint32_t& a, uint32_t b, uint32_t c) {
+    asm("v_sad_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+}
+
 // Sets the calling thread's sv_last_error() message; returns `code`.
 int set_error(int code, const std::string& msg);
 

@@ -766,11 +766,6 @@ __device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
 }
 
-// v_sad_u32 = |a - b| + c (unsigned).  No clang builtin, and the umax - umin + c pattern is
-// split into four ops inside the ring kernel's body, so inline asm (no hazards: plain VOP3).
-__device__ __forceinline__ void sad_u32_acc(uint32_t& a, uint32_t b, uint32_t c) {   // a = |a - b| + c
-    asm("v_sad_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
-}
 
 // DEFER: a chunk's second step pair is not reduced at the chunk's end (where its DPP /
 // permlane chain ran alone before the next basic block) but in the next chunk's step 1,

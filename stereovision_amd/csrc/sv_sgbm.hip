@@ -316,8 +316,13 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// waves per SIMD the register budget allows (r 3: 160 VGPRs since the window sums update by
+// v_sad_u32; 3 waves measured even with 2, 390 vs 389 frames/s at D=320 w7)
+#ifndef SV_COST_WPE
+#define SV_COST_WPE(R) ((R) == 3 ? 3 : 2)
+#endif
 template <int R>
-__global__ __launch_bounds__(64, 2) void k_sgbm_cost(SgbmArgs a, int vb, int ndg) {
+__global__ __launch_bounds__(64, SV_COST_WPE(R)) void k_sgbm_cost(SgbmArgs a, int vb, int ndg) {
     if (blockIdx.z) a.select_frame(blockIdx.z);   // frame batch
     constexpr int W2 = 2 * R + 1, CL = CostCfg<R>::CL, CP = CL / 2, NRT = CostCfg<R>::NRT;
     __shared__ uint4 rec[2 * CostCfg<R>::NREC];
@@ -374,14 +379,14 @@ __global__ __launch_bounds__(64, 2) void k_sgbm_cost(SgbmArgs a, int vb, int ndg
             for (int k = 0; k < CL + 2 * R; ++k)
                 pcs[k] = bt_cost(buf[k], buf[nL + min(max(xs - R + k, 0), Wb - 1) + roff]);
         }
-        int hs = 0;
+        uint32_t hs = 0;
 #pragma unroll
-        for (int k = 0; k < W2; ++k) hs += pcs[k];
-        int lo = hs;
+        for (int k = 0; k < W2; ++k) hs += (uint32_t)pcs[k];
+        uint32_t lo = hs;
 #pragma unroll
         for (int j = 1; j < CL; ++j) {
-            hs += pcs[j + 2 * R] - pcs[j - 1];
-            if (j & 1) hp[j >> 1] = (uint32_t)(lo & 0xFFFF) | ((uint32_t)hs << 16);
+            sad_u32_acc(hs, (uint32_t)pcs[j - 1], (uint32_t)pcs[j + 2 * R]);   // hs - leaving + entering
+            if (j & 1) hp[j >> 1] = (lo & 0xFFFFu) | (hs << 16);
             else lo = hs;
         }
     };
@@ -424,8 +429,8 @@ __global__ __launch_bounds__(64, 2) void k_sgbm_cost(SgbmArgs a, int vb, int ndg
                 uint32_t hp[CP];
                 hrow(rec + cur * NB, hp);
 #pragma unroll
-                for (int j = 0; j < CP; ++j) {
-                    acc[j] = pk_sub16(pk_add16(acc[j], hp[j]), ring[u][j]);
+                for (int j = 0; j < CP; ++j) {   // both u16 halves: acc - leaving + entering
+                    sad_u32_acc(acc[j], ring[u][j], hp[j]);
                     ring[u][j] = hp[j];
                 }
                 if (active) store(y0 + t0 + u, acc);

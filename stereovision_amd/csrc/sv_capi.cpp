@@ -128,6 +128,7 @@ struct sv_ctx {
     // multi-device entry points: int16 x16 medians a context sends to the root (peers) or
     // receives from the peers (root), 2 B/px over xGMI
     DevBuf gm16;
+    DevBuf keys;       // split ring kind (SAD, D > 256): two argmin-key planes
     std::vector<float> hl_a, hl_b;
     std::vector<uint8_t> hl_u8;
     std::vector<HostEnt> hl_ent;
@@ -428,6 +429,12 @@ int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int 
         a.HL = c->hog[0].as<uint16_t>();
         a.HR = c->hog[1].as<uint16_t>();
         a.fs_hist = a.nf > 1 ? fh : 0;
+    }
+    if (sv::ring_split(cost, win, num_disp) && a.X1 > a.X0) {
+        const long long ke = sv::ring_split_elems(a.nf, fs_out, row1, opitch);
+        SV_HIP(c->keys.ensure((size_t)(2 * ke) * sizeof(uint32_t)));
+        a.keys = c->keys.as<uint32_t>();
+        a.keys_stride = ke;
     }
     SV_LAUNCH(c, SV_K_MATCH, s, sv::launch_match(a, plan, cost, s));
     return 0;

@@ -68,6 +68,10 @@ struct MatchParams {
     // share one
     unsigned* work_ctr;
     int xcd_map;           // ring kind: XCD-aware tile order (launch_ring_rl)
+    // split ring (SAD, 256 < D <= 512): two argmin-key planes laid out like `out` (opitch,
+    // fs_out) as u32, `keys_stride` elements apart; the caller owns them (ring_split_elems)
+    uint32_t* keys;
+    long long keys_stride;
 };
 
 // Host-side launchers (return hipError_t as int).
@@ -75,6 +79,10 @@ int plan_match(int num_disp, int win, int cost, MatchPlan* plan);
 uint64_t max_cost(int win, int cost);   // largest window cost of a (win, cost) pair
 size_t match_lds_bytes(const MatchPlan& p, int r, int cost);
 int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t s);
+// D > 256 SAD windows run the ring kind twice (d < 256, d >= 256) into key planes and merge:
+// whether a launch takes that form, and the elements of one key plane it needs
+bool ring_split(int cost, int win, int num_disp);
+long long ring_split_elems(int nf, long long fs_out, int row1, int opitch);
 int launch_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v, hipStream_t s);
 
 int launch_gray(const uint8_t* bgr, int H, int W, int pitch, uint8_t* gray, hipStream_t s);

@@ -771,7 +771,9 @@ __device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
 // permlane chain ran alone before the next basic block) but in the next chunk's step 1,
 // beside that chunk's first pair: two independent reduce-scatter chains interleaved, +9
 // loop-carried VGPRs (off for r 5, which would spill).
-template <int R, int LPGT, bool DEFER>
+// KEYS (split ring, D > 256): the reduced argmin keys (cost << 16 | idx) go to a.keys as u32
+// (the merge kernel picks the smaller of the two passes' keys), no band-edge fill.
+template <int R, int LPGT, bool DEFER, bool KEYS>
 __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     using P = PackCfg<COST_SAD4, R>;
     constexpr int NW = P::NW, NC = P::NC, W2 = 2 * R + 1;
@@ -789,6 +791,7 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
         a.L += bz * a.fs_in;
         a.R += bz * a.fs_in;
         a.out += bz * a.fs_out;
+        if constexpr (KEYS) a.keys += bz * a.fs_out;
     }
     const int lane = threadIdx.x;
     constexpr int LPG = LPGT;                           // lanes per group (template: no
@@ -834,7 +837,7 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     const int cR0 = cL0 - a.minD - (4 * LPG - 1);       // R index i -> column cR0 + i
     build_all_packs<COST_SAD4, R, RG_DPL>(a, yc, cL0, NL, cR0, NRlog, c0, Lw, Rw, lane);
 
-    if (bx == 0) {  // columns outside the matched band are invalid
+    if (!KEYS && bx == 0) {  // columns outside the matched band are invalid
         const int16_t inv = (int16_t)((a.minD - 1) * 16);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -904,17 +907,20 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     // step t emits column xs + t + eb (join2: the chunk starting at step t emits the lane's
     // pair at column xs + t + eb)
     const int eb = ju - 2 * R + pofs;
-    const int ooff = 2 * ((y + jq) * a.opitch + xs + eb);   // bytes
+    constexpr int OB = KEYS ? 4 : 2;                        // bytes per output element
+    const int ooff = OB * ((y + jq) * a.opitch + xs + eb);   // bytes
     // 32-bit buffer offsets from one SGPR descriptor (no 64-bit per-lane addresses to keep)
-    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFFF, 0x00020000);
+    const auto orsrc = KEYS ? __builtin_amdgcn_make_buffer_rsrc(a.keys, 0, 0x7FFFFFFF, 0x00020000)
+                            : __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFFF, 0x00020000);
     const int emax = ((l & 1) == 0 && l < (join2 ? 32 : 16) && y + jq < a.row1) ? max(0, min(S, a.X1 - xs)) : 0;
 
     // store of a reduced key for the chunk starting at step tt (join2) / of step tt
     auto emit_key = [&](uint32_t key, int tt) {
         // non-emitting lanes store past the buffer's range (dropped by the hardware bounds
         // check, as in composable_kernel): no exec-mask branch
-        const int off = (unsigned)(tt + eb) < (unsigned)emax ? ooff + 2 * tt : (int)0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16), orsrc, off, 0, 0);
+        const int off = (unsigned)(tt + eb) < (unsigned)emax ? ooff + OB * tt : (int)0x80000000u;
+        if constexpr (KEYS) __builtin_amdgcn_raw_buffer_store_b32(key, orsrc, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16), orsrc, off, 0, 0);
     };
     // join2: pair (0,1) in kA, pair (2,3) in kB: one swap joins both
     auto join_pairs = [&](uint32_t kA_, uint32_t kB_) {
@@ -1163,14 +1169,16 @@ size_t ring_lds_bytes(int lpg, int seg, int r) {
     return (size_t)(nl + nrp) * (r <= 5 ? 24 : 32);
 }
 
-template <int R, int LPG>
+template <int R, int LPG, bool KEYS>
 int launch_ring_rl(const MatchParams& a, size_t lds, hipStream_t s) {
     // SV_RING_DEFER=0 (A/B): every pair reduced inside its own chunk
     static const bool defer = [] {
         const char* e = std::getenv("SV_RING_DEFER");
         return !(e && e[0] == '0');
     }();
-    auto fn = (defer && R != 5) ? k_match_ring<R, LPG, R != 5> : k_match_ring<R, LPG, false>;
+    void (*fn)(MatchParams);
+    if constexpr (KEYS) fn = k_match_ring<R, LPG, R != 5, true>;
+    else fn = (defer && R != 5) ? k_match_ring<R, LPG, R != 5, false> : k_match_ring<R, LPG, false, false>;
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return (int)e;
@@ -1187,16 +1195,17 @@ int launch_ring_rl(const MatchParams& a, size_t lds, hipStream_t s) {
     hipLaunchKernelGGL(fn, grid, dim3(64), lds, s, b);
     return (int)hipGetLastError();
 }
-template <int R>
+template <int R, bool KEYS>
 int launch_ring_r(const MatchParams& a, size_t lds, hipStream_t s) {
     switch (a.lpg) {
-        case 16: return launch_ring_rl<R, 16>(a, lds, s);
-        case 32: return launch_ring_rl<R, 32>(a, lds, s);
-        case 64: return launch_ring_rl<R, 64>(a, lds, s);
+        case 16: return launch_ring_rl<R, 16, KEYS>(a, lds, s);
+        case 32: return launch_ring_rl<R, 32, KEYS>(a, lds, s);
+        case 64: return launch_ring_rl<R, 64, KEYS>(a, lds, s);
     }
     return (int)hipErrorInvalidValue;
 }
 
+template <bool KEYS>
 int launch_ring(const MatchParams& a0, hipStream_t s) {
     MatchParams a = a0;
     a.lpg = ring_lpg(a.D);
@@ -1206,18 +1215,57 @@ int launch_ring(const MatchParams& a0, hipStream_t s) {
     const size_t lds = ring_lds_bytes(a.lpg, a.segm, a.r);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
     switch (a.r) {
-        case 2: return launch_ring_r<2>(a, lds, s);
-        case 3: return launch_ring_r<3>(a, lds, s);
-        case 4: return launch_ring_r<4>(a, lds, s);
-        case 5: return launch_ring_r<5>(a, lds, s);
-        case 6: return launch_ring_r<6>(a, lds, s);
-        case 7: return launch_ring_r<7>(a, lds, s);
+        case 2: return launch_ring_r<2, KEYS>(a, lds, s);
+        case 3: return launch_ring_r<3, KEYS>(a, lds, s);
+        case 4: return launch_ring_r<4, KEYS>(a, lds, s);
+        case 5: return launch_ring_r<5, KEYS>(a, lds, s);
+        case 6: return launch_ring_r<6, KEYS>(a, lds, s);
+        case 7: return launch_ring_r<7, KEYS>(a, lds, s);
     }
     return (int)hipErrorInvalidValue;
 }
 
+// Split ring merge: per pixel the smaller of the two passes' keys (pass B's indices shifted
+// past pass A's 256: on equal costs pass A's smaller disparity wins, the first minimum), and
+// the band-edge columns' invalid value.  4 pixels per thread (16-B key loads, one 8-B store)
+// when the pitch, frame stride and map allow it.
+__device__ __forceinline__ int16_t merge_px(uint32_t ka, uint32_t kb, int x, int X0, int X1, int minD) {
+    const uint32_t k = min(ka, kb + 256u);
+    return (int16_t)(x >= X0 && x < X1 ? ((int)(k & 0xFFFFu) + minD) * 16 : (minD - 1) * 16);
+}
+__global__ __launch_bounds__(256) void k_merge_ring_keys(const uint32_t* __restrict__ ka,
+                                                         const uint32_t* __restrict__ kb, int16_t* __restrict__ out,
+                                                         int opitch, long long fs_out, int row0, int W, int X0, int X1,
+                                                         int minD, int vec) {
+    const int x = 4 * (int)(blockIdx.x * 256 + threadIdx.x);
+    if (x >= W) return;
+    const size_t i = (size_t)blockIdx.z * fs_out + (size_t)(row0 + (int)blockIdx.y) * opitch + x;
+    if (vec && x + 4 <= W) {
+        const uint4 a = *reinterpret_cast<const uint4*>(ka + i);
+        const uint4 b = *reinterpret_cast<const uint4*>(kb + i);
+        const uint32_t lo = (uint16_t)merge_px(a.x, b.x, x, X0, X1, minD) |
+                            ((uint32_t)(uint16_t)merge_px(a.y, b.y, x + 1, X0, X1, minD) << 16);
+        const uint32_t hi = (uint16_t)merge_px(a.z, b.z, x + 2, X0, X1, minD) |
+                            ((uint32_t)(uint16_t)merge_px(a.w, b.w, x + 3, X0, X1, minD) << 16);
+        *reinterpret_cast<uint2*>(out + i) = make_uint2(lo, hi);
+        return;
+    }
+    for (int q = 0; q < 4 && x + q < W; ++q) out[i + q] = merge_px(ka[i + q], kb[i + q], x + q, X0, X1, minD);
+}
+
 
 }  // namespace
+
+// D in (256, 512]: the ring kind twice, d in [0, 256) (64-lane groups) and [256, D) (its
+// own group width), each into a key plane, then k_merge_ring_keys — the four-row kind it
+// replaces ran 2.3x slower per cell (1080p D=320 w7: 2,322 us per 16 frames against 805 for
+// D=256, round 4)
+bool ring_split(int cost, int win, int num_disp) {
+    return num_disp > 256 && num_disp <= 512 && ring_kind(cost, win, 256) && ring_kind(cost, win, num_disp - 256);
+}
+long long ring_split_elems(int nf, long long fs_out, int row1, int opitch) {
+    return ((long long)(nf > 1 ? nf - 1 : 0) * fs_out + (long long)(row1 + 3) * opitch + 64 + 3) & ~3LL;
+}
 
 uint64_t max_cost(int win, int cost) {
     return cost == COST_SAD ? (uint64_t)win * win * 255
@@ -1286,7 +1334,26 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
     // (2 * (row * out_pitch + x) per frame); maps whose last row lies past 2^31 bytes take
     // the size_t-addressed four-row kind instead
     const bool ring_fits = 2LL * ((long long)(a.row1 + 3) * a.opitch + a.W + 64) < 0x7FFFFFFFLL;
-    if (ring_kind(cost, a.win, a.D) && ring_fits) return launch_ring(a, s);
+    if (ring_kind(cost, a.win, a.D) && ring_fits) return launch_ring<false>(a, s);
+    if (ring_split(cost, a.win, a.D) && a.keys) {
+        // (key planes: 4-byte elements, so half the 2^31-byte range of the int16 maps)
+        if (4LL * ((long long)(a.row1 + 3) * a.opitch + a.W + 64) >= 0x7FFFFFFFLL) return (int)hipErrorInvalidValue;
+        MatchParams pa = a, pb = a;
+        pa.D = 256;
+        pb.minD = a.minD + 256;
+        pb.D = a.D - 256;
+        pb.keys = a.keys + a.keys_stride;
+        int e = launch_ring<true>(pa, s);
+        if (!e) e = launch_ring<true>(pb, s);
+        if (e) return e;
+        const int nf = a.nf > 1 ? a.nf : 1;
+        const long long fso = nf > 1 ? a.fs_out : 0LL;
+        const int vec = (a.opitch % 4 == 0 && fso % 4 == 0 && a.keys_stride % 4 == 0 &&
+                         ((uintptr_t)a.out & 7) == 0 && ((uintptr_t)a.keys & 15) == 0) ? 1 : 0;
+        hipLaunchKernelGGL(k_merge_ring_keys, dim3((a.W + 1023) / 1024, a.row1 - a.row0, nf), dim3(256), 0, s, pa.keys,
+                           pb.keys, a.out, a.opitch, fso, a.row0, a.W, a.X0, a.X1, a.minD, vec);
+        return (int)hipGetLastError();
+    }
     const size_t lds = match_lds_bytes(p, a.r, cost);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
     MatchParams b = a;

@@ -448,7 +448,7 @@ __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g,
 // with 64x16 LDS tiles; 94 -> 87 -> 69 us in 2-frame batches with a ring of the last 2r+1 row
 // sums; 65 -> 60.5 us with the vertical-first form below, which holds 49 VGPRs instead of 127;
 // round 4 rows per wave, C5 HOG 2-frame batches, per launch of 4 images: 32 252, 48 249,
-// 64 261, 96 265, 128 268 us.)
+// 64 261, 96 265, 128 268 us; two rows per step with the LDS sums 248 -> 256 us.)
 constexpr int HS_ROWS = 48;
 
 template <int CTRL>

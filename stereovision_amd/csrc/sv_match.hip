@@ -802,15 +802,15 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     // reads the leaving column's cost after the entering one is computed, so the two cannot
     // share a register: the cost ring gets M = W2 + 1 slots (the entering cost goes to the
     // slot whose value left the window one step earlier) and keeps static register names.
-    // r 5: 16 more ring VGPRs spill 4-9 VGPRs, which still pays for 32-lane groups (1080p
-    // D=128 win 11: 572 -> 555 us per 16 frames) but not for 16-lane ones (VGA D=64 win 11:
-    // 122 -> 139 us), so those and the unmeasured 64-lane groups keep the sub/add form;
+    // r 5: the 16 more ring VGPRs first spilled 4-9 VGPRs to scratch (1080p D=128 win 11:
+    // 572 -> 555 us per 16 frames with 32-lane groups, VGA D=64 win 11 122 -> 139 us with
+    // 16-lane ones); without the left-pack prefetch (LPF) every group width fits in 252-255.
     // r 6..7 (packed halves) take it too: 16 / 14 slots of 8 words.
     // PK: the two u16 halves of a cost word update as ONE 32-bit v_sad_u32 as well: each half
     // of the key holds its leaving cost as a summand, so key >= leaving as 32-bit integers with
     // no borrow between the halves, and key - leaving + entering stays below 2^16 per half (no
     // carry): the packed result is exact.
-    constexpr bool SADU = PK || R <= 4 || (R == 5 && LPGT == 32);
+    constexpr bool SADU = PK || R <= 5;
     constexpr int M = SADU ? W2 + 1 : W2;               // cost ring slots
     constexpr int U = M % 4 == 0 ? M : M % 2 == 0 ? 2 * M : 4 * M;   // lcm(4, M) steps per body
     constexpr int NCH = U / 4;                          // chunks per body
@@ -884,6 +884,10 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     // offsets are never dereferenced)
     PackPtr<COST_SAD4, R> rb = Rp + (rslot(iR0, c0, RG_DPL) - e0 * (RG_DPL + 1));
     PackPtr<COST_SAD4, R> lb = Lp + (g * S - 4 * e0);
+    // LPF: the left pack is loaded one step ahead (off for r 5 + SADU, whose 32-lane body is
+    // 4 VGPRs over the 256 a wave of two per SIMD may hold: the 6 registers of the prefetched
+    // pack take its spills out of the loop)
+    constexpr bool LPF = !(R == 5 && SADU);
     Pk<NW> Lnext = ld<COST_SAD4, R, true>(lb + 4 * e0);
     // after the reduce-scatter lane l's key is (row jq, step ju) of the chunk; the first 16
     // lanes of a group emit
@@ -964,8 +968,8 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                 const int slot = (4 * ch + u) % M, oslot = (4 * ch + u + 1) % M;
                 // this step's packs: L (every k) and the entering right column (k = 0 only)
                 rn[u] = ld<COST_SAD4, R, true>(rb + (ch * (RG_DPL + 1) + u));
-                const Pk<NW> Lc = Lnext;                 // loaded one step ahead
-                Lnext = ld<COST_SAD4, R, true>(lb + (4 * ch + u + 1));
+                const Pk<NW> Lc = LPF ? Lnext : ld<COST_SAD4, R, true>(lb + (4 * ch + u));
+                if constexpr (LPF) Lnext = ld<COST_SAD4, R, true>(lb + (4 * ch + u + 1));
                 // !SADU: the leaving column's costs need no LDS data: subtract them while the
                 // loads are in flight; k = 0 (the fresh right pack) last
                 if constexpr (!SADU) {

@@ -82,6 +82,7 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
 // D > 256 SAD windows run the ring kind twice (d < 256, d >= 256) into key planes and merge:
 // whether a launch takes that form, and the elements of one key plane it needs
 bool ring_split(int cost, int win, int num_disp);
+bool ring_ssd(int cost, int win, int num_disp);   // SSD windows 5..9, D <= 256: the ring kind
 long long ring_split_elems(int nf, long long fs_out, int row1, int opitch);
 int launch_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v, hipStream_t s);
 

@@ -773,7 +773,12 @@ __device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
 // loop-carried VGPRs (off for r 5, which would spill).
 // KEYS (split ring, D > 256): the reduced argmin keys (cost << 16 | idx) go to a.keys as u32
 // (the merge kernel picks the smaller of the two passes' keys), no band-edge fill.
-template <int R, int LPGT, bool DEFER, bool KEYS>
+// SSD (r <= 4): the same packs and ring with squared differences, Σ(L-R)² = ΣL² + ΣR² - 2ΣLR
+// over each output row's window column: v_dot4_u32_u8 on the common and per-row words (the
+// packs' zero bytes add nothing), ΣL² once per step, ΣR² per disparity slot; the column cost
+// enters pre-shifted by dbits, (ΣL² + ΣR²) << dbits - ΣLR << (dbits + 1) by one
+// v_mad_i32_i24, and the window update is the same v_sad_u32.
+template <int R, int LPGT, bool DEFER, bool KEYS, bool SSD = false>
 __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     using P = PackCfg<COST_SAD4, R>;
     constexpr int NW = P::NW, NC = P::NC, W2 = 2 * R + 1;
@@ -865,7 +870,7 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
 #pragma unroll
     for (int k = 0; k < RG_DPL; ++k) {
         const int idx = 4 * l + k;
-        const uint32_t base = PK ? 0u : idx < a.D ? (uint32_t)idx : (0x8000u << 16) | (uint32_t)idx;
+        const uint32_t base = PK ? 0u : idx < a.D ? (uint32_t)idx : (SSD ? a.pad_key : 0x8000u << 16) | (uint32_t)idx;
         lab[k] = (uint32_t)idx;
 #pragma unroll
         for (int q = 0; q < RQ; ++q) h[k][q] = base;
@@ -924,7 +929,8 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
         // check, as in composable_kernel): no exec-mask branch
         const int off = (unsigned)(tt + eb) < (unsigned)emax ? ooff + OB * tt : (int)0x80000000u;
         if constexpr (KEYS) __builtin_amdgcn_raw_buffer_store_b32(key, orsrc, off, 0, 0);
-        else __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(((int)(key & 0xFFFFu) + a.minD) * 16), orsrc, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b16(
+            (uint16_t)(((int)(key & (SSD ? (1u << a.dbits) - 1u : 0xFFFFu)) + a.minD) * 16), orsrc, off, 0, 0);
     };
     // join2: pair (0,1) in kA, pair (2,3) in kB: one swap joins both
     auto join_pairs = [&](uint32_t kA_, uint32_t kB_) {
@@ -970,6 +976,16 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                 rn[u] = ld<COST_SAD4, R, true>(rb + (ch * (RG_DPL + 1) + u));
                 const Pk<NW> Lc = LPF ? Lnext : ld<COST_SAD4, R, true>(lb + (4 * ch + u));
                 if constexpr (LPF) Lnext = ld<COST_SAD4, R, true>(lb + (4 * ch + u + 1));
+                // SSD: ΣL² of this step's left pack per output row, pre-shifted by dbits
+                uint32_t sqL[4];
+                if constexpr (SSD) {
+                    uint32_t sc = 0u;
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) sc = __builtin_amdgcn_udot4(Lc.w[i], Lc.w[i], sc, false);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        sqL[q] = __builtin_amdgcn_udot4(Lc.w[NC + q], Lc.w[NC + q], sc, false) << a.dbits;
+                }
                 // !SADU: the leaving column's costs need no LDS data: subtract them while the
                 // loads are in flight; k = 0 (the fresh right pack) last
                 if constexpr (!SADU) {
@@ -998,6 +1014,22 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
                             if constexpr (SADU) sad_u32_acc(h[k][j], ring[oslot][k][j], c);
                             else h[k][j] = pk_add16(h[k][j], c);
                             ring[slot][k][j] = c;
+                        }
+                    } else if constexpr (SSD) {
+                        uint32_t cn = 0u, sr = 0u;
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) {
+                            cn = __builtin_amdgcn_udot4(Lc.w[i], Rk.w[i], cn, false);
+                            sr = __builtin_amdgcn_udot4(Rk.w[i], Rk.w[i], sr, false);
+                        }
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const uint32_t lr = __builtin_amdgcn_udot4(Lc.w[NC + q], Rk.w[NC + q], cn, false);
+                            const uint32_t rr = __builtin_amdgcn_udot4(Rk.w[NC + q], Rk.w[NC + q], sr, false);
+                            const uint32_t t = (rr << a.dbits) + sqL[q];
+                            const uint32_t c = (uint32_t)__mul24((int)lr, -(2 << a.dbits)) + t;
+                            sad_u32_acc(h[k][q], ring[oslot][k][q], c);
+                            ring[slot][k][q] = c;
                         }
                     } else {
                         uint32_t cn = 0u;
@@ -1173,7 +1205,7 @@ size_t ring_lds_bytes(int lpg, int seg, int r) {
     return (size_t)(nl + nrp) * (r <= 5 ? 24 : 32);
 }
 
-template <int R, int LPG, bool KEYS>
+template <int R, int LPG, bool KEYS, bool SSD>
 int launch_ring_rl(const MatchParams& a, size_t lds, hipStream_t s) {
     // SV_RING_DEFER=0 (A/B): every pair reduced inside its own chunk
     static const bool defer = [] {
@@ -1181,7 +1213,8 @@ int launch_ring_rl(const MatchParams& a, size_t lds, hipStream_t s) {
         return !(e && e[0] == '0');
     }();
     void (*fn)(MatchParams);
-    if constexpr (KEYS) fn = k_match_ring<R, LPG, R != 5, true>;
+    if constexpr (SSD) fn = k_match_ring<R, LPG, R != 5, false, true>;
+    else if constexpr (KEYS) fn = k_match_ring<R, LPG, R != 5, true>;
     else fn = (defer && R != 5) ? k_match_ring<R, LPG, R != 5, false> : k_match_ring<R, LPG, false, false>;
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1199,34 +1232,44 @@ int launch_ring_rl(const MatchParams& a, size_t lds, hipStream_t s) {
     hipLaunchKernelGGL(fn, grid, dim3(64), lds, s, b);
     return (int)hipGetLastError();
 }
-template <int R, bool KEYS>
+template <int R, bool KEYS, bool SSD = false>
 int launch_ring_r(const MatchParams& a, size_t lds, hipStream_t s) {
     switch (a.lpg) {
-        case 16: return launch_ring_rl<R, 16, KEYS>(a, lds, s);
-        case 32: return launch_ring_rl<R, 32, KEYS>(a, lds, s);
-        case 64: return launch_ring_rl<R, 64, KEYS>(a, lds, s);
+        case 16: return launch_ring_rl<R, 16, KEYS, SSD>(a, lds, s);
+        case 32: return launch_ring_rl<R, 32, KEYS, SSD>(a, lds, s);
+        case 64: return launch_ring_rl<R, 64, KEYS, SSD>(a, lds, s);
     }
     return (int)hipErrorInvalidValue;
 }
 
-template <bool KEYS>
+template <bool KEYS, bool SSD = false>
 int launch_ring(const MatchParams& a0, hipStream_t s) {
     MatchParams a = a0;
     a.lpg = ring_lpg(a.D);
     a.lpg_log2 = a.lpg == 16 ? 4 : a.lpg == 32 ? 5 : 6;
-    a.dbits = 16;
+    a.dbits = SSD ? a.lpg_log2 + 2 : 16;   // SSD keys: (cost << log2(4 LPG)) | idx
+    if (SSD) a.pad_key = (uint32_t)((max_cost(a.win, COST_SSD) + 1) << a.dbits);
     a.segm = ring_seg(a.lpg, a.r, a.X1 - a.X0, (long long)((a.row1 - a.row0 + 3) / 4) * (a.nf > 1 ? a.nf : 1));
     const size_t lds = ring_lds_bytes(a.lpg, a.segm, a.r);
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-    switch (a.r) {
-        case 2: return launch_ring_r<2, KEYS>(a, lds, s);
-        case 3: return launch_ring_r<3, KEYS>(a, lds, s);
-        case 4: return launch_ring_r<4, KEYS>(a, lds, s);
-        case 5: return launch_ring_r<5, KEYS>(a, lds, s);
-        case 6: return launch_ring_r<6, KEYS>(a, lds, s);
-        case 7: return launch_ring_r<7, KEYS>(a, lds, s);
+    if constexpr (SSD) {
+        switch (a.r) {
+            case 2: return launch_ring_r<2, false, true>(a, lds, s);
+            case 3: return launch_ring_r<3, false, true>(a, lds, s);
+            case 4: return launch_ring_r<4, false, true>(a, lds, s);
+        }
+        return (int)hipErrorInvalidValue;
+    } else {
+        switch (a.r) {
+            case 2: return launch_ring_r<2, KEYS>(a, lds, s);
+            case 3: return launch_ring_r<3, KEYS>(a, lds, s);
+            case 4: return launch_ring_r<4, KEYS>(a, lds, s);
+            case 5: return launch_ring_r<5, KEYS>(a, lds, s);
+            case 6: return launch_ring_r<6, KEYS>(a, lds, s);
+            case 7: return launch_ring_r<7, KEYS>(a, lds, s);
+        }
+        return (int)hipErrorInvalidValue;
     }
-    return (int)hipErrorInvalidValue;
 }
 
 // Split ring merge: per pixel the smaller of the two passes' keys (pass B's indices shifted
@@ -1264,6 +1307,16 @@ __global__ __launch_bounds__(256) void k_merge_ring_keys(const uint32_t* __restr
 // own group width), each into a key plane, then k_merge_ring_keys — the four-row kind it
 // replaces ran 2.3x slower per cell (1080p D=320 w7: 2,322 us per 16 frames against 805 for
 // D=256, round 4)
+// SSD windows 5..9 with D <= 256 take the ring kind's SSD form when the keys (cost << dbits |
+// idx, padding lanes above every real key) fit 32 bits
+bool ring_ssd(int cost, int win, int num_disp) {
+    if (cost != COST_SSD || win < 5 || win > 9 || num_disp < 1 || num_disp > 256) return false;
+    if (!ring_kind(COST_SAD, win, num_disp)) return false;   // (SV_RING=0 switches it off too)
+    const int lpg = ring_lpg(num_disp), dbits = (lpg == 16 ? 4 : lpg == 32 ? 5 : 6) + 2;
+    const uint64_t cmax = max_cost(win, COST_SSD);
+    const uint64_t top = num_disp < 4 * lpg ? (2 * cmax + 2) << dbits : (cmax << dbits) + (uint64_t)(4 * lpg);
+    return top < (1ull << 32);
+}
 bool ring_split(int cost, int win, int num_disp) {
     return num_disp > 256 && num_disp <= 512 && ring_kind(cost, win, 256) && ring_kind(cost, win, num_disp - 256);
 }
@@ -1339,6 +1392,7 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
     // the size_t-addressed four-row kind instead
     const bool ring_fits = 2LL * ((long long)(a.row1 + 3) * a.opitch + a.W + 64) < 0x7FFFFFFFLL;
     if (ring_kind(cost, a.win, a.D) && ring_fits) return launch_ring<false>(a, s);
+    if (ring_ssd(cost, a.win, a.D) && ring_fits) return launch_ring<false, true>(a, s);
     if (ring_split(cost, a.win, a.D) && a.keys) {
         // (key planes: 4-byte elements, so half the 2^31-byte range of the int16 maps)
         if (4LL * ((long long)(a.row1 + 3) * a.opitch + a.W + 64) >= 0x7FFFFFFFLL) return (int)hipErrorInvalidValue;

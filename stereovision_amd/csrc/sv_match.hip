@@ -1257,7 +1257,6 @@ int launch_ring(const MatchParams& a0, hipStream_t s) {
             case 2: return launch_ring_r<2, false, true>(a, lds, s);
             case 3: return launch_ring_r<3, false, true>(a, lds, s);
             case 4: return launch_ring_r<4, false, true>(a, lds, s);
-            case 5: return launch_ring_r<5, false, true>(a, lds, s);
         }
         return (int)hipErrorInvalidValue;
     } else {

@@ -1102,7 +1102,8 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
         return !(e && e[0] == '0');
     }();
     // (D <= 128 measured even: 703 vs 707 frames/s per call at D=128, so the concurrent form
-    // stays there; D=320: 337 -> 359 per call, 373 -> 416 at batch 4)
+    // stays there; D=320: 337 -> 359 per call, 373 -> 416 at batch 4.  Round 4, with the deep
+    // one-wave variant also for D <= 128: 1080p D=128 712 -> 719, VGA D=64 7,160 -> 5,640)
     const bool vwta = !fused && vwta_on && pv.lpc == 32 && a.D > 128;
     // deep: the vertical path + WTA of a launch this small (at most ~1 wave per SIMD: one
     // 1080p frame is ~800 waves) takes the variant with one wave per SIMD and a 3x deeper

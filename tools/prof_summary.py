@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile.sh output dir into profiles/<tag>_summary.md and update
-profiles/pmc_summary.json (HBM bytes per k_match launch, read by bench.py)."""
+profiles/pmc_summary.json (HBM bytes per k_match launch; a record, bench.py measures live)."""
 import collections
 import csv
 import glob

@@ -133,10 +133,7 @@ struct sv_ctx {
     std::vector<uint8_t> hl_u8;
     std::vector<HostEnt> hl_ent;
     bool hl_valid = false;
-    hipEvent_t cev[8] = {};
-    // host-buffer frame path: band k's outputs come back on `dstream` (after cev[k] on the
-    // compute stream), `dev_done[k]` marks their arrival
-    hipStream_t dstream = nullptr;
+    // host-buffer frame path: `dev_done[k]` marks the arrival of output piece k
     hipEvent_t dev_done[8] = {};
     hipEvent_t tmr[2] = {nullptr, nullptr};   // sv_timer_begin / sv_timer_end
     // SGBM: second stream + fork/join events for the vertical path beside the horizontal ones
@@ -735,14 +732,8 @@ void sv_destroy(sv_ctx* c) {
             (void)hipEventDestroy(c->region.a);
             (void)hipEventDestroy(c->region.b);
         }
-        for (auto e : c->cev)
-            if (e) (void)hipEventDestroy(e);
         for (auto e : c->dev_done)
             if (e) (void)hipEventDestroy(e);
-        if (c->dstream) {
-            (void)hipStreamSynchronize(c->dstream);
-            (void)hipStreamDestroy(c->dstream);
-        }
         for (auto e : c->tmr)
             if (e) (void)hipEventDestroy(e);
         if (c->sg_aux) {
@@ -2068,22 +2059,14 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
     }
     if (prof) { const double t = now_ms(); tm[0] = t - tp; tp = t; }
 
-    // Row bands, pipelined: band k's input rows are staged and uploaded, then every
-    // disparity row whose window lies in the rows uploaded so far, then every median row
-    // whose 5x5 neighbourhood is computed, and those output rows go back on the download
-    // stream while band k+1 is staged (the H2D and D2H directions overlap).  SGBM's top-down
-    // path spans the frame: one band.
-    const char* be = std::getenv("SV_HOST_BANDS");   // A/B (read per call): 1, 2 or 4 bands
-    const int bv = be ? std::atoi(be) : 1;
-    const int bands_env = bv == 2 || bv == 4 ? bv : 1;
-    const int nband = (cost != SV_COST_SGBM && H >= 64 * bands_env) ? bands_env : 1;
-    // one band: the outputs come back on the compute stream itself (no cross-stream wait)
-    const int npiece = 8 / nband;   // D2H pieces per band, each with its arrival event
-    if (nband > 1 && !c->dstream) SV_HIP(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
-    hipStream_t ds = nband > 1 ? c->dstream : c->stream;
-    const int below = win / 2 + 1;   // input rows below a disparity row (HOG: window + gradient)
-    int d_done = 0, m_done = 0;
-    int bands[8][2] = {};   // output rows of each D2H piece
+    // One pass over the whole frame (round 3 also built pipelined row bands, band k's outputs
+    // returning on a download stream while band k+1 uploaded: bit-exact but no faster in
+    // rounds 3 and 4, so it was removed): stage + upload, gray, disparity, median, then the
+    // outputs return in 8 pieces on the compute stream, each behind its own event so the host
+    // expansion of one piece runs while the next is in flight.
+    constexpr int npiece = 8;
+    hipStream_t ds = c->stream;
+    int bands[npiece][2] = {};   // output rows of each D2H piece
     std::atomic<int> bad{0};
     sv::HostPool& pool = sv::HostPool::get();
     auto expand = [&](int k) -> int {   // host expansion of piece k's medians
@@ -2114,73 +2097,45 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
         return 0;
     };
     const uint8_t* src[2] = {left, right};
-    for (int k = 0; k < nband; ++k) {
-        const int y0 = (int)((long long)H * k / nband), y1 = (int)((long long)H * (k + 1) / nband);
-        const bool last = k == nband - 1;
-        for (int i = 0; i < 2; ++i) {
-            uint8_t* stage = c->hin.as<uint8_t>() + (size_t)i * row * H;
-            uint8_t* dst = channels == 1 ? c->gray[i].as<uint8_t>() : c->img[i].as<uint8_t>();
-            rc = stage_rows(c, src[i], y0, y1, row, stride, stage, dst, nband == 1 ? 6 : 2);
-            if (rc) return rc;
-            if (channels == 3)
-                SV_LAUNCH(c, SV_K_GRAY, c->stream,
-                          sv::launch_gray(c->img[i].as<uint8_t>() + (size_t)y0 * row, y1 - y0, W, (int)row,
-                                          c->gray[i].as<uint8_t>() + (size_t)y0 * W, c->stream));
-        }
-        const int d1 = last ? H : std::max(d_done, y1 - below);
-        if (d1 > d_done) {
-            rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp,
-                                   num_disp, win, cost, d_done, d1, c->d16.as<int16_t>(), W, c->stream);
-            if (rc) return rc;
-            d_done = d1;
-        }
-        const int m1 = last ? H : std::max(m_done, d_done - 2);
-        if (m1 > m_done) {
-            SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
-                      sv::launch_median_i16(c->d16.as<int16_t>(), H, W, m_done, m1, reg ? c->fb.as<float>() : nullptr,
-                                            mp, c->stream));
-            if (ds != c->stream) {
-                if (!c->cev[k]) SV_HIP(hipEventCreateWithFlags(&c->cev[k], hipEventDisableTiming));
-                SV_HIP(hipEventRecord(c->cev[k], c->stream));
-                SV_HIP(hipStreamWaitEvent(ds, c->cev[k], 0));
-            }
-            for (int j = 0; j < npiece; ++j) {
-                const int q = k * npiece + j;
-                const int p0 = m_done + (int)((long long)(m1 - m_done) * j / npiece);
-                const int p1 = m_done + (int)((long long)(m1 - m_done) * (j + 1) / npiece);
-                bands[q][0] = p0;
-                bands[q][1] = p1;
-                if (p1 <= p0) continue;
-                const size_t i0 = (size_t)p0 * W, m = (size_t)(p1 - p0) * W;
-                if (reg) {
-                    SV_HIP(hipMemcpyAsync(o.disp + i0, c->fb.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
-                    SV_HIP(hipMemcpyAsync(o.a + i0, c->fa.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
-                    if (o.u8) SV_HIP(hipMemcpyAsync(o.u8 + i0, c->u8.as<uint8_t>() + i0, m, hipMemcpyDeviceToHost, ds));
-                    if (scaled)
-                        SV_HIP(hipMemcpyAsync(o.b + i0, c->fc.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
-                    if (o.bgr)
-                        SV_HIP(hipMemcpyAsync(o.bgr + 3 * i0, c->bgr.as<uint8_t>() + 3 * i0, 3 * m,
-                                              hipMemcpyDeviceToHost, ds));
-                } else {
-                    SV_HIP(hipMemcpyAsync(c->hout.as<int16_t>() + i0, c->m16.as<int16_t>() + i0, m * 2,
-                                          hipMemcpyDeviceToHost, ds));
-                    if (!c->dev_done[q]) SV_HIP(hipEventCreateWithFlags(&c->dev_done[q], hipEventDisableTiming));
-                    SV_HIP(hipEventRecord(c->dev_done[q], ds));
-                }
-            }
-            m_done = m1;
-        }
-        if (prof && k == 0) { const double t = now_ms(); tm[1] = t - tp; tp = t; }
-        if (!reg && k > 0) {   // the previous band's expansion runs while this band is in flight
-            for (int j = 0; j < npiece; ++j) {
-                rc = expand((k - 1) * npiece + j);
-                if (rc) return rc;
-            }
+    for (int i = 0; i < 2; ++i) {
+        uint8_t* stage = c->hin.as<uint8_t>() + (size_t)i * row * H;
+        uint8_t* dst = channels == 1 ? c->gray[i].as<uint8_t>() : c->img[i].as<uint8_t>();
+        rc = stage_rows(c, src[i], 0, H, row, stride, stage, dst, 6);
+        if (rc) return rc;
+        if (channels == 3)
+            SV_LAUNCH(c, SV_K_GRAY, c->stream,
+                      sv::launch_gray(c->img[i].as<uint8_t>(), H, W, (int)row, c->gray[i].as<uint8_t>(), c->stream));
+    }
+    rc = enqueue_disparity(c, c->gray[0].as<uint8_t>(), c->gray[1].as<uint8_t>(), H, W, W, min_disp, num_disp, win,
+                           cost, 0, H, c->d16.as<int16_t>(), W, c->stream);
+    if (rc) return rc;
+    SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
+              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, reg ? c->fb.as<float>() : nullptr, mp,
+                                    c->stream));
+    for (int q = 0; q < npiece; ++q) {
+        const int p0 = (int)((long long)H * q / npiece), p1 = (int)((long long)H * (q + 1) / npiece);
+        bands[q][0] = p0;
+        bands[q][1] = p1;
+        if (p1 <= p0) continue;
+        const size_t i0 = (size_t)p0 * W, m = (size_t)(p1 - p0) * W;
+        if (reg) {
+            SV_HIP(hipMemcpyAsync(o.disp + i0, c->fb.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
+            SV_HIP(hipMemcpyAsync(o.a + i0, c->fa.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
+            if (o.u8) SV_HIP(hipMemcpyAsync(o.u8 + i0, c->u8.as<uint8_t>() + i0, m, hipMemcpyDeviceToHost, ds));
+            if (scaled) SV_HIP(hipMemcpyAsync(o.b + i0, c->fc.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
+            if (o.bgr)
+                SV_HIP(hipMemcpyAsync(o.bgr + 3 * i0, c->bgr.as<uint8_t>() + 3 * i0, 3 * m, hipMemcpyDeviceToHost, ds));
+        } else {
+            SV_HIP(hipMemcpyAsync(c->hout.as<int16_t>() + i0, c->m16.as<int16_t>() + i0, m * 2, hipMemcpyDeviceToHost,
+                                  ds));
+            if (!c->dev_done[q]) SV_HIP(hipEventCreateWithFlags(&c->dev_done[q], hipEventDisableTiming));
+            SV_HIP(hipEventRecord(c->dev_done[q], ds));
         }
     }
+    if (prof) { const double t = now_ms(); tm[1] = t - tp; tp = t; }
     if (!reg) {
-        for (int j = 0; j < npiece; ++j) {
-            rc = expand((nband - 1) * npiece + j);
+        for (int q = 0; q < npiece; ++q) {
+            rc = expand(q);
             if (rc) return rc;
         }
     }

@@ -645,18 +645,14 @@ def test_ring_kind_huge_out_pitch_falls_back_exactly(engine, win, D):
             engine.dev_free(p)
 
 
-@pytest.mark.parametrize("bands", ["1", "2", "4"])
 @pytest.mark.parametrize("H,W,D,win,cost", [(127, 200, 64, 9, "sad"), (256, 208, 64, 9, "sad"),
                                             (257, 240, 96, 15, "sad"), (301, 256, 64, 11, "ssd"),
-                                            (260, 320, 64, 7, "hog"), (1080, 1920, 128, 9, "sad")])
-def test_host_path_row_bands_match_oracle(engine, monkeypatch, bands, H, W, D, win, cost):
-    """The host-buffer frame path can run a frame as pipelined row bands (SV_HOST_BANDS, read
-    per call; frames of >= 64 rows per band): each band's disparity rows start once their
-    window's input rows are uploaded, each band's outputs return on a download stream while
-    the next band uploads.  Every output, on both the fresh-array path (int16 medians + host
-    expansion in 8 pieces) and the registered-output path (device epilogue + DMA), equals the
-    whole-frame C oracle."""
-    monkeypatch.setenv("SV_HOST_BANDS", bands)
+                                            (301, 256, 64, 7, "ssd"), (260, 320, 64, 7, "hog"),
+                                            (90, 700, 320, 7, "sad"), (1080, 1920, 128, 9, "sad")])
+def test_host_path_matches_oracle(engine, H, W, D, win, cost):
+    """The host-buffer frame path (stage + upload, gray, disparity, median, outputs back in 8
+    pieces): every output, on both the fresh-array path (int16 medians + host expansion per
+    piece) and the registered-output path (device epilogue + DMA), equals the C oracle."""
     L, R, _ = stereo_pair(H, W, D, seed=H + W + win)
     bl, br = to_bgr(L), to_bgr(R)
     g0, g1 = C.gray(bl), C.gray(br)

@@ -1867,10 +1867,9 @@ int stage_rows(sv_ctx* c, const uint8_t* src, int y0, int y1, size_t row, int st
     // runtime's own pinned staging, pipelined with its DMA): measured faster than copying
     // into our pinned buffer on the pool threads (1080p create_depth_map 1.03-1.11k vs
     // 0.79-0.89k frames/s per call, 1.49-1.57k vs 0.72-1.18k with 4 in flight,
-    // gpurun_out/host3).  SV_HOST_STAGE=1 (read per call) restores the pinned copy; strided
-    // rows always take it.
-    const char* se = std::getenv("SV_HOST_STAGE");
-    if (!(se && se[0] == '1') && (size_t)stride == row) {
+    // gpurun_out/host3; round 4 the same rates either way, profiles/r04_misc/
+    // host_stage_ab_r04h.txt); strided rows take the pinned copy.
+    if ((size_t)stride == row) {
         SV_HIP(hipMemcpyAsync(dev + (size_t)y0 * row, src + (size_t)y0 * row, (size_t)(y1 - y0) * row,
                               hipMemcpyHostToDevice, c->stream));
         return 0;

@@ -1060,16 +1060,8 @@ int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStre
         return e && e[0] == 'l';
     }();
     if (!lds && W >= 8 && H >= 8) {
-        // SV_HARRIS_HB (A/B): output rows per wave
-        static const int hb = [] {
-            const char* e = std::getenv("SV_HARRIS_HB");
-            const int v = e ? std::atoi(e) : 8;
-            return v == 16 || v == 32 ? v : 8;
-        }();
-#define SV_HARRIS_L(HB, PF)                                                                                    \
-        hipLaunchKernelGGL((k_harris_dpp<HB, PF>), dim3((W + 59) / 60, (H + HB - 1) / HB, nf), dim3(64), 0, s, g, \
-                           H, W, pitch, out, fs_in, fs_out)
-        // 8 rows: C2 16.8 us per 16 VGA frames (16: 17.7, 32: 21.0; 1080p 99 / 98 / 105 us)
+        // 8 output rows per wave: C2 16.8 us per 16 VGA frames (16 rows: 17.7, 32: 21.0; 1080p
+        // 99 / 98 / 105 us; the SV_HARRIS_HB A/B switch was removed in round 4)
         // SV_HARRIS=dpp1 (A/B): one column per lane everywhere
         static const bool one = [] {
             const char* e = std::getenv("SV_HARRIS");
@@ -1082,10 +1074,8 @@ int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStre
                                pitch, out, fs_in, fs_out);
             return (int)hipGetLastError();
         }
-        if (hb == 16) SV_HARRIS_L(16, 4);
-        else if (hb == 32) SV_HARRIS_L(32, 4);
-        else SV_HARRIS_L(8, 4);
-#undef SV_HARRIS_L
+        hipLaunchKernelGGL((k_harris_dpp<8, 4>), dim3((W + 59) / 60, (H + 7) / 8, nf), dim3(64), 0, s, g, H, W, pitch,
+                           out, fs_in, fs_out);
         return (int)hipGetLastError();
     }
     hipLaunchKernelGGL(k_harris_lds, dim3((W + HX2 - 1) / HX2, (H + HY2 - 1) / HY2, nf), dim3(256), 0, s, g,

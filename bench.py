@@ -541,6 +541,11 @@ def parse_args(argv=None):
                          "final disparity rows', 2 B/px over xGMI); full: also create_depth_map's "
                          "depth f32 / disparity f32 / u8 for every frame, expanded on GPU 0 from "
                          "the gathered medians (k_post_m16, 11 B/px of GPU 0's HBM per peer frame)")
+    ap.add_argument("--gather-format", default="auto", choices=["auto", "i16", "u8"],
+                    help="launched frames mode, --root-outputs m16: the gathered disparity rows as "
+                         "int16 x16 (2 B/px) or as u8 disparity indices d - min_disp + 1 (1 B/px: "
+                         "SAD/SSD/HOG disparities are whole pixels, exact for num_disp <= 255); "
+                         "auto: u8 where exact")
     ap.add_argument("--rehearse", action="store_true",
                     help="one process: run --gpus N logical GPUs on the visible devices (logical "
                          "GPU k on device k %% devices: own context, stream and buffers; gathers "
@@ -639,6 +644,12 @@ def main():
         dR.append(a.upload(R))
     gather_all = (gather_on or rowtile) and not launched and len(engines) > 1
     root_full = args.root_outputs == "full"
+    # u8 disparity indices over xGMI (1 B/px) where they are exact: integer-disparity costs,
+    # num_disp <= 255, and GPU 0 holds the gathered maps only (no expansion from int16 medians)
+    gather_u8 = (args.gather_format != "i16" and not root_full and args.cost != "sgbm" and D <= 255)
+    if args.gather_format == "u8" and not gather_u8:
+        raise SystemExit("--gather-format u8 needs --root-outputs m16, an integer cost and num_disp <= 255")
+    gel = 1 if gather_u8 else 2     # bytes per gathered pixel
     out_frames = 1 if rowtile else B * (len(engines) if gather_all else 1)
     depth = [a.alloc(4 * n_px * out_frames) for a in arenas]
     disp = [a.alloc(4 * n_px * out_frames) for a in arenas]
@@ -704,10 +715,10 @@ def main():
         ceng = Engine(devices[0])
         cstream = ceng.stream
         all_engines.append(ceng)
-        gset = [(depth[0], disp[0], norm[0], arenas[0].alloc(2 * n_px * B)),
+        gset = [(depth[0], disp[0], norm[0], arenas[0].alloc(gel * n_px * B)),
                 (arenas[0].alloc(4 * n_px * B), arenas[0].alloc(4 * n_px * B), arenas[0].alloc(n_px * B),
-                 arenas[0].alloc(2 * n_px * B))]
-        gathered = [arenas[0].alloc(2 * n_px * B * world) if rank == 0 else 0 for _ in range(2)]
+                 arenas[0].alloc(gel * n_px * B))]
+        gathered = [arenas[0].alloc(gel * n_px * B * world) if rank == 0 else 0 for _ in range(2)]
         # --root-outputs full: rank 0 expands the peers' gathered medians into create_depth_map's
         # outputs (its own frames already have them), double-buffered like the gathers
         nexp = n_px * B * (world - 1)
@@ -802,7 +813,7 @@ def main():
             else:
                 e.depth_map_batch_dev(dL[k] + f * n_px, dR[k] + f * n_px, B, H, W, W, n_px, 0, D, win,
                                       0.3, 2.0, depth_o[k], disp_o[k], norm_o[k], cost=args.cost,
-                                      d_med16=med_o)
+                                      d_med16=0 if gather_u8 else med_o, d_d8=med_o if gather_u8 else 0)
             if harris and (rectify or med_o or B == 1):   # one launch over the batch's left frames
                 e.harris_batch_dev(gL if rectify else dL[k] + f * n_px, B, H, W, W, n_px,
                                    hmaps_l[i % nstreams][k])
@@ -812,7 +823,7 @@ def main():
             eng.event_record(2 * gs, eng.stream)        # set gs computed
             eng.stream_wait_event(2 * gs, cstream)      # the gather follows it
             ceng.profile_region_begin("gather", cstream)
-            gather_frames(pg, gset[gs][3], B, gathered[gs], 2 * n_px, stream=cstream)
+            gather_frames(pg, gset[gs][3], B, gathered[gs], gel * n_px, stream=cstream)
             ceng.profile_region_end(cstream)
             if expanded is not None:   # the peers' frames, after the gather on the same stream
                 xd, xp, xu = expanded[gs]
@@ -962,9 +973,13 @@ def main():
                             Lz, Rz = hostL[0][f0 + z], hostR[0][f0 + z]
                         else:   # rank r's inputs, regenerated from its seed
                             Lz, Rz, _ = stereo_pair(H, W, D, seed=1000 * r + f0 + z)
-                        m16 = eng.to_host(gathered[last % 2] + 2 * n_px * (r * B + z), (H, W), np.int16)
-                        ver.disparity(f"rank {r} frame {f0 + z} (gathered on rank 0)", Lz, Rz,
-                                      m16.astype(np.float32) / np.float32(16.0))
+                        if gather_u8:   # d = d8 + min_disp - 1 (min_disp 0 here)
+                            d8 = eng.to_host(gathered[last % 2] + n_px * (r * B + z), (H, W), np.uint8)
+                            got = d8.astype(np.float32) - np.float32(1.0)
+                        else:
+                            m16 = eng.to_host(gathered[last % 2] + 2 * n_px * (r * B + z), (H, W), np.int16)
+                            got = m16.astype(np.float32) / np.float32(16.0)
+                        ver.disparity(f"rank {r} frame {f0 + z} (gathered on rank 0)", Lz, Rz, got)
                         if expanded is not None and r > 0:
                             xd, xp, xu = expanded[last % 2]
                             ver.frame(f"rank {r} frame {f0 + z} (expanded on rank 0)", Lz, Rz,
@@ -1069,8 +1084,8 @@ def main():
                 gbytes += 2 * (b["r1"] - b["r0"]) * W    # int16 x16 median rows
                 if band_inputs:
                     sbytes += 2 * (b["in1"] - b["in0"]) * W
-        elif gather_on:   # launched: the int16 x16 disparity maps; one process: all three outputs
-            gbytes = 2 * n_px * B * (ngpu - 1)   # int16 x16 medians (both process models)
+        elif gather_on:   # the disparity maps: u8 indices (launched, where exact) or int16 x16
+            gbytes = (gel if launched else 2) * n_px * B * (ngpu - 1)
     dist = dist_summary(ngpu, launched, pg, comms, gather=gather_on, rowtile=rowtile,
                         gather_ms=gath_ms, gather_n=gath_n, scatter_ms=scat_ms, scatter_n=scat_n,
                         gather_wall_s=gather_wall[0], steps=args.steps, gather_bytes=gbytes,
@@ -1079,14 +1094,19 @@ def main():
                                       else None),
                         gathered_maps=("row bands as int16 x16 medians, expanded on GPU 0 into depth f32 + "
                                        "disparity f32 + depth u8" if rowtile else
-                                       "disparity of every frame as int16 x16 (OpenCV's fixed point; the "
-                                       "f32 map is it / 16 exactly)"
+                                       ("disparity of every frame as u8 indices d - min_disp + 1 (whole-pixel "
+                                        "disparities: exact; the f32 map is d8 + min_disp - 1)"
+                                        if (launched and gather_u8) else
+                                        "disparity of every frame as int16 x16 (OpenCV's fixed point; the "
+                                        "f32 map is it / 16 exactly)")
                                        + (", expanded on GPU 0 into depth f32 + disparity f32 + depth u8"
                                           if root_full else "")
                                        + (", overlapped with the next step (communication stream, "
                                           "double-buffered maps)" if launched else
                                           ", two context lanes so a step's gather overlaps the next step"))
                         if (gather_on or rowtile) else None)
+    if dist is not None and gather_on and not rowtile:
+        dist["gather_format"] = "u8 disparity index" if (launched and gather_u8) else "int16 x16"
     parallelism = (f"row-tiled x{ngpu}" + (" (band inputs scattered from GPU 0)" if band_inputs else "")
                    + " + band gather" if rowtile else
                    f"frame-sharded x{ngpu}" + (" + gather to GPU 0" if gather_on else ""))

@@ -265,6 +265,19 @@ int sv_depth_map_batch_m16_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t
                                float* d_depth, float* d_disparity, uint8_t* d_norm,
                                int16_t* d_med16, void* stream);
 
+/* sv_depth_map_batch_dev that also writes each frame's median map as a u8 disparity index
+ * d8 = median / 16 - (min_disp - 1) into d_d8 (dense per frame): SAD / SSD / HOG disparities are
+ * whole pixels, so every median is a multiple of 16 and, with num_disp <= 255, d8 holds it
+ * exactly (0 = the invalid value min_disp - 1; d_disparity = d8 + min_disp - 1) — a quarter of
+ * the f32 map's bytes for the frame gather over xGMI (replaces the gather of
+ * fused_depth_map.py:2591-2598's per-frame results).  SGBM (sub-pixel) or num_disp > 255: -EINVAL. */
+int sv_depth_map_batch_d8_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
+                              int n_frames, int H, int W, int pitch, int64_t frame_stride,
+                              int min_disp, int num_disp, int win, int cost, float min_depth,
+                              float max_depth, float depth_range, float min_disp_global,
+                              float* d_depth, float* d_disparity, uint8_t* d_norm,
+                              uint8_t* d_d8, void* stream);
+
 /* C2 (BASELINE.json: "Harris+disparity"): sv_depth_map_batch_dev plus the Harris response
  * (cornerHarris(3, 3, 0.04) convention) of every LEFT frame into d_harris
  * (dense f32 per frame).  The response is computed by extra blocks of the median launch (the

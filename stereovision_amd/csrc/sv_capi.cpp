@@ -1005,6 +1005,37 @@ int sv_depth_map_batch_m16_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* 
     return 0;
 }
 
+int sv_depth_map_batch_d8_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, int n_frames, int H, int W,
+                              int pitch, int64_t frame_stride, int min_disp, int num_disp, int win, int cost,
+                              float min_depth, float max_depth, float depth_range, float min_disp_global,
+                              float* d_depth, float* d_disparity, uint8_t* d_norm, uint8_t* d_d8, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_left, H, W) || check_image(d_right, H, W) || !d_depth || !d_disparity || !d_norm || !d_d8 ||
+        n_frames < 0)
+        return fail(SV_EINVAL, "bad depth-map arguments");
+    if (cost == SV_COST_SGBM || num_disp < 1 || num_disp > 255)
+        return fail(SV_EINVAL, "u8 disparity indices need an integer-disparity cost and num_disp <= 255");
+    if (pitch < W) return fail(SV_EINVAL, "pitch smaller than width");
+    if (n_frames > 1 && frame_stride < (int64_t)pitch * H) return fail(SV_EINVAL, "frame stride smaller than a frame");
+    if (n_frames == 0) return 0;
+    hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
+    const long long fs = (long long)H * W;
+    SV_HIP(c->d16.ensure((size_t)n_frames * fs * sizeof(int16_t)));
+    int rc = enqueue_disparity(c, d_left, d_right, H, W, pitch, min_disp, num_disp, win, cost, 0, H,
+                               c->d16.as<int16_t>(), W, s, n_frames, frame_stride, fs);
+    if (rc) return rc;
+    sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
+                                  num_disp, d_depth, d_norm, nullptr);
+    rc = attach_lut(c, pp, s);
+    if (rc) return rc;
+    pp.out_d8 = d_d8;   // median / 16 - (min_disp - 1): 0 = invalid, 1 + d - min_disp otherwise
+    pp.d8_base = min_disp - 1;
+    SV_LAUNCH(c, SV_K_MEDIAN, s,
+              sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, d_disparity, pp, s, n_frames, fs, fs));
+    return 0;
+}
+
 int sv_depth_map_harris_batch_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d_right, int n_frames, int H,
                                   int W, int pitch, int64_t frame_stride, int min_disp, int num_disp, int win,
                                   int cost, float min_depth, float max_depth, float depth_range,

@@ -794,6 +794,7 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
         if (pp.out_b) pp.out_b += o;
         if (pp.out_bgr) pp.out_bgr += 3 * o;
         if (pp.out_m16) pp.out_m16 += o;
+        if (pp.out_d8) pp.out_d8 += o;
     }
     const int x0 = blockIdx.x * MQ_W, y0 = row0 + blockIdx.y * MQ_H;
     {   // thread -> tile column t % 128 (clamped once), rows t / 128, +2, ...; the 4 columns
@@ -959,12 +960,18 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
         const uint32_t i = (uint32_t)y * W + x;
         const bool vec = x + 3 < W && (W & 3) == 0 &&
                          (((uintptr_t)disp | (uintptr_t)pp.out_a | (uintptr_t)pp.out_b) & 15) == 0 &&
-                         (((uintptr_t)pp.out_u8 | (uintptr_t)pp.out_bgr) & 3) == 0 && ((uintptr_t)pp.out_m16 & 7) == 0;
+                         (((uintptr_t)pp.out_u8 | (uintptr_t)pp.out_bgr | (uintptr_t)pp.out_d8) & 3) == 0 &&
+                         ((uintptr_t)pp.out_m16 & 7) == 0;
         if (vec) {
             if (disp)
                 at(reinterpret_cast<float4*>(disp), i >> 2) =
                     make_float4((float)mv[0] / 16.0f, (float)mv[1] / 16.0f, (float)mv[2] / 16.0f, (float)mv[3] / 16.0f);
             if (pp.out_m16) at(reinterpret_cast<uint2*>(pp.out_m16), i >> 2) = raw;
+            if (pp.out_d8)
+                at(reinterpret_cast<uint32_t*>(pp.out_d8), i >> 2) =
+                    (uint32_t)(uint8_t)((mv[0] >> 4) - pp.d8_base) | ((uint32_t)(uint8_t)((mv[1] >> 4) - pp.d8_base) << 8) |
+                    ((uint32_t)(uint8_t)((mv[2] >> 4) - pp.d8_base) << 16) |
+                    ((uint32_t)(uint8_t)((mv[3] >> 4) - pp.d8_base) << 24);
             if (pp.mode == POST_NONE) continue;
             PostVals o[4];
 #pragma unroll
@@ -989,6 +996,7 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
             if (x + q >= W) break;
             if (disp) at(disp, i + q) = (float)mv[q] / 16.0f;
             if (pp.out_m16) at(pp.out_m16, i + q) = (int16_t)mv[q];
+            if (pp.out_d8) at(pp.out_d8, i + q) = (uint8_t)((mv[q] >> 4) - pp.d8_base);
             if (pp.mode == POST_NONE) continue;
             const PostVals o = post_median(pp, mv[q]);
             at(pp.out_a, i + q) = o.a;

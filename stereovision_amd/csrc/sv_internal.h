@@ -247,6 +247,10 @@ struct PostParams {
     // 2 B/px over PCIe instead of 9-11); the f32 disparity output of the median kernel is
     // then optional (disp == nullptr).
     int16_t* out_m16;
+    // Optional u8 disparity index map: m / 16 - d8_base, for integer-disparity costs (SAD / SSD /
+    // HOG: every median is a multiple of 16) with D <= 255 — 1 B/px for a gather over xGMI.
+    uint8_t* out_d8;
+    int d8_base;
     // Optional lookup table of the post-processing as a function of the int16 x16 median
     // value m in [lut_m0, lut_m0 + lut_n), built by launch_post_lut with the same f32 ops
     // (bit-identical to evaluating post_one per pixel; replaces two IEEE divisions).

@@ -36,7 +36,7 @@ EXPORTED = [
     "sv_depth_map_dev", "sv_harris_dev", "sv_hog_hist_dev", "sv_profile_enable",
     "sv_profile_read", "sv_profile_reset", "sv_disparity_rows", "sv_dev_alloc", "sv_dev_free",
     "sv_copy_to_device", "sv_copy_to_host", "sv_host_register", "sv_host_unregister", "sv_timer_begin", "sv_timer_end", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
-    "sv_depth_map_batch_dev", "sv_depth_map_batch_m16_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
+    "sv_depth_map_batch_dev", "sv_depth_map_batch_m16_dev", "sv_depth_map_batch_d8_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
     "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
     "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
     "sv_select_ranks", "sv_affine_f32_dev", "sv_sgbm", "sv_sgbm_dev", "sv_filter_speckles",
@@ -191,6 +191,10 @@ def _declare(lib):
                                         ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
                                         _c_float, _c_float, _c_float, _vp, _vp, _vp, _vp, _vp],
                                        _c_int),
+        "sv_depth_map_batch_d8_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
+                                       ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                       _c_float, _c_float, _c_float, _vp, _vp, _vp, _vp, _vp],
+                                      _c_int),
         "sv_init_undistort_rectify_map": ([_vp, _f64p, _NullableF64, _c_int, _NullableF64,
                                            _NullableF64, _c_int, _c_int, _c_int, _i16p, _u16p],
                                           _c_int),
@@ -798,18 +802,23 @@ class Engine:
                             pitch: int, frame_stride: int, min_disp: int, num_disp: int,
                             win: int, min_depth: float, max_depth: float, d_depth: int,
                             d_disp: int, d_norm: int, cost="sad", min_disp_global=None,
-                            stream: int = 0, d_med16: int = 0, d_harris: int = 0):
+                            stream: int = 0, d_med16: int = 0, d_harris: int = 0, d_d8: int = 0):
         """d_med16 (optional): also the int16 x16 median maps (d_disp = d_med16 / 16 exactly).
+        d_d8 (optional): also the u8 disparity indices d_disp - (min_disp - 1) (integer costs,
+        num_disp <= 255; sv_depth_map_batch_d8_dev).
         d_harris (optional): also the Harris response of every left frame, computed inside the
-        median launch (sv_depth_map_harris_batch_dev; not combinable with d_med16)."""
+        median launch (sv_depth_map_harris_batch_dev; not combinable with d_med16 / d_d8)."""
         mdg = min_disp if min_disp_global is None else min_disp_global
         args = (self._h, d_left, d_right, int(n_frames), H, W, pitch, int(frame_stride),
                 int(min_disp), int(num_disp), int(win), _cost(cost), np.float32(min_depth),
                 np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
                 np.float32(mdg), d_depth, d_disp, d_norm)
-        if d_harris:
-            if d_med16:
-                raise ValueError("d_harris and d_med16 are separate entry points")
+        if sum(1 for p in (d_harris, d_med16, d_d8) if p) > 1:
+            raise ValueError("d_harris, d_med16 and d_d8 are separate entry points")
+        if d_d8:
+            _check("sv_depth_map_batch_d8_dev",
+                   self.lib.sv_depth_map_batch_d8_dev(*args, d_d8, stream or None))
+        elif d_harris:
             _check("sv_depth_map_harris_batch_dev",
                    self.lib.sv_depth_map_harris_batch_dev(*args, d_harris, stream or None))
         elif d_med16:

@@ -129,6 +129,43 @@ def test_multi_gpu_m16_dev_gathers_int16_medians(ctxs, ndev, counts, cost, win):
         root.dev_free(d_m16)
 
 
+def test_depth_map_batch_d8_dev_indices(engine):
+    """sv_depth_map_batch_d8_dev: u8 disparity indices d - min_disp + 1 beside the f32 outputs
+    (whole-pixel disparities: d8 + min_disp - 1 == the f32 disparity exactly, 0 = invalid), for
+    SAD, SSD and HOG, a negative min_disp and num_disp 255; SGBM and num_disp > 255 refused."""
+    from stereovision_amd.engine import SVError
+    for cost, D, win, mind in (("sad", 64, 9, 0), ("ssd", 48, 7, -5), ("hog", 32, 9, 3), ("sad", 255, 7, 0)):
+        nf, H, W = 2, 40, 330
+        L = np.stack([stereo_pair(H, W, D, seed=s)[0] for s in range(nf)])
+        R = np.stack([stereo_pair(H, W, D, seed=s)[1] for s in range(nf)])
+        n = H * W
+        dL, dR = engine.dev_alloc(L.nbytes), engine.dev_alloc(R.nbytes)
+        bufs = [engine.dev_alloc(4 * n * nf), engine.dev_alloc(4 * n * nf), engine.dev_alloc(n * nf),
+                engine.dev_alloc(n * nf)]
+        try:
+            engine.to_device(dL, L)
+            engine.to_device(dR, R)
+            engine.depth_map_batch_dev(dL, dR, nf, H, W, W, n, mind, D, win, 0.3, 2.0, bufs[0], bufs[1],
+                                       bufs[2], cost=cost, d_d8=bufs[3])
+            engine.synchronize()
+            disp = engine.to_host(bufs[1], (nf, H, W), np.float32)
+            d8 = engine.to_host(bufs[3], (nf, H, W), np.uint8)
+            np.testing.assert_array_equal(d8.astype(np.float32) + np.float32(mind - 1), disp)
+            for z in range(nf):
+                exp = C.disparity16(L[z], R[z], mind, D, win, {"sad": 0, "ssd": 1, "hog": 2}[cost])
+                assert (exp % 16 == 0).all()
+        finally:
+            for p in [dL, dR] + bufs:
+                engine.dev_free(p)
+    p = engine.dev_alloc(64 * 64 * 4)
+    try:
+        for cost, D in (("sgbm", 64), ("sad", 256)):
+            with pytest.raises(SVError):
+                engine.depth_map_batch_dev(p, p, 1, 8, 8, 8, 64, 0, D, 5, 0.3, 2.0, p, p, p, cost=cost, d_d8=p)
+    finally:
+        engine.dev_free(p)
+
+
 @pytest.mark.parametrize("mode", [POST_DEPTH, POST_SCALED, POST_NONE])
 def test_post_m16_dev_equals_median_epilogue(engine, mode):
     """sv_post_m16_dev over the int16 x16 medians reproduces the median kernel's own
@@ -350,18 +387,21 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("mode,root_outputs", [("frames", "m16"), ("frames", "full"), ("rowtile", "m16")])
-def test_bench_under_torch_distributed_run_two_ranks(mode, root_outputs):
+@pytest.mark.parametrize("mode,root_outputs,fmt", [("frames", "m16", "auto"), ("frames", "m16", "i16"),
+                                                   ("frames", "full", "auto"), ("rowtile", "m16", "auto")])
+def test_bench_under_torch_distributed_run_two_ranks(mode, root_outputs, fmt):
     """The driver's N>1 launch: torch.distributed.run starts 2 bench.py workers (torch-free).
     On a 1-GPU box both ranks share the GPU, so the group falls back to the file store (RCCL
     refuses two ranks on one device); on a multi-GPU box it is RCCL.  The gather is on by
-    default; rank 0 checks every rank's gathered maps (frames) / the reassembled frame from
-    band-only inputs (rowtile) against the C oracle: `verified` must be true."""
+    default (u8 disparity indices where exact, else int16 x16); rank 0 checks every rank's
+    gathered maps (frames) / the reassembled frame from band-only inputs (rowtile) against the
+    C oracle: `verified` must be true."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
            "--steps", "3", "--warmup", "1", "--height", "96", "--width", "400", "--num-disp", "64",
            "--frames", "2", "--batch", "2", "--mode", mode, "--no-live-pmc", "--no-aux",
-           "--no-host-path", "--no-cpu-baseline", "--hang-timeout", "90", "--root-outputs", root_outputs]
+           "--no-host-path", "--no-cpu-baseline", "--hang-timeout", "90", "--root-outputs", root_outputs,
+           "--gather-format", fmt]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     import json
@@ -379,8 +419,10 @@ def test_bench_under_torch_distributed_run_two_ranks(mode, root_outputs):
     checked = res["verify"]["checked"]
     if mode == "frames":     # both ranks' first and last frame, from rank 0's gathered stacks
         assert sum("gathered on rank 0" in c for c in checked) == 4, checked
-        assert d["gather_bytes_per_step"] == 2 * 96 * 400 * 2 * 1     # 2 B/px, B frames, 1 peer
         full = root_outputs == "full"
+        u8 = fmt == "auto" and not full   # D = 64: u8 indices are exact
+        assert d["gather_format"] == ("u8 disparity index" if u8 else "int16 x16")
+        assert d["gather_bytes_per_step"] == (1 if u8 else 2) * 96 * 400 * 2 * 1   # B/px, B frames, 1 peer
         assert d["root_outputs"] == root_outputs
         assert sum("expanded on rank 0" in c for c in checked) == (2 if full else 0), checked
         assert (d["root_expand_us_per_step"] is not None) == full

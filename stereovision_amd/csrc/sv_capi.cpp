@@ -153,6 +153,11 @@ struct sv_ctx {
     } lut_key, hl_key;
     hipEvent_t lut_ev = nullptr;
     hipStream_t lut_stream = nullptr;   // stream the table was built on
+    // the whole-disparity table (lut_shift 4: integer-cost depth-map batches), cached apart
+    DevBuf lutw;
+    LutKey lutw_key;
+    hipEvent_t lutw_ev = nullptr;
+    hipStream_t lutw_stream = nullptr;
     HostBuf hin, hout;
     // Cross-stream ordering of the context's scratch (d16, the post table, HOG histograms,
     // SGBM volumes, reduction accumulators): `*_dev` calls may pass any stream, so a call on
@@ -439,38 +444,47 @@ int enqueue_disparity(sv_ctx* c, const uint8_t* L, const uint8_t* R, int H, int 
 
 // Attach the cached post-processing table for the median kernel (built on first use of a
 // parameter set; covers every int16 x16 value a map with this (min_disp, num_disp) holds).
-int attach_lut(sv_ctx* c, sv::PostParams& pp, hipStream_t s) {
+// whole: the median map holds whole disparities only (medians of an integer-cost matcher's
+// int16 x16 output: multiples of 16), so the table can hold one entry per disparity
+int attach_lut(sv_ctx* c, sv::PostParams& pp, hipStream_t s, bool whole = false) {
     pp.lut_n = 0;
+    pp.lut_shift = 0;
     if (pp.mode == SV_POST_NONE || pp.num_disp <= 0 || pp.num_disp > 512) return 0;
     sv_ctx::LutKey k;
     k.mode = pp.mode;
     k.min_disp = pp.min_disp;
     k.num_disp = pp.num_disp;
     k.m0 = (pp.min_disp - 1) * 16;
-    k.n = (pp.num_disp + 1) * 16;
+    k.n = whole ? pp.num_disp + 1 : (pp.num_disp + 1) * 16;
     k.minf = pp.minf;
     k.maxf = pp.maxf;
     k.rangef = pp.rangef;
     k.mdg = pp.min_disp_global;
+    DevBuf& buf = whole ? c->lutw : c->lut;
+    sv_ctx::LutKey& key = whole ? c->lutw_key : c->lut_key;
+    hipEvent_t& ev = whole ? c->lutw_ev : c->lut_ev;
+    hipStream_t& bs = whole ? c->lutw_stream : c->lut_stream;
     const size_t n = (size_t)k.n;
-    float* la = c->lut.as<float>();
-    if (!(k == c->lut_key) || !c->lut_ev) {
-        SV_HIP(c->lut.ensure(n * (2 * sizeof(float) + 1)));
-        la = c->lut.as<float>();
-        if (!c->lut_ev) SV_HIP(hipEventCreateWithFlags(&c->lut_ev, hipEventDisableTiming));
-        int e = sv::launch_post_lut(pp, k.m0, k.n, la, reinterpret_cast<uint8_t*>(la + 2 * n), la + n, s);
+    float* la = buf.as<float>();
+    if (!(k == key) || !ev) {
+        SV_HIP(buf.ensure(n * (2 * sizeof(float) + 1)));
+        la = buf.as<float>();
+        if (!ev) SV_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        int e = sv::launch_post_lut(pp, k.m0, k.n, whole ? 16 : 1, la, reinterpret_cast<uint8_t*>(la + 2 * n), la + n,
+                                    s);
         if (e) return hipfail(e, "launch_post_lut");
-        SV_HIP(hipEventRecord(c->lut_ev, s));
-        c->lut_key = k;
-        c->lut_stream = s;
-    } else if (s != c->lut_stream) {
-        SV_HIP(hipStreamWaitEvent(s, c->lut_ev, 0));   // built earlier on another stream
+        SV_HIP(hipEventRecord(ev, s));
+        key = k;
+        bs = s;
+    } else if (s != bs) {
+        SV_HIP(hipStreamWaitEvent(s, ev, 0));   // built earlier on another stream
     }
     pp.lut_a = la;
     pp.lut_b = la + n;
     pp.lut_u8 = reinterpret_cast<const uint8_t*>(la + 2 * n);
     pp.lut_m0 = k.m0;
     pp.lut_n = k.n;
+    pp.lut_shift = whole ? 4 : 0;
     return 0;
 }
 
@@ -723,6 +737,7 @@ void sv_destroy(sv_ctx* c) {
                           &c->hist_copies, &c->cmap, &c->bgr, &c->m16,
                           &c->cc_size, &c->sg_rec};
         if (c->lut_ev) (void)hipEventDestroy(c->lut_ev);
+        if (c->lutw_ev) (void)hipEventDestroy(c->lutw_ev);
         if (c->scr_ev) (void)hipEventDestroy(c->scr_ev);
         if (c->xev) (void)hipEventDestroy(c->xev);
         if (c->sev) (void)hipEventDestroy(c->sev);
@@ -997,7 +1012,7 @@ int sv_depth_map_batch_m16_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* 
     if (rc) return rc;
     sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
                                   num_disp, d_depth, d_norm, nullptr);
-    rc = attach_lut(c, pp, s);
+    rc = attach_lut(c, pp, s, cost != SV_COST_SGBM);
     if (rc) return rc;
     pp.out_m16 = d_med16;   // nullable: the int16 x16 medians beside the f32 disparity
     SV_LAUNCH(c, SV_K_MEDIAN, s,
@@ -1027,7 +1042,7 @@ int sv_depth_map_batch_d8_dev(sv_ctx* c, const uint8_t* d_left, const uint8_t* d
     if (rc) return rc;
     sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
                                   num_disp, d_depth, d_norm, nullptr);
-    rc = attach_lut(c, pp, s);
+    rc = attach_lut(c, pp, s, cost != SV_COST_SGBM);
     if (rc) return rc;
     pp.out_d8 = d_d8;   // median / 16 - (min_disp - 1): 0 = invalid, 1 + d - min_disp otherwise
     pp.d8_base = min_disp - 1;
@@ -1057,7 +1072,7 @@ int sv_depth_map_harris_batch_dev(sv_ctx* c, const uint8_t* d_left, const uint8_
     if (rc) return rc;
     sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
                                   num_disp, d_depth, d_norm, nullptr);
-    rc = attach_lut(c, pp, s);
+    rc = attach_lut(c, pp, s, cost != SV_COST_SGBM);
     if (rc) return rc;
     const long long fin = n_frames > 1 ? frame_stride : 0;
     if (W >= 8 && H >= 8) {   // the Harris response rides in the median launch (extra blocks)

@@ -698,7 +698,7 @@ __device__ __forceinline__ T& at(T* base, uint32_t i) {
 }
 
 __device__ __forceinline__ PostVals post_median(const PostParams& pp, int mv) {
-    const uint32_t li = (uint32_t)(mv - pp.lut_m0);
+    const uint32_t li = (uint32_t)(mv - pp.lut_m0) >> pp.lut_shift;
     if (li < (uint32_t)pp.lut_n) {   // table lookup (exact)
         PostVals o;
         o.a = at(pp.lut_a, li);
@@ -1047,9 +1047,9 @@ __global__ void k_post(const float* __restrict__ disp, int n, PostParams pp) {
     if (i < n) post_one(pp, (size_t)i, disp[i]);
 }
 
-__global__ void k_post_lut(PostParams pp, int m0, int n) {
+__global__ void k_post_lut(PostParams pp, int m0, int n, int step) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) post_one(pp, (size_t)i, (float)(m0 + i) / 16.0f);
+    if (i < n) post_one(pp, (size_t)i, (float)(m0 + i * step) / 16.0f);
 }
 
 }  // namespace
@@ -1194,7 +1194,7 @@ int launch_median_f32(const float* in, int H, int W, float* out, hipStream_t s) 
     return (int)hipGetLastError();
 }
 
-int launch_post_lut(const PostParams& pp, int m0, int n, float* lut_a, uint8_t* lut_u8,
+int launch_post_lut(const PostParams& pp, int m0, int n, int step, float* lut_a, uint8_t* lut_u8,
                     float* lut_b, hipStream_t s) {
     if (n <= 0 || pp.mode == POST_NONE) return 0;
     PostParams q = pp;
@@ -1204,7 +1204,7 @@ int launch_post_lut(const PostParams& pp, int m0, int n, float* lut_a, uint8_t* 
     q.out_bgr = nullptr;
     q.out_m16 = nullptr;
     q.lut_n = 0;
-    hipLaunchKernelGGL(k_post_lut, dim3((n + 255) / 256), dim3(256), 0, s, q, m0, n);
+    hipLaunchKernelGGL(k_post_lut, dim3((n + 255) / 256), dim3(256), 0, s, q, m0, n, step);
     return (int)hipGetLastError();
 }
 

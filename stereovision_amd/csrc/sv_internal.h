@@ -258,6 +258,10 @@ struct PostParams {
     const uint8_t* lut_u8;
     const float* lut_b;
     int lut_m0, lut_n;
+    // 4: the table holds whole disparities only (entry i = value lut_m0 + 16 i), for maps whose
+    // medians are all multiples of 16 (integer-disparity costs): (D + 1) entries instead of
+    // 16 (D + 1), so the epilogue's lookups stay in L1 at large D
+    int lut_shift;
 };
 // Harris response computed by extra blocks of the median launch (C2): the left gray frames
 // at g (+ z*fs_in bytes, row pitch `pitch`), f32 responses at out (+ z*fs_out floats, row
@@ -281,7 +285,7 @@ int launch_median_f32(const float* in, int H, int W, float* out, hipStream_t s);
 int launch_post_m16(const int16_t* in, long long n, float* disp, const PostParams& pp, hipStream_t s);
 int launch_post(const float* disp, int n, const PostParams& pp, hipStream_t s);
 // Evaluates the post-processing of pp.mode for m = m0 .. m0+n-1 (d = m/16) into the tables.
-int launch_post_lut(const PostParams& pp, int m0, int n, float* lut_a, uint8_t* lut_u8,
+int launch_post_lut(const PostParams& pp, int m0, int n, int step, float* lut_a, uint8_t* lut_u8,
                     float* lut_b, hipStream_t s);
 
 }  // namespace sv

@@ -50,8 +50,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from stereovision_amd.engine import (POST_DEPTH, Communicator, Engine, device_count,  # noqa: E402
-                                     depth_map_rows_multi, depth_map_rows_scatter, get_engine,
-                                     multi_gpu_depth_map_dev, multi_gpu_m16_dev)
+                                     depth_map_rows_map, depth_map_rows_multi, depth_map_rows_scatter,
+                                     get_engine, multi_gpu_depth_map_dev, multi_gpu_map_dev)
 from stereovision_amd.synthetic import stereo_batch, stereo_pair, synthetic_calibration, to_bgr  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -445,6 +445,31 @@ def fetch_maps(eng, d_depth, d_disp, d_norm, index, n_px, H, W):
             eng.to_host(d_norm + n_px * index, (H, W), np.uint8))
 
 
+def map_to_disp(eng, d_map, index, n_px, H, W, u8):
+    """Frame `index` of a dense stack of gathered maps -> the f32 disparity it encodes: u8
+    indices d8 + min_disp - 1 (min_disp 0 here) or int16 x16 / 16."""
+    if u8:
+        return eng.to_host(d_map + n_px * index, (H, W), np.uint8).astype(np.float32) - np.float32(1.0)
+    return eng.to_host(d_map + 2 * n_px * index, (H, W), np.int16).astype(np.float32) / np.float32(16.0)
+
+
+def init_comms(devices, required: bool):
+    """One process, N devices: an RCCL group (ncclCommInitAll) -> (comms, "").  When it
+    cannot start: (None, reason) — the caller gathers with hipMemcpyPeerAsync
+    and names the fallback in the line — or SystemExit with --require-rccl.
+    SV_RCCL_INIT_FAIL=1 makes the init fail as ncclCommInitAll would (the fallback's test)."""
+    try:
+        if os.environ.get("SV_RCCL_INIT_FAIL", "") not in ("", "0"):
+            raise RuntimeError("ncclCommInitAll: forced failure (SV_RCCL_INIT_FAIL)")
+        return Communicator.init_all(devices), ""
+    except Exception as ex:
+        reason = f"ncclCommInitAll failed: {ex}"
+        if required:
+            raise SystemExit(f"RCCL group over devices {devices} unavailable ({ex}) and --require-rccl given")
+        log(f"RCCL group unavailable ({ex}); gathering with peer copies (hipMemcpyPeerAsync)")
+        return None, reason
+
+
 def agreed_extra_warmup(pg, spent_s: float, steps_done: int, warmup_seconds: float) -> int:
     """Warm-up steps every rank runs after its first W (one-process-per-GPU launches): each
     rank estimates how many more steps fill --warmup-seconds at its own rate, and all take the
@@ -532,20 +557,21 @@ def parse_args(argv=None):
                     help="frames mode, N > 1: no gather (the compute-only weak-scaling curve)")
     ap.add_argument("--full-frame-inputs", action="store_true",
                     help="rowtile: every GPU holds the full frame (no input scatter in the step)")
-    ap.add_argument("--allow-peer-copies", action="store_true",
-                    help="one process, N devices: gather with peer copies if RCCL cannot start "
-                         "(default: exit non-zero)")
+    ap.add_argument("--require-rccl", action="store_true",
+                    help="N distinct devices: exit non-zero when RCCL cannot start (default: one "
+                         "process gathers with hipMemcpyPeerAsync, one process per GPU through the "
+                         "file store, and the line names the fallback: backend + rccl_reason)")
     ap.add_argument("--root-outputs", default="m16", choices=["m16", "full"],
-                    help="frames mode, N > 1: what GPU 0 holds after each step's gather — m16: "
-                         "every frame's disparity rows as int16 x16 (north_star's 'gather of the "
-                         "final disparity rows', 2 B/px over xGMI); full: also create_depth_map's "
-                         "depth f32 / disparity f32 / u8 for every frame, expanded on GPU 0 from "
-                         "the gathered medians (k_post_m16, 11 B/px of GPU 0's HBM per peer frame)")
+                    help="N > 1 (frames and rowtile): what GPU 0 holds after each step's gather — "
+                         "m16: the disparity rows only (north_star's 'gather of the final "
+                         "disparity rows', --gather-format), nothing expanded on GPU 0; full: also "
+                         "create_depth_map's depth f32 / disparity f32 / u8, expanded on GPU 0 from "
+                         "the gathered int16 medians (k_post_m16, 11 B/px of GPU 0's HBM per peer "
+                         "pixel)")
     ap.add_argument("--gather-format", default="auto", choices=["auto", "i16", "u8"],
-                    help="launched frames mode, --root-outputs m16: the gathered disparity rows as "
-                         "int16 x16 (2 B/px) or as u8 disparity indices d - min_disp + 1 (1 B/px: "
-                         "SAD/SSD/HOG disparities are whole pixels, exact for num_disp <= 255); "
-                         "auto: u8 where exact")
+                    help="--root-outputs m16: the gathered disparity rows as int16 x16 (2 B/px) or "
+                         "as u8 disparity indices d - min_disp + 1 (1 B/px: SAD/SSD/HOG disparities "
+                         "are whole pixels, exact for num_disp <= 255); auto: u8 where exact")
     ap.add_argument("--rehearse", action="store_true",
                     help="one process: run --gpus N logical GPUs on the visible devices (logical "
                          "GPU k on device k %% devices: own context, stream and buffers; gathers "
@@ -594,7 +620,7 @@ def main():
         world_env = int(os.environ["WORLD_SIZE"])
         collective = rowtile or (world_env > 1 and not args.no_gather)
         backend = args.dist_backend or "auto"
-        pg = init_process_group(backend=backend, strict=collective)
+        pg = init_process_group(backend=backend, strict=collective and args.require_rccl)
         rank, world = pg.rank, pg.world
         devices = [pg.device]
     else:
@@ -645,11 +671,13 @@ def main():
     gather_all = (gather_on or rowtile) and not launched and len(engines) > 1
     root_full = args.root_outputs == "full"
     # u8 disparity indices over xGMI (1 B/px) where they are exact: integer-disparity costs,
-    # num_disp <= 255, and GPU 0 holds the gathered maps only (no expansion from int16 medians)
+    # num_disp <= 255, and GPU 0 holds the gathered maps only (no expansion from int16 medians);
+    # frames and rowtile, launched and one-process alike
     gather_u8 = (args.gather_format != "i16" and not root_full and args.cost != "sgbm" and D <= 255)
     if args.gather_format == "u8" and not gather_u8:
         raise SystemExit("--gather-format u8 needs --root-outputs m16, an integer cost and num_disp <= 255")
     gel = 1 if gather_u8 else 2     # bytes per gathered pixel
+    gather_desc = "u8 disparity index" if gather_u8 else "int16 x16"
     out_frames = 1 if rowtile else B * (len(engines) if gather_all else 1)
     depth = [a.alloc(4 * n_px * out_frames) for a in arenas]
     disp = [a.alloc(4 * n_px * out_frames) for a in arenas]
@@ -680,17 +708,14 @@ def main():
                                   world=world, engine=eng) for _ in range(2 if world > 1 else 1)]
         tile = tiles[0]
     comms, comm_reason = None, ""
-    if shared_devices:
+    forced_fail = os.environ.get("SV_RCCL_INIT_FAIL", "") not in ("", "0")
+    if shared_devices and not forced_fail:
         comm_reason = "rehearsal: logical GPUs share a device (device copies, no RCCL)"
     elif not launched and len(engines) > 1 and (gather_on or rowtile):
-        try:
-            comms = Communicator.init_all(devices)
-        except Exception as ex:
-            comm_reason = f"ncclCommInitAll failed: {ex}"
-            if not args.allow_peer_copies:
-                raise SystemExit(f"RCCL group over devices {devices} unavailable ({ex}); "
-                                 "pass --allow-peer-copies to gather with peer copies")
-            log(f"RCCL group unavailable ({ex}); gathering with peer copies")
+        # one process, N devices: an RCCL group, or — when ncclCommInitAll fails — the gather
+        # by hipMemcpyPeerAsync (SURVEY.md §5's fallback), named in the line (backend "peer",
+        # rccl_reason) instead of ending the run
+        comms, comm_reason = init_comms(devices, args.require_rccl)
     # one process, N devices, gather: two lanes of contexts (own streams, scratch, RCCL
     # group and root outputs each) that consecutive steps alternate over, so one step's
     # gather overlaps the next step's kernels
@@ -698,7 +723,11 @@ def main():
     if gather_all:
         comms2 = None
         if comms is not None:
-            comms2 = Communicator.init_all(devices)
+            comms2, why2 = init_comms(devices, args.require_rccl)
+            if comms2 is None:   # both lanes gather the same way
+                for c in comms:
+                    c.close()
+                comms, comm_reason = None, why2
         engines2 = [Engine(d) for d in devices]
         all_engines.extend(engines2)
         glanes = [(engines, comms, depth[0], disp[0], norm[0], arenas[0].alloc(2 * n_px * out_frames)),
@@ -743,7 +772,10 @@ def main():
                 # the gather of frame i's int16 x16 medians (+ the root's expansion)
                 t = rt["t"]
                 u = (t + 1) % len(tiles)
-                bo = "full" if rank == 0 else "m16"
+                # gather-only (--root-outputs m16): every rank, the root included, writes only its
+                # band of the map (int16 x16 or u8 indices); full: the root's band is expanded by
+                # its own epilogue and the peers' int16 bands after the gather
+                bo = ("full" if rank == 0 else "m16") if root_full else ("d8" if gather_u8 else "m16")
 
                 def scatter_into(x):
                     ceng.profile_region_begin("scatter", cstream)
@@ -763,13 +795,17 @@ def main():
                     scatter_into(u)
                 eng.stream_wait_event(6 + t, cstream)
                 ceng.profile_region_begin("gather", cstream)
-                tiles[t].gather(pg, stream=cstream)
+                tiles[t].gather(pg, stream=cstream, expand=root_full)
                 ceng.profile_region_end(cstream)
                 rt["last"], rt["t"] = t, u
             else:   # one process: two lanes of contexts alternate, so frame i+1's scatter and
                     # kernels overlap frame i's gather and expansion
-                le, lc, ldep, ldis, lnor, _ = glanes[i % 2]
-                if band_inputs:
+                le, lc, ldep, ldis, lnor, lmap = glanes[i % 2]
+                if not root_full:   # gather-only: the full map on device 0, nothing expanded
+                    depth_map_rows_map(le, lc, dL[0] if band_inputs else dL, dR[0] if band_inputs else dR,
+                                       H, W, W, 0, D, win, lmap, fmt="d8" if gather_u8 else "m16",
+                                       scatter=band_inputs, cost=args.cost)
+                elif band_inputs:
                     depth_map_rows_scatter(le, lc, dL[0], dR[0], H, W, W, 0, D, win, 0.3, 2.0,
                                            ldep, ldis, lnor, cost=args.cost)
                 else:
@@ -777,15 +813,16 @@ def main():
                                          ldep, ldis, lnor, cost=args.cost)
                 rt["last"] = i % 2
             return
-        if gather_all:     # one process, N devices, maps gathered on device 0 (2 B/px)
-            le, lc, ldep, ldis, lnor, lm16 = glanes[i % 2]
+        if gather_all:     # one process, N devices, maps gathered on device 0 (1 or 2 B/px)
+            le, lc, ldep, ldis, lnor, lmap = glanes[i % 2]
             if root_full:
                 multi_gpu_depth_map_dev(le, lc, [p + f * n_px for p in dL],
                                         [p + f * n_px for p in dR], [B] * len(le), H, W, W, n_px,
                                         0, D, win, 0.3, 2.0, ldep, ldis, lnor, cost=args.cost)
             else:
-                multi_gpu_m16_dev(le, lc, [p + f * n_px for p in dL], [p + f * n_px for p in dR],
-                                  [B] * len(le), H, W, W, n_px, 0, D, win, lm16, cost=args.cost)
+                multi_gpu_map_dev(le, lc, [p + f * n_px for p in dL], [p + f * n_px for p in dR],
+                                  [B] * len(le), H, W, W, n_px, 0, D, win, lmap,
+                                  fmt="d8" if gather_u8 else "m16", cost=args.cost)
             return
         engs, depth_o, disp_o, norm_o = lanes[i % nstreams]
         med_o = 0
@@ -922,19 +959,28 @@ def main():
         f0 = (last * B) % F
         zs = sorted({0, B - 1})
         if rowtile:
-            if launched:
-                if rank == 0:
-                    tl = tiles[rt["last"]]
+            where = "rank 0" if launched else "device 0"
+            if launched and rank == 0:
+                tl = tiles[rt["last"]]
+                if root_full:
                     ver.frame("full frame gathered on rank 0", hostL[0][0], hostR[0][0],
                               eng.to_host(tl.out_a, (H, W), np.float32),
                               eng.to_host(tl.disp, (H, W), np.float32),
                               eng.to_host(tl.out_u8, (H, W), np.uint8))
-            else:
-                od, op, on = (glanes[rt["last"]][2:5] if glanes else (depth[0], disp[0], norm[0]))
-                ver.frame("full frame gathered on device 0", hostL[0][0], hostR[0][0],
-                          *fetch_maps(eng, od, op, on, 0, n_px, H, W))
+                else:
+                    ver.disparity(f"full-frame map gathered on rank 0 ({gather_desc})", hostL[0][0],
+                                  hostR[0][0], map_to_disp(eng, tl.m16, 0, n_px, H, W, gather_u8))
+            elif not launched:
+                if root_full or not glanes:
+                    od, op, on = (glanes[rt["last"]][2:5] if glanes else (depth[0], disp[0], norm[0]))
+                    ver.frame(f"full frame gathered on {where}", hostL[0][0], hostR[0][0],
+                              *fetch_maps(eng, od, op, on, 0, n_px, H, W))
+                else:
+                    ver.disparity(f"full-frame map gathered on {where} ({gather_desc})", hostL[0][0],
+                                  hostR[0][0], map_to_disp(eng, glanes[rt["last"]][5], 0, n_px, H, W,
+                                                           gather_u8))
         elif gather_all:
-            _, _, ldep, ldis, lnor, lm16 = glanes[last % 2]
+            _, _, ldep, ldis, lnor, lmap = glanes[last % 2]
             for k in range(len(engines)):
                 for z in zs:
                     tag = f"device {k} frame {f0 + z} (gathered on device 0)"
@@ -942,9 +988,8 @@ def main():
                         ver.frame(tag, hostL[k][f0 + z], hostR[k][f0 + z],
                                   *fetch_maps(eng, ldep, ldis, lnor, k * B + z, n_px, H, W))
                     else:
-                        m16 = eng.to_host(lm16 + 2 * n_px * (k * B + z), (H, W), np.int16)
-                        ver.disparity(tag + " int16 x16", hostL[k][f0 + z], hostR[k][f0 + z],
-                                      m16.astype(np.float32) / np.float32(16.0))
+                        ver.disparity(f"{tag} {gather_desc}", hostL[k][f0 + z], hostR[k][f0 + z],
+                                      map_to_disp(eng, lmap, k * B + z, n_px, H, W, gather_u8))
         else:
             engs, depth_o, disp_o, norm_o = lanes[last % nstreams]
             if gathered is not None:
@@ -973,12 +1018,7 @@ def main():
                             Lz, Rz = hostL[0][f0 + z], hostR[0][f0 + z]
                         else:   # rank r's inputs, regenerated from its seed
                             Lz, Rz, _ = stereo_pair(H, W, D, seed=1000 * r + f0 + z)
-                        if gather_u8:   # d = d8 + min_disp - 1 (min_disp 0 here)
-                            d8 = eng.to_host(gathered[last % 2] + n_px * (r * B + z), (H, W), np.uint8)
-                            got = d8.astype(np.float32) - np.float32(1.0)
-                        else:
-                            m16 = eng.to_host(gathered[last % 2] + 2 * n_px * (r * B + z), (H, W), np.int16)
-                            got = m16.astype(np.float32) / np.float32(16.0)
+                        got = map_to_disp(eng, gathered[last % 2], r * B + z, n_px, H, W, gather_u8)
                         ver.disparity(f"rank {r} frame {f0 + z} (gathered on rank 0)", Lz, Rz, got)
                         if expanded is not None and r > 0:
                             xd, xp, xu = expanded[last % 2]
@@ -1081,32 +1121,28 @@ def main():
             from stereovision_amd.distributed import band_layout
             for k in range(1, ngpu):
                 b = band_layout(H, k, ngpu, win)
-                gbytes += 2 * (b["r1"] - b["r0"]) * W    # int16 x16 median rows
+                gbytes += gel * (b["r1"] - b["r0"]) * W    # int16 x16 median rows or u8 indices
                 if band_inputs:
                     sbytes += 2 * (b["in1"] - b["in0"]) * W
         elif gather_on:   # the disparity maps: u8 indices (launched, where exact) or int16 x16
-            gbytes = (gel if launched else 2) * n_px * B * (ngpu - 1)
+            gbytes = gel * n_px * B * (ngpu - 1)
     dist = dist_summary(ngpu, launched, pg, comms, gather=gather_on, rowtile=rowtile,
                         gather_ms=gath_ms, gather_n=gath_n, scatter_ms=scat_ms, scatter_n=scat_n,
                         gather_wall_s=gather_wall[0], steps=args.steps, gather_bytes=gbytes,
                         scatter_bytes=sbytes, reason=comm_reason, expand_ms=exp_ms, expand_n=exp_n,
-                        root_outputs=(("full" if (rowtile or root_full) else "m16") if (gather_on or rowtile)
-                                      else None),
-                        gathered_maps=("row bands as int16 x16 medians, expanded on GPU 0 into depth f32 + "
-                                       "disparity f32 + depth u8" if rowtile else
-                                       ("disparity of every frame as u8 indices d - min_disp + 1 (whole-pixel "
-                                        "disparities: exact; the f32 map is d8 + min_disp - 1)"
-                                        if (launched and gather_u8) else
-                                        "disparity of every frame as int16 x16 (OpenCV's fixed point; the "
-                                        "f32 map is it / 16 exactly)")
+                        root_outputs=("full" if root_full else "m16") if (gather_on or rowtile) else None,
+                        gathered_maps=(("row bands of the disparity" if rowtile else "disparity of every frame")
+                                       + (" as u8 indices d - min_disp + 1 (whole-pixel disparities: exact; "
+                                          "the f32 map is d8 + min_disp - 1)" if gather_u8 else
+                                          " as int16 x16 (OpenCV's fixed point; the f32 map is it / 16 exactly)")
                                        + (", expanded on GPU 0 into depth f32 + disparity f32 + depth u8"
-                                          if root_full else "")
+                                          if root_full else ", nothing expanded on GPU 0")
                                        + (", overlapped with the next step (communication stream, "
-                                          "double-buffered maps)" if launched else
+                                          "double-buffered)" if launched else
                                           ", two context lanes so a step's gather overlaps the next step"))
                         if (gather_on or rowtile) else None)
-    if dist is not None and gather_on and not rowtile:
-        dist["gather_format"] = "u8 disparity index" if (launched and gather_u8) else "int16 x16"
+    if dist is not None and (gather_on or rowtile):
+        dist["gather_format"] = gather_desc
     parallelism = (f"row-tiled x{ngpu}" + (" (band inputs scattered from GPU 0)" if band_inputs else "")
                    + " + band gather" if rowtile else
                    f"frame-sharded x{ngpu}" + (" + gather to GPU 0" if gather_on else ""))

@@ -214,6 +214,13 @@ int sv_median_post_m16_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W, i
                            float min_disp_global, int min_disp, int num_disp, float* d_disparity,
                            float* d_out_a, uint8_t* d_out_u8, float* d_out_b, int16_t* d_med16,
                            void* stream);
+/* The 5x5 median of disparity rows [row0, row1) (cv2.medianBlur(disparity, 5),
+ * depth_map.py:912) written only as a map for a gather (SV_MAP_M16: int16 x16; SV_MAP_D8: u8
+ * indices median / 16 - (min_disp - 1), integer-disparity maps with num_disp <= 255), at
+ * full-frame offsets of d_map (row y at d_map + y*W elements): a row band's share of a
+ * gather-only row tiling. */
+int sv_median_map_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W, int row0, int row1,
+                      int map_format, int min_disp, int num_disp, void* d_map, void* stream);
 /* The post-processing of n median values d_med16 (int16 x16, e.g. maps gathered over xGMI):
  * d_disparity = m / 16 (nullable), and mode's outputs element-wise, exactly as the median
  * kernel's epilogue writes them (depth_map.py:915-936 / fused_depth_map.py:1010-1024). */
@@ -367,6 +374,25 @@ int sv_multi_gpu_m16_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
                          const int* n_frames, int H, int W, int pitch, int64_t frame_stride,
                          int min_disp, int num_disp, int win, int cost, int16_t* d_med16);
 
+/* Gather-only map formats of the multi-device entry points (north_star: "a trivial RCCL
+ * gather of the final disparity rows"): the root receives only the median map, nothing is
+ * expanded there (sv_post_m16_dev / disparity = d8 + min_disp - 1 give the outputs).
+ *   SV_MAP_M16  int16 x16 medians (OpenCV's fixed-point disparity after medianBlur,
+ *               depth_map.py:909-912), 2 B/px over xGMI
+ *   SV_MAP_D8   u8 disparity indices median / 16 - (min_disp - 1) (0 = invalid), 1 B/px:
+ *               exact for the integer-disparity costs (SAD / SSD / HOG) with num_disp <= 255 */
+#define SV_MAP_M16 1
+#define SV_MAP_D8 2
+
+/* C4 gather-only, any map format: as sv_multi_gpu_m16_dev (which is this with SV_MAP_M16),
+ * the maps of every frame land in d_map on ctxs[0]'s device (dense, context order; element
+ * size 2 or 1).  SV_MAP_D8 with SGBM or num_disp > 255: -EINVAL. */
+int sv_multi_gpu_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
+                         const uint8_t* const* d_left, const uint8_t* const* d_right,
+                         const int* n_frames, int H, int W, int pitch, int64_t frame_stride,
+                         int min_disp, int num_disp, int win, int cost, int map_format,
+                         void* d_map);
+
 /* C5: ONE frame row-tiled over ndev contexts.  Every context holds the full gray frame
  * (d_left[k]/d_right[k] on its device; the window and median halos are read locally, so the
  * bands reassemble bit-exactly); context k computes output rows [H*k/ndev, H*(k+1)/ndev)
@@ -390,6 +416,17 @@ int sv_depth_map_rows_scatter(sv_ctx* const* ctxs, sv_comm* const* comms, int nd
                               float min_depth, float max_depth, float depth_range,
                               float min_disp_global, float* d_depth, float* d_disparity,
                               uint8_t* d_norm);
+/* C5 gather-only (replaces the disparity create_depth_map returns, depth_map.py:909-912, for
+ * a row-tiled frame): as sv_depth_map_rows_multi (scatter = 0: every context holds the full
+ * frame at d_left[k] / d_right[k]) or sv_depth_map_rows_scatter (scatter != 0: the frame is
+ * at d_left[0] / d_right[0] on the root only), but the root receives only the full H x W map
+ * (SV_MAP_M16 / SV_MAP_D8) in d_map — its own band written by its median epilogue, the
+ * peers' bands gathered — and expands nothing. */
+int sv_depth_map_rows_map(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
+                          const uint8_t* const* d_left, const uint8_t* const* d_right, int scatter,
+                          int H, int W, int pitch, int min_disp, int num_disp, int win, int cost,
+                          int map_format, void* d_map);
+
 /* Row bands of a `world`-way row tiling for rank `rank`: out6 = {r0, r1 (output rows), h0, h1
  * (disparity rows incl. the median halo), in0, in1 (input rows the band reads)}.  Device
  * buffers holding only input rows [in0, in1) must keep SV_BAND_MARGIN spare rows above and

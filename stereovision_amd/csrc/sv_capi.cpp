@@ -167,6 +167,10 @@ struct sv_ctx {
     hipEvent_t scr_ev = nullptr;
     hipEvent_t xev = nullptr;   // multi-device entry points: this context's part is enqueued
     hipEvent_t sev = nullptr;   // sv_depth_map_rows_scatter: the root's inputs are ready
+    // multi-device entry points (root): recorded on the root stream once the root's previous
+    // users of its receive buffer (gm16) are ordered before it; peer copies into gm16 wait
+    // for it (RCCL receives run on the root stream and need no event)
+    hipEvent_t gev = nullptr;
     hipEvent_t wev[16] = {};    // sv_event_record / sv_stream_wait_event slots
     bool prof = false;
     std::vector<EvPair> pending;
@@ -525,6 +529,39 @@ sv::PostParams make_post(int mode, float minf, float maxf, float rangef, float m
     return pp;
 }
 
+// Gather-only outputs of the multi-device entry points: instead of create_depth_map's outputs
+// (the root expands the peers' int16 x16 medians with k_post_m16), the full median map lands
+// on the root as int16 x16 (SV_MAP_M16) or u8 disparity indices (SV_MAP_D8: median / 16 −
+// (min_disp − 1), 1 B/px) and nothing is expanded (sv_post_m16_dev turns it into the outputs).
+struct MapOut {
+    int fmt = 0;           // 0: create_depth_map outputs on the root
+    void* map = nullptr;   // fmt != 0: the root's full map (frames dense, or one frame)
+    int d8_base = 0;
+    size_t el() const { return fmt == SV_MAP_D8 ? 1 : 2; }
+};
+
+int check_map(int fmt, const void* map, int cost, int num_disp) {
+    if (fmt != SV_MAP_M16 && fmt != SV_MAP_D8) return fail(SV_EINVAL, "map format must be SV_MAP_M16 or SV_MAP_D8");
+    if (!map) return fail(SV_EINVAL, "null map");
+    if (fmt == SV_MAP_D8 && (cost == SV_COST_SGBM || num_disp < 1 || num_disp > 255))
+        return fail(SV_EINVAL, "u8 disparity indices need an integer-disparity cost and num_disp <= 255");
+    return 0;
+}
+
+// Median epilogue of a context that only produces a map: int16 x16 or u8 indices into `dst`
+// (full-frame element offsets), no post-processing outputs.
+sv::PostParams map_post(int fmt, void* dst, int d8_base) {
+    sv::PostParams pp = make_post(SV_POST_NONE, 0.f, 0.f, 0.f, 0.f, 0, 0, nullptr, nullptr, nullptr);
+    if (fmt == SV_MAP_D8) {
+        pp.out_d8 = static_cast<uint8_t*>(dst);
+        pp.d8_base = d8_base;
+    } else {
+        pp.out_m16 = static_cast<int16_t*>(dst);
+    }
+    return pp;
+}
+
+
 // Stage two host images (HxW or HxWx3, any stride) into the context's device gray buffers.
 int stage_pair(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H, int W, int channels,
                int stride) {
@@ -735,12 +772,13 @@ void sv_destroy(sv_ctx* c) {
                           &c->rmap1, &c->rmap2, &c->rdst[0], &c->rdst[1], &c->stats, &c->sel,
                           &c->sg_hsum, &c->sg_c, &c->sg_l, &c->sg_lt, &c->sg_band, &c->cc_parent,
                           &c->hist_copies, &c->cmap, &c->bgr, &c->m16,
-                          &c->cc_size, &c->sg_rec};
+                          &c->cc_size, &c->sg_rec, &c->gm16, &c->keys, &c->lutw};
         if (c->lut_ev) (void)hipEventDestroy(c->lut_ev);
         if (c->lutw_ev) (void)hipEventDestroy(c->lutw_ev);
         if (c->scr_ev) (void)hipEventDestroy(c->scr_ev);
         if (c->xev) (void)hipEventDestroy(c->xev);
         if (c->sev) (void)hipEventDestroy(c->sev);
+        if (c->gev) (void)hipEventDestroy(c->gev);
         for (auto e : c->wev)
             if (e) (void)hipEventDestroy(e);
         if (c->region_open) {
@@ -789,7 +827,8 @@ int sv_release_scratch(sv_ctx* c) {
     // allocates what it needs again
     DevBuf* bufs[] = {&c->img[0], &c->img[1], &c->gray[0], &c->gray[1], &c->d16, &c->fa, &c->fb, &c->fc,
                       &c->u8, &c->harris, &c->hog[0], &c->hog[1], &c->fin, &c->sg_hsum, &c->sg_c,
-                      &c->sg_l, &c->sg_lt, &c->sg_band, &c->sg_rec, &c->cc_parent, &c->cc_size, &c->m16};
+                      &c->sg_l, &c->sg_lt, &c->sg_band, &c->sg_rec, &c->cc_parent, &c->cc_size, &c->m16,
+                      &c->gm16, &c->keys};
     for (auto* b : bufs) b->release();
     return 0;
 }
@@ -877,6 +916,22 @@ int sv_median_post_m16_dev(sv_ctx* c, const int16_t* d_disp16, int H, int W, int
     if (lrc) return lrc;
     pp.out_m16 = d_med16;
     SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(d_disp16, H, W, row0, row1, d_disparity, pp, s));
+    return 0;
+}
+
+int sv_median_map_dev(sv_ctx* c, const int16_t* d_disp16, int H, int W, int row0, int row1, int map_format,
+                      int min_disp, int num_disp, void* d_map, void* stream) {
+    SV_ENTER(c);
+    if (check_image(d_disp16, H, W)) return fail(SV_EINVAL, "bad median arguments");
+    int rc = check_map(map_format, d_map, SV_COST_SAD, num_disp);
+    if (rc) return rc;
+    if ((long long)H * W >= (1LL << 30)) return fail(SV_EINVAL, "frame too large for the median kernel");
+    if (row0 < 0) row0 = 0;
+    if (row1 > H) row1 = H;
+    hipStream_t s = pick(c, stream);
+    SV_SCRATCH(c, s);
+    sv::PostParams pp = map_post(map_format, d_map, min_disp - 1);
+    SV_LAUNCH(c, SV_K_MEDIAN, s, sv::launch_median_i16(d_disp16, H, W, row0, row1, nullptr, pp, s));
     return 0;
 }
 
@@ -1242,6 +1297,14 @@ int scratch_mark(sv_ctx* c, hipStream_t s) {
     c->scr_stream = s;
     return 0;
 }
+// The root's receive buffers are free once its stream reaches this point (every earlier
+// reader of gm16 / the caller's map is on the root stream, ordered by scratch_wait): peer
+// copies of the gather wait for it.
+int recv_ready(sv_ctx* root) {
+    if (!root->gev) SV_HIP(hipEventCreateWithFlags(&root->gev, hipEventDisableTiming));
+    SV_HIP(hipEventRecord(root->gev, root->stream));
+    return 0;
+}
 int join_event(sv_ctx* c, hipStream_t s) {
     if (!c->xev) SV_HIP(hipEventCreateWithFlags(&c->xev, hipEventDisableTiming));
     SV_HIP(hipEventRecord(c->xev, s));
@@ -1338,6 +1401,9 @@ int gather_blocks_impl(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
     for (int k = 1; k < ndev; ++k) {
         sv_ctx* c = ctxs[k];
         SV_HIP(hipSetDevice(c->device));
+        // the root's receive buffer may still be read by an earlier call's work on the root
+        // stream (the expansion of the previous gather): copy only after it (recv_ready)
+        if (root->gev) SV_HIP(hipStreamWaitEvent(c->stream, root->gev, 0));
         for (const Block& b : blocks[k]) {
             int rc = peer_copy(root, c, b.dst, b.src, b.bytes, c->stream);
             if (rc) return rc;
@@ -1369,20 +1435,22 @@ int expand_on_root(sv_ctx* root, size_t n, size_t in_off, size_t off, float min_
 }
 
 // Median (+ post) of output rows [r0, r1) of context k's disparity band: the root writes the
-// create_depth_map outputs in place, a peer only its int16 x16 medians (c->gm16, full-frame
-// layout) for the gather.
+// create_depth_map outputs in place (or, gather-only, its rows of the map), a peer only its
+// int16 x16 medians / u8 indices (c->gm16, full-frame layout) for the gather.
 int band_median(sv_ctx* c, int k, int H, int W, int r0, int r1, float min_depth, float max_depth, float depth_range,
                 float min_disp_global, int min_disp, int num_disp, float* d_depth, float* d_disparity,
-                uint8_t* d_norm, hipStream_t s) {
-    sv::PostParams pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp,
-                                  num_disp, d_depth, d_norm, nullptr);
-    float* o_disp = d_disparity;
+                uint8_t* d_norm, const MapOut& mo, hipStream_t s) {
+    sv::PostParams pp;
+    float* o_disp = nullptr;
     if (k > 0) {
         SV_HIP(c->gm16.ensure((size_t)H * W * sizeof(int16_t)));
-        pp = make_post(SV_POST_NONE, 0.f, 0.f, 0.f, 0.f, 0, 0, nullptr, nullptr, nullptr);
-        pp.out_m16 = c->gm16.as<int16_t>();
-        o_disp = nullptr;
+        pp = map_post(mo.fmt ? mo.fmt : SV_MAP_M16, c->gm16.p, mo.d8_base);
+    } else if (mo.fmt) {
+        pp = map_post(mo.fmt, mo.map, mo.d8_base);
     } else {
+        pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
+                       d_depth, d_norm, nullptr);
+        o_disp = d_disparity;
         int rc = attach_lut(c, pp, s);
         if (rc) return rc;
     }
@@ -1406,13 +1474,13 @@ int multi_prologue(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev) {
 }  // namespace
 
 namespace {
-// C4 over ndev contexts.  d_med16 == nullptr: create_depth_map outputs on the root (its own
-// frames written by its median epilogue, the peers' from their gathered int16 x16 medians);
-// else only the int16 x16 medians of every frame, gathered into d_med16.
+// C4 over ndev contexts.  mo.fmt == 0: create_depth_map outputs on the root (its own frames
+// written by its median epilogue, the peers' from their gathered int16 x16 medians); else only
+// the map of every frame (int16 x16 or u8 indices), gathered into mo.map.
 int multi_frames(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
                  const uint8_t* const* d_right, const int* n_frames, int H, int W, int pitch, int64_t frame_stride,
                  int min_disp, int num_disp, int win, int cost, float min_depth, float max_depth, float depth_range,
-                 float min_disp_global, float* d_depth, float* d_disparity, uint8_t* d_norm, int16_t* d_med16) {
+                 float min_disp_global, float* d_depth, float* d_disparity, uint8_t* d_norm, const MapOut& mo) {
     int rc = multi_prologue(ctxs, comms, ndev);
     if (rc) return rc;
     sv::MatchPlan plan;
@@ -1440,12 +1508,14 @@ int multi_frames(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uin
     size_t total = 0;
     for (int k = 0; k < ndev; ++k) total += (size_t)n_frames[k];
     const size_t n0 = (size_t)n_frames[0];   // the root's own frames come first
-    // the peers' int16 x16 medians land in the root's gm16 (frames n0 .. total-1, dense)
+    const size_t el = mo.fmt ? mo.el() : sizeof(int16_t);
+    // the peers' maps land in mo.map (gather-only) or the root's gm16 (frames n0 .. total-1, dense)
     SV_HIP(hipSetDevice(root->device));
     rc = scratch_wait(root, root->stream);
+    if (!rc) rc = recv_ready(root);
     if (rc) return rc;
-    if (total > n0 && !d_med16) SV_HIP(root->gm16.ensure((total - n0) * n * sizeof(int16_t)));
-    int16_t* recv = d_med16 ? d_med16 + n0 * n : root->gm16.as<int16_t>();   // peers' medians
+    if (total > n0 && !mo.fmt) SV_HIP(root->gm16.ensure((total - n0) * n * sizeof(int16_t)));
+    uint8_t* recv = mo.fmt ? static_cast<uint8_t*>(mo.map) + n0 * n * el : root->gm16.as<uint8_t>();
     size_t f_off = 0;
     for (int k = 0; k < ndev; ++k) {
         sv_ctx* c = ctxs[k];
@@ -1461,13 +1531,13 @@ int multi_frames(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uin
         rc = enqueue_disparity(c, d_left[k], d_right[k], H, W, pitch, min_disp, num_disp, win, cost, 0, H,
                                c->d16.as<int16_t>(), W, s, nf, frame_stride, (long long)n);
         if (rc) return rc;
-        sv::PostParams pp = make_post(SV_POST_NONE, 0.f, 0.f, 0.f, 0.f, 0, 0, nullptr, nullptr, nullptr);
+        sv::PostParams pp;
         float* o_disp = nullptr;
-        if (k > 0) {   // peers: only the int16 x16 medians (2 B/px), sent to the root
+        if (k > 0) {   // peers: only the map (2 or 1 B/px), sent to the root
             SV_HIP(c->gm16.ensure((size_t)nf * n * sizeof(int16_t)));
-            pp.out_m16 = c->gm16.as<int16_t>();
-        } else if (d_med16) {
-            pp.out_m16 = d_med16;
+            pp = map_post(mo.fmt ? mo.fmt : SV_MAP_M16, c->gm16.p, mo.d8_base);
+        } else if (mo.fmt) {
+            pp = map_post(mo.fmt, mo.map, mo.d8_base);
         } else {       // the root's own frames: create_depth_map's outputs in place
             pp = make_post(SV_POST_DEPTH, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
                            d_depth + off * n, d_norm + off * n, nullptr);
@@ -1479,39 +1549,22 @@ int multi_frames(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uin
                   sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, o_disp, pp, s, nf, (long long)n,
                                         (long long)n));
         active.push_back(k);
-        if (k > 0) blocks[k] = {{recv + (off - n0) * n, c->gm16.p, (size_t)nf * n * sizeof(int16_t)}};
+        if (k > 0) blocks[k] = {{recv + (off - n0) * n * el, c->gm16.p, (size_t)nf * n * el}};
     }
     rc = gather_blocks(ctxs, comms, ndev, blocks, active);
-    if (rc || d_med16) return rc;
+    if (rc || mo.fmt) return rc;
     return expand_on_root(root, (total - n0) * n, 0, n0 * n, min_depth, max_depth, depth_range, min_disp_global,
                           min_disp, num_disp, d_depth, d_disparity, d_norm);
 }
-}  // namespace
 
-int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
-                               const uint8_t* const* d_right, const int* n_frames, int H, int W, int pitch,
-                               int64_t frame_stride, int min_disp, int num_disp, int win, int cost, float min_depth,
-                               float max_depth, float depth_range, float min_disp_global, float* d_depth,
-                               float* d_disparity, uint8_t* d_norm) {
-    if (!d_left || !d_right || !n_frames || !d_depth || !d_disparity || !d_norm) return fail(SV_EINVAL, "null arguments");
-    return multi_frames(ctxs, comms, ndev, d_left, d_right, n_frames, H, W, pitch, frame_stride, min_disp, num_disp,
-                        win, cost, min_depth, max_depth, depth_range, min_disp_global, d_depth, d_disparity, d_norm,
-                        nullptr);
-}
-
-int sv_multi_gpu_m16_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
-                         const uint8_t* const* d_right, const int* n_frames, int H, int W, int pitch,
-                         int64_t frame_stride, int min_disp, int num_disp, int win, int cost, int16_t* d_med16) {
-    if (!d_left || !d_right || !n_frames || !d_med16) return fail(SV_EINVAL, "null arguments");
-    return multi_frames(ctxs, comms, ndev, d_left, d_right, n_frames, H, W, pitch, frame_stride, min_disp, num_disp,
-                        win, cost, 0.f, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, d_med16);
-}
-
-int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
-                            const uint8_t* const* d_right, int H, int W, int pitch, int min_disp, int num_disp,
-                            int win, int cost, float min_depth, float max_depth, float depth_range,
-                            float min_disp_global, float* d_depth, float* d_disparity, uint8_t* d_norm) {
-    if (!d_left || !d_right || !d_depth || !d_disparity || !d_norm) return fail(SV_EINVAL, "null arguments");
+// C5: one frame row-tiled over ndev contexts.  scatter: the frame is on the root only
+// (d_left[0] / d_right[0]) and context k > 0 first receives its band's input rows into its
+// scratch; else every context holds the full frame.  Outputs: create_depth_map's (mo.fmt 0,
+// the peers' bands expanded on the root) or the gathered map only.
+int rows_impl(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
+              const uint8_t* const* d_right, bool scatter, int H, int W, int pitch, int min_disp, int num_disp,
+              int win, int cost, float min_depth, float max_depth, float depth_range, float min_disp_global,
+              float* d_depth, float* d_disparity, uint8_t* d_norm, const MapOut& mo) {
     int rc = multi_prologue(ctxs, comms, ndev);
     if (rc) return rc;
     sv::MatchPlan plan;
@@ -1519,65 +1572,8 @@ int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev
     if (rc) return rc;
     if (cost == SV_COST_SGBM && ndev > 1) return fail(SV_EINVAL, "SGBM cannot be row-tiled (top-down path)");
     if (pitch < W) return fail(SV_EINVAL, "pitch smaller than width");
-    for (int k = 0; k < ndev; ++k)
+    for (int k = 0; k < (scatter ? 1 : ndev); ++k)
         if (check_image(d_left[k], H, W) || check_image(d_right[k], H, W)) return fail(SV_EINVAL, "null frames");
-    MultiLock lock(ctxs, ndev);
-    if (!lock.ok) return fail(SV_ENOMEM, "lock allocation failed");
-    const size_t n = (size_t)H * W;
-    std::vector<std::vector<Block>> blocks;
-    std::vector<int> active;
-    try {
-        blocks.resize(ndev);
-        active.reserve(ndev);
-    } catch (...) {
-        return fail(SV_ENOMEM, "allocation failed");
-    }
-    sv_ctx* root = ctxs[0];
-    SV_HIP(hipSetDevice(root->device));
-    rc = scratch_wait(root, root->stream);
-    if (rc) return rc;
-    SV_HIP(root->gm16.ensure(n * sizeof(int16_t)));
-    for (int k = 0; k < ndev; ++k) {
-        sv_ctx* c = ctxs[k];
-        const int r0 = (int)((long long)H * k / ndev), r1 = (int)((long long)H * (k + 1) / ndev);
-        if (r1 <= r0) continue;
-        const int h0 = r0 - 2 > 0 ? r0 - 2 : 0, h1 = r1 + 2 < H ? r1 + 2 : H;   // 5x5 median halo
-        SV_HIP(hipSetDevice(c->device));
-        hipStream_t s = c->stream;
-        rc = scratch_wait(c, s);
-        if (rc) return rc;
-        SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
-        rc = enqueue_disparity(c, d_left[k], d_right[k], H, W, pitch, min_disp, num_disp, win, cost, h0, h1,
-                               c->d16.as<int16_t>(), W, s);
-        if (rc) return rc;
-        rc = band_median(c, k, H, W, r0, r1, min_depth, max_depth, depth_range, min_disp_global, min_disp, num_disp,
-                         d_depth, d_disparity, d_norm, s);
-        if (rc) return rc;
-        active.push_back(k);
-        if (k > 0) {
-            const size_t o = (size_t)r0 * W, m = (size_t)(r1 - r0) * W;
-            blocks[k] = {{root->gm16.as<int16_t>() + o, c->gm16.as<int16_t>() + o, m * sizeof(int16_t)}};
-        }
-    }
-    rc = gather_blocks(ctxs, comms, ndev, blocks, active);
-    if (rc) return rc;
-    const size_t rr1 = (size_t)((long long)H / ndev) * W;   // the root's band ends at row H / ndev
-    return expand_on_root(root, n - rr1, rr1, rr1, min_depth, max_depth, depth_range, min_disp_global, min_disp,
-                          num_disp, d_depth, d_disparity, d_norm);
-}
-
-int sv_depth_map_rows_scatter(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* d_left,
-                              const uint8_t* d_right, int H, int W, int pitch, int min_disp, int num_disp, int win,
-                              int cost, float min_depth, float max_depth, float depth_range, float min_disp_global,
-                              float* d_depth, float* d_disparity, uint8_t* d_norm) {
-    if (!d_left || !d_right || !d_depth || !d_disparity || !d_norm) return fail(SV_EINVAL, "null arguments");
-    int rc = multi_prologue(ctxs, comms, ndev);
-    if (rc) return rc;
-    sv::MatchPlan plan;
-    rc = check_match(H, W, min_disp, num_disp, win, cost, &plan);
-    if (rc) return rc;
-    if (cost == SV_COST_SGBM && ndev > 1) return fail(SV_EINVAL, "SGBM cannot be row-tiled (top-down path)");
-    if (pitch < W) return fail(SV_EINVAL, "pitch smaller than width");
     MultiLock lock(ctxs, ndev);
     if (!lock.ok) return fail(SV_ENOMEM, "lock allocation failed");
     const size_t n = (size_t)H * W;
@@ -1595,93 +1591,162 @@ int sv_depth_map_rows_scatter(sv_ctx* const* ctxs, sv_comm* const* comms, int nd
     for (int k = 0; k < ndev; ++k) band_rows_of(H, k, ndev, win, rows[k]);
     SV_HIP(hipSetDevice(root->device));
     rc = scratch_wait(root, root->stream);
+    if (!rc) rc = recv_ready(root);
     if (rc) return rc;
-    SV_HIP(root->gm16.ensure(n * sizeof(int16_t)));
-    // 1. scatter: context k > 0 receives input rows [in0, in1) of both images into its scratch
-    //    (img[0], img[1]: SV_BAND_MARGIN spare rows above and below, never read as data)
-    for (int k = 1; k < ndev; ++k) {
-        sv_ctx* c = ctxs[k];
-        if (rows[k].r1 <= rows[k].r0) continue;
-        SV_HIP(hipSetDevice(c->device));
-        rc = scratch_wait(c, c->stream);
-        if (rc) return rc;
-        const size_t bytes = (size_t)(rows[k].in1 - rows[k].in0 + 2 * SV_BAND_MARGIN) * pitch;
-        SV_HIP(c->img[0].ensure(bytes));
-        SV_HIP(c->img[1].ensure(bytes));
-    }
-    SV_HIP(hipSetDevice(root->device));
-    const bool timed = ndev > 1 && root->prof && !root->region_open;
-    if (timed) root->prof_begin(SV_K_SCATTER, root->stream);
-    if (comms && ndev > 1) {
-        rc = sv::comm_group_start();
-        if (rc) return rc;
-        int erc = 0;
-        for (int k = 1; k < ndev && !erc; ++k) {
-            if (rows[k].r1 <= rows[k].r0) continue;
-            const size_t off = (size_t)rows[k].in0 * pitch, bytes = (size_t)(rows[k].in1 - rows[k].in0) * pitch;
-            for (int i = 0; i < 2 && !erc; ++i) {
-                const uint8_t* src = (i ? d_right : d_left) + off;
-                uint8_t* dst = ctxs[k]->img[i].as<uint8_t>() + (size_t)SV_BAND_MARGIN * pitch;
-                erc = sv::comm_send(comms[0], src, bytes, k, root->stream);
-                if (!erc) erc = sv::comm_recv(comms[k], dst, bytes, 0, ctxs[k]->stream);
-            }
-        }
-        rc = sv::comm_group_end();
-        if (erc) return erc;
-        if (rc) return rc;
-    } else if (ndev > 1) {
-        if (!root->sev) SV_HIP(hipEventCreateWithFlags(&root->sev, hipEventDisableTiming));
-        SV_HIP(hipEventRecord(root->sev, root->stream));
+    const size_t el = mo.fmt ? mo.el() : sizeof(int16_t);
+    if (!mo.fmt) SV_HIP(root->gm16.ensure(n * sizeof(int16_t)));
+    uint8_t* recv = mo.fmt ? static_cast<uint8_t*>(mo.map) : root->gm16.as<uint8_t>();
+    if (scatter) {
+        // 1. context k > 0 receives input rows [in0, in1) of both images into its scratch
+        //    (img[0], img[1]: SV_BAND_MARGIN spare rows above and below, never read as data)
         for (int k = 1; k < ndev; ++k) {
             sv_ctx* c = ctxs[k];
             if (rows[k].r1 <= rows[k].r0) continue;
             SV_HIP(hipSetDevice(c->device));
-            SV_HIP(hipStreamWaitEvent(c->stream, root->sev, 0));
-            const size_t off = (size_t)rows[k].in0 * pitch, bytes = (size_t)(rows[k].in1 - rows[k].in0) * pitch;
-            for (int i = 0; i < 2; ++i) {
-                rc = peer_copy(c, root, ctxs[k]->img[i].as<uint8_t>() + (size_t)SV_BAND_MARGIN * pitch,
-                               (i ? d_right : d_left) + off, bytes, c->stream);
-                if (rc) return rc;
+            rc = scratch_wait(c, c->stream);
+            if (rc) return rc;
+            const size_t bytes = (size_t)(rows[k].in1 - rows[k].in0 + 2 * SV_BAND_MARGIN) * pitch;
+            SV_HIP(c->img[0].ensure(bytes));
+            SV_HIP(c->img[1].ensure(bytes));
+        }
+        SV_HIP(hipSetDevice(root->device));
+        const bool timed = ndev > 1 && root->prof && !root->region_open;
+        if (timed) root->prof_begin(SV_K_SCATTER, root->stream);
+        if (comms && ndev > 1) {
+            rc = sv::comm_group_start();
+            if (rc) return rc;
+            int erc = 0;
+            for (int k = 1; k < ndev && !erc; ++k) {
+                if (rows[k].r1 <= rows[k].r0) continue;
+                const size_t off = (size_t)rows[k].in0 * pitch, bytes = (size_t)(rows[k].in1 - rows[k].in0) * pitch;
+                for (int i = 0; i < 2 && !erc; ++i) {
+                    const uint8_t* src = (i ? d_right[0] : d_left[0]) + off;
+                    uint8_t* dst = ctxs[k]->img[i].as<uint8_t>() + (size_t)SV_BAND_MARGIN * pitch;
+                    erc = sv::comm_send(comms[0], src, bytes, k, root->stream);
+                    if (!erc) erc = sv::comm_recv(comms[k], dst, bytes, 0, ctxs[k]->stream);
+                }
+            }
+            rc = sv::comm_group_end();
+            if (erc) return erc;
+            if (rc) return rc;
+        } else if (ndev > 1) {
+            if (!root->sev) SV_HIP(hipEventCreateWithFlags(&root->sev, hipEventDisableTiming));
+            SV_HIP(hipEventRecord(root->sev, root->stream));
+            for (int k = 1; k < ndev; ++k) {
+                sv_ctx* c = ctxs[k];
+                if (rows[k].r1 <= rows[k].r0) continue;
+                SV_HIP(hipSetDevice(c->device));
+                SV_HIP(hipStreamWaitEvent(c->stream, root->sev, 0));
+                const size_t off = (size_t)rows[k].in0 * pitch, bytes = (size_t)(rows[k].in1 - rows[k].in0) * pitch;
+                for (int i = 0; i < 2; ++i) {
+                    rc = peer_copy(c, root, ctxs[k]->img[i].as<uint8_t>() + (size_t)SV_BAND_MARGIN * pitch,
+                                   (i ? d_right[0] : d_left[0]) + off, bytes, c->stream);
+                    if (rc) return rc;
+                }
             }
         }
+        SV_HIP(hipSetDevice(root->device));
+        if (timed) root->prof_end(root->stream);
     }
-    SV_HIP(hipSetDevice(root->device));
-    if (timed) root->prof_end(root->stream);
-    // 2. every context: disparity of its band + median halo, median + post of its band
+    // 2. every context: disparity of its band + median halo, median (+ post) of its band
     for (int k = 0; k < ndev; ++k) {
         sv_ctx* c = ctxs[k];
         const SvRows& b = rows[k];
         if (b.r1 <= b.r0) continue;
         SV_HIP(hipSetDevice(c->device));
         hipStream_t s = c->stream;
-        if (k == 0) {
+        if (k == 0 || !scatter) {
             rc = scratch_wait(c, s);
             if (rc) return rc;
         }
-        // band images addressed as full frames: row y of the frame at base + y * pitch for
-        // y in [in0, in1) (the kernels clamp rows to [0, H) and read only [in0, in1))
-        const ptrdiff_t shift = ((ptrdiff_t)SV_BAND_MARGIN - b.in0) * pitch;
-        const uint8_t* L = k ? c->img[0].as<uint8_t>() + shift : d_left;
-        const uint8_t* R = k ? c->img[1].as<uint8_t>() + shift : d_right;
+        const uint8_t* L = d_left[scatter ? 0 : k];
+        const uint8_t* R = d_right[scatter ? 0 : k];
+        if (scatter && k > 0) {
+            // band images addressed as full frames: row y of the frame at base + y * pitch for
+            // y in [in0, in1) (the kernels clamp rows to [0, H) and read only [in0, in1))
+            const ptrdiff_t shift = ((ptrdiff_t)SV_BAND_MARGIN - b.in0) * pitch;
+            L = c->img[0].as<uint8_t>() + shift;
+            R = c->img[1].as<uint8_t>() + shift;
+        }
         SV_HIP(c->d16.ensure(n * sizeof(int16_t)));
         rc = enqueue_disparity(c, L, R, H, W, pitch, min_disp, num_disp, win, cost, b.h0, b.h1,
                                c->d16.as<int16_t>(), W, s);
         if (rc) return rc;
         rc = band_median(c, k, H, W, b.r0, b.r1, min_depth, max_depth, depth_range, min_disp_global, min_disp,
-                         num_disp, d_depth, d_disparity, d_norm, s);
+                         num_disp, d_depth, d_disparity, d_norm, mo, s);
         if (rc) return rc;
         active.push_back(k);
         if (k > 0) {
-            const size_t o = (size_t)b.r0 * W, m = (size_t)(b.r1 - b.r0) * W;
-            blocks[k] = {{root->gm16.as<int16_t>() + o, c->gm16.as<int16_t>() + o, m * sizeof(int16_t)}};
+            const size_t o = (size_t)b.r0 * W * el, m = (size_t)(b.r1 - b.r0) * W * el;
+            blocks[k] = {{recv + o, c->gm16.as<uint8_t>() + o, m}};
         }
     }
-    // 3. the peers' int16 x16 median bands -> the root (2 B/px), expanded there
+    // 3. the peers' bands of the map -> the root (2 or 1 B/px), expanded there unless gather-only
     rc = gather_blocks(ctxs, comms, ndev, blocks, active);
-    if (rc) return rc;
+    if (rc || mo.fmt) return rc;
     const size_t rr1 = (size_t)rows[0].r1 * W;
     return expand_on_root(root, n - rr1, rr1, rr1, min_depth, max_depth, depth_range, min_disp_global, min_disp,
                           num_disp, d_depth, d_disparity, d_norm);
+}
+}  // namespace
+
+int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
+                               const uint8_t* const* d_right, const int* n_frames, int H, int W, int pitch,
+                               int64_t frame_stride, int min_disp, int num_disp, int win, int cost, float min_depth,
+                               float max_depth, float depth_range, float min_disp_global, float* d_depth,
+                               float* d_disparity, uint8_t* d_norm) {
+    if (!d_left || !d_right || !n_frames || !d_depth || !d_disparity || !d_norm) return fail(SV_EINVAL, "null arguments");
+    return multi_frames(ctxs, comms, ndev, d_left, d_right, n_frames, H, W, pitch, frame_stride, min_disp, num_disp,
+                        win, cost, min_depth, max_depth, depth_range, min_disp_global, d_depth, d_disparity, d_norm,
+                        MapOut{});
+}
+
+int sv_multi_gpu_m16_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
+                         const uint8_t* const* d_right, const int* n_frames, int H, int W, int pitch,
+                         int64_t frame_stride, int min_disp, int num_disp, int win, int cost, int16_t* d_med16) {
+    return sv_multi_gpu_map_dev(ctxs, comms, ndev, d_left, d_right, n_frames, H, W, pitch, frame_stride, min_disp,
+                                num_disp, win, cost, SV_MAP_M16, d_med16);
+}
+
+int sv_multi_gpu_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
+                         const uint8_t* const* d_right, const int* n_frames, int H, int W, int pitch,
+                         int64_t frame_stride, int min_disp, int num_disp, int win, int cost, int map_format,
+                         void* d_map) {
+    if (!d_left || !d_right || !n_frames) return fail(SV_EINVAL, "null arguments");
+    int rc = check_map(map_format, d_map, cost, num_disp);
+    if (rc) return rc;
+    MapOut mo{map_format, d_map, min_disp - 1};
+    return multi_frames(ctxs, comms, ndev, d_left, d_right, n_frames, H, W, pitch, frame_stride, min_disp, num_disp,
+                        win, cost, 0.f, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, mo);
+}
+
+int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
+                            const uint8_t* const* d_right, int H, int W, int pitch, int min_disp, int num_disp,
+                            int win, int cost, float min_depth, float max_depth, float depth_range,
+                            float min_disp_global, float* d_depth, float* d_disparity, uint8_t* d_norm) {
+    if (!d_left || !d_right || !d_depth || !d_disparity || !d_norm) return fail(SV_EINVAL, "null arguments");
+    return rows_impl(ctxs, comms, ndev, d_left, d_right, false, H, W, pitch, min_disp, num_disp, win, cost,
+                     min_depth, max_depth, depth_range, min_disp_global, d_depth, d_disparity, d_norm, MapOut{});
+}
+
+int sv_depth_map_rows_scatter(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* d_left,
+                              const uint8_t* d_right, int H, int W, int pitch, int min_disp, int num_disp, int win,
+                              int cost, float min_depth, float max_depth, float depth_range, float min_disp_global,
+                              float* d_depth, float* d_disparity, uint8_t* d_norm) {
+    if (!d_left || !d_right || !d_depth || !d_disparity || !d_norm) return fail(SV_EINVAL, "null arguments");
+    return rows_impl(ctxs, comms, ndev, &d_left, &d_right, true, H, W, pitch, min_disp, num_disp, win, cost,
+                     min_depth, max_depth, depth_range, min_disp_global, d_depth, d_disparity, d_norm, MapOut{});
+}
+
+int sv_depth_map_rows_map(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, const uint8_t* const* d_left,
+                          const uint8_t* const* d_right, int scatter, int H, int W, int pitch, int min_disp,
+                          int num_disp, int win, int cost, int map_format, void* d_map) {
+    if (!d_left || !d_right) return fail(SV_EINVAL, "null arguments");
+    int rc = check_map(map_format, d_map, cost, num_disp);
+    if (rc) return rc;
+    MapOut mo{map_format, d_map, min_disp - 1};
+    return rows_impl(ctxs, comms, ndev, d_left, d_right, scatter != 0, H, W, pitch, min_disp, num_disp, win, cost,
+                     0.f, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, mo);
 }
 
 int sv_band_rows_in(int H, int rank, int world, int win, int cost, int* out6) {

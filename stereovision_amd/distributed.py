@@ -339,7 +339,9 @@ def init_process_group(device: int | None = None, backend: str = "auto",
     LOCAL_RANK (world 1 when unset).  backend: "auto" (RCCL unless it cannot run: ranks
     sharing a GPU, library missing), "rccl" (required), "host" (file store only).
     strict: with "auto", ranks on DISTINCT devices must get RCCL (RuntimeError otherwise);
-    only ranks sharing a GPU (a 1-GPU rehearsal) may fall back to the file store."""
+    only ranks sharing a GPU (a 1-GPU rehearsal) may fall back to the file store.  Without
+    strict, an ncclCommInitRank failure on any rank makes every rank fall back to the file
+    store together (`reason` names it; SV_RCCL_INIT_FAIL=1 forces it, for tests)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -369,7 +371,25 @@ def init_process_group(device: int | None = None, backend: str = "auto",
         if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
             os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")   # single-node bootstrap
         uid = store.broadcast(Communicator.unique_id() if rank == 0 else None)
-        comm = Communicator.init_rank(device, world, rank, uid)
+        err = ""
+        try:
+            if os.environ.get("SV_RCCL_INIT_FAIL", "") not in ("", "0"):
+                raise RuntimeError("forced failure (SV_RCCL_INIT_FAIL)")
+            comm = Communicator.init_rank(device, world, rank, uid)
+        except Exception as ex:   # decided collectively below: every rank falls back together
+            err = f"ncclCommInitRank failed on rank {rank}: {ex}"
+        errs = [e.decode() for e in store.allgather(err.encode()) if e]
+        if errs:
+            if comm is not None:
+                comm.close()
+                comm = None
+            reason = errs[0]
+            if backend == "rccl" or strict:
+                raise RuntimeError(f"RCCL required on devices {devs} but unusable: {reason}")
+            use_rccl = False
+            if rank == 0:
+                _log(f"RCCL init failed ({reason}); barriers/reductions through the file store, "
+                     "gathers through host staging")
     elif rank == 0:
         _log(f"RCCL not used ({reason}); barriers/reductions through the file store, "
              "gathers through host staging")
@@ -411,6 +431,7 @@ class RowTiledDepthMap:
         self.m16 = e.dev_alloc(2 * n)
         self.rows = self.r1 - self.r0
         self._post = None   # the post parameters of the last compute (the root's expansion)
+        self._band_outputs = None   # what the last compute wrote ("full", "m16" or "d8")
         # band-only inputs: input rows [in0, in1) with BAND_MARGIN spare rows either side
         self.band_bytes = (self.in1 - self.in0) * W
         nb = self.band_bytes + 2 * BAND_MARGIN * W
@@ -431,10 +452,14 @@ class RowTiledDepthMap:
 
     def compute(self, d_left: int = 0, d_right: int = 0, mode: int = POST_DEPTH, min_depth: float = 0.3,
                 max_depth: float = 2.0, min_disp_global=None, stream: int = 0, band_outputs: str = "full"):
-        """Enqueue this rank's band: int16 x16 medians at their full-frame row offsets of
-        self.m16 and (band_outputs="full") the outputs in self.disp / self.out_a / self.out_u8
-        (/ self.out_b for POST_SCALED).  d_left/d_right: full-frame gray images, or 0 for the
-        band buffers filled by :meth:`scatter`."""
+        """Enqueue this rank's band: its median map at full-frame row offsets of self.m16 —
+        int16 x16, or with band_outputs="d8" u8 disparity indices median/16 - (min_disp - 1)
+        (1 B/px for the gather; integer costs, num_disp <= 255) — and (band_outputs="full")
+        the outputs in self.disp / self.out_a / self.out_u8 (/ self.out_b for POST_SCALED).
+        d_left/d_right: full-frame gray images, or 0 for the band buffers filled by
+        :meth:`scatter`."""
+        if band_outputs not in ("full", "m16", "d8"):
+            raise ValueError(f"band_outputs must be 'full', 'm16' or 'd8', got {band_outputs!r}")
         e, H, W = self.engine, self.H, self.W
         s = self._stream(stream)
         if not d_left:   # band buffer addressed as a full frame (row y at base + y * W)
@@ -446,7 +471,11 @@ class RowTiledDepthMap:
         self._post = dict(min_depth=min_depth, max_depth=max_depth, min_disp_global=mdg,
                           min_disp=self.min_disp, num_disp=self.num_disp)
         self._mode = mode
-        if band_outputs == "m16":
+        self._band_outputs = band_outputs
+        if band_outputs == "d8":
+            e.median_map_dev(self.d16, H, W, self.r0, self.r1, self.m16, "d8", min_disp=self.min_disp,
+                             num_disp=self.num_disp, stream=s)
+        elif band_outputs == "m16":
             e.median_post_m16_dev(self.d16, H, W, self.r0, self.r1, POST_NONE, d_med16=self.m16, stream=s)
         else:
             e.median_post_m16_dev(self.d16, H, W, self.r0, self.r1, mode, d_disparity=self.disp,
@@ -455,12 +484,18 @@ class RowTiledDepthMap:
                                   stream=s, **self._post)
 
     def gather(self, pg: "ProcessGroup", root: int = 0, stream: int = 0, expand: bool = True):
-        """Every rank's band of int16 x16 medians into the root's self.m16 (in place, 2 B/px),
-        then (expand) the root turns the other ranks' rows into its full-frame outputs; on the
-        engine stream unless `stream` is given (never the communicator's own stream: ADVICE
-        r02).  The root's own band must have been computed with band_outputs="full"."""
+        """Every rank's band of the median map into the root's self.m16 (in place: 2 B/px
+        int16 x16, or 1 B/px when the bands were computed with band_outputs="d8"), then
+        (expand) the root turns the other ranks' rows into its full-frame outputs; on the engine
+        stream unless `stream` is given (never the communicator's own stream: ADVICE r02).
+        Gather-only (expand=False) leaves the full map in the root's self.m16.  Expanding needs
+        int16 maps and the root's own band computed with band_outputs="full"."""
         s = self._stream(stream)
-        gather_rows(pg, self.m16, self.H, self.W * 2, root=root, stream=s)
+        el = 1 if self._band_outputs == "d8" else 2
+        if expand and pg.rank == root and self._band_outputs != "full":
+            raise ValueError("gather(expand=True) on the root needs compute(band_outputs='full') "
+                             f"there (the root's own rows), got {self._band_outputs!r}")
+        gather_rows(pg, self.m16, self.H, self.W * el, root=root, stream=s)
         if not expand or pg.rank != root or self._post is None:
             return
         e, W, mode = self.engine, self.W, self._mode

@@ -49,6 +49,7 @@ EXPORTED = [
     "sv_comm_scatterv", "sv_depth_map_rows_scatter", "sv_band_rows_in", "sv_release_scratch",
     "sv_frame_stats_batch_dev", "sv_select_count_batch", "sv_select_ranks_batch", "sv_event_record",
     "sv_stream_wait_event", "sv_median_post_m16_dev", "sv_post_m16_dev", "sv_multi_gpu_m16_dev",
+    "sv_multi_gpu_map_dev", "sv_depth_map_rows_map", "sv_median_map_dev",
     "sv_depth_map_harris_batch_dev",
 ]
 BAND_MARGIN = 8   # SV_BAND_MARGIN: spare rows around a band-only input buffer
@@ -269,6 +270,15 @@ def _declare(lib):
                                   ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                                   ctypes.POINTER(_c_int), _c_int, _c_int, _c_int,
                                   ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _vp], _c_int),
+        "sv_median_map_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
+                              _c_int),
+        "sv_multi_gpu_map_dev": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
+                                  ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                  ctypes.POINTER(_c_int), _c_int, _c_int, _c_int,
+                                  ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_int, _vp], _c_int),
+        "sv_depth_map_rows_map": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
+                                   ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int, _c_int, _c_int,
+                                   _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp], _c_int),
         "sv_depth_map_rows_multi": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
                                      ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int, _c_int, _c_int,
                                      _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float,
@@ -746,6 +756,14 @@ class Engine:
             np.float32(min_disp_global), int(min_disp), int(num_disp), d_disparity or None,
             d_out_a or None, d_out_u8 or None, d_out_b or None, d_med16 or None, stream or None))
 
+    def median_map_dev(self, d_disp16: int, H: int, W: int, row0: int, row1: int, d_map: int,
+                       fmt="m16", min_disp: int = 0, num_disp: int = 0, stream: int = 0):
+        """sv_median_map_dev: median of rows [row0, row1) written only as a gather map at
+        full-frame offsets of d_map (``fmt`` "m16": int16 x16, "d8": u8 indices)."""
+        _check("sv_median_map_dev", self.lib.sv_median_map_dev(
+            self._h, d_disp16, H, W, row0, row1, _map_format(fmt), int(min_disp), int(num_disp), d_map,
+            stream or None))
+
     def post_m16_dev(self, d_med16: int, n: int, mode: int, d_disparity: int = 0, d_out_a: int = 0,
                      d_out_u8: int = 0, d_out_b: int = 0, min_depth=0.0, max_depth=0.0,
                      min_disp_global=0.0, min_disp=0, num_disp=0, stream: int = 0):
@@ -1129,6 +1147,53 @@ def multi_gpu_m16_dev(engines, comms, d_left, d_right, n_frames, H: int, W: int,
     _check("sv_multi_gpu_m16_dev", lib.sv_multi_gpu_m16_dev(
         _handles(engines), ch, nd, _ptrs(d_left), _ptrs(d_right), nf, H, W, pitch,
         int(frame_stride), int(min_disp), int(num_disp), int(win), _cost(cost), d_med16))
+
+
+MAP_M16, MAP_D8 = 1, 2   # SV_MAP_M16 / SV_MAP_D8
+_MAP_FORMATS = {"m16": MAP_M16, "i16": MAP_M16, "d8": MAP_D8, "u8": MAP_D8}
+
+
+def _map_format(fmt) -> int:
+    if isinstance(fmt, str):
+        if fmt not in _MAP_FORMATS:
+            raise ValueError(f"map format must be one of {sorted(_MAP_FORMATS)}, got {fmt!r}")
+        return _MAP_FORMATS[fmt]
+    return int(fmt)
+
+
+def multi_gpu_map_dev(engines, comms, d_left, d_right, n_frames, H: int, W: int, pitch: int,
+                      frame_stride: int, min_disp: int, num_disp: int, win: int, d_map: int,
+                      fmt="m16", cost="sad"):
+    """C4 gather-only (sv_multi_gpu_map_dev): engine k computes disparity + median over its
+    n_frames[k] frames and only the median maps are gathered into d_map on engines[0]'s
+    device (context order): ``fmt="m16"`` int16 x16 (2 B/px), ``"d8"`` u8 disparity indices
+    median/16 - (min_disp - 1) (1 B/px; integer costs, num_disp <= 255).  Enqueue only."""
+    engines = list(engines)
+    nd = len(engines)
+    lib = engines[0].lib
+    ch = None if comms is None else _handles([c.handle for c in comms])
+    nf = (_c_int * nd)(*[int(v) for v in n_frames])
+    _check("sv_multi_gpu_map_dev", lib.sv_multi_gpu_map_dev(
+        _handles(engines), ch, nd, _ptrs(d_left), _ptrs(d_right), nf, H, W, pitch,
+        int(frame_stride), int(min_disp), int(num_disp), int(win), _cost(cost), _map_format(fmt), d_map))
+
+
+def depth_map_rows_map(engines, comms, d_left, d_right, H: int, W: int, pitch: int, min_disp: int,
+                       num_disp: int, win: int, d_map: int, fmt="m16", scatter: bool = False,
+                       cost="sad"):
+    """C5 gather-only (sv_depth_map_rows_map): one frame row-tiled over the engines; the
+    root (engines[0]) receives only the full-frame median map (int16 x16 or u8 indices) in
+    d_map and expands nothing.  ``scatter``: d_left / d_right are the root's frame (one
+    pointer each) and the other engines receive just their bands' input rows; else lists with
+    the full frame on every engine's device.  Enqueue only."""
+    engines = list(engines)
+    lib = engines[0].lib
+    ch = None if comms is None else _handles([c.handle for c in comms])
+    if scatter:
+        d_left, d_right = [d_left], [d_right]
+    _check("sv_depth_map_rows_map", lib.sv_depth_map_rows_map(
+        _handles(engines), ch, len(engines), _ptrs(d_left), _ptrs(d_right), int(bool(scatter)), H, W,
+        pitch, int(min_disp), int(num_disp), int(win), _cost(cost), _map_format(fmt), d_map))
 
 
 def depth_map_rows_multi(engines, comms, d_left, d_right, H: int, W: int, pitch: int, min_disp: int,

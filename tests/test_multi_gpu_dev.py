@@ -25,8 +25,8 @@ import pytest
 
 import sv_oracle_c as C
 from stereovision_amd.engine import (POST_DEPTH, POST_NONE, POST_SCALED, Communicator, Engine,
-                                     device_count, depth_map_rows_multi, multi_gpu_depth_map_dev,
-                                     multi_gpu_m16_dev)
+                                     device_count, depth_map_rows_map, depth_map_rows_multi,
+                                     multi_gpu_depth_map_dev, multi_gpu_m16_dev, multi_gpu_map_dev)
 from stereovision_amd.synthetic import stereo_pair
 
 pytestmark = pytest.mark.gpu
@@ -127,6 +127,156 @@ def test_multi_gpu_m16_dev_gathers_int16_medians(ctxs, ndev, counts, cost, win):
             e.dev_free(a)
             e.dev_free(b)
         root.dev_free(d_m16)
+
+
+@pytest.mark.parametrize("ndev,counts,cost,win,mind", [(8, [2, 1, 0, 3, 1, 1, 2, 1], "sad", 9, 0),
+                                                        (3, [1, 0, 2], "hog", 7, 3), (2, [2, 1], "ssd", 5, -7),
+                                                        (1, [2], "sad", 11, 0)])
+def test_multi_gpu_map_dev_gathers_u8_indices(ctxs, ndev, counts, cost, win, mind):
+    """sv_multi_gpu_map_dev(SV_MAP_D8): the one-process C4 gather at 1 B/px — every frame's u8
+    disparity index d - min_disp + 1 lands on ctxs[0]'s device in context order and encodes
+    the C oracle's median map exactly (d8 + min_disp - 1)."""
+    H, W, D = 37, 300, 48
+    es = ctxs[:ndev]
+    total = sum(counts)
+    frames = [stereo_pair(H, W, D, seed=1300 + f)[:2] for f in range(total)]
+    dLs, dRs, f0 = [], [], 0
+    for e, n in zip(es, counts):
+        Ls = np.stack([frames[f0 + z][0] for z in range(n)]) if n else np.zeros((1, H, W), np.uint8)
+        Rs = np.stack([frames[f0 + z][1] for z in range(n)]) if n else np.zeros((1, H, W), np.uint8)
+        dLs.append(_upload(e, Ls))
+        dRs.append(_upload(e, Rs))
+        f0 += n
+    root = es[0]
+    d_map = root.dev_alloc(H * W * total)
+    try:
+        for _ in range(2):
+            multi_gpu_map_dev(es, None, dLs, dRs, counts, H, W, W, H * W, mind, D, win, d_map, fmt="d8",
+                              cost=cost)
+        root.synchronize()
+        d8 = root.to_host(d_map, (total, H, W), np.uint8)
+        for f, (L, R) in enumerate(frames):
+            d16 = C.disparity16(L, R, mind, D, win, {"sad": 0, "ssd": 1, "hog": 2}[cost])
+            np.testing.assert_array_equal(d8[f].astype(np.float32) + np.float32(mind - 1), C.median5_f32(d16),
+                                          err_msg=f"frame {f}")
+    finally:
+        for e, a, b in zip(es, dLs, dRs):
+            e.dev_free(a)
+            e.dev_free(b)
+        root.dev_free(d_map)
+
+
+def test_back_to_back_gathers_without_sync(ctxs):
+    """two enqueue-only C4 calls with peer-copy gathers, no synchronisation in
+    between.  The peers' copies of call 2 into the root's receive buffer must wait until call
+    1's expansion on the root stream has read it; both calls' outputs stay bit-exact (also the
+    rows forms, which share the receive buffer)."""
+    H, W, D, win = 41, 256, 64, 9
+    es = ctxs[:4]
+    n = H * W
+    root = es[0]
+    sets = []
+    for c in range(2):
+        fr = [stereo_pair(H, W, D, seed=1500 + 10 * c + k)[:2] for k in range(len(es))]
+        sets.append((fr, [_upload(e, f[0]) for e, f in zip(es, fr)], [_upload(e, f[1]) for e, f in zip(es, fr)]))
+    outs = [[root.dev_alloc(4 * n * len(es)), root.dev_alloc(4 * n * len(es)), root.dev_alloc(n * len(es))]
+            for _ in range(2)]
+    rows_out = [[root.dev_alloc(4 * n), root.dev_alloc(4 * n), root.dev_alloc(n)] for _ in range(2)]
+    try:
+        for rep in range(3):
+            for c in range(2):
+                _, dLs, dRs = sets[c]
+                multi_gpu_depth_map_dev(es, None, dLs, dRs, [1] * len(es), H, W, W, n, 0, D, win, 0.3, 2.0,
+                                        *outs[c])
+            for c in range(2):
+                _, dLs, dRs = sets[c]
+                depth_map_rows_multi(es, None, dLs, dRs, H, W, W, 0, D, win, 0.3, 2.0, *rows_out[c])
+            root.synchronize()
+            for c in range(2):
+                fr = sets[c][0]
+                for k, (L, R) in enumerate(fr):
+                    e_disp, e_depth, e_norm = _oracle(L, R, D, win)
+                    np.testing.assert_array_equal(root.to_host(outs[c][1] + 4 * n * k, (H, W), np.float32), e_disp)
+                    np.testing.assert_array_equal(root.to_host(outs[c][0] + 4 * n * k, (H, W), np.float32), e_depth)
+                    np.testing.assert_array_equal(root.to_host(outs[c][2] + n * k, (H, W), np.uint8), e_norm)
+                # rows form: every context holds its own frame, so band k is frame k's rows
+                got = root.to_host(rows_out[c][1], (H, W), np.float32)
+                for k in range(len(es)):   # band k comes from context k's frame
+                    r0, r1 = H * k // len(es), H * (k + 1) // len(es)
+                    np.testing.assert_array_equal(got[r0:r1], _oracle(*fr[k], D, win)[0][r0:r1])
+    finally:
+        for _, dLs, dRs in sets:
+            for e, a, b in zip(es, dLs, dRs):
+                e.dev_free(a)
+                e.dev_free(b)
+        for o in outs + rows_out:
+            for p in o:
+                root.dev_free(p)
+
+
+@pytest.mark.parametrize("ndev,H,cost,win,fmt,scatter", [(8, 131, "sad", 9, "d8", True), (3, 29, "sad", 15, "m16", True),
+                                                         (4, 57, "hog", 5, "d8", False), (2, 64, "ssd", 7, "m16", False),
+                                                         (1, 40, "sad", 9, "d8", True)])
+def test_depth_map_rows_map_gather_only(ctxs, ndev, H, cost, win, fmt, scatter):
+    """sv_depth_map_rows_map: the root receives only the full-frame map (int16 x16 / u8
+    indices): its own band from its median epilogue, the peers' bands gathered; nothing is
+    expanded.  Twice (the second call reuses scratch), band-only or full-frame inputs."""
+    W, D = 400, 64
+    L, R, _ = stereo_pair(H, W, D, seed=ndev * 31 + H)
+    es = ctxs[:ndev]
+    root = es[0]
+    el = 1 if fmt == "d8" else 2
+    if scatter:
+        dL, dR = _upload(root, L), _upload(root, R)
+        srcs = [(root, dL), (root, dR)]
+    else:
+        dL, dR = [_upload(e, L) for e in es], [_upload(e, R) for e in es]
+        srcs = list(zip(es, dL)) + list(zip(es, dR))
+    d_map = root.dev_alloc(el * H * W)
+    try:
+        for _ in range(2):
+            depth_map_rows_map(es, None, dL, dR, H, W, W, 0, D, win, d_map, fmt=fmt, scatter=scatter, cost=cost)
+        root.synchronize()
+        e_disp = _oracle(L, R, D, win, cost)[0]
+        if fmt == "d8":
+            got = root.to_host(d_map, (H, W), np.uint8).astype(np.float32) - np.float32(1)
+        else:
+            got = root.to_host(d_map, (H, W), np.int16).astype(np.float32) / np.float32(16)
+        np.testing.assert_array_equal(got, e_disp)
+    finally:
+        for e, p in srcs:
+            e.dev_free(p)
+        root.dev_free(d_map)
+
+
+def test_median_map_dev_rows_and_formats(engine):
+    """sv_median_map_dev: a row band's median written only as a map (int16 x16 / u8 indices)
+    at full-frame offsets, rows outside the band untouched; num_disp > 255 refused for u8."""
+    from stereovision_amd.engine import SVError
+    H, W, D, win, md = 50, 210, 40, 7, -4
+    L, R, _ = stereo_pair(H, W, D, seed=5)
+    e, n = engine, H * W
+    dL, dR, d16 = _upload(e, L), _upload(e, R), e.dev_alloc(2 * n)
+    m16, d8 = e.dev_alloc(2 * n), e.dev_alloc(n)
+    try:
+        e.to_device(m16, np.full(n, 0x7777, np.int16))
+        e.to_device(d8, np.full(n, 0xAB, np.uint8))
+        e.disparity_dev(dL, dR, H, W, W, md, D, win, "sad", 0, H, d16, W)
+        e.median_map_dev(d16, H, W, 9, 33, m16, "m16", min_disp=md, num_disp=D)
+        e.median_map_dev(d16, H, W, 9, 33, d8, "d8", min_disp=md, num_disp=D)
+        e.synchronize()
+        exp = C.median5_f32(C.disparity16(L, R, md, D, win, 0))
+        g16 = e.to_host(m16, (H, W), np.int16)
+        g8 = e.to_host(d8, (H, W), np.uint8)
+        np.testing.assert_array_equal(g16[9:33].astype(np.float32) / np.float32(16), exp[9:33])
+        np.testing.assert_array_equal(g8[9:33].astype(np.float32) + np.float32(md - 1), exp[9:33])
+        assert (g16[:9] == 0x7777).all() and (g16[33:] == 0x7777).all()
+        assert (g8[:9] == 0xAB).all() and (g8[33:] == 0xAB).all()
+        with pytest.raises(SVError):
+            e.median_map_dev(d16, H, W, 0, H, d8, "d8", min_disp=0, num_disp=256)
+    finally:
+        for p in (dL, dR, d16, m16, d8):
+            e.dev_free(p)
 
 
 def test_depth_map_batch_d8_dev_indices(engine):
@@ -388,7 +538,8 @@ def _port():
 
 
 @pytest.mark.parametrize("mode,root_outputs,fmt", [("frames", "m16", "auto"), ("frames", "m16", "i16"),
-                                                   ("frames", "full", "auto"), ("rowtile", "m16", "auto")])
+                                                   ("frames", "full", "auto"), ("rowtile", "m16", "auto"),
+                                                   ("rowtile", "m16", "i16"), ("rowtile", "full", "auto")])
 def test_bench_under_torch_distributed_run_two_ranks(mode, root_outputs, fmt):
     """The driver's N>1 launch: torch.distributed.run starts 2 bench.py workers (torch-free).
     On a 1-GPU box both ranks share the GPU, so the group falls back to the file store (RCCL
@@ -426,22 +577,30 @@ def test_bench_under_torch_distributed_run_two_ranks(mode, root_outputs, fmt):
         assert d["root_outputs"] == root_outputs
         assert sum("expanded on rank 0" in c for c in checked) == (2 if full else 0), checked
         assert (d["root_expand_us_per_step"] is not None) == full
-    else:
+    elif root_outputs == "full":
         assert checked == ["full frame gathered on rank 0"]
+        assert d["root_expand_us_per_step"] is not None
+    else:    # gather-only row tiling: the map only, nothing expanded on rank 0
+        assert checked == [f"full-frame map gathered on rank 0 ({d['gather_format']})"], checked
+        assert d["gather_format"] == ("u8 disparity index" if fmt == "auto" else "int16 x16")
+        assert d["root_expand_us_per_step"] is None
 
 
-@pytest.mark.parametrize("ngpu,mode,root_outputs", [(2, "frames", "m16"), (3, "frames", "full"),
-                                                    (4, "rowtile", "m16")])
-def test_bench_one_process_rehearsal(ngpu, mode, root_outputs):
+@pytest.mark.parametrize("ngpu,mode,root_outputs,fmt", [(2, "frames", "m16", "auto"), (3, "frames", "full", "auto"),
+                                                        (3, "frames", "m16", "i16"), (4, "rowtile", "m16", "auto"),
+                                                        (3, "rowtile", "m16", "i16"), (2, "rowtile", "full", "auto")])
+def test_bench_one_process_rehearsal(ngpu, mode, root_outputs, fmt):
     """`bench.py --gpus N` without a launcher (ONE process drives N GPUs: the gather lanes, two
-    context sets, sv_multi_gpu_m16_dev / sv_multi_gpu_depth_map_dev / sv_depth_map_rows_scatter)
-    on N logical GPUs of this box (--rehearse: contexts of the visible devices, gathers as
-    device copies): runs end to end and every gathered map of the last step is bit-exact
-    against the C oracle; the line reports 2 B/px of gather traffic."""
+    context sets, sv_multi_gpu_map_dev / sv_multi_gpu_depth_map_dev / sv_depth_map_rows_map /
+    sv_depth_map_rows_scatter) on N logical GPUs of this box (--rehearse: contexts of the
+    visible devices, gathers as device copies): runs end to end and every gathered map of the
+    last step is bit-exact against the C oracle; the line reports the gather traffic — u8
+    indices (1 B/px) by default, int16 x16 (2 B/px) with --gather-format i16 or full outputs."""
     H, W, B = 96, 400, 2
     cmd = [sys.executable, "bench.py", "--gpus", str(ngpu), "--rehearse", "--steps", "3",
            "--warmup", "1", "--height", str(H), "--width", str(W), "--num-disp", "64",
            "--frames", "4", "--batch", str(B), "--mode", mode, "--root-outputs", root_outputs,
+           "--gather-format", fmt,
            "--no-live-pmc", "--no-aux", "--no-host-path", "--no-cpu-baseline", "--hang-timeout", "90"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
@@ -450,15 +609,39 @@ def test_bench_one_process_rehearsal(ngpu, mode, root_outputs):
     assert res["n_gpus"] == ngpu and res["verified"] is True, res["verify"]
     d = res["distributed"]
     assert d["process_model"] == "one process, all devices" and d["gather"] is True
+    assert d["root_outputs"] == root_outputs
+    u8 = root_outputs == "m16" and fmt == "auto"
+    assert d["gather_format"] == ("u8 disparity index" if u8 else "int16 x16")
+    assert (d["root_expand_us_per_step"] is not None) == (root_outputs == "full")
     checked = res["verify"]["checked"]
     if mode == "frames":
         assert len(checked) == 2 * ngpu, checked
-        assert d["gather_bytes_per_step"] == 2 * H * W * B * (ngpu - 1)
-        assert d["root_outputs"] == root_outputs
-        assert (d["root_expand_us_per_step"] is not None) == (root_outputs == "full")
+        assert d["gather_bytes_per_step"] == (1 if u8 else 2) * H * W * B * (ngpu - 1)
     else:
-        assert checked == ["full frame gathered on device 0"]
-        assert d["root_outputs"] == "full" and d["root_expand_us_per_step"] is not None
+        band0 = H // ngpu
+        assert d["gather_bytes_per_step"] == (1 if u8 else 2) * (H - band0) * W
+        assert len(checked) == 1 and "gathered on device 0" in checked[0], checked
+
+
+def test_bench_rccl_init_failure_falls_back_to_peer_copies():
+    """when ncclCommInitAll fails, the one-process N-GPU bench gathers with
+    hipMemcpyPeerAsync instead of exiting, names the fallback (backend "peer", rccl_reason) and
+    still verifies its gathered maps (SV_RCCL_INIT_FAIL=1 forces the failure)."""
+    import json
+    cmd = [sys.executable, "bench.py", "--gpus", "3", "--rehearse", "--steps", "3", "--warmup", "1",
+           "--height", "96", "--width", "400", "--num-disp", "64", "--frames", "2", "--batch", "2",
+           "--no-live-pmc", "--no-aux", "--no-host-path", "--no-cpu-baseline", "--hang-timeout", "90"]
+    env = dict(os.environ, SV_RCCL_INIT_FAIL="1")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=150, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    d = res["distributed"]
+    assert res["verified"] is True, res["verify"]
+    assert d["backend"] == "peer" and d["rccl_ranks"] == 0
+    assert "ncclCommInitAll failed" in d["rccl_reason"] and "SV_RCCL_INIT_FAIL" in d["rccl_reason"]
+    # --require-rccl: the same failure ends the run
+    r = subprocess.run(cmd + ["--require-rccl"], cwd=ROOT, capture_output=True, text=True, timeout=150, env=env)
+    assert r.returncode != 0 and "require-rccl" in (r.stdout + r.stderr)
 
 
 def test_bench_single_gpu_verifies_its_timed_outputs():

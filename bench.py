@@ -329,6 +329,10 @@ def host_path(H, W, D, win, seconds=3.0):
                    "f32, colormap u8x3) NumPy, one synchronous call per frame",
            "bytes_h2d_per_frame": 6 * H * W}
     try:
+        out["per_call"] = host_path_stages(DM, frames, H, W)
+    except Exception as e:  # reported, never required
+        out["per_call"] = {"error": str(e)}
+    try:
         from stereovision_amd.pipeline import DepthMapPipeline
     except ImportError:
         return out
@@ -353,6 +357,47 @@ def host_path(H, W, D, win, seconds=3.0):
     finally:
         pipe.close()
     return out
+
+
+def host_path_stages(DM, frames, H, W, calls=300, seconds=1.5):
+    """Where a synchronous create_depth_map call's time goes (a separate, profiled run of the
+    same calls): device events around each image upload (SV_K_H2D), the kernels and the
+    outputs' download (SV_K_D2H) on the engine's stream, and the host stages of the call
+    (sv_host_profile_*).  Device spans are per call (both images for h2d / gray); their sum
+    against the wall time shows what bounds the call."""
+    from stereovision_amd.engine import host_profile
+    eng = get_engine()
+    host_profile(enable=True, reset=True)
+    eng.profile(True)
+    eng.profile_reset()
+    m, t0 = 0, time.perf_counter()
+    try:
+        while m < calls and time.perf_counter() - t0 < seconds:
+            DM.create_depth_map(*frames[m % len(frames)])
+            m += 1
+        wall = time.perf_counter() - t0
+    finally:
+        eng.profile(False)
+        hp = host_profile(enable=False, reset=True)
+    dev = {k: eng.profile_read(k) for k in ("h2d", "gray", "match", "median", "d2h")}
+    eng.profile_reset()
+    us = {f"{k}_us": round(ms * 1e3 / m, 1) for k, (ms, _) in dev.items()}
+    kernel_us = us["gray_us"] + us["match_us"] + us["median_us"]
+    # the outputs that cross PCIe: registered output arrays come back by DMA (depth f32 +
+    # disparity f32 + colormap BGR = 11 B/px), else the int16 medians (2 B/px) + host expansion
+    dma = hp["expand"] is not None and hp["expand"] < 0.01
+    d2h_bytes = 11 * H * W if dma else 2 * H * W
+    return {"calls": m, "wall_us": round(wall * 1e6 / m, 1), **us,
+            "kernel_us": round(kernel_us, 1),
+            "device_sum_us": round(us["h2d_us"] + kernel_us + us["d2h_us"], 1),
+            "h2d_GBps": round(6 * H * W / (us["h2d_us"] * 1e-6) / 1e9, 1) if us["h2d_us"] else None,
+            "d2h_bytes": d2h_bytes,
+            "d2h_path": ("registered output arrays filled by DMA" if dma else
+                         "int16 medians + host expansion"),
+            "d2h_GBps": round(d2h_bytes / (us["d2h_us"] * 1e-6) / 1e9, 1) if us["d2h_us"] else None,
+            "host_ms": {k: (round(v, 3) if v is not None else None) for k, v in hp.items() if k != "calls"},
+            "note": "device spans from HIP events on the call's stream (h2d: both BGR images from the "
+                    "caller's pageable arrays, staged by the HIP runtime); host_ms = sv_host_profile stages"}
 
 
 # ---- live PMC (rocprofv3 passes over a short child run of this script) -----------------------

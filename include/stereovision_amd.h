@@ -91,7 +91,9 @@ enum sv_kernel {
     SV_K_AFFINE = 11, SV_K_SGBM = 12, SV_K_SPECKLE = 13,
     SV_K_GATHER = 14,   /* multi-GPU gathers to the root (RCCL / peer copies), root stream */
     SV_K_SCATTER = 15,  /* multi-GPU input scatters (row bands + halos), per context stream */
-    SV_NKERNELS = 16
+    SV_K_H2D = 16,      /* host-buffer entry points: the frame pair's upload (per image) */
+    SV_K_D2H = 17,      /* host-buffer entry points: the outputs' download */
+    SV_NKERNELS = 18
 };
 
 int sv_version(void);
@@ -582,6 +584,15 @@ int sv_copy_to_host(sv_ctx* ctx, void* dst, const void* src, uint64_t bytes);
  * the numpy outputs depth_map.py:937-939 returns. */
 int sv_host_register(void* ptr, uint64_t bytes);
 int sv_host_unregister(void* ptr);
+
+/* Host-side stage timings of the host-buffer entry points (process-wide, off by default):
+ * ms6 = accumulated {prepare, stage + issue (the pageable uploads are synchronous), wait for
+ * the first output piece, host expansion, wait for the rest, total} milliseconds over `calls`
+ * calls since the last reset.  The device side of the same calls is the context's event
+ * profile (sv_profile_enable): SV_K_H2D (one event pair per image upload), SV_K_GRAY,
+ * SV_K_MATCH, SV_K_MEDIAN and SV_K_D2H. */
+int sv_host_profile_enable(int enable);
+int sv_host_profile_read(double* ms6, long long* calls, int reset);
 
 /* ---- profiling: HIP events around every kernel this context launches -------------- */
 int sv_profile_enable(sv_ctx* ctx, int on);

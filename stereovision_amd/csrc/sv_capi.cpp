@@ -2069,18 +2069,26 @@ int expand_rows(const int16_t* med, size_t a, size_t b, int m0, int nl, const Ho
     return nbad;
 }
 
-// SV_HOST_PROFILE=1: stage timings of the host-buffer path on stderr every 200 calls
-// (diagnostic; the default path pays one getenv at first use).
+// Host-side stage timings of the host-buffer path (sv_host_profile_enable / _read; the
+// device side — uploads, kernels, downloads — is the context's own event profile,
+// SV_K_H2D / SV_K_GRAY / SV_K_MATCH / SV_K_MEDIAN / SV_K_D2H).  SV_HOST_PROFILE=1 also prints
+// the averages on stderr every 200 calls.
 struct HostProf {
-    bool on = std::getenv("SV_HOST_PROFILE") != nullptr;
+    std::atomic<bool> on{std::getenv("SV_HOST_PROFILE") != nullptr};
+    bool print = std::getenv("SV_HOST_PROFILE") != nullptr;
     std::mutex mu;
-    double t[6] = {0, 0, 0, 0, 0, 0};
-    long n = 0;
+    double t[6] = {0, 0, 0, 0, 0, 0};     // since the last print (stderr)
+    double acc[6] = {0, 0, 0, 0, 0, 0};   // since the last reset (sv_host_profile_read)
+    long n = 0, nacc = 0;
     void add(const double* d) {
         std::lock_guard<std::mutex> lk(mu);
-        for (int i = 0; i < 6; ++i) t[i] += d[i];
-        if (++n % 200 == 0) {
-            std::fprintf(stderr, "[sv host] per call (ms): stage %.3f  issue %.3f  wait-first %.3f  expand %.3f  "
+        for (int i = 0; i < 6; ++i) {
+            t[i] += d[i];
+            acc[i] += d[i];
+        }
+        ++nacc;
+        if (print && ++n % 200 == 0) {
+            std::fprintf(stderr, "[sv host] per call (ms): prepare %.3f  stage+issue %.3f  wait-first %.3f  expand %.3f  "
                          "wait-rest %.3f  total %.3f\n", t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n);
             for (double& v : t) v = 0;
             n = 0;
@@ -2210,7 +2218,9 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
     for (int i = 0; i < 2; ++i) {
         uint8_t* stage = c->hin.as<uint8_t>() + (size_t)i * row * H;
         uint8_t* dst = channels == 1 ? c->gray[i].as<uint8_t>() : c->img[i].as<uint8_t>();
+        c->prof_begin(SV_K_H2D, c->stream);   // (profile on: device events around each upload)
         rc = stage_rows(c, src[i], 0, H, row, stride, stage, dst, 6);
+        c->prof_end(c->stream);
         if (rc) return rc;
         if (channels == 3)
             SV_LAUNCH(c, SV_K_GRAY, c->stream,
@@ -2222,6 +2232,7 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
     SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
               sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, reg ? c->fb.as<float>() : nullptr, mp,
                                     c->stream));
+    c->prof_begin(SV_K_D2H, ds);
     for (int q = 0; q < npiece; ++q) {
         const int p0 = (int)((long long)H * q / npiece), p1 = (int)((long long)H * (q + 1) / npiece);
         bands[q][0] = p0;
@@ -2242,6 +2253,7 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
             SV_HIP(hipEventRecord(c->dev_done[q], ds));
         }
     }
+    c->prof_end(ds);
     if (prof) { const double t = now_ms(); tm[1] = t - tp; tp = t; }
     if (!reg) {
         for (int q = 0; q < npiece; ++q) {
@@ -2263,6 +2275,24 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
 }  // namespace
 
 extern "C" {
+
+int sv_host_profile_enable(int enable) {
+    host_prof().on = enable != 0;
+    return 0;
+}
+
+int sv_host_profile_read(double* ms6, long long* calls, int reset) {
+    HostProf& hp = host_prof();
+    std::lock_guard<std::mutex> lk(hp.mu);
+    if (ms6)
+        for (int i = 0; i < 6; ++i) ms6[i] = hp.acc[i];
+    if (calls) *calls = hp.nacc;
+    if (reset) {
+        for (double& v : hp.acc) v = 0;
+        hp.nacc = 0;
+    }
+    return 0;
+}
 
 int sv_host_register(void* ptr, uint64_t bytes) {
     if (!ptr || bytes == 0) return fail(SV_EINVAL, "null or empty host range");

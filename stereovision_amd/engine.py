@@ -25,7 +25,7 @@ COSTS = {"sad": 0, "ssd": 1, "hog": 2, "sgbm": 3}
 POST_NONE, POST_DEPTH, POST_SCALED = 0, 1, 2
 KERNELS = {"gray": 0, "harris": 1, "hog": 2, "match": 3, "median": 4, "post": 5, "remap": 6,
            "undistort": 7, "resize": 8, "stats": 9, "select": 10, "affine": 11, "sgbm": 12,
-           "speckle": 13, "gather": 14, "scatter": 15}
+           "speckle": 13, "gather": 14, "scatter": 15, "h2d": 16, "d2h": 17}
 
 # Every symbol include/stereovision_amd.h declares (checked by tests/test_capi.py).
 EXPORTED = [
@@ -35,7 +35,7 @@ EXPORTED = [
     "sv_hog_hist", "sv_gray_dev", "sv_disparity_dev", "sv_median_post_dev",
     "sv_depth_map_dev", "sv_harris_dev", "sv_hog_hist_dev", "sv_profile_enable",
     "sv_profile_read", "sv_profile_reset", "sv_disparity_rows", "sv_dev_alloc", "sv_dev_free",
-    "sv_copy_to_device", "sv_copy_to_host", "sv_host_register", "sv_host_unregister", "sv_timer_begin", "sv_timer_end", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
+    "sv_copy_to_device", "sv_copy_to_host", "sv_host_register", "sv_host_unregister", "sv_host_profile_enable", "sv_host_profile_read", "sv_timer_begin", "sv_timer_end", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
     "sv_depth_map_batch_dev", "sv_depth_map_batch_m16_dev", "sv_depth_map_batch_d8_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
     "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
     "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
@@ -176,6 +176,9 @@ def _declare(lib):
         "sv_copy_to_device": ([_vp, _vp, _vp, ctypes.c_uint64], _c_int),
         "sv_copy_to_host": ([_vp, _vp, _vp, ctypes.c_uint64], _c_int),
         "sv_host_register": ([_vp, ctypes.c_uint64], _c_int),
+        "sv_host_profile_enable": ([_c_int], _c_int),
+        "sv_host_profile_read": ([ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), _c_int],
+                                 _c_int),
         "sv_host_unregister": ([_vp], _c_int),
         "sv_timer_begin": ([_vp, _vp], _c_int),
         "sv_timer_end": ([_vp, _vp, ctypes.POINTER(ctypes.c_double)], _c_int),
@@ -1233,6 +1236,23 @@ def band_rows_in(H: int, rank: int, world: int, win: int, cost="sad") -> dict:
     out = (_c_int * 6)()
     _check("sv_band_rows_in", load_library().sv_band_rows_in(H, rank, world, win, _cost(cost), out))
     return dict(zip(("r0", "r1", "h0", "h1", "in0", "in1"), list(out)))
+
+
+HOST_STAGES = ("prepare", "stage_issue", "wait_first", "expand", "wait_rest", "total")
+
+
+def host_profile(enable: bool | None = None, reset: bool = False) -> dict:
+    """Host-side stage timings of the host-buffer entry points (sv_host_profile_*):
+    ``enable`` switches collection on/off; returns the mean ms per call of each stage in
+    HOST_STAGES since the last reset (and resets when asked)."""
+    lib = load_library()
+    if enable is not None:
+        lib.sv_host_profile_enable(int(bool(enable)))
+    ms = (ctypes.c_double * 6)()
+    n = ctypes.c_longlong()
+    _check("sv_host_profile_read", lib.sv_host_profile_read(ms, ctypes.byref(n), int(reset)))
+    calls = n.value
+    return {"calls": calls, **{k: (ms[i] / calls if calls else None) for i, k in enumerate(HOST_STAGES)}}
 
 
 class Communicator:

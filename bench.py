@@ -387,7 +387,9 @@ def host_path_stages(DM, frames, H, W, calls=300, seconds=1.5):
     # disparity f32 + colormap BGR = 11 B/px), else the int16 medians (2 B/px) + host expansion
     dma = hp["expand"] is not None and hp["expand"] < 0.01
     d2h_bytes = 11 * H * W if dma else 2 * H * W
+    regs = getattr(eng, "_registered", {})
     return {"calls": m, "wall_us": round(wall * 1e6 / m, 1), **us,
+            "outputs_registered": len(regs), "registration_refused": bool(getattr(eng, "_noreg", False)),
             "kernel_us": round(kernel_us, 1),
             "device_sum_us": round(us["h2d_us"] + kernel_us + us["d2h_us"], 1),
             "h2d_GBps": round(6 * H * W / (us["h2d_us"] * 1e-6) / 1e9, 1) if us["h2d_us"] else None,
@@ -981,6 +983,9 @@ def main():
         m2, n2 = glanes[1][0][0].profile_read("scatter")
         scat_ms, scat_n = scat_ms + m2, scat_n + n2
     exp_ms, exp_n = (ceng or eng).profile_read("post")
+    if ceng is not None and rowtile:   # the tiles' expansion runs on the compute context's engine
+        m2, n2 = eng.profile_read("post")
+        exp_ms, exp_n = exp_ms + m2, exp_n + n2
     if glanes:
         m2, n2 = glanes[1][0][0].profile_read("post")
         exp_ms, exp_n = exp_ms + m2, exp_n + n2

@@ -2099,6 +2099,12 @@ HostProf& host_prof() {
     static HostProf* p = new HostProf();
     return *p;
 }
+int env_int(const char* name, int dflt, int lo, int hi) {
+    const char* e = std::getenv(name);
+    if (!e) return dflt;
+    const int v = std::atoi(e);
+    return v < lo ? lo : v > hi ? hi : v;
+}
 double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -2182,9 +2188,17 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
     // rounds 3 and 4, so it was removed): stage + upload, gray, disparity, median, then the
     // outputs return in 8 pieces on the compute stream, each behind its own event so the host
     // expansion of one piece runs while the next is in flight.
-    constexpr int npiece = 8;
+    // D2H pieces: every hipMemcpyAsync costs ~15-90 us of copy-engine setup on these boxes
+    // (tools/microbench/pcie_rate: 4.1 MB pinned in 1 piece 0.08-0.33 ms, 8 pieces 0.2-1.0 ms),
+    // so the DMA path (nothing to overlap on the host) downloads each output in one piece and
+    // the expansion path in a few, whose host expansion overlaps the next piece's transfer.
+    // SV_HOST_PIECES / SV_HOST_PIECES_DMA override (A/B measurements).
+    static const int pieces_exp = env_int("SV_HOST_PIECES", 4, 1, 8);
+    static const int pieces_dma = env_int("SV_HOST_PIECES_DMA", 1, 1, 8);
+    constexpr int kmaxp = 8;
+    const int npiece = reg ? pieces_dma : pieces_exp;
     hipStream_t ds = c->stream;
-    int bands[npiece][2] = {};   // output rows of each D2H piece
+    int bands[kmaxp][2] = {};   // output rows of each D2H piece
     std::atomic<int> bad{0};
     sv::HostPool& pool = sv::HostPool::get();
     auto expand = [&](int k) -> int {   // host expansion of piece k's medians

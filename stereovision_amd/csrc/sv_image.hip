@@ -698,8 +698,11 @@ __device__ __forceinline__ T& at(T* base, uint32_t i) {
 }
 
 __device__ __forceinline__ PostVals post_median(const PostParams& pp, int mv) {
-    const uint32_t li = (uint32_t)(mv - pp.lut_m0) >> pp.lut_shift;
-    if (li < (uint32_t)pp.lut_n) {   // table lookup (exact)
+    const uint32_t dm = (uint32_t)(mv - pp.lut_m0);
+    const uint32_t li = dm >> pp.lut_shift;
+    // the whole-disparity table (lut_shift 4) holds multiples of 16 only: any other median (a
+    // sub-pixel map passed through these entry points) takes the exact path below
+    if (li < (uint32_t)pp.lut_n && (dm & ((1u << pp.lut_shift) - 1u)) == 0) {   // table lookup (exact)
         PostVals o;
         o.a = at(pp.lut_a, li);
         o.u = at(pp.lut_u8, li);

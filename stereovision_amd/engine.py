@@ -449,19 +449,26 @@ class Engine:
         result never pay for it): the C path then DMAs the outputs straight into it."""
         if getattr(self, "_noreg", False) or not hasattr(self, "lib"):
             return
+        # keyed by id with the address only: a strong reference here would count against
+        # _set_unreferenced, so a registered set would never be handed out again (every
+        # other call then allocated, page-faulted and registered a fresh set)
         regs = self.__dict__.setdefault("_registered", {})
         for a in arrs:
             if a.nbytes and id(a) not in regs:
                 if self.lib.sv_host_register(a.ctypes.data, a.nbytes) != 0:
                     self._noreg = True     # e.g. a page-lock limit: keep the host expansion
                     return
-                regs[id(a)] = a
+                regs[id(a)] = a.ctypes.data
 
     def _unregister(self, arrs):
         regs = self.__dict__.get("_registered", {})
         for a in arrs:
             if regs.pop(id(a), None) is not None:
                 self.lib.sv_host_unregister(a.ctypes.data)
+
+    def registered_outputs(self) -> int:
+        """Output arrays currently page-locked for the DMA path (diagnostics)."""
+        return len(self.__dict__.get("_registered", {}))
 
     def upload(self, name: str, a: np.ndarray) -> int:
         """Copy a host array into the named scratch buffer; returns its device pointer."""

@@ -55,3 +55,41 @@ def test_pool_is_bounded_and_keyed_by_shape():
     other = p.outputs((((2, 2), np.float32),))
     assert other[0].shape == (2, 2) and len(p._recycle) == 2
     assert len({id(h[0]) for h in held}) == 5   # every held set distinct
+
+
+class _FakeLib:
+    def __init__(self):
+        self.registered = {}
+
+    def sv_host_register(self, ptr, nbytes):
+        self.registered[ptr] = nbytes
+        return 0
+
+    def sv_host_unregister(self, ptr):
+        self.registered.pop(ptr)
+        return 0
+
+
+class _RegPool(_Pool):
+    def __init__(self):
+        super().__init__()
+        self.lib = _FakeLib()
+
+
+def test_registered_set_is_reused_every_call():
+    """A set page-locked on its first reuse must keep being handed out: the registry may not
+    hold a reference that makes the set look referenced (round 5: it did, so every other
+    call allocated, page-faulted and registered a fresh 20 MB set and took the host
+    expansion path)."""
+    p = _RegPool()
+    ids = _ids(p.outputs(SPEC))          # fresh set (not registered yet)
+    for _ in range(6):                   # released every time: the same set, registered once
+        got = p.outputs(SPEC)
+        assert _ids(got) == ids
+        del got
+    assert len(p._recycle[next(iter(p._recycle))]) == 1
+    assert len(p.lib.registered) == 3
+    # popping a set from a full slot unregisters it
+    held = [p.outputs(SPEC) for _ in range(4)]
+    assert len(p.lib.registered) <= 9
+    del held

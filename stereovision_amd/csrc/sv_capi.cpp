@@ -2191,9 +2191,11 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
     // D2H pieces: every hipMemcpyAsync costs ~15-90 us of copy-engine setup on these boxes
     // (tools/microbench/pcie_rate: 4.1 MB pinned in 1 piece 0.08-0.33 ms, 8 pieces 0.2-1.0 ms),
     // so the DMA path (nothing to overlap on the host) downloads each output in one piece and
-    // the expansion path in a few, whose host expansion overlaps the next piece's transfer.
+    // the expansion path in two, the second's transfer under the first's host expansion
+    // (round 5 A/B, profiles/r05b/host_ab.txt: 2 pieces 1.47-1.51k frames/s per call, 4
+    // pieces 1.41-1.45k, 8 pieces 1.23-1.35k).
     // SV_HOST_PIECES / SV_HOST_PIECES_DMA override (A/B measurements).
-    static const int pieces_exp = env_int("SV_HOST_PIECES", 4, 1, 8);
+    static const int pieces_exp = env_int("SV_HOST_PIECES", 2, 1, 8);
     static const int pieces_dma = env_int("SV_HOST_PIECES_DMA", 1, 1, 8);
     constexpr int kmaxp = 8;
     const int npiece = reg ? pieces_dma : pieces_exp;

@@ -401,7 +401,11 @@ class Engine:
         self.device = device
         self._scratch: dict[str, tuple[int, int]] = {}
         self._recycle: dict[tuple, list] = {}
-        self._noreg = os.environ.get("SV_REGISTER_OUTPUTS", "1") == "0"
+        # page-locking recycled outputs (the device epilogue then fills them by DMA, 11 B/px
+        # over PCIe) measured slower than downloading the int16 medians (2 B/px) and expanding
+        # them on the host (round 5, profiles/r05b/host_ab.txt: 1.26k vs 1.47k frames/s per
+        # call, 2.0k vs 2.9k with 4 in flight): opt-in with SV_REGISTER_OUTPUTS=1
+        self._noreg = os.environ.get("SV_REGISTER_OUTPUTS", "0") != "1"
 
     # -- lifetime -------------------------------------------------------------------
     def close(self):

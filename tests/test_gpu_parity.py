@@ -611,14 +611,18 @@ def test_registered_outputs_dma_path_matches_host_expansion(engine, scaled):
     t = colormap.table("turbo")
     call = (lambda: engine.stereo_scaled_color(Lb, Rb, 0, 64, 9, t)) if scaled else \
         (lambda: engine.depth_map_color(Lb, Rb, 0, 64, 9, 0.3, 2.0, t))
-    first = [a.copy() for a in call()]          # fresh set: host expansion
-    for _ in range(3):                          # released -> reused -> registered -> DMA
-        got = call()
-        for g, e in zip(got, first):
-            np.testing.assert_array_equal(g, e)
-        del got
-    regs = getattr(engine, "_registered", {})
-    assert regs, "no output set was registered"
+    noreg = engine._noreg
+    engine._noreg = False                       # the DMA path is opt-in (SV_REGISTER_OUTPUTS=1)
+    try:
+        first = [a.copy() for a in call()]      # fresh set: host expansion
+        for _ in range(3):                      # released -> reused -> registered -> DMA
+            got = call()
+            for g, e in zip(got, first):
+                np.testing.assert_array_equal(g, e)
+            del got
+        assert engine.registered_outputs(), "no output set was registered"
+    finally:
+        engine._noreg = noreg
 
 
 @pytest.mark.parametrize("win,D", [(9, 128), (15, 256)])

@@ -133,6 +133,57 @@ def test_strict_group_refuses_file_store_on_distinct_devices():
     assert all("RCCL required on distinct devices" in msg for _, msg in res), res
 
 
+def _init_fail_worker(rank, world, path, strict, q):
+    """RCCL loads on every rank, but ncclCommInitRank fails on rank 1 only."""
+    os.environ.update({"WORLD_SIZE": str(world), "RANK": str(rank), "LOCAL_RANK": str(rank),
+                       "SV_RDZV_DIR": path})
+
+    class _Comm:
+        nranks = world
+
+        def close(self):
+            q.put((rank, "closed"))
+
+    def _init_rank(device, nranks, r, uid):
+        if r == 1:
+            raise RuntimeError("ncclCommInitRank: unhandled system error")
+        return _Comm()
+    E.Communicator.available = staticmethod(lambda: True)
+    E.Communicator.unique_id = staticmethod(lambda: b"\0" * 128)
+    E.Communicator.init_rank = staticmethod(_init_rank)
+    try:
+        pg = SD.init_process_group(device=rank, backend="auto", timeout=60, strict=strict)
+        q.put((rank, f"{pg.backend}|{pg.reason}"))
+        pg.close()
+    except RuntimeError as e:
+        q.put((rank, "raised: " + str(e)))
+
+
+@pytest.mark.parametrize("strict", [False, True])
+def test_rccl_init_failure_on_one_rank_falls_back_on_every_rank(strict):
+    """VERDICT r04 Next #1: an ncclCommInitRank failure on any rank is decided collectively —
+    every rank closes its communicator and uses the file store (backend "host", the failure
+    named), or, strict (--require-rccl), every rank raises; no rank is left in a collective."""
+    path = tempfile.mkdtemp(prefix="sv_bench_initfail_")
+    os.rmdir(path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_init_fail_worker, args=(k, 2, path, strict, q)) for k in range(2)]
+    for p in ps:
+        p.start()
+    res = []
+    for _ in range(3):   # one result per rank + rank 0's "closed" (its init succeeded)
+        res.append(q.get(timeout=120))
+    for p in ps:
+        p.join(timeout=60)
+    msgs = {r: m for r, m in res if m != "closed"}
+    assert (0, "closed") in res and sorted(msgs) == [0, 1], res   # rank 0 gave its communicator back
+    if strict:
+        assert all(m.startswith("raised:") and "ncclCommInitRank failed on rank 1" in m for m in msgs.values()), res
+    else:
+        assert all(m.startswith("host|") and "ncclCommInitRank failed on rank 1" in m for m in msgs.values()), res
+
+
 class _FakeEngine:
     stream = 0xABC
 

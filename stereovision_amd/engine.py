@@ -406,6 +406,7 @@ class Engine:
         # them on the host (round 5, profiles/r05b/host_ab.txt: 1.26k vs 1.47k frames/s per
         # call, 2.0k vs 2.9k with 4 in flight): opt-in with SV_REGISTER_OUTPUTS=1
         self._noreg = os.environ.get("SV_REGISTER_OUTPUTS", "0") != "1"
+        self._out_lock = threading.Lock()
 
     # -- lifetime -------------------------------------------------------------------
     def close(self):
@@ -437,16 +438,29 @@ class Engine:
         frames writes into resident pages instead of page-faulting 20+ MB of new memory per
         1080p frame.  At most 3 sets per shape are kept."""
         key = tuple((tuple(sh), np.dtype(dt).str) for sh, dt in specs)
-        sets = self._recycle.setdefault(key, [])
-        for arrs in sets:
-            if _set_unreferenced(arrs):
-                self._register(arrs)
-                return tuple(arrs)
-        arrs = [np.empty(sh, dt) for sh, dt in specs]
-        sets.append(arrs)
-        if len(sets) > 3:
-            self._unregister(sets.pop(0))
-        return tuple(arrs)
+        # the reference calls the path from a 2-worker thread pool (fused_depth_map.py:2299,
+        # :2591-2598): the check-and-take must be atomic, or two threads could both find a
+        # released set and share it
+        with self._out_lock:
+            sets = self._recycle.setdefault(key, [])
+            for arrs in sets:
+                if _set_unreferenced(arrs):
+                    self._register(arrs)
+                    return tuple(arrs)
+            arrs = [np.empty(sh, dt) for sh, dt in specs]
+            if len(sets) < 3:
+                sets.append(arrs)
+            else:
+                # a full slot evicts its oldest RELEASED set (never one a caller — or another
+                # thread's call in flight — still holds: unregistering it could pull pinned
+                # pages from under a DMA); when every kept set is in use the new one is handed
+                # out untracked
+                for i in range(len(sets)):
+                    if _set_unreferenced(sets[i]):
+                        self._unregister(sets.pop(i))
+                        sets.append(arrs)
+                        break
+            return tuple(arrs)
 
     def _register(self, arrs):
         """Page-lock a recycled output set (on its first reuse, so callers that keep every

@@ -249,6 +249,44 @@ def test_depth_map_rows_map_gather_only(ctxs, ndev, H, cost, win, fmt, scatter):
         root.dev_free(d_map)
 
 
+@pytest.mark.parametrize("fmt", ["d8", "m16"])
+def test_gather_only_maps_with_empty_shares(ctxs, fmt):
+    """Edge cases of the gather-only forms: a root with no frames of its own, peers with none,
+    and a row tiling with more contexts than rows (empty bands), all bit-exact."""
+    H, W, D, win = 5, 96, 16, 3
+    L, R, _ = stereo_pair(H, W, D, seed=77)
+    el = 1 if fmt == "d8" else 2
+    root = ctxs[0]
+    e_disp = _oracle(L, R, D, win)[0]
+    dL = [_upload(e, L) for e in ctxs]
+    dR = [_upload(e, R) for e in ctxs]
+    d_map = root.dev_alloc(el * H * W * 2)
+    try:
+        counts = [0, 1, 0, 0, 0, 0, 1, 0]            # frame 0 from context 1, frame 1 from 6
+        multi_gpu_map_dev(ctxs, None, dL, dR, counts, H, W, W, H * W, 0, D, win, d_map, fmt=fmt)
+        root.synchronize()
+        if fmt == "d8":
+            got = root.to_host(d_map, (2, H, W), np.uint8).astype(np.float32) - np.float32(1)
+        else:
+            got = root.to_host(d_map, (2, H, W), np.int16).astype(np.float32) / np.float32(16)
+        np.testing.assert_array_equal(got[0], e_disp)
+        np.testing.assert_array_equal(got[1], e_disp)
+        for scatter in (False, True):                # 8 contexts, 5 rows: 3 empty bands
+            depth_map_rows_map(ctxs, None, dL[0] if scatter else dL, dR[0] if scatter else dR, H, W, W, 0,
+                               D, win, d_map, fmt=fmt, scatter=scatter)
+            root.synchronize()
+            if fmt == "d8":
+                got = root.to_host(d_map, (H, W), np.uint8).astype(np.float32) - np.float32(1)
+            else:
+                got = root.to_host(d_map, (H, W), np.int16).astype(np.float32) / np.float32(16)
+            np.testing.assert_array_equal(got, e_disp)
+    finally:
+        for e, a, b in zip(ctxs, dL, dR):
+            e.dev_free(a)
+            e.dev_free(b)
+        root.dev_free(d_map)
+
+
 def test_median_map_dev_rows_and_formats(engine):
     """sv_median_map_dev: a row band's median written only as a map (int16 x16 / u8 indices)
     at full-frame offsets, rows outside the band untouched; num_disp > 255 refused for u8."""

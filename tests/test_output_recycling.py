@@ -1,6 +1,9 @@
 """Output recycling of the host-buffer entry points (Engine.outputs): a set of output arrays
 is handed out again only when the caller holds no reference to any of them (CPU test: the
 pool logic needs no device)."""
+import sys
+import threading
+
 import numpy as np
 
 from stereovision_amd import engine as EN
@@ -13,6 +16,7 @@ class _Pool:
 
     def __init__(self):
         self._recycle = {}
+        self._out_lock = threading.Lock()
 
 
 SPEC = (((6, 5), np.float32), ((6, 5), np.float32), ((6, 5, 3), np.uint8))
@@ -93,3 +97,60 @@ def test_registered_set_is_reused_every_call():
     held = [p.outputs(SPEC) for _ in range(4)]
     assert len(p.lib.registered) <= 9
     del held
+
+
+def test_full_slot_never_evicts_a_held_set():
+    """Eviction from a full slot takes the oldest RELEASED set only: a set another call still
+    holds is never unregistered from under it (its DMA may be in flight)."""
+    p = _RegPool()
+    held = [p.outputs(SPEC) for _ in range(3)]        # fills the slot, all held
+    for _ in range(3):
+        extra = p.outputs(SPEC)                       # untracked: the slot keeps the held sets
+        assert all(_ids(extra) != _ids(h) for h in held)
+        del extra
+    assert [_ids(s) for s in p._recycle[next(iter(p._recycle))]] == [_ids(h) for h in held]
+    del held[1]
+    new = p.outputs(SPEC)                             # the released one is reused
+    assert _ids(new) not in [_ids(h) for h in held]
+
+
+def test_concurrent_callers_never_share_a_set(monkeypatch):
+    """Two threads taking and releasing output sets (the reference's 2-worker pool): no set is
+    ever handed to both at once.  The check is widened on purpose (a thread switch right after
+    a set is found released) so that an unlocked check-and-take would be caught."""
+    import time
+    orig = EN._set_unreferenced
+
+    def slow(arrs):
+        free = orig(arrs)
+        if free:
+            time.sleep(0.0002)
+        return free
+    monkeypatch.setattr(EN, "_set_unreferenced", slow)
+    p = _Pool()
+    in_use, lock, errors = set(), threading.Lock(), []
+    old = sys.getswitchinterval()
+    sys.setswitchinterval(1e-6)
+
+    def worker():
+        for _ in range(300):
+            got = p.outputs(SPEC)
+            key = id(got[0])
+            with lock:
+                if key in in_use:
+                    errors.append(key)
+                in_use.add(key)
+            time.sleep(0.0001)                        # hold it for a moment
+            with lock:
+                in_use.discard(key)
+            del got
+
+    try:
+        ts = [threading.Thread(target=worker) for _ in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    finally:
+        sys.setswitchinterval(old)
+    assert not errors

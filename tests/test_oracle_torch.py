@@ -19,8 +19,17 @@ import sv_oracle as O
 import sv_oracle_c as C
 from stereovision_amd.synthetic import stereo_pair
 
-torch = pytest.importorskip("torch")
-F = torch.nn.functional
+torch = F = None
+
+
+@pytest.fixture(autouse=True)
+def _torch():
+    """torch is imported by the tests themselves, never at collection: the GPU test process
+    collects this module too (deselected), and must map exactly one HIP runtime — ROCm's, not
+    torch's bundled copy (test_gpu_parity.py::test_row_tiled_module_and_single_hip_runtime)."""
+    global torch, F
+    torch = pytest.importorskip("torch")
+    F = torch.nn.functional
 
 
 def _wta_torch(L, R, min_disp, num_disp, win, ssd=False):

@@ -84,7 +84,8 @@ def pmc_summary(outdir):
     agg = {}
     for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            k = (r["Kernel_Name"].split("(")[0][:60], r["Counter_Name"])
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+            k = (name.split("(")[0][:60], r["Counter_Name"])
             agg.setdefault(k, []).append(float(r["Counter_Value"]))
     rows = sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:24]
     return "\n".join(f"  {k[0]:<60} {k[1]:<22} mean {sum(v) / len(v):.4g}  n {len(v)}" for k, v in rows)

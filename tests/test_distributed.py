@@ -75,6 +75,16 @@ def _row_tiled_worker(rank, world, port, H, W, D, win, q):
         comm = GlooBufferComm(dist, buf)
         SD.gather_rows(comm, 0, H, 4 * W)
         SD.gather_rows(comm, 4 * H * W, H, 4 * W)
+        # gather-only row tiling (--root-outputs m16): the bands' maps only, as u8 disparity
+        # indices d - min_disp + 1 (1 B/px) and as int16 x16 medians (2 B/px)
+        med16 = np.zeros((H, W), np.int16)
+        med16[r0:r1] = O.median5(d16[h0:h1])[r0 - h0:r1 - h0]
+        d8 = np.zeros((H, W), np.uint8)
+        d8[r0:r1] = (med16[r0:r1] // 16 + 1).astype(np.uint8)       # min_disp 0: index d + 1
+        mbuf = np.concatenate([d8.ravel(), med16.view(np.uint8).ravel()])
+        mcomm = GlooBufferComm(dist, mbuf)
+        SD.gather_rows(mcomm, 0, H, W)
+        SD.gather_rows(mcomm, H * W, H, 2 * W)
         # frame gather: rank k contributes k+1 frames of 6 bytes filled with k
         counts = [k + 1 for k in range(world)]
         fbuf = np.full(6 * counts[rank], rank, np.uint8)
@@ -88,8 +98,11 @@ def _row_tiled_worker(rank, world, port, H, W, D, win, q):
             ref_depth, _ = O.depth_post(ref_disp, 0.3, 2.0)
             frames = fcomm.buf[fbuf.size:]
             exp_frames = np.concatenate([np.full(6 * counts[k], k, np.uint8) for k in range(world)])
+            got_d8 = mbuf[:H * W].reshape(H, W).astype(np.float32) - np.float32(1)
+            got_m16 = mbuf[H * W:].view(np.int16).reshape(H, W).astype(np.float32) / np.float32(16)
             q.put(bool(np.array_equal(got_disp, ref_disp) and np.array_equal(got_depth, ref_depth)
-                       and np.array_equal(frames, exp_frames)))
+                       and np.array_equal(frames, exp_frames) and np.array_equal(got_d8, ref_disp)
+                       and np.array_equal(got_m16, ref_disp)))
     finally:
         dist.destroy_process_group()
 

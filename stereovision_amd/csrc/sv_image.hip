@@ -2,7 +2,8 @@
 //
 //  * k_gray        cv2.cvtColor(BGR2GRAY), 14-bit fixed point   (depth_map.py:871-880)
 //  * k_harris_lds  Harris response, cornerHarris(3, 3, 0.04) convention (north_star)
-//  * k_hog_hist    per-pixel 9-bin gradient orientation + window histograms (north_star)
+//  * k_hog_hist_cr per-pixel 9-bin gradient orientation + window histograms (north_star),
+//                  4 columns per lane (k_hog_hist: the 64x16 tile form for > 2 GB records)
 //  * k_median_i16  medianBlur(disparity, 5) on the int16 x16 map, fused with the
 //                  reference's post-processing (depth_map.py:909-937 or
 //                  fused_depth_map.py:1004-1029) so the filtered map never round-trips HBM
@@ -438,52 +439,50 @@ __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g,
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// HOG window histograms, strip form: one wave = 64 consecutive (clamped) columns walking down
-// HS rows; lane j outputs column x0 + j - r for j in [r, 63 - r]; no LDS tiles; a row's 50..64
-// records (contiguous in HBM) are staged in 1.3 KB of LDS and leave as 16-byte stores.
-// Packed u16 halves stay exact: a window sum is <= 57,375 per bin, and the 32-bit prefix
-// sums across the wave may carry between halves (or wrap) only in values whose difference
-// P(j + r) - P(j - r - 1) is exact modulo 2^32 and below 2^32.  (4K, r = 7: 122 us per image
-// with 64x16 LDS tiles; 94 -> 87 -> 69 us in 2-frame batches with a ring of the last 2r+1 row
-// sums; 65 -> 60.5 us with the vertical-first form below, which holds 49 VGPRs instead of 127;
-// round 4 rows per wave, C5 HOG 2-frame batches, per launch of 4 images: 32 252, 48 249,
-// 64 261, 96 265, 128 268 us; two rows per step with the LDS sums 248 -> 256 us.)
-constexpr int HS_ROWS = 48;
-
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_add(uint32_t v) {   // v + (lane shifted by CTRL, else 0)
-    return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
-}
-template <int CTRL, int ROWM>
-__device__ __forceinline__ uint32_t dpp_add_rm(uint32_t v) {
-    return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWM, 0xF, false);
-}
-
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-// Vertical-first (round 4): each lane first keeps the VERTICAL window sum V of its own column
-// (5 packed dwords) over a register ring of the last 2r+1 pixel CODES (bin << 8 | magnitude,
-// one VGPR each instead of 5 dwords of row sums: 127 -> ~60 VGPRs, twice the waves per SIMD
-// for a kernel that is latency-bound), and the horizontal window sum of V is taken across the
-// wave only for rows that emit (prefix by DPP, P(j + r) - P(j - r - 1) by two ds_bpermute), so
-// the 2r warm-up rows of a strip skip the scan.  Same sums, same records: bit-identical.
-__device__ __forceinline__ void hog_onehot(uint32_t code, uint32_t (&o)[5]) {
-    const uint32_t b = code >> 8;
-    const uint32_t w = (code & 0xFFu) << ((b & 1u) << 4);
-    const uint32_t sel = 1u << (b >> 1);
-#pragma unroll
-    for (int k = 0; k < 5; ++k) o[k] = w & (uint32_t)(((int)(sel << (31 - k))) >> 31);
-}
+// ---------------------------------------------------------------------------------------
+// HOG window histograms, column-run form (round 5): lane L owns K = 4 CONSECUTIVE columns, so the horizontal window sum is a running sum inside the lane over the
+// vertical sums of its K columns and the r columns either side, which belong to the HL =
+// ceil(r / K) neighbour lanes on each side (read from LDS) — instead of a 64-lane prefix scan
+// per row; lanes HL .. 63-HL emit, the HL lanes at each end are the halo.  Per step (one image
+// row) a lane loads the K + 2 bytes of the one new Sobel row, forms the K Sobel pairs as
+// packed u16 (S = a0 + 2a1 + a2, D = a2 - a0), the magnitudes packed, and each bin with 4
+// v_dot2 on the sign-normalised (gx, gy) pair (the 8 boundary tests of k_hog_hist folded
+// into 4: below).  Vertical window sums: 5 packed dwords per column in LDS, one ds_add /
+// ds_sub per code; the last 2r+1 codes per column in a register ring of
+// packed u16 (slot = step mod 2r+1 through s_set_gpr_idx, so the body is not unrolled 2r+1
+// times).  Records are staged in LDS and leave as coalesced 16-byte stores.
+// Bins: with (gx', gy') sign-normalised (gy' > 0, or gy' = 0 and gx' >= 0) and F_k =
+// cos_k gy' - sin_k |gx'|, k_hog_hist's b = sum_k [cos_k gy' >= sin_k gx'] + [-cos_k gy' >=
+// sin_k gx'] is 4 - #{F_k < 0} for gx' >= 0 and 8 - #{F_k > 0} for gx' < 0 (cos_k, sin_k > 0:
+// one of each pair of tests is decided by the sign of gx'), i.e. base - #{G_k < 0} with G_k =
+// dot2((gx', gx' < 0 ? -gy' : gy'), (-sin_k, cos_k)) — except for gx' = gy' = 0, where the
+// magnitude is 0 and the bin never matters.
+constexpr int HC_K = 4, HC_ROWS = 24;
+template <int r, int K>
+struct HogCr {
+    static constexpr int HL = (r + K - 1) / K;        // halo lanes per side (a window reaches HL lanes)
+    static constexpr int NOUT = (64 - 2 * HL) * K;     // columns a wave emits
+    static constexpr int NP = K / 2 + 1;               // packed byte pairs per image row and lane
+    static constexpr int NCH = (NOUT * 20 / 16 + 63) / 64;   // 16-byte chunks per lane and row
+};
 
-#ifndef SV_HOG_LV
-#define SV_HOG_LV 1
-#endif
-template <int r, int RP, bool LV = SV_HOG_LV>
-__global__ __launch_bounds__(64, RP == 1 ? 8 : 5) void k_hog_hist_vf(const uint8_t* __restrict__ g, int H, int W, int pitch,
-                                                       int row0, int row1, uint16_t* __restrict__ hist, int hs_rows,
-                                                       const uint8_t* __restrict__ g1, uint16_t* __restrict__ hist1,
-                                                       long long fs_in, long long fs_hist) {
+typedef short v2i16 __attribute__((ext_vector_type(2)));
+typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2u16 as_u2(uint32_t v) { return __builtin_bit_cast(v2u16, v); }
+__device__ __forceinline__ v2i16 as_i2(uint32_t v) { return __builtin_bit_cast(v2i16, v); }
+__device__ __forceinline__ uint32_t u2_as(v2u16 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t i2_as(v2i16 v) { return __builtin_bit_cast(uint32_t, v); }
+
+template <int r, int K>
+__global__ __launch_bounds__(64) void k_hog_hist_cr(const uint8_t* __restrict__ g, int H, int W, int pitch,
+                                                     int row0, int row1, uint16_t* __restrict__ hist, int hs_rows,
+                                                     const uint8_t* __restrict__ g1, uint16_t* __restrict__ hist1,
+                                                     long long fs_in, long long fs_hist) {
+    using C = HogCr<r, K>;
+    constexpr int HL = C::HL, NOUT = C::NOUT, NP = C::NP;
     if (blockIdx.z) {   // image pairs: z = 2 * frame + (0 left, 1 right)
         const int f = blockIdx.z >> 1;
         if (blockIdx.z & 1) {
@@ -493,135 +492,205 @@ __global__ __launch_bounds__(64, RP == 1 ? 8 : 5) void k_hog_hist_vf(const uint8
         g += f * fs_in;
         hist += f * fs_hist;
     }
-    constexpr int W2 = 2 * r + 1, NOUT = 64 - 2 * r;
+    constexpr int W2 = 2 * r + 1;
     const int lane = threadIdx.x;
     const int x0 = blockIdx.x * NOUT;
+    const int xs = x0 + (lane - HL) * K;   // this lane's first column (< 0 or >= W: halo / past the edge)
     const int ys = row0 + blockIdx.y * hs_rows;
     const int ye = min(ys + hs_rows, row1);
-    const int xx = clampi(x0 - r + lane, 0, W - 1);
-    const int xm = refl101(xx - 1, W), xp = refl101(xx + 1, W);
-    const int src_hi = (lane + r) << 2, src_lo = (lane - r - 1) << 2;
-    const uint32_t lo_mask = lane >= r + 1 ? ~0u : 0u;
-    const int xo = x0 + lane - r;
-    const bool out_lane = lane >= r && lane < 64 - r && xo < W;
-    const auto hdst = __builtin_amdgcn_make_buffer_rsrc(hist, 0, 0x7FFFFFFF, 0x00020000);
-    const int nbytes = 20 * min(NOUT, W - x0);
-    __shared__ __attribute__((aligned(16))) uint32_t stage[64 * 5 + 4];
+    const int nsteps = ye - ys + 2 * r;
     const auto gsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(g), 0, 0x7FFFFFFF, 0x00020000);
+    const auto hdst = __builtin_amdgcn_make_buffer_rsrc(hist, 0, 0x7FFFFFFF, 0x00020000);
 
-    uint32_t ring[W2], V[5];
+    // the K + 2 byte columns xs-1 .. xs+K: reflect-101 (the neighbours of columns 0 and W-1),
+    // then clamped (columns past the edge read something valid; their codes are replaced below)
+    int bcol[K + 2];
 #pragma unroll
-    for (int s2 = 0; s2 < W2; ++s2) ring[s2] = 0u;   // code 0 = bin 0, magnitude 0: adds nothing
+    for (int i = 0; i < K + 2; ++i) bcol[i] = clampi(refl101(xs - 1 + i, W), 0, W - 1);
+    auto load_row = [&](int row, int (&b)[K + 2]) {
 #pragma unroll
-    for (int k = 0; k < 5; ++k) V[k] = 0u;
-    // LV: the lane's 5 vertical sums live in LDS ([bin pair][lane]) and each code lands as ONE
-    // ds_add_u32 / ds_sub_u32 at its bin pair instead of a 5-dword one-hot add in VALU.
-    __shared__ uint32_t vsum[LV ? 5 * 64 : 1];
-    if constexpr (LV) {
+        for (int i = 0; i < K + 2; ++i) b[i] = (int)__builtin_amdgcn_raw_buffer_load_b8(gsrc, bcol[i], row * pitch, 0);
+    };
+    auto pack_row = [&](const int (&b)[K + 2], uint32_t (&p)[NP]) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) vsum[k * 64 + lane] = 0u;
+        for (int m = 0; m < NP; ++m) p[m] = (uint32_t)b[2 * m] | ((uint32_t)b[2 * m + 1] << 16);
+    };
+    auto crow = [&](int t) { return clampi(ys - r + t, 0, H - 1); };
+
+    // vertical window sums, [bin pair][column j][lane] (conflict-free: lane-consecutive)
+    __shared__ uint32_t vs[5 * K * 64];
+#pragma unroll
+    for (int i = 0; i < 5 * K; ++i) vs[i * 64 + lane] = 0u;
+
+    uint32_t R0[NP], R1[NP], R2[NP];
+    int nb[K + 2];
+    {
+        const int c = crow(0);
+        load_row(refl101(c - 1, H), nb);
+        pack_row(nb, R0);
+        load_row(c, nb);
+        pack_row(nb, R1);
+        load_row(refl101(c + 1, H), nb);
+        pack_row(nb, R2);
     }
 
-    const int nsteps = ye - ys + 2 * r;
-    auto load_step = [&](int t, int (&n)[8]) {
-        const int c = clampi(ys - r + t, 0, H - 1);
-        const int om = refl101(c - 1, H) * pitch, oc = c * pitch, op = refl101(c + 1, H) * pitch;
-        auto ldb = [&](int col, int row) { return (int)__builtin_amdgcn_raw_buffer_load_b8(gsrc, col, row, 0); };
-        n[0] = ldb(xm, om); n[1] = ldb(xx, om); n[2] = ldb(xp, om);
-        n[3] = ldb(xm, oc); n[4] = ldb(xp, oc);
-        n[5] = ldb(xm, op); n[6] = ldb(xx, op); n[7] = ldb(xp, op);
-    };
-    int nb[RP][8];
+    // the code ring: K/2 packed dwords (K u16 codes) per slot, slot = step mod 2r+1 (uniform:
+    // s_set_gpr_idx-relative moves, no per-slot copy of the loop body)
+    typedef uint32_t v16u __attribute__((ext_vector_type(16)));
+    v16u ring[K / 2];
 #pragma unroll
-    for (int rr = 0; rr < RP; ++rr) load_step(rr, nb[rr]);
-    for (int t0 = 0; t0 < nsteps; t0 += RP * W2) {
+    for (int q = 0; q < K / 2; ++q) ring[q] = (v16u)(0u);   // code 0: adds nothing
+
+    // a row's records (NOUT of them, contiguous in HBM) are staged in LDS and leave as 16-byte
+    // chunks over all 64 lanes: the same NCH + 3 stores per row on every path (a chunk past the
+    // row's end rewrites the last whole chunk's bytes, a tail dword past it the last dword's,
+    // both with the same values), so the next step's wait for its prefetched row counts them
+    // and never waits on them.  (Dropping such stores by an offset past num_records did not
+    // work: the stores landed 2 GB past the buffer.)
+    __shared__ __attribute__((aligned(16))) uint32_t stage[NOUT * 5];
+    const int nbytes = 20 * min(NOUT, W - x0);   // >= 20
+    const int last16 = (nbytes & ~15) - 16, tb = nbytes & ~15, owner = (tb >> 4) & 63;
+
+    const bool first_wave = x0 == 0;
+    const bool last_wave = x0 + (64 - HL) * K > W;   // some column of this wave is >= W
+    const int jw = (W - 1 - x0) % K, lw = (W - 1 - x0) / K + HL;   // column W-1: lane lw, j jw
+    uint32_t code[K];
+    int cprev = -1;
+    int slot = 0;
+    uint32_t Rn[NP];   // the packed row the next advancing step brings in
+    // one row of codes: Sobel, bins, the edge columns, the ring and the vertical sums
+    auto step = [&](int t) {
+        const int c = crow(t);
+        if (c != cprev) {   // uniform: a new Sobel centre row (clamped rows repeat the codes)
+            if (cprev >= 0) {
 #pragma unroll
-        for (int j = 0; j < W2; ++j) {
-            const int tb = t0 + RP * j;
-            if (tb >= nsteps) break;
-            uint32_t code[RP];
-#pragma unroll
-            for (int rr = 0; rr < RP; ++rr) {
-                const int a00 = nb[rr][0], a01 = nb[rr][1], a02 = nb[rr][2], a10 = nb[rr][3], a12 = nb[rr][4];
-                const int a20 = nb[rr][5], a21 = nb[rr][6], a22 = nb[rr][7];
-                load_step(tb + RP + rr, nb[rr]);
-                int gx = (a02 + 2 * a12 + a22) - (a00 + 2 * a10 + a20);
-                int gy = (a20 + 2 * a21 + a22) - (a00 + 2 * a01 + a02);
-                const uint32_t m = (uint32_t)(abs(gx) + abs(gy)) >> 3;
-                if (gy < 0 || (gy == 0 && gx < 0)) { gx = -gx; gy = -gy; }
-                int b = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int cy = kHogCos[k] * gy, sx = kHogSin[k] * gx;
-                    b += (cy >= sx) + (-cy >= sx);
+                for (int m = 0; m < NP; ++m) {
+                    R0[m] = R1[m];
+                    R1[m] = R2[m];
+                    R2[m] = Rn[m];
                 }
-                code[rr] = ((uint32_t)b << 8) | m;
+            }
+            cprev = c;
+            uint32_t S[NP], D[NP];
+#pragma unroll
+            for (int m = 0; m < NP; ++m) {
+                S[m] = u2_as(as_u2(R0[m]) + (as_u2(R1[m]) << (unsigned short)1) + as_u2(R2[m]));
+                D[m] = u2_as(as_u2(R2[m]) - as_u2(R0[m]));
             }
 #pragma unroll
-            for (int rr = 0; rr < RP; ++rr) {
-                const int t = tb + rr;
-                if (t >= nsteps) break;
-                const int slot = (RP * j + rr) % W2;      // = t mod W2 (t0 is a multiple of W2)
-                if constexpr (LV) {
-                    // code = bin << 8 | m: bin pair = code >> 9, half = bit 8 -> shift 16
-                    const uint32_t cn = code[rr], co = ring[slot];
-                    ring[slot] = cn;
-                    __hip_atomic_fetch_add(&vsum[(cn >> 9) * 64 + lane], (cn & 0xFFu) << ((cn >> 4) & 16u),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                    __hip_atomic_fetch_sub(&vsum[(co >> 9) * 64 + lane], (co & 0xFFu) << ((co >> 4) & 16u),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                    if (t < 2 * r) continue;
+            for (int q = 0; q < K / 2; ++q) {
+                const v2i16 gx = as_i2(u2_as(as_u2(S[q + 1]) - as_u2(S[q])));
+                const uint32_t dmid = __builtin_amdgcn_alignbyte(D[q + 1], D[q], 2);   // (D[2q+1], D[2q+2])
+                const v2i16 gy = as_i2(u2_as(as_u2(D[q]) + (as_u2(dmid) << (unsigned short)1) + as_u2(D[q + 1])));
+                const v2i16 ax = __builtin_elementwise_max(gx, -gx), ay = __builtin_elementwise_max(gy, -gy);
+                const uint32_t mm = u2_as((as_u2(i2_as(ax)) + as_u2(i2_as(ay))) >> (unsigned short)3);
 #pragma unroll
-                    for (int k = 0; k < 5; ++k) V[k] = vsum[k * 64 + lane];
-                } else {
-                    uint32_t on[5], of[5];
-                    hog_onehot(code[rr], on);
-                    hog_onehot(ring[slot], of);
-                    ring[slot] = code[rr];
+                for (int h = 0; h < 2; ++h) {
+                    // p = (gy << 16) | gx, then sign-normalised: flip iff (gy, gx) < (0, 0)
+                    const uint32_t p = __builtin_amdgcn_perm(i2_as(gy), i2_as(gx), h ? 0x07060302u : 0x05040100u);
+                    const int vkey = (int)p - (int)((p & 0x8000u) << 1);   // gy * 65536 + gx
+                    const uint32_t fm = (uint32_t)(vkey >> 31);
+                    const uint32_t pn = u2_as(as_u2(p ^ fm) - as_u2(fm));
+                    const uint32_t gm = (uint32_t)((int)(pn << 16) >> 31);    // gx' < 0
+                    const uint32_t hm = gm & 0xFFFF0000u;
+                    const v2i16 qv = as_i2(u2_as(as_u2(pn ^ hm) - as_u2(hm)));
+                    uint32_t nneg = 0;
 #pragma unroll
-                    for (int k = 0; k < 5; ++k) V[k] = V[k] + on[k] - of[k];
-                    if (t < 2 * r) continue;   // uniform: warm-up rows only fill the vertical window
-                }
-                // horizontal window of V across the wave: inclusive prefix (row_shr 1, 2, 4, 8,
-                // row_bcast 15 / 31), then P(j + r) - P(j - r - 1)
-                uint32_t pf[5];
-#pragma unroll
-                for (int k = 0; k < 5; ++k) pf[k] = V[k];
-#define SV_HOG_SCAN(F) _Pragma("unroll") for (int k = 0; k < 5; ++k) pf[k] = F(pf[k]);
-                SV_HOG_SCAN(dpp_add<0x111>)
-                SV_HOG_SCAN(dpp_add<0x112>)
-                SV_HOG_SCAN(dpp_add<0x114>)
-                SV_HOG_SCAN(dpp_add<0x118>)
-                SV_HOG_SCAN((dpp_add_rm<0x142, 0xA>))
-                SV_HOG_SCAN((dpp_add_rm<0x143, 0xC>))
-#undef SV_HOG_SCAN
-                uint32_t hv[5];
-#pragma unroll
-                for (int k = 0; k < 5; ++k) {
-                    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_hi, (int)pf[k]);
-                    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lo, (int)pf[k]);
-                    hv[k] = hi - (lo & lo_mask);
-                }
-                const int rs = (ys + t - 2 * r) * W * 20 + x0 * 20;
-                const int ra = rs & 15, ro = rs - ra;
-                if (out_lane)
-#pragma unroll
-                    for (int k = 0; k < 5; ++k) stage[(ra >> 2) + (lane - r) * 5 + k] = hv[k];
-                __syncthreads();   // (one wave: orders the staging, fences the compiler)
-                const int e = ra + nbytes;
-                for (int b0 = 16 * lane; b0 < e; b0 += 16 * 64) {
-                    const int b1 = b0 + 16;
-                    if (b0 >= ra && b1 <= e) {
-                        const v4u q = *reinterpret_cast<const v4u*>(stage + (b0 >> 2));
-                        __builtin_amdgcn_raw_buffer_store_b128(q, hdst, b0, ro, 0);
-                    } else if (b1 > ra) {
-                        for (int o = max(b0, ra); o < min(b1, e); o += 4)
-                            __builtin_amdgcn_raw_buffer_store_b32(stage[o >> 2], hdst, o, ro, 0);
+                    for (int k = 0; k < 4; ++k) {
+                        const v2i16 w = {(short)-kHogSin[k], (short)kHogCos[k]};
+                        nneg += (uint32_t)__builtin_amdgcn_sdot2(qv, w, 0, false) >> 31;
                     }
+                    const uint32_t b = 4u + (gm & 4u) - nneg;
+                    const uint32_t m = h ? mm >> 16 : mm & 0xFFFFu;
+                    code[2 * q + h] = (b << 8) | m;
                 }
-                __syncthreads();
+            }
+            // columns past the image edge take the edge column's code (clamped positions)
+            if (first_wave) {
+                const uint32_t c0 = __builtin_amdgcn_readlane(code[0], HL);
+                if (lane < HL)
+#pragma unroll
+                    for (int j = 0; j < K; ++j) code[j] = c0;
+            }
+            if (last_wave) {
+                uint32_t cw = code[0];
+#pragma unroll
+                for (int j = 1; j < K; ++j) cw = jw == j ? code[j] : cw;
+                const uint32_t cwb = __builtin_amdgcn_readlane(cw, lw);
+#pragma unroll
+                for (int j = 0; j < K; ++j) code[j] = xs + j >= W ? cwb : code[j];
             }
         }
+#pragma unroll
+        for (int q = 0; q < K / 2; ++q) {
+            const uint32_t nc = code[2 * q] | (code[2 * q + 1] << 16), oc = ring[q][slot];
+            ring[q][slot] = nc;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int j = 2 * q + h;
+                const uint32_t cn = code[j], co = h ? oc >> 16 : oc & 0xFFFFu;
+                __hip_atomic_fetch_add(&vs[((cn >> 9) * K + j) * 64 + lane], (cn & 0xFFu) << ((cn >> 4) & 16u),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                __hip_atomic_fetch_sub(&vs[((co >> 9) * K + j) * 64 + lane], (co & 0xFFu) << ((co >> 4) & 16u),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            }
+        }
+        slot = slot + 1 == W2 ? 0 : slot + 1;
+    };
+    // each iteration loads the row step t + 1 brings in if it advances (unconditionally, at its
+    // top) and packs it at its end, after the stores: no loaded register lives across the
+    // back edge (a copy there would wait for the load), and the wait counts the stores
+    auto prefetch = [&](int t) { load_row(refl101(crow(min(t + 1, nsteps - 1)) + 1, H), nb); };
+    for (int t = 0; t < 2 * r && t < nsteps; ++t) {   // warm-up: the vertical window only
+        prefetch(t);
+        step(t);
+        pack_row(nb, Rn);
+    }
+    const bool own = lane >= HL && lane < 64 - HL;
+    uint32_t* srec = &stage[(own ? lane - HL : 0) * 5 * K];
+    for (int t = 2 * r; t < nsteps; ++t) {
+        prefetch(t);
+        step(t);
+        // horizontal window: a running sum over columns -r .. K-1+r, the outer ones the
+        // neighbour lanes' vertical sums (read from LDS; LDS ops of a wave complete in order);
+        // each plane's K sums go straight to the row's staging area
+#pragma unroll
+        for (int p = 0; p < 5; ++p) {
+            uint32_t v[K + 2 * r];
+#pragma unroll
+            for (int i = 0; i < K + 2 * r; ++i) {
+                const int col = i - r;
+                const int dl = col >= 0 ? col / K : -((K - 1 - col) / K);   // source lane offset
+                const int sl = min(max(lane + dl, 0), 63);
+                v[i] = vs[(p * K + (col - dl * K)) * 64 + sl];
+            }
+            uint32_t h = v[0];
+#pragma unroll
+            for (int i = 1; i <= 2 * r; ++i) h += v[i];
+            if (own) srec[p] = h;
+#pragma unroll
+            for (int j = 1; j < K; ++j) {
+                h += v[j + 2 * r] - v[j - 1];
+                if (own) srec[5 * j + p] = h;
+            }
+        }
+        __syncthreads();   // (one wave: orders the staging, fences the compiler)
+        const int soff = ((ys + t - 2 * r) * W + x0) * 20;
+#pragma unroll
+        for (int k = 0; k < C::NCH; ++k) {
+            int b0 = 16 * (lane + 64 * k);
+            b0 = b0 + 16 <= nbytes ? b0 : last16;
+            const v4u q = *reinterpret_cast<const v4u*>(&stage[b0 >> 2]);
+            __builtin_amdgcn_raw_buffer_store_b128(q, hdst, b0, soff, 0);
+        }
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {   // the tail chunk (nbytes is a multiple of 4, not always of 16)
+            int o = tb + 4 * d;
+            o = lane == owner && o < nbytes ? o : nbytes - 4;
+            __builtin_amdgcn_raw_buffer_store_b32(stage[o >> 2], hdst, o, soff, 0);
+        }
+        pack_row(nb, Rn);
+        __syncthreads();
     }
 }
 
@@ -1094,14 +1163,29 @@ int launch_harris(const uint8_t* g, int H, int W, int pitch, float* out, hipStre
     return (int)hipGetLastError();
 }
 
-// rows per strip wave (SV_HOG_ROWS: A/B)
-static int hog_strip_rows() {
-    static const int v = [] {
-        const char* e = std::getenv("SV_HOG_ROWS");
+// The column-run kernel over nz images (nz = 1: g0 / h0; else z = 2 * frame + side).
+// SV_HOG_CR_ROWS: rows per strip wave (A/B; 24 by default: 4K, 4 images per launch, 16 / 24 /
+// 32 / 48 rows measured 1,552 / 1,572 / 1,564 / 1,558 C5 HOG frames/s).
+static int launch_hog_strips(const uint8_t* g0, const uint8_t* g1, int H, int W, int pitch, int r, int row0,
+                             int row1, uint16_t* h0, uint16_t* h1, int nz, long long fs_in, long long fs_hist,
+                             hipStream_t s) {
+    static const int hc_rows = [] {
+        const char* e = std::getenv("SV_HOG_CR_ROWS");
         const int x = e ? std::atoi(e) : 0;
-        return x >= 8 && x <= 4096 ? x : HS_ROWS;
+        return x >= 4 && x <= 4096 ? x : HC_ROWS;
     }();
-    return v;
+    switch (r) {
+#define SV_HOG_C(R)                                                                                              \
+    case R: {                                                                                                   \
+        constexpr int NOUT = HogCr<R, HC_K>::NOUT;                                                              \
+        const dim3 grid((W + NOUT - 1) / NOUT, (row1 - row0 + hc_rows - 1) / hc_rows, nz);                      \
+        hipLaunchKernelGGL((k_hog_hist_cr<R, HC_K>), grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0,     \
+                           hc_rows, g1, h1, fs_in, fs_hist);                                                    \
+    } break;
+        SV_HOG_C(0) SV_HOG_C(1) SV_HOG_C(2) SV_HOG_C(3) SV_HOG_C(4) SV_HOG_C(5) SV_HOG_C(6) SV_HOG_C(7)
+#undef SV_HOG_C
+    }
+    return (int)hipGetLastError();
 }
 
 int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0, int row1,
@@ -1115,16 +1199,9 @@ int launch_hog_hist(const uint8_t* g, int H, int W, int pitch, int win, int row0
         const char* e = std::getenv("SV_HOG_STRIP");
         return e ? std::atoi(e) : 1;
     }();
-    // (the strip kernel addresses through 32-bit buffer offsets)
-    if (strip && (long long)H * W * 20 < (1LL << 31) && (long long)H * pitch < (1LL << 31)) {
-        const int hs_rows = hog_strip_rows();
-        const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + hs_rows - 1) / hs_rows);
-        switch (r) {
-#define SV_HOG_S(R) case R: hipLaunchKernelGGL((k_hog_hist_vf<R, 1>), grid, dim3(64), 0, s, g, H, W, pitch, row0, row1, hist, hs_rows, g, hist, 0LL, 0LL); break;
-            SV_HOG_S(0) SV_HOG_S(1) SV_HOG_S(2) SV_HOG_S(3) SV_HOG_S(4) SV_HOG_S(5) SV_HOG_S(6) SV_HOG_S(7)
-#undef SV_HOG_S
-        }
-        return (int)hipGetLastError();
+    // (the strip kernels address through 32-bit buffer offsets, stores below 0x7FFFFFF0)
+    if (strip && (long long)H * W * 20 < (1LL << 31) - (1LL << 20) && (long long)H * pitch < (1LL << 31)) {
+        return launch_hog_strips(g, g, H, W, pitch, r, row0, row1, hist, hist, 1, 0, 0, s);
     }
     const dim3 grid((W + GT_W - 1) / GT_W, (row1 - row0 + GT_H - 1) / GT_H);
     switch (r) {
@@ -1147,7 +1224,7 @@ int launch_hog_hist_pairs(const uint8_t* g0, const uint8_t* g1, int H, int W, in
         const char* e = std::getenv("SV_HOG_STRIP");
         return e ? std::atoi(e) : 1;
     }();
-    if (!(strip && (long long)H * W * 20 < (1LL << 31) && (long long)H * pitch < (1LL << 31))) {
+    if (!(strip && (long long)H * W * 20 < (1LL << 31) - (1LL << 20) && (long long)H * pitch < (1LL << 31))) {
         for (int z = 0; z < nf; ++z) {   // the tile kernel: image by image
             int e = launch_hog_hist(g0 + z * fs_in, H, W, pitch, win, row0, row1, h0 + z * fs_hist, s);
             if (!e) e = launch_hog_hist(g1 + z * fs_in, H, W, pitch, win, row0, row1, h1 + z * fs_hist, s);
@@ -1155,14 +1232,7 @@ int launch_hog_hist_pairs(const uint8_t* g0, const uint8_t* g1, int H, int W, in
         }
         return 0;
     }
-    const int hs_rows = hog_strip_rows();
-    const dim3 grid((W + 64 - 2 * r - 1) / (64 - 2 * r), (row1 - row0 + hs_rows - 1) / hs_rows, 2 * nf);
-    switch (r) {
-#define SV_HOG_P(R) case R: hipLaunchKernelGGL((k_hog_hist_vf<R, 1>), grid, dim3(64), 0, s, g0, H, W, pitch, row0, row1, h0, hs_rows, g1, h1, fs_in, fs_hist); break;
-        SV_HOG_P(0) SV_HOG_P(1) SV_HOG_P(2) SV_HOG_P(3) SV_HOG_P(4) SV_HOG_P(5) SV_HOG_P(6) SV_HOG_P(7)
-#undef SV_HOG_P
-    }
-    return (int)hipGetLastError();
+    return launch_hog_strips(g0, g1, H, W, pitch, r, row0, row1, h0, h1, 2 * nf, fs_in, fs_hist, s);
 }
 
 int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float* disp,

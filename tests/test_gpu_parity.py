@@ -140,10 +140,13 @@ def test_hog_hist_matches_oracle(engine, win):
 
 
 @pytest.mark.parametrize("H,W,win", [(1, 1, 3), (2, 70, 15), (150, 211, 15), (131, 64, 13), (97, 130, 5),
-                                     (70, 51, 1), (65, 300, 7)])
+                                     (70, 51, 1), (65, 300, 7), (40, 1000, 15), (37, 993, 9), (70, 497, 3),
+                                     (33, 1489, 7), (5, 2000, 1), (66, 1100, 11), (9, 496, 15), (3, 504, 13),
+                                     (11, 241, 15), (12, 481, 11), (13, 249, 9), (7, 248, 5), (8, 257, 1)])
 def test_hog_hist_strip_shapes(engine, H, W, win):
-    """The strip kernel: 64-lane column strips with 2r-column overlaps, 64-row strips,
-    images narrower than a strip or than the window, 1-pixel images (reflect-101 of size 1)."""
+    """The column-run kernel: waves of 240 / 248 / 256 columns (4 columns per lane, 2 / 1 / 0
+    halo lanes a side), 24-row strips, images narrower than a wave or than the window, widths
+    one past a wave / ending in a halo lane, 1-pixel images (reflect-101 of size 1)."""
     rng = np.random.default_rng(H * 1000 + W + win)
     g = rng.integers(0, 256, (H, W), dtype=np.uint8)
     g[:, ::7] = 255                      # strong edges: large magnitudes in every bin

@@ -729,8 +729,8 @@ def test_two_parameter_sets_alternating_on_two_streams(engine):
 
 
 def test_hog_band_only_inputs_both_histogram_kernels():
-    """band-only inputs with cost=HOG through both histogram kernels (the strip
-    form and the 64x16 tile form, SV_HOG_STRIP=0, each in a child): a band buffer holds only
+    """band-only inputs with cost=HOG through both histogram kernels (the
+    column-run form and the 64x16 tile form, SV_HOG_STRIP=0, each in a child): a band buffer holds only
     the input rows [in0, in1) plus SV_BAND_MARGIN poisoned rows either side, the band's last
     16-row tile starts at its last disparity row ((h1 - h0 - 1) % 16 == 0 for rank 1), and the
     band's disparity rows equal the full-frame oracle's."""

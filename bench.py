@@ -732,10 +732,13 @@ def main():
     disp = [a.alloc(4 * n_px * out_frames) for a in arenas]
     norm = [a.alloc(n_px * out_frames) for a in arenas]
     # --streams S: S-1 extra contexts per GPU (own stream, own outputs) that steps alternate over
-    # default: 3 streams for frames <= 1 MP (launch-bound); 2 for HOG (the histogram kernel,
-    # write-bound, overlaps the VALU-bound match of the other stream's frames: C5 HOG
-    # 1,564 -> 1,637 frames/s, profiles/r05t); 1 otherwise
-    req_streams = args.streams if args.streams > 0 else (3 if n_px <= 1_000_000 else 2 if args.cost == "hog" else 1)
+    # default: 3 streams for frames <= 1 MP (launch-bound); 2 for HOG and for 4K frames (the
+    # write-bound histograms / the median of one stream's batch beside the VALU-bound match of
+    # the other's: C5 HOG 1,564 -> 1,637-1,651, C5 SAD 2,920 -> 3,035 frames/s,
+    # profiles/r05h_hog); 1 otherwise (1080p SAD: 2 streams +2.0%, 2 x 8-frame batches +2.9%,
+    # left at one stream so the roofline's launch times stay those of a launch alone)
+    req_streams = args.streams if args.streams > 0 else (
+        3 if n_px <= 1_000_000 else 2 if (args.cost == "hog" or n_px >= 4_000_000) else 1)
     nstreams = max(1, req_streams) if not (rowtile or args.rectify or gather_on) else 1
     lanes = [(engines, depth, disp, norm)]
     for _ in range(nstreams - 1):

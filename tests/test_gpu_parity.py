@@ -153,6 +153,35 @@ def test_hog_hist_strip_shapes(engine, H, W, win):
     np.testing.assert_array_equal(engine.hog_hist(g, win), O.hog_hist(g, win))
 
 
+@pytest.mark.parametrize("win", [1, 3, 5, 7, 9, 11, 13, 15])
+def test_hog_hist_dev_row_bands_every_radius(engine, win):
+    """sv_hog_hist_dev over row bands [row0, row1) at every radius (0..7: 0, 1 and 2 halo
+    lanes a side), an image 2.5 waves wide with a pitch > W: the band's rows bit-exact, the
+    rows outside it untouched (sentinel)."""
+    H, W, pitch = 75, 600, 616
+    rng = np.random.default_rng(win)
+    g = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    g[:, ::11] = 255
+    img = np.zeros((H, pitch), np.uint8)
+    img[:, :W] = g
+    exp = O.hog_hist(g, win)                                   # [9, H, W]
+    dimg = engine.dev_alloc(img.nbytes)
+    dout = engine.dev_alloc(H * W * 20)
+    try:
+        engine.to_device(dimg, img)
+        for row0, row1 in ((0, H), (17, 53), (74, 75), (0, 1)):
+            engine.to_device(dout, np.full((H, W, 10), 0xBEEF, np.uint16))
+            engine.hog_hist_dev(dimg, H, W, pitch, win, row0, row1, dout)
+            engine.synchronize()
+            got = engine.to_host(dout, (H, W, 10), np.uint16)
+            np.testing.assert_array_equal(got[row0:row1, :, :9].transpose(2, 0, 1), exp[:, row0:row1])
+            assert (got[row0:row1, :, 9] == 0).all()              # the pad bin
+            assert (got[:row0] == 0xBEEF).all() and (got[row1:] == 0xBEEF).all()
+    finally:
+        engine.dev_free(dimg)
+        engine.dev_free(dout)
+
+
 def test_harris_within_tolerance(engine):
     for H, W, seed in [(50, 70, 0), (1, 40, 1), (17, 1, 2), (128, 300, 3)]:
         rng = np.random.default_rng(seed)

@@ -101,3 +101,31 @@ def test_random_scaled_path_matches_numpy_oracle(engine, seed):
     np.testing.assert_array_equal(dn, e_dn, err_msg=f"seed {seed}")
     np.testing.assert_array_equal(du, e_du, err_msg=f"seed {seed}")
     np.testing.assert_array_equal(cf, e_cf, err_msg=f"seed {seed}")
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_hog_hist_bands_match_oracle(engine, seed):
+    """The HOG window histograms alone over random sizes (one pixel to ~3 column-run waves),
+    windows, pitches, textures and row bands [row0, row1), against the NumPy oracle."""
+    rng = np.random.default_rng(5000 + seed)
+    win = int(rng.choice([1, 3, 5, 7, 9, 11, 13, 15]))
+    H = int(rng.choice([1, 2, 3, 9, 24, 25, 49, 70]))
+    W = int(rng.choice([1, 5, 63, 239, 240, 241, 248, 256, 481, 700]))
+    pitch = W + int(rng.integers(0, 9))
+    g = _texture(rng, H, W, int(rng.integers(0, 4)))
+    row0 = int(rng.integers(0, H))
+    row1 = int(rng.integers(row0 + 1, H + 1))
+    img = np.zeros((H, pitch), np.uint8)
+    img[:, :W] = g
+    dimg, dout = engine.dev_alloc(img.nbytes), engine.dev_alloc(H * W * 20)
+    try:
+        engine.to_device(dimg, img)
+        engine.hog_hist_dev(dimg, H, W, pitch, win, row0, row1, dout)
+        engine.synchronize()
+        got = engine.to_host(dout, (H, W, 10), np.uint16)[row0:row1]
+    finally:
+        engine.dev_free(dimg)
+        engine.dev_free(dout)
+    exp = O.hog_hist(g, win)[:, row0:row1]
+    np.testing.assert_array_equal(got[:, :, :9].transpose(2, 0, 1), exp, err_msg=f"{H}x{W} p{pitch} win {win} rows {row0}:{row1}")
+    assert (got[:, :, 9] == 0).all()

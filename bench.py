@@ -591,10 +591,10 @@ def parse_args(argv=None):
     ap.add_argument("--batch", type=int, default=None,
                     help="frames mode: frames per step and GPU, one launch per kernel over the "
                          "batch (sv_depth_map_batch_dev); 1 = one frame per call (latency mode). "
-                         "Default 16; 26 for the metric config, whose k_match grid is 1,890 waves "
-                         "per frame: 26 frames = 49,140 waves = 24.0 rounds of the 2,048 wave "
-                         "slots (16 frames = 14.8 rounds, a last round 77%% full): +0.9%% frames/s "
-                         "(profiles/r05ag)")
+                         "Default 16; 26 for 1920x1080 (not SGBM): the metric config's k_match grid "
+                         "is 1,890 waves per frame, 26 frames = 49,140 waves = 24.0 rounds of the "
+                         "2,048 wave slots (16 frames = 14.8 rounds, a last round 77%% full): +0.9%% "
+                         "frames/s, C3 (win 11) +1.1%% (profiles/r05ag, r05ai)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed loop")
@@ -655,9 +655,9 @@ def parse_args(argv=None):
                          "than this many seconds (a rank stuck in a collective fails loudly)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
-    if args.batch is None:
-        metric_cfg = (args.height, args.width, args.num_disp, args.win, args.cost) == (1080, 1920, 128, 9, "sad")
-        args.batch = 26 if metric_cfg and args.mode == "frames" else 16
+    if args.batch is None:   # 1080p frames: 26 (whole rounds of k_match waves; C3 win 11 +1.1% too)
+        full_hd = (args.height, args.width) == (1080, 1920) and args.cost != "sgbm"
+        args.batch = 26 if full_hd and args.mode == "frames" else 16
     if args.frames is None:
         args.frames = args.batch
     if args.pmc_child:

@@ -36,6 +36,19 @@ def test_gather_is_the_default_for_multi_gpu_frames():
     assert not bench.parse_args([]).no_verify
 
 
+def test_default_batch_fills_whole_wave_rounds_at_1080p():
+    """26-frame steps at 1920x1080 (the metric config's k_match grid: 24.0 rounds of the wave
+    slots), 16 elsewhere and for SGBM / row tiling; an explicit batch or frame count wins."""
+    assert (bench.parse_args([]).batch, bench.parse_args([]).frames) == (26, 26)
+    assert bench.parse_args(["--win", "11"]).batch == 26
+    assert bench.parse_args(["--height", "480", "--width", "640", "--num-disp", "64"]).batch == 16
+    assert bench.parse_args(["--cost", "sgbm"]).batch == 16
+    assert bench.parse_args(["--mode", "rowtile"]).batch == 16
+    a = bench.parse_args(["--batch", "8"])
+    assert (a.batch, a.frames) == (8, 8)
+    assert bench.parse_args(["--frames", "4"]).frames == 4
+
+
 def _dist_worker(rank, world, path, q):
     os.environ.update({"WORLD_SIZE": str(world), "RANK": str(rank), "LOCAL_RANK": str(rank),
                        "SV_RDZV_DIR": path})

@@ -442,17 +442,19 @@ __global__ __launch_bounds__(256) void k_hog_hist(const uint8_t* __restrict__ g,
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------------------
-// HOG window histograms, column-run form (round 5): lane L owns K = 4 CONSECUTIVE columns, so the horizontal window sum is a running sum inside the lane over the
-// vertical sums of its K columns and the r columns either side, which belong to the HL =
-// ceil(r / K) neighbour lanes on each side (read from LDS) — instead of a 64-lane prefix scan
-// per row; lanes HL .. 63-HL emit, the HL lanes at each end are the halo.  Per step (one image
-// row) a lane loads the K + 2 bytes of the one new Sobel row, forms the K Sobel pairs as
-// packed u16 (S = a0 + 2a1 + a2, D = a2 - a0), the magnitudes packed, and each bin with 4
-// v_dot2 on the sign-normalised (gx, gy) pair (the 8 boundary tests of k_hog_hist folded
-// into 4: below).  Vertical window sums: 5 packed dwords per column in LDS, one ds_add /
-// ds_sub per code; the last 2r+1 codes per column in a register ring of
-// packed u16 (slot = step mod 2r+1 through s_set_gpr_idx, so the body is not unrolled 2r+1
-// times).  Records are staged in LDS and leave as coalesced 16-byte stores.
+// HOG window histograms, column-run form (round 5): lane L owns K = 4 CONSECUTIVE columns,
+// so the horizontal window sum is a running sum inside the lane over the vertical sums of its
+// K columns and of the r columns either side, which belong to the HL = ceil(r / K) neighbour
+// lanes on each side (read from LDS) — instead of a 64-lane prefix scan per row; lanes
+// HL .. 63-HL emit, the HL lanes at each end are the halo.  Per step (one image row) a lane
+// loads the K + 2 bytes of the one new Sobel row, forms the K Sobel pairs as packed u16
+// (S = a0 + 2a1 + a2, D = a2 - a0), the magnitudes packed, and each bin with 4 v_dot2 on the
+// sign-normalised (gx, gy) pair (the 8 boundary tests of k_hog_hist folded into 4: below).
+// Vertical window sums: 5 packed dwords per column in LDS, one ds_add / ds_sub per code; the
+// last 2r+1 codes per column in a register ring of packed u16 (slot = step mod 2r+1 through
+// s_set_gpr_idx, so the body is not unrolled 2r+1 times).  Records are staged in LDS and
+// leave as coalesced 16-byte stores.  118 VGPRs and 9.9 KB of LDS at r = 7 (4 waves per
+// SIMD); 4K r = 7, 4 images per launch: 205 us (round 4's 64-lane strips: 249).
 // Bins: with (gx', gy') sign-normalised (gy' > 0, or gy' = 0 and gx' >= 0) and F_k =
 // cos_k gy' - sin_k |gx'|, k_hog_hist's b = sum_k [cos_k gy' >= sin_k gx'] + [-cos_k gy' >=
 // sin_k gx'] is 4 - #{F_k < 0} for gx' >= 0 and 8 - #{F_k > 0} for gx' < 0 (cos_k, sin_k > 0:

@@ -1016,8 +1016,11 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
         mp[h + 2] = (a0 >> 16) | (a1 & 0xFFFF0000u);
     }
     // park the medians in LDS, then re-read them as 4 consecutive columns of one row per
-    // thread so the outputs leave as 16-byte (f32) and 4-byte (u8) stores
-    __shared__ __attribute__((aligned(8))) uint32_t med[MQ_H][MQ_W / 2];
+    // thread so the outputs leave as 16-byte (f32) and 4-byte (u8) stores.  med aliases srt
+    // (every wave has read its ranks by the barrier): 17.9 KB of LDS, 8 blocks per CU
+    static_assert(sizeof(srt) >= MQ_H * (MQ_W / 2) * sizeof(uint32_t), "med must fit in srt");
+    auto med = reinterpret_cast<uint32_t (*)[MQ_W / 2]>(&srt[0][0][0]);
+    __syncthreads();
     med[tb][tx >> 1] = mp[0];
     med[tb + 1][tx >> 1] = mp[1];
     med[tb + 2][tx >> 1] = mp[2];

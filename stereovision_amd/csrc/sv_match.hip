@@ -259,6 +259,31 @@ __device__ __forceinline__ void transpose4(uint32_t a, uint32_t b, uint32_t c, u
     o[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
 }
 
+// 4-row kind: the pack words of 4 columns from their 2r+4 window rows (one dword = the 4
+// columns of a row, rows y-r .. y+r+3); same layout as build_pack.
+template <int R>
+__device__ __forceinline__ void sad4_group_words(const uint32_t (&rw)[2 * R + 4],
+                                                 uint32_t (&w)[PackCfg<COST_SAD4, R>::NW][4]) {
+    constexpr int NC = PackCfg<COST_SAD4, R>::NW - 4, NCR = 2 * R - 2;
+#pragma unroll
+    for (int m = 0; m < NC; ++m) {
+        uint32_t d[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) d[t] = 4 * m + t < NCR ? rw[3 + 4 * m + t] : 0u;
+        transpose4(d[0], d[1], d[2], d[3], w[m]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t d[3];
+        int n = 0;
+#pragma unroll
+        for (int j = q; j <= 2; ++j) d[n++] = rw[j];
+#pragma unroll
+        for (int j = 2 * R + 1; j <= 2 * R + q; ++j) d[n++] = rw[j];
+        transpose4(d[0], d[1], d[2], 0u, w[NC + q]);
+    }
+}
+
 // Pack words of the 4 columns cg..cg+3 (all inside [0, W), 4-byte aligned rows) around
 // output row y; same layout as build_pack.
 template <int COST, int ND>
@@ -270,27 +295,10 @@ __device__ __forceinline__ void build_group(const MatchParams& a, const uint8_t*
         return *reinterpret_cast<const uint32_t*>(img + (size_t)yy * a.pitch + cg);
     };
     if constexpr (COST == COST_SAD4) {
-        constexpr int R = ND, NC = PackCfg<COST, ND>::NW - 4, NCR = 2 * R - 2;
-        uint32_t rw[2 * R + 4];
+        uint32_t rw[2 * ND + 4];
 #pragma unroll
-        for (int j = 0; j < 2 * R + 4; ++j) rw[j] = row(j);
-#pragma unroll
-        for (int m = 0; m < NC; ++m) {
-            uint32_t d[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) d[t] = 4 * m + t < NCR ? rw[3 + 4 * m + t] : 0u;
-            transpose4(d[0], d[1], d[2], d[3], w[m]);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t d[3];
-            int n = 0;
-#pragma unroll
-            for (int j = q; j <= 2; ++j) d[n++] = rw[j];
-#pragma unroll
-            for (int j = 2 * R + 1; j <= 2 * R + q; ++j) d[n++] = rw[j];
-            transpose4(d[0], d[1], d[2], 0u, w[NC + q]);
-        }
+        for (int j = 0; j < 2 * ND + 4; ++j) rw[j] = row(j);
+        sad4_group_words<ND>(rw, w);
         return;
     }
     const int nsh = a.win;                                   // transposed rows
@@ -365,6 +373,73 @@ __device__ __forceinline__ void build_all_packs(const MatchParams& a, int y, int
             }
         }
     }
+    }
+}
+
+// The ring kind's packs (4-row kind, radius R): as build_all_packs, but each lane issues
+// the row loads of up to MF of its 4-column groups before it transposes any of them, so a
+// wave waits for its global loads once per MF groups instead of once per group (the
+// per-group form left ~8% of k_match's time in the segment prologue).  Groups touching the
+// image border load from column 0 (unused) and take build_pack afterwards.
+template <int R, int MF, int DPL>
+__device__ __forceinline__ void build_ring_packs(const MatchParams& a, int y, int cL0, int NL, int cR0,
+                                                 int NRlog, int c0, PackOut<COST_SAD4, R> Lp,
+                                                 PackOut<COST_SAD4, R> Rp, int lane) {
+    constexpr int NW = PackCfg<COST_SAD4, R>::NW, NRW = 2 * R + 4;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(a.L) | reinterpret_cast<uintptr_t>(a.R) |
+                           (uintptr_t)a.pitch) & 3u) == 0;
+    if (!aligned) {
+        build_all_packs<COST_SAD4, R, DPL>(a, y, cL0, NL, cR0, NRlog, c0, Lp, Rp, lane);
+        return;
+    }
+    const int aL = cL0 & ~3, aR = cR0 & ~3;                  // floor to a multiple of 4
+    const int gL = (cL0 + NL - aL + 3) >> 2, gR = (cR0 + NRlog - aR + 3) >> 2;
+    const int G = gL + gR;
+    uint32_t roff[NRW];                                      // row offsets (wave-uniform)
+#pragma unroll
+    for (int j = 0; j < NRW; ++j) roff[j] = (uint32_t)clampi(y - R + j, 0, a.H - 1) * (uint32_t)a.pitch;
+    for (int g0 = 0; g0 < G; g0 += 64 * MF) {
+        uint32_t rw[MF][NRW];
+#pragma unroll
+        for (int m = 0; m < MF; ++m) {
+            const int gi = g0 + lane + 64 * m;
+            const bool right = gi >= gL;
+            const int cg = right ? aR + 4 * (gi - gL) : aL + 4 * gi;
+            const bool in = gi < G && cg >= 0 && cg + 4 <= a.W;
+            const uint8_t* img = (right ? a.R : a.L) + (in ? cg : 0);
+#pragma unroll
+            for (int j = 0; j < NRW; ++j) rw[m][j] = *reinterpret_cast<const uint32_t*>(img + roff[j]);
+        }
+#pragma unroll
+        for (int m = 0; m < MF; ++m) {
+            const int gi = g0 + lane + 64 * m;
+            if (gi >= G) continue;
+            const bool right = gi >= gL;
+            const int cg = right ? aR + 4 * (gi - gL) : aL + 4 * gi;
+            const int cfirst = right ? cR0 : cL0, n = right ? NRlog : NL;
+            const PackOut<COST_SAD4, R> base = right ? Rp : Lp;
+            if (cg >= 0 && cg + 4 <= a.W) {
+                uint32_t w[NW][4];
+                sad4_group_words<R>(rw[m], w);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int idx = cg + k - cfirst;
+                    if (idx < 0 || idx >= n) continue;
+                    uint32_t v[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[i] = i < NW ? w[i < NW ? i : 0][k] : 0u;
+                    put<COST_SAD4, R>(base + (right ? rslot(idx, c0, DPL) : idx), v);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int idx = cg + k - cfirst;
+                    if (idx < 0 || idx >= n) continue;
+                    build_pack<COST_SAD4, R>(a, right ? a.R : a.L, nullptr, cg + k, y,
+                                             base + (right ? rslot(idx, c0, DPL) : idx));
+                }
+            }
+        }
     }
 }
 
@@ -840,7 +915,7 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     const int xw = a.X0 + bx * WC;
     const int cL0 = xw - R;                             // L index i -> column cL0 + i
     const int cR0 = cL0 - a.minD - (4 * LPG - 1);       // R index i -> column cR0 + i
-    build_all_packs<COST_SAD4, R, RG_DPL>(a, yc, cL0, NL, cR0, NRlog, c0, Lw, Rw, lane);
+    build_ring_packs<R, 3, RG_DPL>(a, yc, cL0, NL, cR0, NRlog, c0, Lw, Rw, lane);
 
     if (!KEYS && bx == 0) {  // columns outside the matched band are invalid
         const int16_t inv = (int16_t)((a.minD - 1) * 16);

@@ -55,7 +55,8 @@ from stereovision_amd.engine import (POST_DEPTH, Communicator, Engine, device_co
 from stereovision_amd.synthetic import stereo_batch, stereo_pair, synthetic_calibration, to_bgr  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-VALU_ISSUE_PEAK = 1024 * 2.4e9 / 2   # 256 CU x 4 SIMD, one wave64 VALU instr per 2 cycles
+N_SIMD = 1024                        # 256 CU x 4 SIMD
+VALU_ISSUE_PEAK = N_SIMD * 2.4e9 / 2   # one wave64 VALU instr per 2 cycles per SIMD
 
 
 def log(*a):
@@ -1152,8 +1153,9 @@ def main():
             "bytes_per_launch": k_bytes,
             "bytes_rule": "SURVEY.md §8(d): 6 B/px (2 u8 images + f32 disparity) x pixels per launch",
             "achieved_note": "algorithmic bytes over the live launch time (HIP events), not a counter-"
-                             "observed HBM rate: the 16 resident frames (66 MB) live in the 256 MB "
-                             "Infinity Cache; the kernel's limiter is VALU issue (see `valu`)",
+                             f"observed HBM rate: the {F} resident frames ({2 * F * npx / 1e6:.0f} MB of "
+                             "inputs) live in the 256 MB Infinity Cache; the kernel's limiter is VALU "
+                             "issue (see `valu`)",
             "kernel_bytes_per_launch": k_bytes_kernel,
             "frac_kernel_bytes": round(k_bytes_kernel / k_avg_s / 1e9 / HBM_PEAK_GBS, 5),
             "avg_launch_us": round(k_avg_s * 1e6, 2), "launches": match_n,
@@ -1172,7 +1174,15 @@ def main():
                      "frac": round(insts / k_avg_s / VALU_ISSUE_PEAK, 4) if insts else None,
                      "insts_per_launch": round(insts) if insts else None,
                      "insts_per_wave_cell": (round(insts / (npx * D / 64), 3) if insts else None),
-                     "cells_per_s": round(npx * D / k_avg_s)},
+                     "cells_per_s": round(npx * D / k_avg_s),
+                     # the issue rate against the valu_rate microbenchmark at the kernel's 2 waves
+                     # per SIMD (independent chains): the VOP3 integer ops k_match issues (v_sad_*,
+                     # v_min3, DPP mins) sustain 2.06-2.22 ns per wave-instruction per SIMD, a mixed
+                     # v_sad_u8 + v_min_u32 stream 1.88 ns, v_add 1.37 ns
+                     "ns_per_wave_instr_per_simd": (round(N_SIMD * k_avg_s / insts * 1e9, 3) if insts else None),
+                     "microbench_ns_per_wave_instr": {"v_sad_u8/v_sad_hi_u8/v_sad_u32": 2.2, "v_min3_u32/v_min_u32_dpp": 2.15,
+                                                      "mixed v_sad_u8 + v_min_u32": 1.88, "v_add_u32": 1.37,
+                                                      "source": "profiles/r05a/valu_rate_wps2.txt"}},
             "pmc": {"source": "rocprofv3 --pmc, 3 separate passes over a 6-step child run of this "
                               "script on this box (mean per k_match dispatch)",
                     "traffic_note": "traffic = 2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024): the guide's "

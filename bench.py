@@ -1153,7 +1153,7 @@ def main():
             "bytes_per_launch": k_bytes,
             "bytes_rule": "SURVEY.md §8(d): 6 B/px (2 u8 images + f32 disparity) x pixels per launch",
             "achieved_note": "algorithmic bytes over the live launch time (HIP events), not a counter-"
-                             f"observed HBM rate: the {F} resident frames ({2 * F * npx / 1e6:.0f} MB of "
+                             f"observed HBM rate: the {F} resident frames ({2 * F * n_px / 1e6:.0f} MB of "
                              "inputs) live in the 256 MB Infinity Cache; the kernel's limiter is VALU "
                              "issue (see `valu`)",
             "kernel_bytes_per_launch": k_bytes_kernel,

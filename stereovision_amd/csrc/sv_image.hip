@@ -210,13 +210,10 @@ __device__ __forceinline__ int dpp_shl1_keep(int v) {   // lane j+1 (lane 63 kee
     return t;
 }
 
+// One wave's band: output columns x0 .. x0+247, rows y0 .. y0+HB-1 of one frame.
 template <int HB, int PF>
-__global__ __launch_bounds__(64) void k_harris_dpp4(const uint8_t* __restrict__ g, int H, int W, int pitch,
-                                                    float* __restrict__ out, long long fs_in, long long fs_out) {
-    g += blockIdx.z * fs_in;
-    out += blockIdx.z * fs_out;
-    const int lane = threadIdx.x;
-    const int x0 = blockIdx.x * 248, y0 = blockIdx.y * HB;
+__device__ __forceinline__ void harris_wave4(const uint8_t* __restrict__ g, int H, int W, int pitch,
+                                             float* __restrict__ out, int x0, int y0, int lane) {
     const int c0 = x0 - 4 + 4 * lane;                               // first column of the lane
     // interior: every lane's 4 columns inside the image and dword-aligned rows (uniform)
     const bool fast = x0 >= 4 && x0 + 252 <= W && ((pitch & 3) == 0) && ((((uintptr_t)g) & 3) == 0);
@@ -323,6 +320,13 @@ __global__ __launch_bounds__(64) void k_harris_dpp4(const uint8_t* __restrict__ 
             }
         }
     }
+}
+
+template <int HB, int PF>
+__global__ __launch_bounds__(64) void k_harris_dpp4(const uint8_t* __restrict__ g, int H, int W, int pitch,
+                                                    float* __restrict__ out, long long fs_in, long long fs_out) {
+    harris_wave4<HB, PF>(g + blockIdx.z * fs_in, H, W, pitch, out + blockIdx.z * fs_out, blockIdx.x * 248,
+                         blockIdx.y * HB, threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -848,10 +852,18 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
     // C2's Harris response rides in the median launch instead of a launch of its own
     if ((int)blockIdx.x >= hp.mbx) {
         const int w = (int)(blockIdx.x - hp.mbx) * 4 + (int)(threadIdx.x >> 6);
-        const int x0 = w * 60, y0 = row0 + (int)blockIdx.y * MQ_H;
-        if (x0 < W && y0 < row1)
-            harris_wave<MQ_H, 4>(hp.g + blockIdx.z * hp.fs_in, H, W, hp.pitch, hp.out + blockIdx.z * hp.fs_out, x0,
-                                 y0, threadIdx.x & 63);
+        const int y0 = row0 + (int)blockIdx.y * MQ_H;
+        if (hp.form) {   // 248 columns per wave, one dword per lane-row (W >= 256)
+            const int x0 = w * 248;
+            if (x0 < W && y0 < row1)
+                harris_wave4<MQ_H, 4>(hp.g + blockIdx.z * hp.fs_in, H, W, hp.pitch, hp.out + blockIdx.z * hp.fs_out,
+                                      x0, y0, threadIdx.x & 63);
+        } else {
+            const int x0 = w * 60;
+            if (x0 < W && y0 < row1)
+                harris_wave<MQ_H, 4>(hp.g + blockIdx.z * hp.fs_in, H, W, hp.pitch, hp.out + blockIdx.z * hp.fs_out,
+                                     x0, y0, threadIdx.x & 63);
+        }
         return;
     }
     // t2[r][c] = (tile row r, tile row r+2) of column x0-2+c; tile row r = image row y0-2+r
@@ -1248,10 +1260,18 @@ int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float
     HarrisParams hp{};
     hp.mbx = (W + MQ_W - 1) / MQ_W;
     int hbx = 0;
-    if (harris && harris->g) {   // Harris of rows [row0, row1): 4 waves of 60 columns per block
+    if (harris && harris->g) {   // Harris of rows [row0, row1): 4 waves of 60 (248) columns per block
         hp = *harris;
         hp.mbx = (W + MQ_W - 1) / MQ_W;
-        hbx = ((W + 59) / 60 + 3) / 4;
+        // 248-column waves (k_harris_dpp4's form) from W >= 256: a quarter of the waves and one
+        // dword load per lane-row where the band is interior (C2, 640x480 with 3 streams: 238k ->
+        // 254-256k frames/s on one box).  SV_HARRIS_MED4=0 (A/B): 60-column waves everywhere
+        static const bool med4 = [] {
+            const char* e = std::getenv("SV_HARRIS_MED4");
+            return !(e && e[0] == '0');
+        }();
+        hp.form = (med4 && W >= 256) ? 1 : 0;
+        hbx = hp.form ? ((W + 247) / 248 + 3) / 4 : ((W + 59) / 60 + 3) / 4;
     }
     hipLaunchKernelGGL(k_median_i16, dim3(hp.mbx + hbx, (row1 - row0 + MQ_H - 1) / MQ_H, nf),
                        dim3(256), 0, s, in, H, W, row0, row1, disp, pp, fs_in, fs_out, hp);

@@ -273,6 +273,7 @@ struct HarrisParams {
     float* out;
     long long fs_out;
     int mbx;
+    int form;   // 0: 60-column waves, 1: 248-column waves (set by the launcher)
 };
 // nf frames (grid.z): frame z reads in + z*fs_in and writes disp/out_* + z*fs_out elements.
 // harris (nullable): also the Harris response of rows [row0, row1) of each frame.

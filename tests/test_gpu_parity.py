@@ -515,13 +515,16 @@ def test_row_tiled_module_and_single_hip_runtime(engine):
     assert "torch" not in sys.modules
 
 
-@pytest.mark.parametrize("H,W,nf", [(45, 150, 3), (16, 64, 2), (33, 301, 3), (7, 70, 2), (120, 640, 4), (9, 8, 1)])
-def test_depth_map_harris_batch_dev_fused(engine, H, W, nf):
+@pytest.mark.parametrize("H,W,nf,pad", [(45, 150, 3, 3), (16, 64, 2, 3), (33, 301, 3, 3), (7, 70, 2, 3),
+                                        (120, 640, 4, 3), (9, 8, 1, 3), (48, 640, 2, 0), (37, 1000, 2, 4),
+                                        (20, 256, 3, 0), (24, 260, 2, 0)])
+def test_depth_map_harris_batch_dev_fused(engine, H, W, nf, pad):
     """sv_depth_map_harris_batch_dev (C2: Harris blocks inside the median launch) == the C
     oracle frame by frame: the create_depth_map outputs bit-exact and the Harris response of
-    each left frame within 1e-4 (north_star; observed exact), with a row pitch wider than the
-    frame; frames under 8 px take the separate Harris launch."""
-    D, win, pitch = 32, 7, W + 3
+    each left frame within 1e-4 (north_star; observed exact), with row pitches wider than the
+    frame (unaligned) and equal to it (the 248-column waves' dword loads, W >= 256); frames
+    under 8 px take the separate Harris launch."""
+    D, win, pitch = 32, 7, W + pad
     rng = np.random.default_rng(H * W + nf)
     L = np.zeros((nf, H, pitch), np.uint8)
     R = np.zeros((nf, H, pitch), np.uint8)

@@ -843,6 +843,9 @@ __global__ __launch_bounds__(256) void k_post_m16(const int16_t* __restrict__ in
     }
 }
 
+// HF: the Harris blocks this instance carries (0 none, 1 60-column waves, 2 248-column waves):
+// the 248-column form needs 81 VGPRs, which would cost the plain median (36) its occupancy
+template <int HF>
 __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ in, int H, int W,
                                                     int row0, int row1, float* __restrict__ disp,
                                                     PostParams pp, long long fs_in, long long fs_out,
@@ -850,10 +853,10 @@ __global__ __launch_bounds__(256) void k_median_i16(const int16_t* __restrict__ 
     // Harris blocks (hp.g != nullptr): blockIdx.x >= hp.mbx; each wave one DPP band of 60
     // columns x 16 rows of the frame's left image (harris_wave, the k_harris_dpp form), so
     // C2's Harris response rides in the median launch instead of a launch of its own
-    if ((int)blockIdx.x >= hp.mbx) {
+    if (HF != 0 && (int)blockIdx.x >= hp.mbx) {
         const int w = (int)(blockIdx.x - hp.mbx) * 4 + (int)(threadIdx.x >> 6);
         const int y0 = row0 + (int)blockIdx.y * MQ_H;
-        if (hp.form) {   // 248 columns per wave, one dword per lane-row (W >= 256)
+        if constexpr (HF == 2) {   // 248 columns per wave, one dword per lane-row (W >= 256)
             const int x0 = w * 248;
             if (x0 < W && y0 < row1)
                 harris_wave4<MQ_H, 4>(hp.g + blockIdx.z * hp.fs_in, H, W, hp.pitch, hp.out + blockIdx.z * hp.fs_out,
@@ -1273,7 +1276,9 @@ int launch_median_i16(const int16_t* in, int H, int W, int row0, int row1, float
         hp.form = (med4 && W >= 256) ? 1 : 0;
         hbx = hp.form ? ((W + 247) / 248 + 3) / 4 : ((W + 59) / 60 + 3) / 4;
     }
-    hipLaunchKernelGGL(k_median_i16, dim3(hp.mbx + hbx, (row1 - row0 + MQ_H - 1) / MQ_H, nf),
+    void (*fn)(const int16_t*, int, int, int, int, float*, PostParams, long long, long long, HarrisParams) =
+        hbx == 0 ? k_median_i16<0> : hp.form ? k_median_i16<2> : k_median_i16<1>;
+    hipLaunchKernelGGL(fn, dim3(hp.mbx + hbx, (row1 - row0 + MQ_H - 1) / MQ_H, nf),
                        dim3(256), 0, s, in, H, W, row0, row1, disp, pp, fs_in, fs_out, hp);
     return (int)hipGetLastError();
 }

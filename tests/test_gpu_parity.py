@@ -517,7 +517,7 @@ def test_row_tiled_module_and_single_hip_runtime(engine):
 
 @pytest.mark.parametrize("H,W,nf,pad", [(45, 150, 3, 3), (16, 64, 2, 3), (33, 301, 3, 3), (7, 70, 2, 3),
                                         (120, 640, 4, 3), (9, 8, 1, 3), (48, 640, 2, 0), (37, 1000, 2, 4),
-                                        (20, 256, 3, 0), (24, 260, 2, 0)])
+                                        (20, 256, 3, 0), (24, 260, 2, 0), (9, 300, 2, 0), (8, 257, 1, 1)])
 def test_depth_map_harris_batch_dev_fused(engine, H, W, nf, pad):
     """sv_depth_map_harris_batch_dev (C2: Harris blocks inside the median launch) == the C
     oracle frame by frame: the create_depth_map outputs bit-exact and the Harris response of

@@ -51,7 +51,7 @@ constexpr int COST_SAD4 = 4;          // internal kind: SAD, four output rows pe
 __host__ __device__ __forceinline__ int seg_width(int lpg, int dpl, int sm = 4) { return (sm * lpg + dpl - 1) / dpl * dpl; }
 __host__ __device__ __forceinline__ int wave_cols(int lpg, int dpl, int sm = 4) { return (64 / lpg) * seg_width(lpg, dpl, sm); }
 // 4-row kind: full-length segments when the common words are split into their own array
-// (24-B packs, r <= 5); half-length for the 32-B packs of r 6..7, which would otherwise
+// (24-B packs, r <= 5); half-length for the 28-B packs of r 6..7, which would otherwise
 // hold the LDS to 1.5 waves per SIMD.
 int seg_mult(int kind, int r) {
     static const int sm4 = [] {
@@ -65,6 +65,8 @@ int seg_mult(int kind, int r) {
 }
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
+
+struct Word3 { uint32_t x, y, z; };   // a 12-byte common-word slot (4-byte aligned)
 
 // A column pack holds NW live dwords inside a 16*Q-byte LDS slot.
 template <int COST, int ND> struct PackCfg {
@@ -83,11 +85,12 @@ template <int COST, int ND> struct PackCfg {
     // HOG (5 words) splits too: word 0 in the 8-byte array, words 1-4 in a 16-byte slot, so
     // a group's 16 lanes (slots DPL+1 apart) read disjoint banks (32-byte slots: 2-way)
     static constexpr int NC = COST == COST_SAD4 ? NW - 4 : (COST == COST_HOG || (COST == COST_SSD && NW == 5)) ? 1 : 0;
-    // (r 6..7: 3 common words in a 16-byte slot of their own)
+    // (r 6..7: 3 common words in a 12-byte slot of their own: 28-B packs, so the ring kind's
+    // LDS holds ~40% longer segments than with a padded 16-byte slot)
     static constexpr bool SPLIT = (COST == COST_SAD4 && NC <= 3) || COST == COST_HOG ||
                                   (COST == COST_SSD && NW == 5);
-    static constexpr int CW = NC <= 2 ? 2 : 4;        // words per slot of the common array
-    using CT = typename std::conditional<CW == 2, uint2, uint4>::type;
+    static constexpr int CW = NC <= 2 ? 2 : 3;        // words per slot of the common array
+    using CT = typename std::conditional<CW == 2, uint2, Word3>::type;
     static constexpr int QX = SPLIT ? 1 : Q;          // uint4 per slot in the main array
     static constexpr int SLOT_BYTES = 16 * QX + (SPLIT ? 4 * CW : 0);
 };
@@ -147,7 +150,7 @@ __device__ __forceinline__ void put(PackOut<COST, ND> p, const uint32_t (&w)[8])
     using P = PackCfg<COST, ND>;
     if constexpr (P::SPLIT) {
         if constexpr (P::CW == 2) *p.c = make_uint2(w[0], P::NC > 1 ? w[1] : 0u);
-        else *p.c = make_uint4(w[0], w[1], w[2], 0u);
+        else *p.c = Word3{w[0], w[1], w[2]};
         p.x[0] = make_uint4(w[P::NC], w[P::NC + 1], w[P::NC + 2], w[P::NC + 3]);
     } else {
         p.x[0] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -861,7 +864,7 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     // (a window costs at most 57375), updated with v_pk_add/sub_u16: 15 ring steps x 16
     // cells fit in 120 VGPRs; the argmin keys (cost << 16) | idx are built per step
     constexpr bool PK = R >= 6;
-    static_assert(P::SPLIT && (P::CW == 2) != PK, "ring kind expects split packs (24 B; 32 B for r 6..7)");
+    static_assert(P::SPLIT && (P::CW == 2) != PK, "ring kind expects split packs (24 B; 28 B for r 6..7)");
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     // XCD-aware tile order (sv_xcd.h): horizontal and vertical neighbours share 2r of their
     // 2r+4 input rows and most right-image columns; each XCD takes a contiguous tile range
@@ -1277,7 +1280,7 @@ size_t ring_lds_bytes(int lpg, int seg, int r) {
     const int tn = (seg + 2 * r + 3) & ~3;
     const int nl = wc - seg + tn + 1, nr = wc - seg + tn + 4 * lpg;
     const int nrp = nr + (nr + 1) / RG_DPL + 1;
-    return (size_t)(nl + nrp) * (r <= 5 ? 24 : 32);
+    return (size_t)(nl + nrp) * (r <= 5 ? 24 : 28);
 }
 
 template <int R, int LPG, bool KEYS, bool SSD>
@@ -1436,7 +1439,7 @@ size_t match_lds_bytes(const MatchPlan& p, int r, int cost) {
                  : kind == COST_SAD4 ? (2 * p.ndw - 2 + 3) / 4 + 4 : 5;
     const int wpb = kind == COST_SAD4 ? 1 : 4;
     const bool split = (kind == COST_SAD4 && nw - 4 <= 3) || kind == COST_HOG || (kind == COST_SSD && nw == 5);
-    const int cw = kind == COST_SAD4 && nw - 4 == 3 ? 4 : 2;
+    const int cw = kind == COST_SAD4 && nw - 4 == 3 ? 3 : 2;
     const int Q = (nw + 3) / 4;
     const int c0 = (p.dpl - (4 * r + 1) % p.dpl) % p.dpl;
     const int wc = wave_cols(p.lpg, p.dpl, seg_mult(kind, r));

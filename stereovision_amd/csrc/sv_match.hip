@@ -89,8 +89,10 @@ template <int COST, int ND> struct PackCfg {
     // LDS holds ~40% longer segments than with a padded 16-byte slot)
     static constexpr bool SPLIT = (COST == COST_SAD4 && NC <= 3) || COST == COST_HOG ||
                                   (COST == COST_SSD && NW == 5);
-    static constexpr int CW = NC <= 2 ? 2 : 3;        // words per slot of the common array
-    using CT = typename std::conditional<CW == 2, uint2, Word3>::type;
+    // (the 4-row kind with one common word, r 2..3: a 4-byte slot, 20-B packs)
+    static constexpr int CW = (COST == COST_SAD4 && NC == 1) ? 1 : NC <= 2 ? 2 : 3;   // words per common slot
+    using CT = typename std::conditional<CW == 1, uint32_t,
+                                         typename std::conditional<CW == 2, uint2, Word3>::type>::type;
     static constexpr int QX = SPLIT ? 1 : Q;          // uint4 per slot in the main array
     static constexpr int SLOT_BYTES = 16 * QX + (SPLIT ? 4 * CW : 0);
 };
@@ -121,10 +123,14 @@ __device__ __forceinline__ Pk<PackCfg<COST, ND>::NW> ld(PackPtr<COST, ND> p) {
     using P = PackCfg<COST, ND>;
     Pk<P::NW> v;
     if constexpr (P::SPLIT) {
-        const typename P::CT c = *p.c;
-        v.w[0] = c.x;
-        if constexpr (P::NC > 1) v.w[1] = c.y;
-        if constexpr (P::NC > 2) v.w[2] = c.z;
+        if constexpr (P::CW == 1) {
+            v.w[0] = *p.c;
+        } else {
+            const typename P::CT c = *p.c;
+            v.w[0] = c.x;
+            if constexpr (P::NC > 1) v.w[1] = c.y;
+            if constexpr (P::NC > 2) v.w[2] = c.z;
+        }
         if constexpr (B128) {
             const uint4 m = *p.x;
             v.w[P::NC] = m.x;
@@ -149,7 +155,8 @@ template <int COST, int ND>
 __device__ __forceinline__ void put(PackOut<COST, ND> p, const uint32_t (&w)[8]) {
     using P = PackCfg<COST, ND>;
     if constexpr (P::SPLIT) {
-        if constexpr (P::CW == 2) *p.c = make_uint2(w[0], P::NC > 1 ? w[1] : 0u);
+        if constexpr (P::CW == 1) *p.c = w[0];
+        else if constexpr (P::CW == 2) *p.c = make_uint2(w[0], P::NC > 1 ? w[1] : 0u);
         else *p.c = Word3{w[0], w[1], w[2]};
         p.x[0] = make_uint4(w[P::NC], w[P::NC + 1], w[P::NC + 2], w[P::NC + 3]);
     } else {
@@ -864,7 +871,7 @@ __global__ __launch_bounds__(64, 2) void k_match_ring(MatchParams a) {
     // (a window costs at most 57375), updated with v_pk_add/sub_u16: 15 ring steps x 16
     // cells fit in 120 VGPRs; the argmin keys (cost << 16) | idx are built per step
     constexpr bool PK = R >= 6;
-    static_assert(P::SPLIT && (P::CW == 2) != PK, "ring kind expects split packs (24 B; 28 B for r 6..7)");
+    static_assert(P::SPLIT && (P::CW == 3) == PK, "ring kind expects split packs (20 B for r 2..3, 24 B for r 4..5, 28 B for r 6..7)");
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     // XCD-aware tile order (sv_xcd.h): horizontal and vertical neighbours share 2r of their
     // 2r+4 input rows and most right-image columns; each XCD takes a contiguous tile range
@@ -1280,7 +1287,7 @@ size_t ring_lds_bytes(int lpg, int seg, int r) {
     const int tn = (seg + 2 * r + 3) & ~3;
     const int nl = wc - seg + tn + 1, nr = wc - seg + tn + 4 * lpg;
     const int nrp = nr + (nr + 1) / RG_DPL + 1;
-    return (size_t)(nl + nrp) * (r <= 5 ? 24 : 28);
+    return (size_t)(nl + nrp) * (r <= 3 ? 20 : r <= 5 ? 24 : 28);
 }
 
 template <int R, int LPG, bool KEYS, bool SSD>
@@ -1439,7 +1446,7 @@ size_t match_lds_bytes(const MatchPlan& p, int r, int cost) {
                  : kind == COST_SAD4 ? (2 * p.ndw - 2 + 3) / 4 + 4 : 5;
     const int wpb = kind == COST_SAD4 ? 1 : 4;
     const bool split = (kind == COST_SAD4 && nw - 4 <= 3) || kind == COST_HOG || (kind == COST_SSD && nw == 5);
-    const int cw = kind == COST_SAD4 && nw - 4 == 3 ? 3 : 2;
+    const int cw = kind == COST_SAD4 && nw - 4 == 3 ? 3 : kind == COST_SAD4 && nw - 4 == 1 ? 1 : 2;
     const int Q = (nw + 3) / 4;
     const int c0 = (p.dpl - (4 * r + 1) % p.dpl) % p.dpl;
     const int wc = wave_cols(p.lpg, p.dpl, seg_mult(kind, r));

@@ -15,7 +15,7 @@ Multi-GPU (frames mode = C4, weak scaling; rowtile mode = C5, strong scaling):
     LOCAL_RANK from the environment, barrier + max-over-ranks through RCCL
     (stereovision_amd.distributed: file rendezvous + sv_comm_* of libsvhip);
   * `python bench.py --gpus N` without a launcher: ONE process drives N devices
-    (sv_multi_gpu_depth_map_dev / sv_depth_map_rows_multi when gathering).
+    (sv_multi_gpu_dev when gathering).
 value = frames of all GPUs / max wall time of the timed region.
 
 Extra JSON fields:
@@ -49,9 +49,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from stereovision_amd.engine import (POST_DEPTH, Communicator, Engine, device_count,  # noqa: E402
-                                     depth_map_rows_map, depth_map_rows_multi, depth_map_rows_scatter,
-                                     get_engine, multi_gpu_depth_map_dev, multi_gpu_map_dev)
+from stereovision_amd.engine import (POST_DEPTH, STAGE_MATCH, STAGE_MEDIAN, Communicator,  # noqa: E402
+                                     Engine, depth_map_rows_map, depth_map_rows_multi,
+                                     depth_map_rows_scatter, device_count, get_engine, map_out,
+                                     multi_gpu_depth_map_dev, multi_gpu_map_dev)
 from stereovision_amd.synthetic import stereo_batch, stereo_pair, synthetic_calibration, to_bgr  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -612,6 +613,13 @@ def parse_args(argv=None):
                     help="frames mode, N > 1: no gather (the compute-only weak-scaling curve)")
     ap.add_argument("--full-frame-inputs", action="store_true",
                     help="rowtile: every GPU holds the full frame (no input scatter in the step)")
+    ap.add_argument("--band-inputs", default="scatter", choices=["scatter", "host"],
+                    help="rowtile, N > 1: where each GPU's band rows come from inside a step — "
+                         "scatter: from GPU 0's HBM over xGMI (RCCL send/recv; launched: on a "
+                         "communicator and stream of its own, so frame i+1's scatter runs beside "
+                         "frame i's gather in the opposite link direction); host: every GPU uploads "
+                         "its own band's rows from page-locked host memory over its own PCIe link "
+                         "(no xGMI scatter; the step is then PCIe-inclusive, so the line says so)")
     ap.add_argument("--require-rccl", action="store_true",
                     help="N distinct devices: exit non-zero when RCCL cannot start (default: one "
                          "process gathers with hipMemcpyPeerAsync, one process per GPU through the "
@@ -639,6 +647,15 @@ def parse_args(argv=None):
                          "alternate over, so one step overlaps the next (separate output buffers "
                          "per stream); 0 = auto: 3 for frames of <= 1 MP (a 16-frame VGA batch "
                          "leaves most of the chip idle between its launches), else 1")
+    ap.add_argument("--schedule", default="lanes", choices=["split", "lanes"],
+                    help="frames mode, one GPU: split = the match launch of batch i on one stream "
+                         "and the median launch of batch i-1 on a second (SV_STAGE_MATCH / "
+                         "SV_STAGE_MEDIAN of sv_depth_map_batch_dev: the HBM-bound median beside "
+                         "the VALU-bound match, k_match launches never overlapping each other); "
+                         "lanes (default) = --streams contexts alternating whole steps.  split "
+                         "measured slower at 1080p (29.8k vs 29.7k one stream / 30.6k two lanes) and "
+                         "4K (2.88k vs 3.14k): the median's sorting network competes with the match "
+                         "for VALU issue, so it does not hide behind it (profiles/r06b)")
     ap.add_argument("--no-aux", action="store_true", help="skip the aux-kernel rooflines")
     ap.add_argument("--harris", action="store_true",
                     help="C2: also compute the Harris response of every left frame (k_harris)")
@@ -656,11 +673,18 @@ def parse_args(argv=None):
                          "than this many seconds (a rank stuck in a collective fails loudly)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
-    if args.batch is None:   # 1080p frames: 26 (whole rounds of k_match waves; C3 win 11 +1.1% too)
-        full_hd = (args.height, args.width) == (1080, 1920) and args.cost != "sgbm"
-        args.batch = 26 if full_hd and args.mode == "frames" else 16
+    full_hd = (args.height, args.width) == (1080, 1920) and args.cost != "sgbm"
+    one_gpu = args.gpus <= 1 and int(os.environ.get("WORLD_SIZE", "1")) <= 1
+    lanes2 = full_hd and args.mode == "frames" and one_gpu and not (args.rectify or args.harris)
+    if args.batch is None:
+        # 1080p frames on one GPU: 8-frame steps alternating over 2 streams (the second lane's
+        # match fills the first one's tail waves: 29.7k -> 30.6-30.7k frames/s, profiles/r06b);
+        # N > 1: 26 (whole rounds of k_match waves, one stream beside the gather stream)
+        args.batch = (8 if lanes2 and args.streams in (0, 2) else 26) if full_hd and args.mode == "frames" else 16
+    if args.streams == 0 and lanes2 and args.schedule != "split":
+        args.streams = 2
     if args.frames is None:
-        args.frames = args.batch
+        args.frames = args.batch * (2 if args.streams == 2 and lanes2 else 1)
     if args.pmc_child:
         args.no_cpu_baseline = args.no_aux = args.no_live_pmc = args.no_host_path = True
         args.no_profile = args.no_verify = True
@@ -709,6 +733,7 @@ def main():
     arenas = [DevArena(e) for e in engines]
     gather_on = (not rowtile) and ngpu > 1 and not args.no_gather
     band_inputs = rowtile and ngpu > 1 and not args.full_frame_inputs
+    host_bands = band_inputs and args.band_inputs == "host"
 
     # resident inputs: F distinct frames per GPU (rowtile: ONE frame, on GPU 0 only unless
     # --full-frame-inputs; the other GPUs receive their band rows inside each step)
@@ -720,6 +745,14 @@ def main():
             L, R = stereo_batch(F, H, W, D, seed=1000 * (rank * len(devices) + k))
         hostL.append(L)
         hostR.append(R)
+        if host_bands:   # every GPU reads its band rows from page-locked host memory
+            if k == 0:
+                for a_ in (L, R):
+                    if e.lib.sv_host_register(a_.ctypes.data, a_.nbytes) != 0:
+                        raise SystemExit("--band-inputs host: sv_host_register failed")
+            dL.append(0)
+            dR.append(0)
+            continue
         if band_inputs and (rank if launched else k) != 0:
             dL.append(0)
             dR.append(0)
@@ -748,9 +781,12 @@ def main():
     # the other's: C5 HOG 1,564 -> 1,637-1,651, C5 SAD 2,920 -> 3,035 frames/s,
     # profiles/r05h_hog); 1 otherwise (1080p SAD: 2 streams +2.0%, 2 x 8-frame batches +2.9%,
     # left at one stream so the roofline's launch times stay those of a launch alone)
+    # --schedule split (default above 1 MP): the match of batch i on the compute stream beside
+    # the median of batch i-1 on a median stream (own context), int16 maps double-buffered
+    split = args.schedule == "split" and not (rowtile or rectify or gather_on or harris or len(engines) > 1 or B == 1)
     req_streams = args.streams if args.streams > 0 else (
         3 if n_px <= 1_000_000 else 2 if (args.cost == "hog" or n_px >= 4_000_000) else 1)
-    nstreams = max(1, req_streams) if not (rowtile or args.rectify or gather_on) else 1
+    nstreams = max(1, req_streams) if not (rowtile or args.rectify or gather_on or split) else 1
     lanes = [(engines, depth, disp, norm)]
     for _ in range(nstreams - 1):
         lanes.append(([Engine(d) for d in devices], [a.alloc(4 * n_px * out_frames) for a in arenas],
@@ -763,8 +799,15 @@ def main():
     if harris:   # per stream lane: its own Harris maps
         hmaps_l = [[a.alloc(4 * n_px * B) for a in arenas] for _ in range(nstreams)]
         hmaps = hmaps_l[0]
+    meng, sd16 = None, None
+    if split:
+        meng = Engine(devices[0])
+        all_engines.append(meng)
+        sd16 = [arenas[0].alloc(2 * n_px * B) for _ in range(2)]
+        sout = map_out(POST_DEPTH, disp[0], depth[0], norm[0], min_depth=0.3, max_depth=2.0,
+                       min_disp_global=0)
     tile = tiles = None
-    rt = {"t": 0, "primed": False, "last": 0}
+    rt = {"t": 0, "primed": False, "last": 0, "n": 0}
     if rowtile and launched:
         from stereovision_amd.distributed import RowTiledDepthMap
         # two tiles (band inputs, medians, outputs each) alternate over consecutive frames, so
@@ -819,10 +862,17 @@ def main():
         nexp = n_px * B * (world - 1)
         expanded = ([(arenas[0].alloc(4 * nexp), arenas[0].alloc(4 * nexp), arenas[0].alloc(nexp))
                      for _ in range(2)] if (root_full and rank == 0) else None)
+    geng, gstream, pg2 = None, 0, None
     if tiles is not None and world > 1:
+        # scatter (root -> peers) on ceng's stream over pg's communicator; the gather (peers ->
+        # root) on geng's stream over a second communicator (pg.dup), so frame i+1's scatter and
+        # frame i's gather use opposite link directions at once
         ceng = Engine(devices[0])
         cstream = ceng.stream
-        all_engines.append(ceng)
+        geng = Engine(devices[0])
+        gstream = geng.stream
+        all_engines += [ceng, geng]
+        pg2 = pg.dup("gather")
     gather_wall = [0.0]
 
     def step(i):
@@ -832,10 +882,10 @@ def main():
                 tile.compute(dL[0], dR[0])
             elif launched:
                 # pipelined over the two tiles (event slots of `eng`: 4+t = tile t's band inputs
-                # scattered, 6+t = tile t computed): compute(i) on the compute stream; on the
-                # communication stream the scatter of frame i+1's band inputs (into the other
-                # tile, whose previous compute the gather before it already waited for), then
-                # the gather of frame i's int16 x16 medians (+ the root's expansion)
+                # in place, 6+t = tile t computed, 8+t = tile t's medians gathered): compute(i) on
+                # the compute stream; frame i+1's band inputs into the other tile on the scatter
+                # stream (after that tile's previous compute), frame i's medians to the root on the
+                # gather stream (after compute(i)) — two streams, two communicators
                 t = rt["t"]
                 u = (t + 1) % len(tiles)
                 # gather-only (--root-outputs m16): every rank, the root included, writes only its
@@ -843,31 +893,47 @@ def main():
                 # its own epilogue and the peers' int16 bands after the gather
                 bo = ("full" if rank == 0 else "m16") if root_full else ("d8" if gather_u8 else "m16")
 
-                def scatter_into(x):
-                    ceng.profile_region_begin("scatter", cstream)
-                    tiles[x].scatter(pg, dL[0], dR[0], stream=cstream)
+                def bands_into(x):
+                    if rt["n"] >= 2:   # the tile's previous frame has been computed
+                        eng.stream_wait_event(6 + x, cstream)
+                    ceng.profile_region_begin("h2d" if host_bands else "scatter", cstream)
+                    if host_bands:
+                        tiles[x].upload(hostL[0][0], hostR[0][0], stream=cstream)
+                    else:
+                        tiles[x].scatter(pg, dL[0], dR[0], stream=cstream)
                     ceng.profile_region_end(cstream)
                     eng.event_record(4 + x, cstream)
+                if rt["n"] >= 2:       # tile t's medians of two frames ago have left
+                    eng.stream_wait_event(8 + t, eng.stream)
                 if band_inputs:
                     if not rt["primed"]:
-                        scatter_into(t)
+                        bands_into(t)
                         rt["primed"] = True
                     eng.stream_wait_event(4 + t, eng.stream)
                     tiles[t].compute(band_outputs=bo)
                 else:
                     tiles[t].compute(dL[0], dR[0], band_outputs=bo)
                 eng.event_record(6 + t, eng.stream)
+                rt["n"] += 1
                 if band_inputs:
-                    scatter_into(u)
-                eng.stream_wait_event(6 + t, cstream)
-                ceng.profile_region_begin("gather", cstream)
-                tiles[t].gather(pg, stream=cstream, expand=root_full)
-                ceng.profile_region_end(cstream)
+                    bands_into(u)
+                eng.stream_wait_event(6 + t, gstream)
+                geng.profile_region_begin("gather", gstream)
+                tiles[t].gather(pg2, stream=gstream, expand=root_full, check=rt["n"] == 1)
+                geng.profile_region_end(gstream)
+                eng.event_record(8 + t, gstream)
                 rt["last"], rt["t"] = t, u
             else:   # one process: two lanes of contexts alternate, so frame i+1's scatter and
                     # kernels overlap frame i's gather and expansion
                 le, lc, ldep, ldis, lnor, lmap = glanes[i % 2]
-                if not root_full:   # gather-only: the full map on device 0, nothing expanded
+                if host_bands:      # every context uploads its band from host memory
+                    if root_full:
+                        depth_map_rows_multi(le, lc, hostL[0][0], hostR[0][0], H, W, W, 0, D, win, 0.3, 2.0,
+                                             ldep, ldis, lnor, cost=args.cost, scatter="host")
+                    else:
+                        depth_map_rows_map(le, lc, hostL[0][0], hostR[0][0], H, W, W, 0, D, win, lmap,
+                                           fmt="d8" if gather_u8 else "m16", scatter="host", cost=args.cost)
+                elif not root_full:   # gather-only: the full map on device 0, nothing expanded
                     depth_map_rows_map(le, lc, dL[0] if band_inputs else dL, dR[0] if band_inputs else dR,
                                        H, W, W, 0, D, win, lmap, fmt="d8" if gather_u8 else "m16",
                                        scatter=band_inputs, cost=args.cost)
@@ -878,6 +944,18 @@ def main():
                     depth_map_rows_multi(le, lc, dL, dR, H, W, W, 0, D, win, 0.3, 2.0,
                                          ldep, ldis, lnor, cost=args.cost)
                 rt["last"] = i % 2
+            return
+        if split:   # event slots of `eng`: k = d16[k] written, 2+k = d16[k] read by its median
+            k = i % 2
+            if i >= 2:
+                eng.stream_wait_event(2 + k, eng.stream)
+            eng.depth_map_batch_ex(dL[0] + f * n_px, dR[0] + f * n_px, B, H, W, W, n_px, 0, D, win, args.cost,
+                                   STAGE_MATCH, sd16[k], None, stream=eng.stream)
+            eng.event_record(k, eng.stream)
+            eng.stream_wait_event(k, meng.stream)
+            meng.depth_map_batch_ex(0, 0, B, H, W, W, n_px, 0, D, win, args.cost, STAGE_MEDIAN, sd16[k], sout,
+                                    stream=meng.stream)
+            eng.event_record(2 + k, meng.stream)
             return
         if gather_all:     # one process, N devices, maps gathered on device 0 (1 or 2 B/px)
             le, lc, ldep, ldis, lnor, lmap = glanes[i % 2]
@@ -964,7 +1042,8 @@ def main():
                 sync_all()
     sync_all()
     warm_s = time.perf_counter() - t_w
-    for pe in [eng] + ([ceng] if ceng is not None else []) + ([glanes[1][0][0]] if glanes else []):
+    for pe in ([eng] + ([ceng] if ceng is not None else []) + ([glanes[1][0][0]] if glanes else [])
+               + ([meng] if meng is not None else []) + ([geng] if geng is not None else [])):
         pe.profile(False)
         pe.profile_reset()
     gather_wall[0] = 0.0
@@ -974,7 +1053,8 @@ def main():
         pg.barrier()
     sync_all()
     t0 = time.perf_counter()
-    prof_engs = [eng] + ([ceng] if ceng is not None else []) + ([glanes[1][0][0]] if glanes else [])
+    prof_engs = ([eng] + ([ceng] if ceng is not None else []) + ([glanes[1][0][0]] if glanes else [])
+                 + ([meng] if meng is not None else []) + ([geng] if geng is not None else []))
     for i in range(args.steps):
         for pe in prof_engs:
             if not args.no_profile and every > 1:
@@ -990,14 +1070,14 @@ def main():
     for pe in prof_engs:
         pe.profile(False)
     match_ms, match_n = eng.profile_read("sgbm" if args.cost == "sgbm" else "match")
-    med_ms, med_n = eng.profile_read("median")
+    med_ms, med_n = (meng or eng).profile_read("median")
     remap_ms, remap_n = eng.profile_read("remap")
     harris_ms, harris_n = eng.profile_read("harris")
-    gath_ms, gath_n = (ceng or eng).profile_read("gather")
+    gath_ms, gath_n = (geng or ceng or eng).profile_read("gather")
     if glanes:   # the second lane's root context times its own gathers
         m2, n2 = glanes[1][0][0].profile_read("gather")
         gath_ms, gath_n = gath_ms + m2, gath_n + n2
-    scat_ms, scat_n = (ceng or eng).profile_read("scatter")
+    scat_ms, scat_n = (ceng or eng).profile_read("h2d" if host_bands and launched else "scatter")
     if glanes:
         m2, n2 = glanes[1][0][0].profile_read("scatter")
         scat_ms, scat_n = scat_ms + m2, scat_n + n2
@@ -1161,7 +1241,12 @@ def main():
             "avg_launch_us": round(k_avg_s * 1e6, 2), "launches": match_n,
             # with S > 1 streams (frames <= 1 MP) lane 0's launches share the device
             # with the other lanes' kernels, so these launch times are contended ones
-            "launch_concurrency": (f"{nstreams} streams: lane 0's launches timed while the other "
+            "launch_concurrency": ("split schedule: k_match launches back to back on the compute "
+                                   "stream, each timed while the previous batch's median runs on the "
+                                   "median stream (HIP events on the compute stream; the rocprofv3 "
+                                   "kernel trace of the same command gives the same durations)"
+                                   if split else
+                                   f"{nstreams} streams: lane 0's launches timed while the other "
                                    f"{nstreams - 1} lanes' kernels share the device (not comparable "
                                    "with single-stream launch times)" if nstreams > 1 else "one stream"),
             # what actually bounds k_match: VALU issue.  SQ_INSTS_VALU per
@@ -1203,7 +1288,7 @@ def main():
             for k in range(1, ngpu):
                 b = band_layout(H, k, ngpu, win)
                 gbytes += gel * (b["r1"] - b["r0"]) * W    # int16 x16 median rows or u8 indices
-                if band_inputs:
+                if band_inputs and not host_bands:
                     sbytes += 2 * (b["in1"] - b["in0"]) * W
         elif gather_on:   # the disparity maps: u8 indices (launched, where exact) or int16 x16
             gbytes = gel * n_px * B * (ngpu - 1)
@@ -1224,7 +1309,28 @@ def main():
                         if (gather_on or rowtile) else None)
     if dist is not None and (gather_on or rowtile):
         dist["gather_format"] = gather_desc
-    parallelism = (f"row-tiled x{ngpu}" + (" (band inputs scattered from GPU 0)" if band_inputs else "")
+    if dist is not None and rowtile:
+        b0 = __import__("stereovision_amd.distributed", fromlist=["band_layout"]).band_layout(H, 0, ngpu, win)
+        dist["band_inputs"] = ("full frame resident on every GPU (no input transfer in the step)"
+                               if not band_inputs else
+                               "host: every GPU uploads its band + halo rows from page-locked host memory "
+                               "over its own PCIe link inside the step (no xGMI scatter; PCIe-inclusive)"
+                               if host_bands else
+                               "scatter: each GPU receives its band + halo rows from GPU 0's HBM over xGMI "
+                               "inside the step")
+        dist["inputs"] = dist["band_inputs"]
+        if host_bands:
+            dist["h2d_bytes_per_step_per_gpu"] = 2 * (b0["in1"] - b0["in0"]) * W
+            dist["scatter_us_per_step"] = None
+            dist["h2d_us_per_step"] = round(scat_ms * 1e3 / scat_n, 2) if scat_n else None
+        if launched and ngpu > 1:
+            dist["comm_streams"] = ("band inputs on a stream of their own " +
+                                    ("(host uploads)" if host_bands else "(RCCL scatter, communicator 1)") +
+                                    "; the band gather on a second stream over communicator 2 (pg.dup): "
+                                    "frame i+1's inputs travel while frame i's medians leave, in opposite "
+                                    "link directions")
+    parallelism = (f"row-tiled x{ngpu}" + ((" (band inputs uploaded from host memory by every GPU)" if host_bands
+                                            else " (band inputs scattered from GPU 0)") if band_inputs else "")
                    + " + band gather" if rowtile else
                    f"frame-sharded x{ngpu}" + (" + gather to GPU 0" if gather_on else ""))
     if ngpu > 1:
@@ -1247,7 +1353,9 @@ def main():
                    "height": H, "width": W, "num_disp": D, "win": win, "cost": args.cost,
                    "frames_resident_per_gpu": 1 if rowtile else F,
                    "frames_per_step_per_gpu": 1 if rowtile else B,
-                   "streams_per_gpu": nstreams,
+                   "streams_per_gpu": 2 if split else nstreams,
+                   "schedule": "split (match stream + median stream)" if split else
+                               (f"lanes ({nstreams} contexts alternating steps)" if nstreams > 1 else "one stream"),
                    "parallelism": parallelism},
         "verified": verified,
         "verify": verify_info,
@@ -1285,7 +1393,7 @@ def main():
     elif harris:
         result["aux_kernels"] = dict(result["aux_kernels"] or {})
         result["aux_kernels"]["k_harris"] = {
-            "fused": "Harris blocks inside the k_median_i16 launch (sv_depth_map_harris_batch_dev): "
+            "fused": "Harris blocks inside the k_median_i16 launch (sv_depth_map_batch_dev, out.harris): "
                      "median_post_avg_us includes them"}
     if solo and not args.no_host_path and args.cost != "sgbm" and not rectify:
         try:
@@ -1310,6 +1418,8 @@ def main():
     if glanes and glanes[1][1]:
         for c in glanes[1][1]:
             c.close()
+    if pg2 is not None:
+        pg2.close()
     if pg is not None:
         pg.close()
     if verified is False:

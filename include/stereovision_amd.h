@@ -10,7 +10,7 @@
  *                                    depth_map.py:894-909, fused_depth_map.py:988-1004
  *                                    (replaced by the north_star SAD/SSD/HOG WTA engine;
  *                                    same int16 x16 output convention)
- *   sv_median5_f32                   cv2.medianBlur(disparity, 5)
+ *   sv_median5_f32, sv_median_rows_dev   cv2.medianBlur(disparity, 5)
  *                                    depth_map.py:912, fused_depth_map.py:1007
  *   sv_depth_post                    depth/clip/mask/normalise NumPy block, depth_map.py:915-937
  *   sv_scaled_post                   clip/normalise/confidence NumPy block,
@@ -81,7 +81,7 @@ enum sv_status {
                          padding disparities in the lane plan (cmax = largest window cost) */
 };
 
-/* post-processing modes of sv_median_post_dev */
+/* post-processing modes of sv_map_out.mode / sv_post_m16_dev */
 enum sv_post { SV_POST_NONE = 0, SV_POST_DEPTH = 1, SV_POST_SCALED = 2 };
 
 /* kernel ids for the profiling counters */
@@ -190,39 +190,42 @@ int sv_disparity_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
                      int pitch, int min_disp, int num_disp, int win, int cost, int row0,
                      int row1, int16_t* d_disp16, int out_pitch, void* stream);
 
-/* medianBlur(.,5)/16 of rows [row0,row1) of an int16 x16 map (halo from the full map),
- * fused with the post-processing `mode` (sv_post).  DEPTH: out_a = depth_final,
- * out_u8 = depth_normalized.  SCALED: out_a = disparity_normalized, out_u8 = its u8
- * image, out_b = confidence. */
-int sv_median_post_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W, int row0, int row1,
-                       int mode, float min_depth, float max_depth, float depth_range,
-                       float min_disp_global, int min_disp, int num_disp, float* d_disparity,
-                       float* d_out_a, uint8_t* d_out_u8, float* d_out_b, void* stream);
+/* Outputs of the median + post-processing epilogue: cv2.medianBlur(disparity, 5) of an int16
+ * x16 disparity map (depth_map.py:909-912, fused_depth_map.py:1004-1007) and the NumPy post
+ * that follows it — SV_POST_DEPTH: depth/clip/mask/normalise (depth_map.py:915-937),
+ * SV_POST_SCALED: clip/normalise/confidence (fused_depth_map.py:1010-1029).  Every pointer is
+ * nullable (not written) and, except cmap_bgr, a device pointer; at least one output must be
+ * set.  One descriptor serves every median launch (row bands, frame batches, the root of a
+ * multi-device call) instead of one entry point per output combination. */
+typedef struct sv_map_out {
+    int mode;                  /* sv_post: what out_a / out_u8 / out_b hold */
+    float min_depth;           /* SV_POST_DEPTH: float32 of the caller's bounds */
+    float max_depth;
+    float depth_range;         /* float32 of (max_depth - min_depth) computed in double
+                                  (NumPy-2 semantics of depth_map.py:936) */
+    float min_disp_global;     /* the module global MIN_DISP (depth_map.py:932) */
+    float* disparity;          /* f32 median / 16 (create_depth_map's `disparity`) */
+    float* out_a;              /* DEPTH: depth_final       SCALED: disparity_normalized */
+    uint8_t* out_u8;           /* DEPTH: depth_normalized  SCALED: its u8 image */
+    float* out_b;              /* SCALED: confidence */
+    int16_t* med16;            /* int16 x16 median map (OpenCV's fixed point; disparity =
+                                  med16 / 16 exactly): 2 B/px for a gather or a download */
+    uint8_t* d8;               /* u8 disparity index median / 16 - (min_disp - 1), 0 =
+                                  invalid: integer-disparity costs (SAD / SSD / HOG) with
+                                  num_disp <= 255, else -EINVAL (1 B/px) */
+    const uint8_t* cmap_bgr;   /* with bgr: the 256 x 3 BGR colormap table (host memory) */
+    uint8_t* bgr;              /* cv2.applyColorMap(out_u8, cmap) (TURBO at depth_map.py:937,
+                                  JET at fused_depth_map.py:1013), H x W x 3 */
+    float* harris;             /* sv_depth_map_batch_dev only: the Harris response of every
+                                  LEFT frame, computed by extra blocks of the median launch */
+} sv_map_out;
 
-/* sv_median_post_dev plus the display colormap in the same epilogue (cv2.applyColorMap of
- * out_u8: TURBO at depth_map.py:937, JET at fused_depth_map.py:1013): cmap_bgr is the 256 x 3
- * BGR table in host memory, d_bgr the H x W x 3 output (rows [row0, row1)). */
-int sv_median_post_color_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W, int row0,
-                             int row1, int mode, float min_depth, float max_depth,
-                             float depth_range, float min_disp_global, int min_disp, int num_disp,
-                             const uint8_t* cmap_bgr, float* d_disparity, float* d_out_a,
-                             uint8_t* d_out_u8, float* d_out_b, uint8_t* d_bgr, void* stream);
-
-/* sv_median_post_dev with an optional int16 x16 median map d_med16 (rows [row0, row1) at
- * their full-frame offsets) beside the outputs; d_disparity may then be NULL, and mode =
- * SV_POST_NONE writes only d_med16 (a row band's medians before a gather). */
-int sv_median_post_m16_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W, int row0, int row1,
-                           int mode, float min_depth, float max_depth, float depth_range,
-                           float min_disp_global, int min_disp, int num_disp, float* d_disparity,
-                           float* d_out_a, uint8_t* d_out_u8, float* d_out_b, int16_t* d_med16,
-                           void* stream);
-/* The 5x5 median of disparity rows [row0, row1) (cv2.medianBlur(disparity, 5),
- * depth_map.py:912) written only as a map for a gather (SV_MAP_M16: int16 x16; SV_MAP_D8: u8
- * indices median / 16 - (min_disp - 1), integer-disparity maps with num_disp <= 255), at
- * full-frame offsets of d_map (row y at d_map + y*W elements): a row band's share of a
- * gather-only row tiling. */
-int sv_median_map_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W, int row0, int row1,
-                      int map_format, int min_disp, int num_disp, void* d_map, void* stream);
+/* Median (+ post) of output rows [row0, row1) of an H x W int16 x16 map (halo rows read from
+ * the full map, so row bands of a multi-GPU split reassemble bit-exactly); outputs at their
+ * full-frame offsets.  cost: the matcher that produced the map (integer-disparity maps use the
+ * whole-disparity post table; SGBM's sub-pixel maps the full one). */
+int sv_median_rows_dev(sv_ctx* ctx, const int16_t* d_disp16, int H, int W, int row0, int row1,
+                       int min_disp, int num_disp, int cost, const sv_map_out* out, void* stream);
 /* The post-processing of n median values d_med16 (int16 x16, e.g. maps gathered over xGMI):
  * d_disparity = m / 16 (nullable), and mode's outputs element-wise, exactly as the median
  * kernel's epilogue writes them (depth_map.py:915-936 / fused_depth_map.py:1010-1024). */
@@ -231,73 +234,39 @@ int sv_post_m16_dev(sv_ctx* ctx, const int16_t* d_med16, int64_t n, int mode, fl
                     int num_disp, float* d_disparity, float* d_out_a, uint8_t* d_out_u8,
                     float* d_out_b, void* stream);
 
-/* Whole app-1 device path on gray device images: disparity -> median -> depth post. */
-int sv_depth_map_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int H, int W,
-                     int pitch, int min_disp, int num_disp, int win, int cost, float min_depth,
-                     float max_depth, float depth_range, float min_disp_global, float* d_depth,
-                     float* d_disparity, uint8_t* d_norm, void* stream);
-
 /* ---- frame batches (one launch per kernel over grid.z) ------------------------------
  * A batch of n_frames equally-shaped gray pairs, frame z at d_left/d_right + z*frame_stride
  * bytes.  Replaces the reference's per-frame loop over the same calls (depth_map.py:837-946
  * called once per captured frame, fused_depth_map.py:2591-2598) when frames are queued:
- * one launch per kernel fills the GPU even for small frames.  Outputs are dense per frame
- * (frame z of an H x W output at + z*H*W elements) except sv_disparity_batch_dev's int16
- * map, which takes an explicit out_pitch / out_frame_stride (elements).  The context's
- * internal scratch is ordered across streams (a call on another stream waits for the
- * previous user of the scratch).  cost = SV_COST_SGBM runs every SGBM stage once per chunk of
- * up to 32 frames (volumes of ~1.5 GB per 1080p D=128 frame, within the scratch budget of
- * sv_release_scratch);
- * chunks of >= 8 frames fuse the right-to-left path with the winner-take-all. */
+ * one launch per kernel fills the GPU even for small frames.  The context's internal scratch
+ * is ordered across streams (a call on another stream waits for the previous user of the
+ * scratch).  cost = SV_COST_SGBM runs every SGBM stage once per chunk of up to 32 frames
+ * (volumes of ~1.5 GB per 1080p D=128 frame, within the scratch budget of
+ * sv_release_scratch); chunks of >= 8 frames fuse the right-to-left path with the
+ * winner-take-all.
+ *
+ * sv_disparity_batch_dev: the int16 x16 maps only, at an explicit out_pitch /
+ * out_frame_stride (elements). */
 int sv_disparity_batch_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
                            int n_frames, int H, int W, int pitch, int64_t frame_stride,
                            int min_disp, int num_disp, int win, int cost, int16_t* d_disp16,
                            int out_pitch, int64_t out_frame_stride, void* stream);
-int sv_median_post_batch_dev(sv_ctx* ctx, const int16_t* d_disp16, int n_frames, int H, int W,
-                             int mode, float min_depth, float max_depth, float depth_range,
-                             float min_disp_global, int min_disp, int num_disp,
-                             float* d_disparity, float* d_out_a, uint8_t* d_out_u8,
-                             float* d_out_b, void* stream);
+/* sv_depth_map_batch_dev: the whole device path (disparity -> median -> post) over the batch,
+ * every output of `out` dense per frame (frame z at + z*H*W elements).  stages:
+ *   SV_STAGE_ALL     both launches; d_disp16 nullable (the context's scratch, else the raw
+ *                    int16 x16 maps are kept there, dense per frame)
+ *   SV_STAGE_MATCH   the disparity launch only, into d_disp16 (required); out unused
+ *   SV_STAGE_MEDIAN  the median launch only, from d_disp16 (required; d_left read only for
+ *                    out->harris) — with SV_STAGE_MATCH on another stream or context, the two
+ *                    launches of consecutive batches overlap (the HBM-bound median beside the
+ *                    VALU-bound match). */
+#define SV_STAGE_MATCH 1
+#define SV_STAGE_MEDIAN 2
+#define SV_STAGE_ALL 3
 int sv_depth_map_batch_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
                            int n_frames, int H, int W, int pitch, int64_t frame_stride,
-                           int min_disp, int num_disp, int win, int cost, float min_depth,
-                           float max_depth, float depth_range, float min_disp_global,
-                           float* d_depth, float* d_disparity, uint8_t* d_norm, void* stream);
-/* sv_depth_map_batch_dev that also writes each frame's median map as int16 x16 (OpenCV's
- * fixed-point disparity, the value the reference divides by 16 at depth_map.py:909, so
- * d_disparity = d_med16 / 16 exactly) into d_med16 (dense per frame; NULL: not written) —
- * half the bytes of the f32 map for a gather over xGMI. */
-int sv_depth_map_batch_m16_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
-                               int n_frames, int H, int W, int pitch, int64_t frame_stride,
-                               int min_disp, int num_disp, int win, int cost, float min_depth,
-                               float max_depth, float depth_range, float min_disp_global,
-                               float* d_depth, float* d_disparity, uint8_t* d_norm,
-                               int16_t* d_med16, void* stream);
-
-/* sv_depth_map_batch_dev that also writes each frame's median map as a u8 disparity index
- * d8 = median / 16 - (min_disp - 1) into d_d8 (dense per frame): SAD / SSD / HOG disparities are
- * whole pixels, so every median is a multiple of 16 and, with num_disp <= 255, d8 holds it
- * exactly (0 = the invalid value min_disp - 1; d_disparity = d8 + min_disp - 1) — a quarter of
- * the f32 map's bytes for the frame gather over xGMI (replaces the gather of
- * fused_depth_map.py:2591-2598's per-frame results).  SGBM (sub-pixel) or num_disp > 255: -EINVAL. */
-int sv_depth_map_batch_d8_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
-                              int n_frames, int H, int W, int pitch, int64_t frame_stride,
-                              int min_disp, int num_disp, int win, int cost, float min_depth,
-                              float max_depth, float depth_range, float min_disp_global,
-                              float* d_depth, float* d_disparity, uint8_t* d_norm,
-                              uint8_t* d_d8, void* stream);
-
-/* C2 (BASELINE.json: "Harris+disparity"): sv_depth_map_batch_dev plus the Harris response
- * (cornerHarris(3, 3, 0.04) convention) of every LEFT frame into d_harris
- * (dense f32 per frame).  The response is computed by extra blocks of the median launch (the
- * register/DPP Harris form), so the path is two launches, not three; frames under 8 px a side
- * take a separate Harris launch. */
-int sv_depth_map_harris_batch_dev(sv_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
-                                  int n_frames, int H, int W, int pitch, int64_t frame_stride,
-                                  int min_disp, int num_disp, int win, int cost, float min_depth,
-                                  float max_depth, float depth_range, float min_disp_global,
-                                  float* d_depth, float* d_disparity, uint8_t* d_norm,
-                                  float* d_harris, void* stream);
+                           int min_disp, int num_disp, int win, int cost, int stages,
+                           int16_t* d_disp16, const sv_map_out* out, void* stream);
 
 /* Frame-sharded batch over several devices from ONE host process:
  * replaces the reference's per-frame loop over create_depth_map (depth_map.py:837-946,
@@ -331,7 +300,12 @@ typedef struct sv_comm sv_comm;
 #define SV_COMM_ID_BYTES 128
 int sv_comm_available(void);
 int sv_comm_unique_id(uint8_t* id);
-int sv_comm_init_rank(int device, int nranks, int rank, const uint8_t* id, sv_comm** out);
+/* sv_comm_init_rank: non-blocking ncclCommInitRankConfig polled until it completes or
+ * timeout_s seconds pass (<= 0: no limit); on an error or the deadline the half-built
+ * communicator is aborted (ncclCommAbort) and -EHIP returned, so a rank whose peers failed
+ * during bootstrap comes back instead of blocking forever. */
+int sv_comm_init_rank(int device, int nranks, int rank, const uint8_t* id, double timeout_s,
+                      sv_comm** out);
 int sv_comm_init_all(int ndev, const int* devices, sv_comm** comms);
 void sv_comm_destroy(sv_comm* comm);
 int sv_comm_rank(sv_comm* comm, int* rank, int* nranks, int* device);
@@ -348,37 +322,7 @@ int sv_comm_scatterv(sv_comm* comm, const void* d_send, const uint64_t* send_off
                      void* stream);
 int sv_comm_synchronize(sv_comm* comm);
 
-/* C4 on device-resident frames, one process driving ndev contexts: context k computes
- * create_depth_map (disparity -> median -> depth post, one launch per kernel over its
- * frames) for n_frames[k] gray pairs at d_left[k]/d_right[k] (+ z*frame_stride bytes, on
- * its own device), and the three outputs of every frame end up in d_depth / d_disparity /
- * d_norm on ctxs[0]'s device, dense, in context order (frame z of context k at index
- * sum(n_frames[:k]) + z).  Only the peers' int16 x16 medians cross xGMI (2 B/px instead of
- * the outputs' 9); the root expands them with the post-processing table (k_post_m16,
- * profiled as SV_K_POST) after the gather.  comms (nullable; else comms[k] must be on ctxs[k]'s
- * device with rank k): the gather runs as RCCL send/recv over xGMI; NULL: hipMemcpyPeerAsync
- * (a plain device copy when two contexts share a device).  Returns after enqueueing: the
- * outputs are complete once ctxs[0]'s stream is (sv_synchronize(ctxs[0])). */
-int sv_multi_gpu_depth_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
-                               const uint8_t* const* d_left, const uint8_t* const* d_right,
-                               const int* n_frames, int H, int W, int pitch, int64_t frame_stride,
-                               int min_disp, int num_disp, int win, int cost, float min_depth,
-                               float max_depth, float depth_range, float min_disp_global,
-                               float* d_depth, float* d_disparity, uint8_t* d_norm);
-
-/* C4 as north_star states it ("a trivial RCCL gather of the final disparity rows"): as
- * sv_multi_gpu_depth_map_dev, but every context's median kernel writes only the int16 x16
- * median maps (OpenCV's fixed-point disparity after medianBlur, depth_map.py:909-912) and
- * those are gathered into d_med16 on ctxs[0]'s device (dense, context order): 2 B/px over
- * xGMI.  sv_post_m16_dev turns any of them into create_depth_map's outputs. */
-int sv_multi_gpu_m16_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
-                         const uint8_t* const* d_left, const uint8_t* const* d_right,
-                         const int* n_frames, int H, int W, int pitch, int64_t frame_stride,
-                         int min_disp, int num_disp, int win, int cost, int16_t* d_med16);
-
-/* Gather-only map formats of the multi-device entry points (north_star: "a trivial RCCL
- * gather of the final disparity rows"): the root receives only the median map, nothing is
- * expanded there (sv_post_m16_dev / disparity = d8 + min_disp - 1 give the outputs).
+/* Gather-only map formats (north_star: "a trivial RCCL gather of the final disparity rows"):
  *   SV_MAP_M16  int16 x16 medians (OpenCV's fixed-point disparity after medianBlur,
  *               depth_map.py:909-912), 2 B/px over xGMI
  *   SV_MAP_D8   u8 disparity indices median / 16 - (min_disp - 1) (0 = invalid), 1 B/px:
@@ -386,48 +330,40 @@ int sv_multi_gpu_m16_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
 #define SV_MAP_M16 1
 #define SV_MAP_D8 2
 
-/* C4 gather-only, any map format: as sv_multi_gpu_m16_dev (which is this with SV_MAP_M16),
- * the maps of every frame land in d_map on ctxs[0]'s device (dense, context order; element
- * size 2 or 1).  SV_MAP_D8 with SGBM or num_disp > 255: -EINVAL. */
-int sv_multi_gpu_map_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
-                         const uint8_t* const* d_left, const uint8_t* const* d_right,
-                         const int* n_frames, int H, int W, int pitch, int64_t frame_stride,
-                         int min_disp, int num_disp, int win, int cost, int map_format,
-                         void* d_map);
-
-/* C5: ONE frame row-tiled over ndev contexts.  Every context holds the full gray frame
- * (d_left[k]/d_right[k] on its device; the window and median halos are read locally, so the
- * bands reassemble bit-exactly); context k computes output rows [H*k/ndev, H*(k+1)/ndev)
- * of create_depth_map and the bands end up in the full H x W d_depth / d_disparity /
- * d_norm on ctxs[0]'s device (the peers' bands cross xGMI as int16 x16 medians and are
- * expanded on the root).  comms / completion as sv_multi_gpu_depth_map_dev. */
-int sv_depth_map_rows_multi(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
-                            const uint8_t* const* d_left, const uint8_t* const* d_right, int H,
-                            int W, int pitch, int min_disp, int num_disp, int win, int cost,
-                            float min_depth, float max_depth, float depth_range,
-                            float min_disp_global, float* d_depth, float* d_disparity,
-                            uint8_t* d_norm);
-
-/* C5 with the frame resident on ctxs[0]'s device only: context k > 0 first receives just the
- * input rows its band reads (sv_band_rows_in: the band, the median halo and the window halo)
- * from the root (RCCL send/recv over xGMI, or peer copies), into its own scratch; then as
- * sv_depth_map_rows_multi.  Profiled as SV_K_SCATTER / SV_K_GATHER on the root stream. */
-int sv_depth_map_rows_scatter(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
-                              const uint8_t* d_left, const uint8_t* d_right, int H, int W,
-                              int pitch, int min_disp, int num_disp, int win, int cost,
-                              float min_depth, float max_depth, float depth_range,
-                              float min_disp_global, float* d_depth, float* d_disparity,
-                              uint8_t* d_norm);
-/* C5 gather-only (replaces the disparity create_depth_map returns, depth_map.py:909-912, for
- * a row-tiled frame): as sv_depth_map_rows_multi (scatter = 0: every context holds the full
- * frame at d_left[k] / d_right[k]) or sv_depth_map_rows_scatter (scatter != 0: the frame is
- * at d_left[0] / d_right[0] on the root only), but the root receives only the full H x W map
- * (SV_MAP_M16 / SV_MAP_D8) in d_map — its own band written by its median epilogue, the
- * peers' bands gathered — and expands nothing. */
-int sv_depth_map_rows_map(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev,
-                          const uint8_t* const* d_left, const uint8_t* const* d_right, int scatter,
-                          int H, int W, int pitch, int min_disp, int num_disp, int win, int cost,
-                          int map_format, void* d_map);
+/* One process driving ndev contexts; replaces the reference's per-frame loop
+ * over create_depth_map (depth_map.py:837-946; fused_depth_map.py:2591-2598 submits frames to a
+ * worker pool) and returns the disparity rows the reference returns (depth_map.py:909-912).
+ *   shard SV_SHARD_FRAMES (C4): context k computes its n_frames[k] frames at left[k] / right[k]
+ *         (+ z*frame_stride bytes, on its own device); outputs dense in context order (frame z
+ *         of context k at index sum(n_frames[:k]) + z).
+ *   shard SV_SHARD_ROWS (C5): ONE frame; context k computes output rows
+ *         [H*k/ndev, H*(k+1)/ndev) (window and median halos read locally, so the bands
+ *         reassemble bit-exactly); n_frames and frame_stride unused.  inputs:
+ *           SV_INPUTS_RESIDENT  every context holds the full gray frame (left[k] on its device)
+ *           SV_INPUTS_SCATTER   the frame is on the root only (left[0]); context k > 0 first
+ *                               receives the input rows its band reads (sv_band_rows_in) over
+ *                               RCCL / peer copies (profiled as SV_K_SCATTER on the root)
+ *           SV_INPUTS_HOST      the frame is in HOST memory (left[0], pinned for overlap: see
+ *                               sv_host_register); every context uploads its own band's input
+ *                               rows over its own PCIe link (no xGMI scatter; SV_K_H2D)
+ *         Frames mode takes SV_INPUTS_RESIDENT only.
+ * out (on ctxs[0]'s device) selects what the root holds: create_depth_map's outputs
+ * (mode SV_POST_DEPTH with disparity, out_a, out_u8: the peers' maps cross xGMI as int16 x16
+ * and are expanded on the root, k_post_m16 profiled as SV_K_POST), or gather-only the map of
+ * every frame / the full frame as med16 (SV_MAP_M16) or d8 (SV_MAP_D8), nothing expanded.
+ * comms (nullable; else comms[k] is rank k of an ndev-rank communicator on ctxs[k]'s device):
+ * gathers / scatters as RCCL send/recv over xGMI; NULL: hipMemcpyPeerAsync (a plain device copy
+ * when two contexts share a device).  Returns after enqueueing: the outputs are complete once
+ * ctxs[0]'s stream is (sv_synchronize(ctxs[0])). */
+#define SV_SHARD_FRAMES 0
+#define SV_SHARD_ROWS 1
+#define SV_INPUTS_RESIDENT 0
+#define SV_INPUTS_SCATTER 1
+#define SV_INPUTS_HOST 2
+int sv_multi_gpu_dev(sv_ctx* const* ctxs, sv_comm* const* comms, int ndev, int shard, int inputs,
+                     const uint8_t* const* left, const uint8_t* const* right, const int* n_frames,
+                     int H, int W, int pitch, int64_t frame_stride, int min_disp, int num_disp,
+                     int win, int cost, const sv_map_out* out);
 
 /* Row bands of a `world`-way row tiling for rank `rank`: out6 = {r0, r1 (output rows), h0, h1
  * (disparity rows incl. the median halo), in0, in1 (input rows the band reads)}.  Device
@@ -522,11 +458,7 @@ int sv_filter_speckles_dev(sv_ctx* ctx, int16_t* d_img, int H, int W, int pitch,
  * hist [256]; the pair's second image follows the first. */
 int sv_frame_stats(sv_ctx* ctx, const uint8_t* img0, const uint8_t* img1, int H, int W, int channels,
                    int stride, uint32_t* block_sum, uint32_t* block_sq, uint32_t* hist);
-int sv_frame_stats_dev(sv_ctx* ctx, const uint8_t* d_img0, const uint8_t* d_img1, int H, int W,
-                       int channels, int pitch, uint32_t* d_block_sum, uint32_t* d_block_sq,
-                       uint32_t* d_hist, void* stream);
-
-/* sv_frame_stats_dev over a batch of n_frames images or pairs in one launch (image z of the
+/* The device version, over a batch of n_frames images or pairs in one launch (image z of the
  * batch: img0 / img1 of frame z / per at + (z / per) * frame_stride bytes, per = 2 with
  * d_img1, else 1); outputs dense per image z: block moments [n_img][bh*bw], hist [n_img][256].
  * detect_camera_occlusion runs once per checked frame (fused_depth_map.py:2515-2522); a
@@ -539,19 +471,15 @@ int sv_frame_stats_batch_dev(sv_ctx* ctx, const uint8_t* d_img0, const uint8_t* 
 /* Order statistics of a float32 device array for np.percentile (calibrate_midas_to_stereo
  * fused_depth_map.py:1169-1257, normalize_to_stereo_range :1503-1554) with the reference's
  * masks as predicates: mask_mode 0 = all elements, 1 = elements > 0 (stereo_disparity > 0),
- * 2 = elements whose d_mask value > thr (stereo_confidence > 0.7).  sv_select_count gives
+ * 2 = elements whose d_mask value > thr (stereo_confidence > 0.7).  sv_select_count_batch gives
  * the number of selected elements and of NaNs among them (np.percentile returns nan if
- * any); sv_select_ranks gives the values of the given 0-based ranks of the ascending
+ * any); sv_select_ranks_batch gives the values of the given 0-based ranks of the ascending
  * sorted selection (nranks <= 4; radix select in three passes of 11/11/10 bits).  Both
- * block until the result is on the host. */
-int sv_select_count(sv_ctx* ctx, const float* d_x, int64_t n, int mask_mode, const float* d_mask,
-                    float thr, int64_t* selected, int64_t* nans);
-int sv_select_ranks(sv_ctx* ctx, const float* d_x, int64_t n, int mask_mode, const float* d_mask,
-                    float thr, const int64_t* ranks, int nranks, float* values);
-/* The same over a batch of n_arrays <= 16 arrays of n elements (array y at d_x + y * x_stride
- * elements, its mask at d_mask + y * mask_stride): one launch + one fold per radix pass for
- * the whole batch (e.g. the disparity maps of queued frames).  selected / nans: [n_arrays];
- * ranks / values: [n_arrays][nranks]. */
+ * block until the result is on the host and take a batch of n_arrays <= 16 arrays of n
+ * elements (array y at d_x + y * x_stride elements, its mask at d_mask + y * mask_stride; one
+ * array: n_arrays = 1): one launch + one fold per radix pass for the whole batch (e.g. the
+ * disparity maps of queued frames).  selected / nans: [n_arrays]; ranks / values:
+ * [n_arrays][nranks]. */
 int sv_select_count_batch(sv_ctx* ctx, const float* d_x, int64_t n, int64_t x_stride, int n_arrays,
                           int mask_mode, const float* d_mask, int64_t mask_stride, float thr,
                           int64_t* selected, int64_t* nans);
@@ -569,11 +497,15 @@ int sv_affine_f32_dev(sv_ctx* ctx, const float* d_x, int64_t n, int mode, float 
 int sv_resize_linear_f32_dev(sv_ctx* ctx, const float* d_src, int sH, int sW, int src_pitch,
                              float* d_dst, int dH, int dW, int dst_pitch, void* stream);
 
-/* ---- device memory helpers (synchronous on the context stream) -------------------- */
+/* ---- device memory helpers ----------------------------------------------------------
+ * sv_copy_to_device / sv_copy_to_host: stream NULL = synchronous on the context stream (the
+ * download first waits for the context's enqueued work); a stream = enqueued on it and
+ * returned at once (the host buffer must stay valid until the stream reaches the copy, and be
+ * page-locked — sv_host_register — for the copy to overlap device work). */
 int sv_dev_alloc(sv_ctx* ctx, uint64_t bytes, void** out);
 int sv_dev_free(sv_ctx* ctx, void* p);
-int sv_copy_to_device(sv_ctx* ctx, void* dst, const void* src, uint64_t bytes);
-int sv_copy_to_host(sv_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+int sv_copy_to_device(sv_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream);
+int sv_copy_to_host(sv_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream);
 
 /* Page-lock a host range and make it device-visible (hipHostRegister, portable).  Output
  * arrays of the host-buffer entry points (sv_depth_map, sv_depth_map_color,

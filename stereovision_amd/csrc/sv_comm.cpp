@@ -10,7 +10,9 @@
 // Blocking helpers (barrier, max-allreduce) run on the communicator's own stream.
 #include <dlfcn.h>
 
+#include <chrono>
 #include <cstring>
+#include <thread>
 #include <mutex>
 #include <new>
 #include <string>
@@ -25,6 +27,8 @@ struct sv_comm {
     ncclComm_t comm = nullptr;
     hipStream_t stream = nullptr;
     void* scratch = nullptr;   // 64 B: barrier / allreduce operand
+    bool nonblocking = false;  // initialised with ncclConfig.blocking = 0: calls may return
+                               // ncclInProgress and are settled by polling (settle)
     std::mutex mu;
 };
 
@@ -42,6 +46,10 @@ struct Rccl {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    // non-blocking initialisation (optional symbols: without them init is the blocking call)
+    decltype(&ncclCommInitRankConfig) init_rank_config = nullptr;
+    decltype(&ncclCommGetAsyncError) async_error = nullptr;
+    decltype(&ncclCommAbort) abort = nullptr;
     std::string load_error;
 };
 
@@ -70,6 +78,9 @@ Rccl& rccl_state() {
         r.group_start = reinterpret_cast<decltype(r.group_start)>(sym("ncclGroupStart"));
         r.group_end = reinterpret_cast<decltype(r.group_end)>(sym("ncclGroupEnd"));
         r.error_string = reinterpret_cast<decltype(r.error_string)>(sym("ncclGetErrorString"));
+        r.init_rank_config = reinterpret_cast<decltype(r.init_rank_config)>(sym("ncclCommInitRankConfig"));
+        r.async_error = reinterpret_cast<decltype(r.async_error)>(sym("ncclCommGetAsyncError"));
+        r.abort = reinterpret_cast<decltype(r.abort)>(sym("ncclCommAbort"));
         if (!r.get_unique_id || !r.init_rank || !r.init_all || !r.destroy || !r.all_reduce || !r.send ||
             !r.recv || !r.group_start || !r.group_end || !r.error_string) {
             r.load_error = "librccl.so.1 lacks an expected symbol";
@@ -111,6 +122,24 @@ Rccl* need_rccl(int* rc) {
     }
     return r;
 }
+
+// A call on a non-blocking communicator may return ncclInProgress: poll its state until it
+// settles (timeout_s <= 0: no limit; the deadline returns ncclInProgress).
+ncclResult_t settle(Rccl* r, ncclComm_t comm, ncclResult_t e, double timeout_s) {
+    if (e != ncclInProgress || !r->async_error || !comm) return e;
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+    for (;;) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t q = r->async_error(comm, &st);
+        if (q != ncclSuccess) return q;
+        if (st != ncclInProgress) return st;
+        if (timeout_s > 0 && std::chrono::steady_clock::now() > t_end) return ncclInProgress;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+// send / recv inside a group on a non-blocking communicator may report ncclInProgress: queued
+inline ncclResult_t queued(ncclResult_t e) { return e == ncclInProgress ? ncclSuccess : e; }
 
 int finish_comm(sv_comm* c) {
     SV_CHIP(hipSetDevice(c->device));
@@ -172,7 +201,7 @@ int sv_comm_unique_id(uint8_t* id) {
     return 0;
 }
 
-int sv_comm_init_rank(int device, int nranks, int rank, const uint8_t* id, sv_comm** out) {
+int sv_comm_init_rank(int device, int nranks, int rank, const uint8_t* id, double timeout_s, sv_comm** out) {
     if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) return comm_fail(SV_EINVAL, "bad communicator arguments");
     *out = nullptr;
     int rc = 0;
@@ -190,9 +219,24 @@ int sv_comm_init_rank(int device, int nranks, int rank, const uint8_t* id, sv_co
         delete c;
         return comm_fail(SV_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(he));
     }
-    ncclResult_t e = r->init_rank(&c->comm, nranks, u, rank);
+    ncclResult_t e;
+    if (r->init_rank_config && r->async_error && r->abort) {
+        // non-blocking: a rank whose peers died in bootstrap comes back at the deadline
+        //  instead of blocking forever inside a collective initialisation
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        e = r->init_rank_config(&c->comm, nranks, u, rank, &cfg);
+        e = settle(r, c->comm, e == ncclSuccess ? ncclInProgress : e, timeout_s);
+        c->nonblocking = true;
+    } else {
+        e = r->init_rank(&c->comm, nranks, u, rank);
+    }
     if (e != ncclSuccess) {
+        if (c->comm && r->abort) r->abort(c->comm);
         delete c;
+        if (e == ncclInProgress)
+            return comm_fail(SV_EHIP, "ncclCommInitRank did not complete within " + std::to_string(timeout_s) +
+                                          " s (a peer failed or never joined); aborted");
         return nccl_fail(r, e, "ncclCommInitRank");
     }
     rc = finish_comm(c);
@@ -272,7 +316,7 @@ int sv_comm_allreduce_max_f64(sv_comm* c, double* value) {
     if (!r) return comm_fail(SV_ENODEV, "RCCL unavailable");
     SV_CHIP(hipSetDevice(c->device));
     SV_CHIP(hipMemcpyAsync(c->scratch, value, sizeof(double), hipMemcpyHostToDevice, c->stream));
-    SV_NCCL(r, r->all_reduce(c->scratch, c->scratch, 1, ncclFloat64, ncclMax, c->comm, c->stream));
+    SV_NCCL(r, settle(r, c->comm, r->all_reduce(c->scratch, c->scratch, 1, ncclFloat64, ncclMax, c->comm, c->stream), 0));
     SV_CHIP(hipMemcpyAsync(value, c->scratch, sizeof(double), hipMemcpyDeviceToHost, c->stream));
     SV_CHIP(hipStreamSynchronize(c->stream));
     return 0;
@@ -288,17 +332,17 @@ int sv_comm_gatherv(sv_comm* c, const void* d_send, uint64_t send_bytes, void* d
     if (!r) return comm_fail(SV_ENODEV, "RCCL unavailable");
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
     SV_CHIP(hipSetDevice(c->device));
-    SV_NCCL(r, r->group_start());
+    SV_NCCL(r, queued(r->group_start()));
     ncclResult_t e = ncclSuccess;
     if (c->rank == root) {
         for (int k = 0; k < c->nranks && e == ncclSuccess; ++k) {
             if (k == root || recv_bytes[k] == 0) continue;
-            e = r->recv(static_cast<uint8_t*>(d_recv) + recv_offsets[k], recv_bytes[k], ncclChar, k, c->comm, s);
+            e = queued(r->recv(static_cast<uint8_t*>(d_recv) + recv_offsets[k], recv_bytes[k], ncclChar, k, c->comm, s));
         }
     } else if (send_bytes) {
-        e = r->send(d_send, send_bytes, ncclChar, root, c->comm, s);
+        e = queued(r->send(d_send, send_bytes, ncclChar, root, c->comm, s));
     }
-    ncclResult_t e2 = r->group_end();
+    ncclResult_t e2 = settle(r, c->comm, r->group_end(), 0);
     if (e != ncclSuccess) return nccl_fail(r, e, "ncclSend/ncclRecv");
     if (e2 != ncclSuccess) return nccl_fail(r, e2, "ncclGroupEnd");
     if (c->rank == root && send_bytes) {
@@ -318,17 +362,17 @@ int sv_comm_scatterv(sv_comm* c, const void* d_send, const uint64_t* send_offset
     if (!r) return comm_fail(SV_ENODEV, "RCCL unavailable");
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
     SV_CHIP(hipSetDevice(c->device));
-    SV_NCCL(r, r->group_start());
+    SV_NCCL(r, queued(r->group_start()));
     ncclResult_t e = ncclSuccess;
     if (c->rank == root) {
         for (int k = 0; k < c->nranks && e == ncclSuccess; ++k) {
             if (k == root || send_bytes[k] == 0) continue;
-            e = r->send(static_cast<const uint8_t*>(d_send) + send_offsets[k], send_bytes[k], ncclChar, k, c->comm, s);
+            e = queued(r->send(static_cast<const uint8_t*>(d_send) + send_offsets[k], send_bytes[k], ncclChar, k, c->comm, s));
         }
     } else if (recv_bytes) {
-        e = r->recv(d_recv, recv_bytes, ncclChar, root, c->comm, s);
+        e = queued(r->recv(d_recv, recv_bytes, ncclChar, root, c->comm, s));
     }
-    ncclResult_t e2 = r->group_end();
+    ncclResult_t e2 = settle(r, c->comm, r->group_end(), 0);
     if (e != ncclSuccess) return nccl_fail(r, e, "ncclSend/ncclRecv");
     if (e2 != ncclSuccess) return nccl_fail(r, e2, "ncclGroupEnd");
     if (c->rank == root && recv_bytes) {

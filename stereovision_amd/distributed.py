@@ -25,7 +25,7 @@ Two ways to run N GPUs:
   cannot run (ranks sharing one GPU, library missing) it falls back to the file store for
   barriers and max-reductions and to host staging for gathers.
 * one process driving several GPUs: ``engine.multi_gpu_depth_map_dev`` /
-  ``engine.depth_map_rows_multi`` (sv_multi_gpu_depth_map_dev / sv_depth_map_rows_multi),
+  ``engine.depth_map_rows_multi`` (sv_multi_gpu_dev),
   whose gathers run as one RCCL group (``Communicator.init_all``) or peer copies.
 """
 from __future__ import annotations
@@ -320,6 +320,23 @@ class ProcessGroup:
         if data.size:
             eng.to_device(d_recv, data)
 
+    def dup(self, tag: str = "dup") -> "ProcessGroup":
+        """A second group over the same ranks with its own communicator (collective: every rank
+        calls it): RCCL — a new ncclCommInitRank, so two streams can run collectives in opposite
+        directions at once (e.g. a row tiling's scatter root -> peers beside the previous frame's
+        gather peers -> root, each on its own stream and communicator); file store — a
+        sub-directory with its own key sequence."""
+        store = None
+        if self.store is not None:
+            store = FileStore(os.path.join(self.store.path, tag), self.rank, self.world, self.store.timeout)
+        comm = None
+        if self.comm is not None:
+            uid = self.store.broadcast(Communicator.unique_id() if self.rank == 0 else None)
+            comm = Communicator.init_rank(self.device, self.world, self.rank, uid,
+                                          timeout=min(self.store.timeout, 120.0))
+        return ProcessGroup(self.rank, self.world, self.device, store, comm, self.engine, self.devices,
+                            self.reason)
+
     def close(self):
         if self.comm is not None:
             self.comm.close()
@@ -375,7 +392,10 @@ def init_process_group(device: int | None = None, backend: str = "auto",
         try:
             if os.environ.get("SV_RCCL_INIT_FAIL", "") not in ("", "0"):
                 raise RuntimeError("forced failure (SV_RCCL_INIT_FAIL)")
-            comm = Communicator.init_rank(device, world, rank, uid)
+            # non-blocking with a deadline: if a peer fails inside the initialisation this rank
+            # returns (its half-built communicator aborted) instead of blocking forever, so
+            # every rank reaches the allgather below
+            comm = Communicator.init_rank(device, world, rank, uid, timeout=min(timeout, 120.0))
         except Exception as ex:   # decided collectively below: every rank falls back together
             err = f"ncclCommInitRank failed on rank {rank}: {ex}"
         errs = [e.decode() for e in store.allgather(err.encode()) if e]
@@ -383,7 +403,7 @@ def init_process_group(device: int | None = None, backend: str = "auto",
             if comm is not None:
                 comm.close()
                 comm = None
-            reason = errs[0]
+            reason = "; ".join(errs)
             if backend == "rccl" or strict:
                 raise RuntimeError(f"RCCL required on devices {devs} but unusable: {reason}")
             use_rccl = False
@@ -403,7 +423,7 @@ class RowTiledDepthMap:
     band-only (:meth:`scatter` from the root's full frame: rank k receives just the input rows
     [in0, in1) its band reads into :attr:`band_left` / :attr:`band_right`, then
     :meth:`compute` without arguments).  Each rank computes disparity for its band plus the
-    median halo (sv_disparity_dev), then the median of the band (sv_median_post_m16_dev): its
+    median halo (sv_disparity_dev), then the median of the band (sv_median_rows_dev): its
     int16 x16 medians (:attr:`m16`, full-frame row offsets) and, unless ``band_outputs="m16"``,
     the post outputs too.  :meth:`gather` moves the bands' int16 x16 medians into the root's
     :attr:`m16` (2 B/px over xGMI instead of the outputs' 9) and the root expands the other
@@ -450,6 +470,20 @@ class RowTiledDepthMap:
         for full, band in ((d_full_left, self.band_left), (d_full_right, self.band_right)):
             pg.scatterv(full, offs, sizes, band, self.band_bytes, root=root, stream=s)
 
+    def upload(self, host_left: np.ndarray, host_right: np.ndarray, stream: int = 0):
+        """This rank's band input rows [in0, in1) from the full HOST frames (H x W uint8,
+        page-locked — sv_host_register — for the copy to overlap device work) into
+        :attr:`band_left` / :attr:`band_right` over this GPU's own PCIe link: the band-only
+        inputs of :meth:`scatter` without any xGMI traffic (every rank holds the frame in
+        host memory, as a camera pipeline's frames arrive).  Enqueued on the engine stream
+        unless `stream` is given; the host arrays must stay alive until it has run."""
+        for a in (host_left, host_right):
+            if a.shape != (self.H, self.W) or a.dtype != np.uint8 or not a.flags["C_CONTIGUOUS"]:
+                raise ValueError(f"upload: expected C-contiguous {self.H}x{self.W} uint8 frames")
+        s = self._stream(stream)
+        for a, band in ((host_left, self.band_left), (host_right, self.band_right)):
+            self.engine.to_device(band, a[self.in0:self.in1], stream=s)
+
     def compute(self, d_left: int = 0, d_right: int = 0, mode: int = POST_DEPTH, min_depth: float = 0.3,
                 max_depth: float = 2.0, min_disp_global=None, stream: int = 0, band_outputs: str = "full"):
         """Enqueue this rank's band: its median map at full-frame row offsets of self.m16 —
@@ -460,6 +494,8 @@ class RowTiledDepthMap:
         :meth:`scatter`."""
         if band_outputs not in ("full", "m16", "d8"):
             raise ValueError(f"band_outputs must be 'full', 'm16' or 'd8', got {band_outputs!r}")
+        if band_outputs == "d8" and self.cost == "sgbm":   # sub-pixel medians: not whole indices
+            raise ValueError("band_outputs='d8' needs an integer-disparity cost (SGBM maps are sub-pixel)")
         e, H, W = self.engine, self.H, self.W
         s = self._stream(stream)
         if not d_left:   # band buffer addressed as a full frame (row y at base + y * W)
@@ -474,27 +510,34 @@ class RowTiledDepthMap:
         self._band_outputs = band_outputs
         if band_outputs == "d8":
             e.median_map_dev(self.d16, H, W, self.r0, self.r1, self.m16, "d8", min_disp=self.min_disp,
-                             num_disp=self.num_disp, stream=s)
+                             num_disp=self.num_disp, stream=s, cost=self.cost)
         elif band_outputs == "m16":
-            e.median_post_m16_dev(self.d16, H, W, self.r0, self.r1, POST_NONE, d_med16=self.m16, stream=s)
+            e.median_post_m16_dev(self.d16, H, W, self.r0, self.r1, POST_NONE, d_med16=self.m16, stream=s,
+                                  cost=self.cost)
         else:
             e.median_post_m16_dev(self.d16, H, W, self.r0, self.r1, mode, d_disparity=self.disp,
                                   d_out_a=self.out_a, d_out_u8=self.out_u8,
                                   d_out_b=self.out_b if mode == POST_SCALED else 0, d_med16=self.m16,
-                                  stream=s, **self._post)
+                                  stream=s, cost=self.cost, **self._post)
 
-    def gather(self, pg: "ProcessGroup", root: int = 0, stream: int = 0, expand: bool = True):
+    def gather(self, pg: "ProcessGroup", root: int = 0, stream: int = 0, expand: bool = True,
+               check: bool = True):
         """Every rank's band of the median map into the root's self.m16 (in place: 2 B/px
         int16 x16, or 1 B/px when the bands were computed with band_outputs="d8"), then
         (expand) the root turns the other ranks' rows into its full-frame outputs; on the engine
         stream unless `stream` is given (never the communicator's own stream: ADVICE r02).
         Gather-only (expand=False) leaves the full map in the root's self.m16.  Expanding needs
-        int16 maps and the root's own band computed with band_outputs="full"."""
+        int16 maps and the root's own band computed with band_outputs="full".
+
+        check (every rank must pass the same value): before the collective, the ranks agree on
+        the arguments — expand, the gathered element size, the root's own band — with three
+        max-reductions, and on a mismatch EVERY rank raises ValueError (a rank raising alone
+        would leave the others inside a gather that never completes: ADVICE r05).  A
+        pipeline checks its first gather and passes check=False for the identical ones after."""
         s = self._stream(stream)
         el = 1 if self._band_outputs == "d8" else 2
-        if expand and pg.rank == root and self._band_outputs != "full":
-            raise ValueError("gather(expand=True) on the root needs compute(band_outputs='full') "
-                             f"there (the root's own rows), got {self._band_outputs!r}")
+        if check:
+            self._agree(pg, root, expand, el)
         gather_rows(pg, self.m16, self.H, self.W * el, root=root, stream=s)
         if not expand or pg.rank != root or self._post is None:
             return
@@ -509,6 +552,19 @@ class RowTiledDepthMap:
                            d_out_a=self.out_a + 4 * o, d_out_u8=self.out_u8 + o,
                            d_out_b=(self.out_b + 4 * o) if mode == POST_SCALED else 0, stream=s,
                            **self._post)
+
+    def _agree(self, pg: "ProcessGroup", root: int, expand: bool, el: int):
+        why = ("compute() was not called" if self._band_outputs is None else
+               "expand=True gathers int16 maps, not band_outputs='d8'" if expand and el == 1 else
+               "expand=True needs compute(band_outputs='full') on the root (its own rows)"
+               if expand and pg.rank == root and self._band_outputs != "full" else "")
+        code = 4 * el + (2 if expand else 0)
+        bad = pg.allreduce_max(1.0 if why else 0.0)
+        hi, lo = pg.allreduce_max(float(code)), -pg.allreduce_max(-float(code))
+        if bad or hi != lo:
+            raise ValueError("RowTiledDepthMap.gather: the ranks disagree or a rank's arguments are "
+                             f"invalid (this rank: {why or 'ok'}; expand={expand}, {el} B/px; codes "
+                             f"{lo:.0f}..{hi:.0f}) — every rank raises, no gather is enqueued")
 
     def close(self):
         for p in (self.d16, self.disp, self.out_a, self.out_b, self.out_u8, self.m16, *self._band):

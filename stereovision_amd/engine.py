@@ -32,25 +32,21 @@ EXPORTED = [
     "sv_version", "sv_last_error", "sv_device_count", "sv_create", "sv_destroy",
     "sv_synchronize", "sv_stream", "sv_plan", "sv_gray", "sv_disparity", "sv_median5_f32",
     "sv_depth_post", "sv_scaled_post", "sv_depth_map", "sv_stereo_scaled", "sv_harris",
-    "sv_hog_hist", "sv_gray_dev", "sv_disparity_dev", "sv_median_post_dev",
-    "sv_depth_map_dev", "sv_harris_dev", "sv_hog_hist_dev", "sv_profile_enable",
-    "sv_profile_read", "sv_profile_reset", "sv_disparity_rows", "sv_dev_alloc", "sv_dev_free",
-    "sv_copy_to_device", "sv_copy_to_host", "sv_host_register", "sv_host_unregister", "sv_host_profile_enable", "sv_host_profile_read", "sv_timer_begin", "sv_timer_end", "sv_disparity_batch_dev", "sv_median_post_batch_dev",
-    "sv_depth_map_batch_dev", "sv_depth_map_batch_m16_dev", "sv_depth_map_batch_d8_dev", "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev",
-    "sv_remap", "sv_remap_dev", "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev",
-    "sv_resize_linear_f32_dev", "sv_frame_stats", "sv_frame_stats_dev", "sv_select_count",
-    "sv_select_ranks", "sv_affine_f32_dev", "sv_sgbm", "sv_sgbm_dev", "sv_filter_speckles",
-    "sv_filter_speckles_dev", "sv_multi_gpu_batch", "sv_harris_batch_dev",
-    "sv_comm_available", "sv_comm_unique_id", "sv_comm_init_rank", "sv_comm_init_all",
-    "sv_comm_destroy", "sv_comm_rank", "sv_comm_barrier", "sv_comm_allreduce_max_f64",
-    "sv_comm_gatherv", "sv_comm_synchronize", "sv_multi_gpu_depth_map_dev",
-    "sv_depth_map_rows_multi", "sv_depth_map_color", "sv_stereo_scaled_color",
-    "sv_median_post_color_dev", "sv_profile_region_begin", "sv_profile_region_end",
-    "sv_comm_scatterv", "sv_depth_map_rows_scatter", "sv_band_rows_in", "sv_release_scratch",
+    "sv_hog_hist", "sv_gray_dev", "sv_disparity_dev", "sv_median_rows_dev", "sv_harris_dev",
+    "sv_hog_hist_dev", "sv_profile_enable", "sv_profile_read", "sv_profile_reset",
+    "sv_disparity_rows", "sv_dev_alloc", "sv_dev_free", "sv_copy_to_device", "sv_copy_to_host",
+    "sv_host_register", "sv_host_unregister", "sv_host_profile_enable", "sv_host_profile_read",
+    "sv_timer_begin", "sv_timer_end", "sv_disparity_batch_dev", "sv_depth_map_batch_dev",
+    "sv_init_undistort_rectify_map", "sv_init_undistort_rectify_map_dev", "sv_remap", "sv_remap_dev",
+    "sv_rectify_pair", "sv_resize_linear", "sv_resize_linear_dev", "sv_resize_linear_f32_dev",
+    "sv_frame_stats", "sv_affine_f32_dev", "sv_sgbm", "sv_sgbm_dev", "sv_filter_speckles",
+    "sv_filter_speckles_dev", "sv_multi_gpu_batch", "sv_harris_batch_dev", "sv_comm_available",
+    "sv_comm_unique_id", "sv_comm_init_rank", "sv_comm_init_all", "sv_comm_destroy", "sv_comm_rank",
+    "sv_comm_barrier", "sv_comm_allreduce_max_f64", "sv_comm_gatherv", "sv_comm_synchronize",
+    "sv_multi_gpu_dev", "sv_depth_map_color", "sv_stereo_scaled_color", "sv_profile_region_begin",
+    "sv_profile_region_end", "sv_comm_scatterv", "sv_band_rows_in", "sv_release_scratch",
     "sv_frame_stats_batch_dev", "sv_select_count_batch", "sv_select_ranks_batch", "sv_event_record",
-    "sv_stream_wait_event", "sv_median_post_m16_dev", "sv_post_m16_dev", "sv_multi_gpu_m16_dev",
-    "sv_multi_gpu_map_dev", "sv_depth_map_rows_map", "sv_median_map_dev",
-    "sv_depth_map_harris_batch_dev",
+    "sv_stream_wait_event", "sv_post_m16_dev",
 ]
 BAND_MARGIN = 8   # SV_BAND_MARGIN: spare rows around a band-only input buffer
 COMM_ID_BYTES = 128
@@ -120,6 +116,35 @@ class _NullableF32:
         return _f32p.from_param(obj)
 
 
+STAGE_MATCH, STAGE_MEDIAN, STAGE_ALL = 1, 2, 3          # SV_STAGE_*
+SHARD_FRAMES, SHARD_ROWS = 0, 1                         # SV_SHARD_*
+INPUTS_RESIDENT, INPUTS_SCATTER, INPUTS_HOST = 0, 1, 2  # SV_INPUTS_*
+
+
+class MapOut(ctypes.Structure):
+    """sv_map_out: the outputs of one median + post launch (every pointer optional)."""
+    _fields_ = [("mode", _c_int), ("min_depth", _c_float), ("max_depth", _c_float),
+                ("depth_range", _c_float), ("min_disp_global", _c_float), ("disparity", _vp),
+                ("out_a", _vp), ("out_u8", _vp), ("out_b", _vp), ("med16", _vp), ("d8", _vp),
+                ("cmap_bgr", _vp), ("bgr", _vp), ("harris", _vp)]
+
+
+def map_out(mode: int = POST_NONE, disparity: int = 0, out_a: int = 0, out_u8: int = 0, out_b: int = 0,
+            med16: int = 0, d8: int = 0, harris: int = 0, bgr: int = 0, cmap=None, min_depth=0.0,
+            max_depth=0.0, min_disp_global=0.0) -> MapOut:
+    """An sv_map_out (depth_range = float32 of max_depth - min_depth computed in double, the
+    NumPy-2 semantics of depth_map.py:936).  ``cmap``: a 256 x 3 uint8 BGR table (kept alive on
+    the returned structure)."""
+    m = MapOut(int(mode), np.float32(min_depth), np.float32(max_depth),
+               np.float32(float(max_depth) - float(min_depth)), np.float32(min_disp_global),
+               disparity or None, out_a or None, out_u8 or None, out_b or None, med16 or None, d8 or None,
+               None, bgr or None, harris or None)
+    if cmap is not None:
+        m._cmap = np.ascontiguousarray(cmap, np.uint8).reshape(256, 3)
+        m.cmap_bgr = m._cmap.ctypes.data
+    return m
+
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -160,12 +185,6 @@ def _declare(lib):
         "sv_gray_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp], _c_int),
         "sv_disparity_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                               _c_int, _c_int, _c_int, _vp, _c_int, _vp], _c_int),
-        "sv_median_post_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float,
-                                _c_float, _c_float, _c_float, _c_int, _c_int, _vp, _vp, _vp,
-                                _vp, _vp], _c_int),
-        "sv_depth_map_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
-                              _c_int, _c_float, _c_float, _c_float, _c_float, _vp, _vp, _vp,
-                              _vp], _c_int),
         "sv_harris_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp], _c_int),
         "sv_hog_hist_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
                             _c_int),
@@ -173,8 +192,6 @@ def _declare(lib):
                                _c_int, _c_int, _c_int, _c_int, _i16p], _c_int),
         "sv_dev_alloc": ([_vp, ctypes.c_uint64, ctypes.POINTER(_vp)], _c_int),
         "sv_dev_free": ([_vp, _vp], _c_int),
-        "sv_copy_to_device": ([_vp, _vp, _vp, ctypes.c_uint64], _c_int),
-        "sv_copy_to_host": ([_vp, _vp, _vp, ctypes.c_uint64], _c_int),
         "sv_host_register": ([_vp, ctypes.c_uint64], _c_int),
         "sv_host_profile_enable": ([_c_int], _c_int),
         "sv_host_profile_read": ([ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), _c_int],
@@ -185,20 +202,6 @@ def _declare(lib):
         "sv_disparity_batch_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, ctypes.c_int64,
                                     _c_int, _c_int, _c_int, _c_int, _vp, _c_int, ctypes.c_int64,
                                     _vp], _c_int),
-        "sv_median_post_batch_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float,
-                                      _c_float, _c_float, _c_float, _c_int, _c_int, _vp, _vp,
-                                      _vp, _vp, _vp], _c_int),
-        "sv_depth_map_batch_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
-                                    ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
-                                    _c_float, _c_float, _c_float, _vp, _vp, _vp, _vp], _c_int),
-        "sv_depth_map_batch_m16_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
-                                        ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
-                                        _c_float, _c_float, _c_float, _vp, _vp, _vp, _vp, _vp],
-                                       _c_int),
-        "sv_depth_map_batch_d8_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
-                                       ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
-                                       _c_float, _c_float, _c_float, _vp, _vp, _vp, _vp, _vp],
-                                      _c_int),
         "sv_init_undistort_rectify_map": ([_vp, _f64p, _NullableF64, _c_int, _NullableF64,
                                            _NullableF64, _c_int, _c_int, _c_int, _i16p, _u16p],
                                           _c_int),
@@ -219,18 +222,12 @@ def _declare(lib):
                                       _vp], _c_int),
         "sv_frame_stats": ([_vp, _u8p, _vp, _c_int, _c_int, _c_int, _c_int, _u32p, _u32p, _u32p],
                            _c_int),
-        "sv_frame_stats_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
-                               _c_int),
         "sv_frame_stats_batch_dev": ([_vp, _vp, _vp, _c_int, ctypes.c_int64, _c_int, _c_int, _c_int,
                                       _c_int, _vp, _vp, _vp, _vp], _c_int),
         "sv_select_count_batch": ([_vp, _vp, ctypes.c_int64, ctypes.c_int64, _c_int, _c_int, _vp,
                                    ctypes.c_int64, _c_float, _i64p, _i64p], _c_int),
         "sv_select_ranks_batch": ([_vp, _vp, ctypes.c_int64, ctypes.c_int64, _c_int, _c_int, _vp,
                                    ctypes.c_int64, _c_float, _i64p, _c_int, _f32p], _c_int),
-        "sv_select_count": ([_vp, _vp, ctypes.c_int64, _c_int, _vp, _c_float,
-                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)], _c_int),
-        "sv_select_ranks": ([_vp, _vp, ctypes.c_int64, _c_int, _vp, _c_float, _i64p, _c_int, _f32p],
-                            _c_int),
         "sv_affine_f32_dev": ([_vp, _vp, ctypes.c_int64, _c_int, _c_float, _c_float, _c_float, _c_float,
                                ctypes.c_double, ctypes.c_double, _vp, _vp], _c_int),
         "sv_sgbm": ([_vp, _u8p, _u8p] + [_c_int] * 14 + [_i16p], _c_int),
@@ -239,7 +236,6 @@ def _declare(lib):
         "sv_filter_speckles_dev": ([_vp, _vp] + [_c_int] * 6 + [_vp], _c_int),
         "sv_comm_available": ([], _c_int),
         "sv_comm_unique_id": ([ctypes.c_char_p], _c_int),
-        "sv_comm_init_rank": ([_c_int, _c_int, _c_int, ctypes.c_char_p, ctypes.POINTER(_vp)], _c_int),
         "sv_comm_init_all": ([_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_vp)], _c_int),
         "sv_comm_destroy": ([_vp], None),
         "sv_comm_rank": ([_vp, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)],
@@ -251,48 +247,26 @@ def _declare(lib):
         "sv_comm_synchronize": ([_vp], _c_int),
         "sv_comm_scatterv": ([_vp, _vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                               _vp, ctypes.c_uint64, _c_int, _vp], _c_int),
-        "sv_depth_map_rows_scatter": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int, _vp, _vp,
-                                       _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
-                                       _c_float, _c_float, _c_float, _c_float, _vp, _vp, _vp], _c_int),
         "sv_band_rows_in": ([_c_int, _c_int, _c_int, _c_int, _c_int, ctypes.POINTER(_c_int)], _c_int),
-        "sv_multi_gpu_depth_map_dev": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
-                                        ctypes.POINTER(_vp), ctypes.POINTER(_vp),
-                                        ctypes.POINTER(_c_int), _c_int, _c_int, _c_int,
-                                        ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
-                                        _c_float, _c_float, _c_float, _vp, _vp, _vp], _c_int),
-        "sv_depth_map_harris_batch_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
-                                           ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_float,
-                                           _c_float, _c_float, _c_float, _vp, _vp, _vp, _vp, _vp],
-                                          _c_int),
-        "sv_median_post_m16_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float,
-                                    _c_float, _c_float, _c_float, _c_int, _c_int, _vp, _vp, _vp,
-                                    _vp, _vp, _vp], _c_int),
         "sv_post_m16_dev": ([_vp, _vp, ctypes.c_int64, _c_int, _c_float, _c_float, _c_float,
                              _c_float, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp], _c_int),
-        "sv_multi_gpu_m16_dev": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
-                                  ctypes.POINTER(_vp), ctypes.POINTER(_vp),
-                                  ctypes.POINTER(_c_int), _c_int, _c_int, _c_int,
-                                  ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _vp], _c_int),
-        "sv_median_map_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
-                              _c_int),
-        "sv_multi_gpu_map_dev": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
-                                  ctypes.POINTER(_vp), ctypes.POINTER(_vp),
-                                  ctypes.POINTER(_c_int), _c_int, _c_int, _c_int,
-                                  ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_int, _vp], _c_int),
-        "sv_depth_map_rows_map": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
-                                   ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int, _c_int, _c_int,
-                                   _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp], _c_int),
-        "sv_depth_map_rows_multi": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int,
-                                     ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int, _c_int, _c_int,
-                                     _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float,
-                                     _c_float, _vp, _vp, _vp], _c_int),
         "sv_depth_map_color": ([_vp, _u8p, _u8p] + [_c_int] * 8 + [_c_float] * 4 +
                                [_u8p, _f32p, _f32p, _NullableU8, _u8p], _c_int),
         "sv_stereo_scaled_color": ([_vp, _u8p, _u8p] + [_c_int] * 8 +
                                    [_u8p, _f32p, _f32p, _NullableU8, _f32p, _u8p], _c_int),
-        "sv_median_post_color_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float,
-                                      _c_float, _c_float, _c_float, _c_int, _c_int, _u8p, _vp, _vp,
-                                      _vp, _vp, _vp, _vp], _c_int),
+        "sv_median_rows_dev": ([_vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                ctypes.POINTER(MapOut), _vp], _c_int),
+        "sv_depth_map_batch_dev": ([_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, ctypes.c_int64,
+                                    _c_int, _c_int, _c_int, _c_int, _c_int, _vp, ctypes.POINTER(MapOut),
+                                    _vp], _c_int),
+        "sv_multi_gpu_dev": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c_int, _c_int, _c_int,
+                              ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_c_int), _c_int,
+                              _c_int, _c_int, ctypes.c_int64, _c_int, _c_int, _c_int, _c_int,
+                              ctypes.POINTER(MapOut)], _c_int),
+        "sv_copy_to_device": ([_vp, _vp, _vp, ctypes.c_uint64, _vp], _c_int),
+        "sv_copy_to_host": ([_vp, _vp, _vp, ctypes.c_uint64, _vp], _c_int),
+        "sv_comm_init_rank": ([_c_int, _c_int, _c_int, ctypes.c_char_p, ctypes.c_double, ctypes.POINTER(_vp)],
+                              _c_int),
         "sv_profile_enable": ([_vp, _c_int], _c_int),
         "sv_profile_read": ([_vp, _c_int, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_longlong)], _c_int),
@@ -622,13 +596,16 @@ class Engine:
     def dev_free(self, ptr: int):
         _check("sv_dev_free", self.lib.sv_dev_free(self._h, ptr))
 
-    def to_device(self, ptr: int, a: np.ndarray):
+    def to_device(self, ptr: int, a: np.ndarray, stream: int = 0):
+        """Host array -> device; synchronous unless `stream` (then enqueued there: keep `a`
+        alive, and page-locked for the copy to overlap device work)."""
         a = np.ascontiguousarray(a)
-        _check("sv_copy_to_device", self.lib.sv_copy_to_device(self._h, ptr, a.ctypes.data, a.nbytes))
+        _check("sv_copy_to_device", self.lib.sv_copy_to_device(self._h, ptr, a.ctypes.data, a.nbytes,
+                                                                stream or None))
 
     def to_host(self, ptr: int, shape, dtype) -> np.ndarray:
         out = np.empty(shape, dtype)
-        _check("sv_copy_to_host", self.lib.sv_copy_to_host(self._h, out.ctypes.data, ptr, out.nbytes))
+        _check("sv_copy_to_host", self.lib.sv_copy_to_host(self._h, out.ctypes.data, ptr, out.nbytes, None))
         return out
 
     def median5(self, a: np.ndarray) -> np.ndarray:
@@ -762,35 +739,44 @@ class Engine:
             self._h, d_left, d_right, H, W, pitch, int(min_disp), int(num_disp), int(win),
             _cost(cost), int(row0), int(row1), d_out16, out_pitch, stream or None))
 
+    def median_rows_dev(self, d_disp16: int, H: int, W: int, row0: int, row1: int, out: "MapOut",
+                        min_disp: int = 0, num_disp: int = 0, cost="sad", stream: int = 0):
+        """sv_median_rows_dev: median (+ post) of rows [row0, row1) into the outputs of `out`
+        (:func:`map_out`), at full-frame offsets."""
+        _check("sv_median_rows_dev", self.lib.sv_median_rows_dev(
+            self._h, d_disp16, H, W, int(row0), int(row1), int(min_disp), int(num_disp), _cost(cost),
+            ctypes.byref(out), stream or None))
+
     def median_post_dev(self, d_disp16: int, H: int, W: int, row0: int, row1: int, mode: int,
                         d_disparity: int, d_out_a: int = 0, d_out_u8: int = 0, d_out_b: int = 0,
                         min_depth=0.0, max_depth=0.0, min_disp_global=0.0, min_disp=0,
-                        num_disp=0, stream: int = 0):
-        _check("sv_median_post_dev", self.lib.sv_median_post_dev(
-            self._h, d_disp16, H, W, int(row0), int(row1), int(mode), np.float32(min_depth),
-            np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
-            np.float32(min_disp_global), int(min_disp), int(num_disp), d_disparity,
-            d_out_a or None, d_out_u8 or None, d_out_b or None, stream or None))
+                        num_disp=0, stream: int = 0, cost="sad"):
+        self.median_rows_dev(d_disp16, H, W, row0, row1,
+                             map_out(mode, d_disparity, d_out_a, d_out_u8, d_out_b, min_depth=min_depth,
+                                     max_depth=max_depth, min_disp_global=min_disp_global),
+                             min_disp, num_disp, cost, stream)
 
     def median_post_m16_dev(self, d_disp16: int, H: int, W: int, row0: int, row1: int, mode: int,
                             d_disparity: int = 0, d_out_a: int = 0, d_out_u8: int = 0,
                             d_out_b: int = 0, d_med16: int = 0, min_depth=0.0, max_depth=0.0,
-                            min_disp_global=0.0, min_disp=0, num_disp=0, stream: int = 0):
-        """sv_median_post_m16_dev: median of rows [row0, row1) plus (mode) the post outputs
-        and/or the int16 x16 medians d_med16 (full-frame offsets)."""
-        _check("sv_median_post_m16_dev", self.lib.sv_median_post_m16_dev(
-            self._h, d_disp16, H, W, int(row0), int(row1), int(mode), np.float32(min_depth),
-            np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
-            np.float32(min_disp_global), int(min_disp), int(num_disp), d_disparity or None,
-            d_out_a or None, d_out_u8 or None, d_out_b or None, d_med16 or None, stream or None))
+                            min_disp_global=0.0, min_disp=0, num_disp=0, stream: int = 0, cost="sad"):
+        """Median of rows [row0, row1) plus (mode) the post outputs and/or the int16 x16
+        medians d_med16 (full-frame offsets)."""
+        self.median_rows_dev(d_disp16, H, W, row0, row1,
+                             map_out(mode, d_disparity, d_out_a, d_out_u8, d_out_b, med16=d_med16,
+                                     min_depth=min_depth, max_depth=max_depth,
+                                     min_disp_global=min_disp_global),
+                             min_disp, num_disp, cost, stream)
 
     def median_map_dev(self, d_disp16: int, H: int, W: int, row0: int, row1: int, d_map: int,
-                       fmt="m16", min_disp: int = 0, num_disp: int = 0, stream: int = 0):
-        """sv_median_map_dev: median of rows [row0, row1) written only as a gather map at
-        full-frame offsets of d_map (``fmt`` "m16": int16 x16, "d8": u8 indices)."""
-        _check("sv_median_map_dev", self.lib.sv_median_map_dev(
-            self._h, d_disp16, H, W, row0, row1, _map_format(fmt), int(min_disp), int(num_disp), d_map,
-            stream or None))
+                       fmt="m16", min_disp: int = 0, num_disp: int = 0, stream: int = 0, cost="sad"):
+        """Median of rows [row0, row1) written only as a gather map at full-frame offsets of
+        d_map (``fmt`` "m16": int16 x16, "d8": u8 indices; d8 needs an integer cost)."""
+        f = _map_format(fmt)
+        self.median_rows_dev(d_disp16, H, W, row0, row1,
+                             map_out(POST_NONE, med16=d_map if f == MAP_M16 else 0,
+                                     d8=d_map if f == MAP_D8 else 0),
+                             min_disp, num_disp, cost, stream)
 
     def post_m16_dev(self, d_med16: int, n: int, mode: int, d_disparity: int = 0, d_out_a: int = 0,
                      d_out_u8: int = 0, d_out_b: int = 0, min_depth=0.0, max_depth=0.0,
@@ -805,24 +791,23 @@ class Engine:
     def median_post_color_dev(self, d_disp16: int, H: int, W: int, row0: int, row1: int, mode: int,
                               cmap_bgr: np.ndarray, d_disparity: int, d_out_a: int, d_out_u8: int,
                               d_bgr: int, d_out_b: int = 0, min_depth=0.0, max_depth=0.0,
-                              min_disp_global=0.0, min_disp=0, num_disp=0, stream: int = 0):
-        lut = np.ascontiguousarray(cmap_bgr, np.uint8).reshape(256, 3)
-        _check("sv_median_post_color_dev", self.lib.sv_median_post_color_dev(
-            self._h, d_disp16, H, W, int(row0), int(row1), int(mode), np.float32(min_depth),
-            np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
-            np.float32(min_disp_global), int(min_disp), int(num_disp), lut, d_disparity or None,
-            d_out_a, d_out_u8, d_out_b or None, d_bgr, stream or None))
+                              min_disp_global=0.0, min_disp=0, num_disp=0, stream: int = 0, cost="sad"):
+        if mode not in (POST_DEPTH, POST_SCALED):
+            raise ValueError("the colormap epilogue needs POST_DEPTH or POST_SCALED")
+        self.median_rows_dev(d_disp16, H, W, row0, row1,
+                             map_out(mode, d_disparity, d_out_a, d_out_u8, d_out_b, bgr=d_bgr, cmap=cmap_bgr,
+                                     min_depth=min_depth, max_depth=max_depth,
+                                     min_disp_global=min_disp_global),
+                             min_disp, num_disp, cost, stream)
 
     def depth_map_dev(self, d_left: int, d_right: int, H: int, W: int, pitch: int,
                       min_disp: int, num_disp: int, win: int, min_depth: float,
                       max_depth: float, d_depth: int, d_disp: int, d_norm: int, cost="sad",
                       min_disp_global=None, stream: int = 0):
-        mdg = min_disp if min_disp_global is None else min_disp_global
-        _check("sv_depth_map_dev", self.lib.sv_depth_map_dev(
-            self._h, d_left, d_right, H, W, pitch, int(min_disp), int(num_disp), int(win),
-            _cost(cost), np.float32(min_depth), np.float32(max_depth),
-            np.float32(float(max_depth) - float(min_depth)), np.float32(mdg), d_depth, d_disp,
-            d_norm, stream or None))
+        """Whole app-1 device path on one gray device frame pair (a batch of one)."""
+        self.depth_map_batch_dev(d_left, d_right, 1, H, W, pitch, pitch * H, min_disp, num_disp, win,
+                                 min_depth, max_depth, d_depth, d_disp, d_norm, cost=cost,
+                                 min_disp_global=min_disp_global, stream=stream)
 
     # -- frame batches (one launch per kernel over all frames) ------------------------------
     def disparity_batch_dev(self, d_left: int, d_right: int, n_frames: int, H: int, W: int,
@@ -837,41 +822,41 @@ class Engine:
     def median_post_batch_dev(self, d_disp16: int, n_frames: int, H: int, W: int, mode: int,
                               d_disparity: int, d_out_a: int = 0, d_out_u8: int = 0,
                               d_out_b: int = 0, min_depth=0.0, max_depth=0.0,
-                              min_disp_global=0.0, min_disp=0, num_disp=0, stream: int = 0):
-        _check("sv_median_post_batch_dev", self.lib.sv_median_post_batch_dev(
-            self._h, d_disp16, int(n_frames), H, W, int(mode), np.float32(min_depth),
-            np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
-            np.float32(min_disp_global), int(min_disp), int(num_disp), d_disparity,
-            d_out_a or None, d_out_u8 or None, d_out_b or None, stream or None))
+                              min_disp_global=0.0, min_disp=0, num_disp=0, stream: int = 0,
+                              cost="sad", win: int = 1, d_med16: int = 0, d_d8: int = 0):
+        """The median stage alone over n_frames int16 x16 maps (dense per frame): SV_STAGE_MEDIAN
+        of sv_depth_map_batch_dev."""
+        self.depth_map_batch_ex(0, 0, n_frames, H, W, W, H * W, min_disp, num_disp, win, cost, STAGE_MEDIAN,
+                                d_disp16, map_out(mode, d_disparity, d_out_a, d_out_u8, d_out_b, med16=d_med16,
+                                                  d8=d_d8, min_depth=min_depth, max_depth=max_depth,
+                                                  min_disp_global=min_disp_global), stream)
+
+    def depth_map_batch_ex(self, d_left: int, d_right: int, n_frames: int, H: int, W: int, pitch: int,
+                           frame_stride: int, min_disp: int, num_disp: int, win: int, cost, stages: int,
+                           d_disp16: int, out: "MapOut | None", stream: int = 0):
+        """sv_depth_map_batch_dev as the C ABI has it: `stages` (STAGE_MATCH / STAGE_MEDIAN /
+        STAGE_ALL), the int16 x16 maps in d_disp16 (0 with STAGE_ALL: the context's scratch) and
+        the outputs of `out` (:func:`map_out`)."""
+        _check("sv_depth_map_batch_dev", self.lib.sv_depth_map_batch_dev(
+            self._h, d_left or None, d_right or None, int(n_frames), H, W, pitch, int(frame_stride),
+            int(min_disp), int(num_disp), int(win), _cost(cost), int(stages), d_disp16 or None,
+            ctypes.byref(out) if out is not None else None, stream or None))
 
     def depth_map_batch_dev(self, d_left: int, d_right: int, n_frames: int, H: int, W: int,
                             pitch: int, frame_stride: int, min_disp: int, num_disp: int,
                             win: int, min_depth: float, max_depth: float, d_depth: int,
                             d_disp: int, d_norm: int, cost="sad", min_disp_global=None,
                             stream: int = 0, d_med16: int = 0, d_harris: int = 0, d_d8: int = 0):
-        """d_med16 (optional): also the int16 x16 median maps (d_disp = d_med16 / 16 exactly).
-        d_d8 (optional): also the u8 disparity indices d_disp - (min_disp - 1) (integer costs,
-        num_disp <= 255; sv_depth_map_batch_d8_dev).
-        d_harris (optional): also the Harris response of every left frame, computed inside the
-        median launch (sv_depth_map_harris_batch_dev; not combinable with d_med16 / d_d8)."""
+        """create_depth_map over a batch of device frame pairs.  d_med16 (optional): also the
+        int16 x16 median maps (d_disp = d_med16 / 16 exactly).  d_d8 (optional): also the u8
+        disparity indices d_disp - (min_disp - 1) (integer costs, num_disp <= 255).  d_harris
+        (optional): also the Harris response of every left frame, computed inside the median
+        launch."""
         mdg = min_disp if min_disp_global is None else min_disp_global
-        args = (self._h, d_left, d_right, int(n_frames), H, W, pitch, int(frame_stride),
-                int(min_disp), int(num_disp), int(win), _cost(cost), np.float32(min_depth),
-                np.float32(max_depth), np.float32(float(max_depth) - float(min_depth)),
-                np.float32(mdg), d_depth, d_disp, d_norm)
-        if sum(1 for p in (d_harris, d_med16, d_d8) if p) > 1:
-            raise ValueError("d_harris, d_med16 and d_d8 are separate entry points")
-        if d_d8:
-            _check("sv_depth_map_batch_d8_dev",
-                   self.lib.sv_depth_map_batch_d8_dev(*args, d_d8, stream or None))
-        elif d_harris:
-            _check("sv_depth_map_harris_batch_dev",
-                   self.lib.sv_depth_map_harris_batch_dev(*args, d_harris, stream or None))
-        elif d_med16:
-            _check("sv_depth_map_batch_m16_dev",
-                   self.lib.sv_depth_map_batch_m16_dev(*args, d_med16, stream or None))
-        else:
-            _check("sv_depth_map_batch_dev", self.lib.sv_depth_map_batch_dev(*args, stream or None))
+        out = map_out(POST_DEPTH, d_disp, d_depth, d_norm, med16=d_med16, d8=d_d8, harris=d_harris,
+                      min_depth=min_depth, max_depth=max_depth, min_disp_global=mdg)
+        self.depth_map_batch_ex(d_left, d_right, n_frames, H, W, pitch, frame_stride, min_disp, num_disp, win,
+                                cost, STAGE_ALL, 0, out, stream)
 
     def harris_batch_dev(self, d_gray: int, n_frames: int, H: int, W: int, pitch: int,
                          frame_stride: int, d_out: int, stream: int = 0):
@@ -989,9 +974,9 @@ class Engine:
 
     def frame_stats_dev(self, d_img0: int, d_img1: int, H: int, W: int, channels: int, pitch: int,
                         d_block_sum: int, d_block_sq: int, d_hist: int, stream: int = 0):
-        _check("sv_frame_stats_dev", self.lib.sv_frame_stats_dev(
-            self._h, d_img0, d_img1 or None, H, W, channels, pitch, d_block_sum, d_block_sq, d_hist,
-            stream or None))
+        """One image or pair: the batch entry point with one frame."""
+        self.frame_stats_batch_dev(d_img0, d_img1, 1, 0, H, W, channels, pitch, d_block_sum, d_block_sq,
+                                   d_hist, stream)
 
     def frame_stats_batch_dev(self, d_img0: int, d_img1: int, n_frames: int, frame_stride: int, H: int,
                               W: int, channels: int, pitch: int, d_block_sum: int, d_block_sq: int,
@@ -1004,19 +989,13 @@ class Engine:
 
     def select_count(self, d_x: int, n: int, mask_mode: int = 0, d_mask: int = 0,
                      thr: float = 0.0) -> tuple[int, int]:
-        sel, nan = ctypes.c_int64(), ctypes.c_int64()
-        _check("sv_select_count", self.lib.sv_select_count(
-            self._h, d_x, int(n), int(mask_mode), d_mask or None, np.float32(thr), ctypes.byref(sel),
-            ctypes.byref(nan)))
-        return sel.value, nan.value
+        sel, nan = self.select_count_batch(d_x, n, n, 1, mask_mode, d_mask, n, thr)
+        return int(sel[0]), int(nan[0])
 
     def select_ranks(self, d_x: int, n: int, ranks, mask_mode: int = 0, d_mask: int = 0,
                      thr: float = 0.0) -> np.ndarray:
-        r = np.ascontiguousarray(np.asarray(ranks, np.int64).ravel())
-        out = np.empty(r.size, np.float32)
-        _check("sv_select_ranks", self.lib.sv_select_ranks(
-            self._h, d_x, int(n), int(mask_mode), d_mask or None, np.float32(thr), r, r.size, out))
-        return out
+        r = np.asarray(ranks, np.int64).reshape(1, -1)
+        return self.select_ranks_batch(d_x, n, n, r, mask_mode, d_mask, n, thr)[0]
 
     def select_count_batch(self, d_x: int, n: int, x_stride: int, n_arrays: int, mask_mode: int = 0,
                            d_mask: int = 0, mask_stride: int = 0, thr: float = 0.0):
@@ -1134,47 +1113,40 @@ def _ptrs(values):
     return (_vp * len(values))(*values)
 
 
-def _depth_args(min_depth, max_depth, min_disp, min_disp_global):
+def multi_gpu_dev(engines, comms, shard: int, inputs: int, left, right, n_frames, H: int, W: int,
+                  pitch: int, frame_stride: int, min_disp: int, num_disp: int, win: int, out: MapOut,
+                  cost="sad"):
+    """sv_multi_gpu_dev: one process driving the contexts of `engines` (SHARD_FRAMES: C4,
+    SHARD_ROWS: C5 with INPUTS_RESIDENT / INPUTS_SCATTER / INPUTS_HOST), the root's outputs
+    selected by `out` (:func:`map_out`).  `comms`: Communicator list (rank k on engines[k]'s
+    device) or None (peer copies).  Enqueue only: synchronize engines[0] before reading."""
+    engines = list(engines)
+    nd = len(engines)
+    lib = engines[0].lib
+    ch = None if comms is None else _handles([c.handle for c in comms])
+    nf = (_c_int * nd)(*[int(v) for v in n_frames]) if n_frames is not None else None
+    _check("sv_multi_gpu_dev", lib.sv_multi_gpu_dev(
+        _handles(engines), ch, nd, int(shard), int(inputs), _ptrs(left), _ptrs(right), nf, H, W, pitch,
+        int(frame_stride), int(min_disp), int(num_disp), int(win), _cost(cost), ctypes.byref(out)))
+
+
+def _full_out(min_depth, max_depth, min_disp, min_disp_global, d_depth, d_disp, d_norm) -> MapOut:
     mdg = min_disp if min_disp_global is None else min_disp_global
-    return (np.float32(min_depth), np.float32(max_depth),
-            np.float32(float(max_depth) - float(min_depth)), np.float32(mdg))
+    return map_out(POST_DEPTH, d_disp, d_depth, d_norm, min_depth=min_depth, max_depth=max_depth,
+                   min_disp_global=mdg)
 
 
 def multi_gpu_depth_map_dev(engines, comms, d_left, d_right, n_frames, H: int, W: int, pitch: int,
                             frame_stride: int, min_disp: int, num_disp: int, win: int,
                             min_depth: float, max_depth: float, d_depth: int, d_disp: int,
                             d_norm: int, cost="sad", min_disp_global=None):
-    """C4 on device-resident frames from ONE process (sv_multi_gpu_depth_map_dev): engine k
-    runs create_depth_map over its n_frames[k] frames (its own device), and every output
-    frame ends up on engines[0]'s device (d_depth/d_disp/d_norm, context order): the peers'
-    int16 x16 medians cross over RCCL (`comms`: Communicator list, rank k on engines[k]'s
-    device) or peer copies (None), 2 B/px, and engines[0] expands them.
-    Enqueue only: synchronize engines[0] before reading the outputs."""
-    engines = list(engines)
-    nd = len(engines)
-    lib = engines[0].lib
-    ch = None if comms is None else _handles([c.handle for c in comms])
-    nf = (_c_int * nd)(*[int(v) for v in n_frames])
-    _check("sv_multi_gpu_depth_map_dev", lib.sv_multi_gpu_depth_map_dev(
-        _handles(engines), ch, nd, _ptrs(d_left), _ptrs(d_right), nf, H, W, pitch,
-        int(frame_stride), int(min_disp), int(num_disp), int(win), _cost(cost),
-        *_depth_args(min_depth, max_depth, min_disp, min_disp_global), d_depth, d_disp, d_norm))
-
-
-def multi_gpu_m16_dev(engines, comms, d_left, d_right, n_frames, H: int, W: int, pitch: int,
-                      frame_stride: int, min_disp: int, num_disp: int, win: int, d_med16: int,
-                      cost="sad"):
-    """C4 as north_star states it (sv_multi_gpu_m16_dev): engine k computes disparity +
-    median over its n_frames[k] frames, and only the int16 x16 median maps (2 B/px) are
-    gathered into d_med16 on engines[0]'s device (context order).  Enqueue only."""
-    engines = list(engines)
-    nd = len(engines)
-    lib = engines[0].lib
-    ch = None if comms is None else _handles([c.handle for c in comms])
-    nf = (_c_int * nd)(*[int(v) for v in n_frames])
-    _check("sv_multi_gpu_m16_dev", lib.sv_multi_gpu_m16_dev(
-        _handles(engines), ch, nd, _ptrs(d_left), _ptrs(d_right), nf, H, W, pitch,
-        int(frame_stride), int(min_disp), int(num_disp), int(win), _cost(cost), d_med16))
+    """C4 on device-resident frames from ONE process: engine k runs create_depth_map over its
+    n_frames[k] frames (its own device), and every output frame ends up on engines[0]'s device
+    (d_depth/d_disp/d_norm, context order): the peers' int16 x16 medians cross over RCCL
+    (`comms`) or peer copies (None), 2 B/px, and engines[0] expands them.  Enqueue only."""
+    multi_gpu_dev(engines, comms, SHARD_FRAMES, INPUTS_RESIDENT, d_left, d_right, n_frames, H, W, pitch,
+                  frame_stride, min_disp, num_disp, win,
+                  _full_out(min_depth, max_depth, min_disp, min_disp_global, d_depth, d_disp, d_norm), cost)
 
 
 MAP_M16, MAP_D8 = 1, 2   # SV_MAP_M16 / SV_MAP_D8
@@ -1189,70 +1161,89 @@ def _map_format(fmt) -> int:
     return int(fmt)
 
 
+def _map_out(d_map: int, fmt) -> MapOut:
+    f = _map_format(fmt)
+    if f not in (MAP_M16, MAP_D8):
+        raise ValueError(f"map format must be m16 or d8, got {fmt!r}")
+    return map_out(POST_NONE, med16=d_map if f == MAP_M16 else 0, d8=d_map if f == MAP_D8 else 0)
+
+
+def multi_gpu_m16_dev(engines, comms, d_left, d_right, n_frames, H: int, W: int, pitch: int,
+                      frame_stride: int, min_disp: int, num_disp: int, win: int, d_med16: int,
+                      cost="sad"):
+    """C4 gather-only with int16 x16 maps (multi_gpu_map_dev with fmt "m16")."""
+    multi_gpu_map_dev(engines, comms, d_left, d_right, n_frames, H, W, pitch, frame_stride, min_disp,
+                      num_disp, win, d_med16, "m16", cost)
+
+
 def multi_gpu_map_dev(engines, comms, d_left, d_right, n_frames, H: int, W: int, pitch: int,
                       frame_stride: int, min_disp: int, num_disp: int, win: int, d_map: int,
                       fmt="m16", cost="sad"):
-    """C4 gather-only (sv_multi_gpu_map_dev): engine k computes disparity + median over its
-    n_frames[k] frames and only the median maps are gathered into d_map on engines[0]'s
-    device (context order): ``fmt="m16"`` int16 x16 (2 B/px), ``"d8"`` u8 disparity indices
-    median/16 - (min_disp - 1) (1 B/px; integer costs, num_disp <= 255).  Enqueue only."""
-    engines = list(engines)
-    nd = len(engines)
-    lib = engines[0].lib
-    ch = None if comms is None else _handles([c.handle for c in comms])
-    nf = (_c_int * nd)(*[int(v) for v in n_frames])
-    _check("sv_multi_gpu_map_dev", lib.sv_multi_gpu_map_dev(
-        _handles(engines), ch, nd, _ptrs(d_left), _ptrs(d_right), nf, H, W, pitch,
-        int(frame_stride), int(min_disp), int(num_disp), int(win), _cost(cost), _map_format(fmt), d_map))
+    """C4 gather-only: engine k computes disparity + median over its n_frames[k] frames and
+    only the median maps are gathered into d_map on engines[0]'s device (context order):
+    ``fmt="m16"`` int16 x16 (2 B/px), ``"d8"`` u8 disparity indices median/16 - (min_disp - 1)
+    (1 B/px; integer costs, num_disp <= 255).  Enqueue only."""
+    multi_gpu_dev(engines, comms, SHARD_FRAMES, INPUTS_RESIDENT, d_left, d_right, n_frames, H, W, pitch,
+                  frame_stride, min_disp, num_disp, win, _map_out(d_map, fmt), cost)
+
+
+def _rows_inputs(scatter) -> int:
+    if scatter in (False, None, 0):
+        return INPUTS_RESIDENT
+    if scatter in (True, 1, "scatter"):
+        return INPUTS_SCATTER
+    if scatter == "host":
+        return INPUTS_HOST
+    raise ValueError(f"scatter must be False, True/'scatter' or 'host', got {scatter!r}")
+
+
+def _rows_ptrs(d_left, d_right, inputs):
+    if inputs == INPUTS_RESIDENT:
+        return d_left, d_right
+    # one frame: a device pointer on the root (scatter) or a host array / pointer (host)
+    def one(x):
+        if isinstance(x, np.ndarray):
+            if x.dtype != np.uint8 or not x.flags["C_CONTIGUOUS"]:
+                raise ValueError("host frames must be C-contiguous uint8")
+            return x.ctypes.data
+        return int(x)
+    return [one(d_left)], [one(d_right)]
 
 
 def depth_map_rows_map(engines, comms, d_left, d_right, H: int, W: int, pitch: int, min_disp: int,
-                       num_disp: int, win: int, d_map: int, fmt="m16", scatter: bool = False,
-                       cost="sad"):
-    """C5 gather-only (sv_depth_map_rows_map): one frame row-tiled over the engines; the
-    root (engines[0]) receives only the full-frame median map (int16 x16 or u8 indices) in
-    d_map and expands nothing.  ``scatter``: d_left / d_right are the root's frame (one
-    pointer each) and the other engines receive just their bands' input rows; else lists with
-    the full frame on every engine's device.  Enqueue only."""
-    engines = list(engines)
-    lib = engines[0].lib
-    ch = None if comms is None else _handles([c.handle for c in comms])
-    if scatter:
-        d_left, d_right = [d_left], [d_right]
-    _check("sv_depth_map_rows_map", lib.sv_depth_map_rows_map(
-        _handles(engines), ch, len(engines), _ptrs(d_left), _ptrs(d_right), int(bool(scatter)), H, W,
-        pitch, int(min_disp), int(num_disp), int(win), _cost(cost), _map_format(fmt), d_map))
+                       num_disp: int, win: int, d_map: int, fmt="m16", scatter=False, cost="sad"):
+    """C5 gather-only: one frame row-tiled over the engines; the root (engines[0]) receives
+    only the full-frame median map (int16 x16 or u8 indices) in d_map and expands nothing.
+    ``scatter``: False — lists with the full frame on every engine's device; True — the root's
+    device frame (one pointer each), the other engines receive just their bands' input rows
+    over xGMI; "host" — a host frame (uint8 arrays, page-locked for overlap), every engine
+    uploads its own band's rows over its own PCIe link.  Enqueue only."""
+    inputs = _rows_inputs(scatter)
+    L, R = _rows_ptrs(d_left, d_right, inputs)
+    multi_gpu_dev(engines, comms, SHARD_ROWS, inputs, L, R, None, H, W, pitch, 0, min_disp, num_disp, win,
+                  _map_out(d_map, fmt), cost)
 
 
 def depth_map_rows_multi(engines, comms, d_left, d_right, H: int, W: int, pitch: int, min_disp: int,
                          num_disp: int, win: int, min_depth: float, max_depth: float, d_depth: int,
-                         d_disp: int, d_norm: int, cost="sad", min_disp_global=None):
-    """C5 from ONE process (sv_depth_map_rows_multi): one frame row-tiled over the engines
-    (each holds the full gray frame on its device), bands gathered to engines[0]'s device
-    into the full-frame outputs.  Enqueue only."""
-    engines = list(engines)
-    lib = engines[0].lib
-    ch = None if comms is None else _handles([c.handle for c in comms])
-    _check("sv_depth_map_rows_multi", lib.sv_depth_map_rows_multi(
-        _handles(engines), ch, len(engines), _ptrs(d_left), _ptrs(d_right), H, W, pitch,
-        int(min_disp), int(num_disp), int(win), _cost(cost),
-        *_depth_args(min_depth, max_depth, min_disp, min_disp_global), d_depth, d_disp, d_norm))
+                         d_disp: int, d_norm: int, cost="sad", min_disp_global=None, scatter=False):
+    """C5 from ONE process: one frame row-tiled over the engines, bands gathered to
+    engines[0]'s device into the full-frame outputs (inputs as :func:`depth_map_rows_map`).
+    Enqueue only."""
+    inputs = _rows_inputs(scatter)
+    L, R = _rows_ptrs(d_left, d_right, inputs)
+    multi_gpu_dev(engines, comms, SHARD_ROWS, inputs, L, R, None, H, W, pitch, 0, min_disp, num_disp, win,
+                  _full_out(min_depth, max_depth, min_disp, min_disp_global, d_depth, d_disp, d_norm), cost)
 
 
 def depth_map_rows_scatter(engines, comms, d_left: int, d_right: int, H: int, W: int, pitch: int,
                            min_disp: int, num_disp: int, win: int, min_depth: float, max_depth: float,
                            d_depth: int, d_disp: int, d_norm: int, cost="sad", min_disp_global=None):
-    """C5 from ONE process with the frame resident on engines[0]'s device only
-    (sv_depth_map_rows_scatter): each other engine receives just the input rows of its band
-    (+ halos, :func:`band_rows_in`), computes its band, and the bands are gathered back into
-    the full-frame outputs on engines[0]'s device.  Enqueue only."""
-    engines = list(engines)
-    lib = engines[0].lib
-    ch = None if comms is None else _handles([c.handle for c in comms])
-    _check("sv_depth_map_rows_scatter", lib.sv_depth_map_rows_scatter(
-        _handles(engines), ch, len(engines), d_left, d_right, H, W, pitch, int(min_disp),
-        int(num_disp), int(win), _cost(cost), *_depth_args(min_depth, max_depth, min_disp, min_disp_global),
-        d_depth, d_disp, d_norm))
+    """C5 with the frame resident on engines[0]'s device only: each other engine receives just
+    the input rows of its band (+ halos, :func:`band_rows_in`), computes its band, and the bands
+    are gathered back into the full-frame outputs on engines[0]'s device.  Enqueue only."""
+    depth_map_rows_multi(engines, comms, d_left, d_right, H, W, pitch, min_disp, num_disp, win, min_depth,
+                         max_depth, d_depth, d_disp, d_norm, cost, min_disp_global, scatter=True)
 
 
 def band_rows_in(H: int, rank: int, world: int, win: int, cost="sad") -> dict:
@@ -1301,12 +1292,16 @@ class Communicator:
         return buf.raw
 
     @classmethod
-    def init_rank(cls, device: int, nranks: int, rank: int, uid: bytes) -> "Communicator":
+    def init_rank(cls, device: int, nranks: int, rank: int, uid: bytes, timeout: float = 120.0) -> "Communicator":
+        """ncclCommInitRank, non-blocking with a deadline: if a peer fails during bootstrap
+        this rank gets an error after `timeout` seconds (the half-built communicator aborted)
+        instead of blocking forever."""
         lib = load_library()
         if len(uid) != COMM_ID_BYTES:
             raise ValueError("unique id must be 128 bytes")
         h = _vp()
-        _check("sv_comm_init_rank", lib.sv_comm_init_rank(device, nranks, rank, uid, ctypes.byref(h)))
+        _check("sv_comm_init_rank", lib.sv_comm_init_rank(device, nranks, rank, uid, float(timeout),
+                                                          ctypes.byref(h)))
         return cls(h, lib)
 
     @classmethod

@@ -36,15 +36,20 @@ def test_gather_is_the_default_for_multi_gpu_frames():
     assert not bench.parse_args([]).no_verify
 
 
-def test_default_batch_fills_whole_wave_rounds_at_1080p():
-    """26-frame steps at 1920x1080 (the metric config's k_match grid: 24.0 rounds of the wave
-    slots), 16 elsewhere and for SGBM / row tiling; an explicit batch or frame count wins."""
-    assert (bench.parse_args([]).batch, bench.parse_args([]).frames) == (26, 26)
-    assert bench.parse_args(["--win", "11"]).batch == 26
+def test_default_batch_and_lanes_at_1080p():
+    """One GPU at 1920x1080: 8-frame steps over 2 stream lanes (16 resident frames, one 8-frame
+    set per lane); N > 1 (gather beside the compute): 26-frame steps on one
+    stream (24.0 rounds of the k_match wave slots); 16 elsewhere and for SGBM / row tiling; an
+    explicit batch, stream or frame count wins."""
+    a = bench.parse_args([])
+    assert (a.batch, a.frames, a.streams, a.schedule) == (8, 16, 2, "lanes")
+    assert bench.parse_args(["--win", "11"]).batch == 8
+    assert bench.parse_args(["--gpus", "2"]).batch == 26
+    assert bench.parse_args(["--streams", "1"]).batch == 26
     assert bench.parse_args(["--height", "480", "--width", "640", "--num-disp", "64"]).batch == 16
     assert bench.parse_args(["--cost", "sgbm"]).batch == 16
     assert bench.parse_args(["--mode", "rowtile"]).batch == 16
-    a = bench.parse_args(["--batch", "8"])
+    a = bench.parse_args(["--batch", "8", "--streams", "1"])
     assert (a.batch, a.frames) == (8, 8)
     assert bench.parse_args(["--frames", "4"]).frames == 4
 
@@ -157,7 +162,7 @@ def _init_fail_worker(rank, world, path, strict, q):
         def close(self):
             q.put((rank, "closed"))
 
-    def _init_rank(device, nranks, r, uid):
+    def _init_rank(device, nranks, r, uid, timeout=120.0):
         if r == 1:
             raise RuntimeError("ncclCommInitRank: unhandled system error")
         return _Comm()
@@ -255,3 +260,118 @@ def test_band_from_its_input_rows_only_matches_the_full_frame(world, H, win, cos
         np.testing.assert_array_equal(d16[b["h0"]:b["h1"]], ref[b["h0"]:b["h1"]])
         med = C.median5_f32(d16[b["h0"]:b["h1"]])[b["r0"] - b["h0"]:b["r1"] - b["h0"]]
         np.testing.assert_array_equal(med, ref_med[b["r0"]:b["r1"]])
+
+
+def _blocking_init_worker(rank, world, path, q):
+    """rank 1's ncclCommInitRank fails while rank 0 is still INSIDE its own
+    (collective) initialisation.  The real sv_comm_init_rank is non-blocking with a deadline:
+    rank 0's call returns an error once the deadline passes (its half-built communicator
+    aborted), so it still reaches the collective decision.  The mock reproduces exactly that:
+    rank 0 blocks until rank 1 has failed, then waits out its deadline and fails."""
+    os.environ.update({"WORLD_SIZE": str(world), "RANK": str(rank), "LOCAL_RANK": str(rank),
+                       "SV_RDZV_DIR": path})
+    marker = os.path.join(path + ".marks", "rank1_failed")
+
+    def _init_rank(device, nranks, r, uid, timeout=120.0):
+        if r == 1:
+            os.makedirs(os.path.dirname(marker), exist_ok=True)
+            open(marker, "w").close()
+            raise RuntimeError("ncclCommInitRank: unhandled system error")
+        import time as _t
+        t_end = _t.monotonic() + 60
+        while not os.path.exists(marker):     # still "inside" the init when the peer dies
+            assert _t.monotonic() < t_end
+            _t.sleep(0.01)
+        _t.sleep(min(timeout, 0.5))            # the deadline (shortened by the test's timeout)
+        raise RuntimeError(f"ncclCommInitRank did not complete within {timeout} s; aborted")
+    E.Communicator.available = staticmethod(lambda: True)
+    E.Communicator.unique_id = staticmethod(lambda: b"\0" * 128)
+    E.Communicator.init_rank = staticmethod(_init_rank)
+    try:
+        pg = SD.init_process_group(device=rank, backend="auto", timeout=60, strict=False)
+        q.put((rank, f"{pg.backend}|{pg.reason}"))
+        pg.close()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, "raised: " + repr(e)))
+
+
+def test_rccl_init_failure_while_a_peer_is_still_initialising():
+    path = tempfile.mkdtemp(prefix="sv_bench_initblock_")
+    os.rmdir(path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_blocking_init_worker, args=(k, 2, path, q)) for k in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    assert sorted(res) == [0, 1], res
+    for m in res.values():   # both ranks fell back together, naming both failures
+        assert m.startswith("host|") and "failed on rank 1" in m and "failed on rank 0" in m, res
+
+
+class _MemEngine:
+    """Engine stand-in for RowTiledDepthMap's bookkeeping (allocations are fake addresses)."""
+    stream = 0x77
+
+    def __init__(self):
+        self.n = 0x1000
+
+    def dev_alloc(self, nbytes):
+        self.n += max(256, nbytes)
+        return self.n
+
+    def dev_free(self, p):
+        pass
+
+
+def _gather_check_worker(rank, world, path, outputs, expand, q):
+    os.environ.update({"WORLD_SIZE": str(world), "RANK": str(rank), "LOCAL_RANK": str(rank),
+                       "SV_RDZV_DIR": path})
+    E.Communicator.available = staticmethod(lambda: False)
+    pg = SD.init_process_group(device=0, backend="host", timeout=60)
+    tile = SD.RowTiledDepthMap(64, 96, 32, 5, device=0, rank=rank, world=world, engine=_MemEngine())
+    tile._band_outputs = outputs[rank]          # what compute() would have recorded
+    called = []
+    pg.gatherv = lambda *a, **k: called.append(a)   # reached only when every rank agreed
+    try:
+        tile.gather(pg, root=0, expand=expand)
+        q.put((rank, f"gathered {len(called)}"))
+    except ValueError as e:
+        q.put((rank, "ValueError: " + str(e)))
+    finally:
+        pg.close()
+
+
+@pytest.mark.parametrize("outputs,expand,ok", [
+    (("m16", "m16"), True, False),     # the root cannot expand without its own band's outputs
+    (("full", "d8"), True, False),     # d8 bands cannot be expanded
+    (("d8", "m16"), False, False),     # element sizes differ: the gather would corrupt rows
+    (("d8", "d8"), False, True),
+    (("full", "m16"), True, True),
+])
+def test_row_tile_gather_arguments_are_agreed_on_every_rank(outputs, expand, ok):
+    """a bad gather argument on ANY rank makes EVERY rank raise before the
+    collective (a root-only raise left the peers in a gather that never completes)."""
+    path = tempfile.mkdtemp(prefix="sv_bench_gchk_")
+    os.rmdir(path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gather_check_worker, args=(k, 2, path, outputs, expand, q)) for k in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    if ok:
+        assert all(m.startswith("gathered 1") for m in res.values()), res
+    else:
+        assert all(m.startswith("ValueError") for m in res.values()), res
+
+
+def test_row_tile_rejects_d8_for_sgbm():
+    """SGBM's sub-pixel medians are not whole-pixel indices."""
+    tile = SD.RowTiledDepthMap(64, 96, 32, 5, cost="sgbm", engine=_MemEngine())
+    with pytest.raises(ValueError, match="integer-disparity"):
+        tile.compute(1, 2, band_outputs="d8")

@@ -3,7 +3,7 @@ the C oracle, plus worst-case-contrast checks of the argmin key of every SAD ker
 
 * C5 — 3840x2160, D=256, 15x15 window (+ HOG descriptor match), row-tiled across 8 GPUs:
   the whole frame in one call, and the 8 row bands of the row-tiled mode computed through
-  the device API (sv_disparity_dev over the band + median halo, sv_median_post_dev over the
+  the device API (sv_disparity_dev over the band + median halo, sv_median_rows_dev over the
   band) and reassembled.  Reference arithmetic replaced: depth_map.py:894-912.
 * C4 — 8 x 1920x1080, D=128, 11x11 window, one frame per GPU: one 8-frame batch
   (sv_depth_map_batch_dev) and sv_multi_gpu_batch over 8 contexts, checked frame by frame.

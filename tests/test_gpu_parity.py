@@ -304,7 +304,7 @@ def test_row_bands_reassemble_bit_exactly_on_gpu(engine, cost, win):
 
 
 def test_device_api_band_pipeline(engine):
-    """sv_disparity_dev + sv_median_post_dev over row bands == the host depth_map path."""
+    """sv_disparity_dev + sv_median_rows_dev over row bands == the host depth_map path."""
     H, W, D, win = 70, 400, 64, 9
     L, R, _ = stereo_pair(H, W, D, seed=5)
     e_depth, e_disp, e_norm = engine.depth_map(L, R, 0, D, win, 0.3, 2.0)
@@ -519,7 +519,7 @@ def test_row_tiled_module_and_single_hip_runtime(engine):
                                         (120, 640, 4, 3), (9, 8, 1, 3), (48, 640, 2, 0), (37, 1000, 2, 4),
                                         (20, 256, 3, 0), (24, 260, 2, 0), (9, 300, 2, 0), (8, 257, 1, 1)])
 def test_depth_map_harris_batch_dev_fused(engine, H, W, nf, pad):
-    """sv_depth_map_harris_batch_dev (C2: Harris blocks inside the median launch) == the C
+    """sv_depth_map_batch_dev with out.harris (C2: Harris blocks inside the median launch) == the C
     oracle frame by frame: the create_depth_map outputs bit-exact and the Harris response of
     each left frame within 1e-4 (north_star; observed exact), with row pitches wider than the
     frame (unaligned) and equal to it (the 248-column waves' dword loads, W >= 256); frames
@@ -605,7 +605,7 @@ def test_colormap_fused_in_the_median_epilogue(engine, H, W):
 
 @pytest.mark.parametrize("H,W", [(70, 400), (33, 130), (17, 63)])
 def test_median_post_color_dev_epilogue(engine, H, W):
-    """sv_median_post_color_dev: the colormap written by the median kernel's epilogue equals
+    """sv_median_rows_dev with out.bgr: the colormap written by the median kernel's epilogue equals
     the table applied to the oracle's u8 image, for both modes, full frame and row bands."""
     from stereovision_amd import colormap
     L, R = _pair(H, W, 64, seed=H * W)
@@ -705,7 +705,7 @@ def test_host_path_matches_oracle(engine, H, W, D, win, cost):
 
 
 def test_depth_map_batch_int16_medians(engine):
-    """sv_depth_map_batch_m16_dev: the int16 x16 median maps beside the f32 outputs (the
+    """sv_depth_map_batch_dev with out.med16: the int16 x16 median maps beside the f32 outputs (the
     multi-GPU bench gathers these): med16 / 16 == the f32 disparity, both == the oracle."""
     nf, H, W, D = 3, 70, 300, 64
     Ls, Rs = [], []
@@ -775,6 +775,9 @@ class _LocalGather:
 
     def __init__(self, engine, tiles, rank):
         self.engine, self.tiles, self.rank, self.world = engine, tiles, rank, len(tiles)
+
+    def allreduce_max(self, value):   # one process: the ranks' checks agree by construction
+        return float(value)
 
     def gatherv(self, d_send, send_bytes, d_recv, offsets, sizes, root=0, stream=0):
         if self.rank != root:

@@ -1,8 +1,8 @@
 """Device-side multi-GPU paths of the C ABI, torch-free.
 
-* sv_multi_gpu_depth_map_dev (C4 from one process): every context computes create_depth_map
+* sv_multi_gpu_dev, SV_SHARD_FRAMES (C4 from one process): every context computes create_depth_map
   for its resident frames and all outputs are gathered onto ctxs[0]'s device.
-* sv_depth_map_rows_multi (C5 from one process): one frame row-tiled over the contexts, the
+* sv_multi_gpu_dev, SV_SHARD_ROWS (C5 from one process): one frame row-tiled over the contexts, the
   bands gathered onto ctxs[0]'s device into the full frame.
 * sv_comm_* (RCCL loaded with dlopen): a communicator per process (init_rank) and a group
   (init_all) on the devices this box has.
@@ -99,7 +99,7 @@ def test_multi_gpu_depth_map_dev_gathers_every_frame(ctxs, ndev, counts, cost, w
                                                    (3, [0, 2, 1], "hog", 7), (2, [1, 2], "ssd", 5),
                                                    (1, [2], "sad", 11)])
 def test_multi_gpu_m16_dev_gathers_int16_medians(ctxs, ndev, counts, cost, win):
-    """sv_multi_gpu_m16_dev: only the int16 x16 medians cross (2 B/px); they equal the C
+    """sv_multi_gpu_dev gather-only (out.med16): only the int16 x16 medians cross (2 B/px); they equal the C
     oracle's median map x 16 frame by frame, in context order."""
     H, W, D = 37, 300, 64
     es = ctxs[:ndev]
@@ -133,7 +133,7 @@ def test_multi_gpu_m16_dev_gathers_int16_medians(ctxs, ndev, counts, cost, win):
                                                         (3, [1, 0, 2], "hog", 7, 3), (2, [2, 1], "ssd", 5, -7),
                                                         (1, [2], "sad", 11, 0)])
 def test_multi_gpu_map_dev_gathers_u8_indices(ctxs, ndev, counts, cost, win, mind):
-    """sv_multi_gpu_map_dev(SV_MAP_D8): the one-process C4 gather at 1 B/px — every frame's u8
+    """sv_multi_gpu_dev gather-only (out.d8): the one-process C4 gather at 1 B/px — every frame's u8
     disparity index d - min_disp + 1 lands on ctxs[0]'s device in context order and encodes
     the C oracle's median map exactly (d8 + min_disp - 1)."""
     H, W, D = 37, 300, 48
@@ -216,17 +216,23 @@ def test_back_to_back_gathers_without_sync(ctxs):
 
 @pytest.mark.parametrize("ndev,H,cost,win,fmt,scatter", [(8, 131, "sad", 9, "d8", True), (3, 29, "sad", 15, "m16", True),
                                                          (4, 57, "hog", 5, "d8", False), (2, 64, "ssd", 7, "m16", False),
-                                                         (1, 40, "sad", 9, "d8", True)])
+                                                         (1, 40, "sad", 9, "d8", True), (8, 131, "sad", 9, "d8", "host"),
+                                                         (3, 29, "ssd", 15, "m16", "host"), (1, 40, "hog", 7, "d8", "host")])
 def test_depth_map_rows_map_gather_only(ctxs, ndev, H, cost, win, fmt, scatter):
-    """sv_depth_map_rows_map: the root receives only the full-frame map (int16 x16 / u8
-    indices): its own band from its median epilogue, the peers' bands gathered; nothing is
-    expanded.  Twice (the second call reuses scratch), band-only or full-frame inputs."""
+    """sv_multi_gpu_dev (SV_SHARD_ROWS), gather-only: the root receives only the full-frame map
+    (int16 x16 / u8 indices): its own band from its median epilogue, the peers' bands gathered;
+    nothing is expanded.  Twice (the second call reuses scratch), with the frame on every
+    context, scattered from the root (SV_INPUTS_SCATTER) or uploaded by every context from
+    host memory (SV_INPUTS_HOST, VERDICT r05 #1)."""
     W, D = 400, 64
     L, R, _ = stereo_pair(H, W, D, seed=ndev * 31 + H)
     es = ctxs[:ndev]
     root = es[0]
     el = 1 if fmt == "d8" else 2
-    if scatter:
+    if scatter == "host":
+        dL, dR = np.ascontiguousarray(L), np.ascontiguousarray(R)
+        srcs = []
+    elif scatter:
         dL, dR = _upload(root, L), _upload(root, R)
         srcs = [(root, dL), (root, dR)]
     else:
@@ -288,7 +294,7 @@ def test_gather_only_maps_with_empty_shares(ctxs, fmt):
 
 
 def test_median_map_dev_rows_and_formats(engine):
-    """sv_median_map_dev: a row band's median written only as a map (int16 x16 / u8 indices)
+    """sv_median_rows_dev (out.med16 / out.d8): a row band's median written only as a map (int16 x16 / u8 indices)
     at full-frame offsets, rows outside the band untouched; num_disp > 255 refused for u8."""
     from stereovision_amd.engine import SVError
     H, W, D, win, md = 50, 210, 40, 7, -4
@@ -318,7 +324,7 @@ def test_median_map_dev_rows_and_formats(engine):
 
 
 def test_depth_map_batch_d8_dev_indices(engine):
-    """sv_depth_map_batch_d8_dev: u8 disparity indices d - min_disp + 1 beside the f32 outputs
+    """sv_depth_map_batch_dev with out.d8: u8 disparity indices d - min_disp + 1 beside the f32 outputs
     (whole-pixel disparities: d8 + min_disp - 1 == the f32 disparity exactly, 0 = invalid), for
     SAD, SSD and HOG, a negative min_disp and num_disp 255; SGBM and num_disp > 255 refused."""
     from stereovision_amd.engine import SVError
@@ -416,6 +422,83 @@ def _rows_multi(es, comms, L, R, D, win, cost="sad"):
             root.dev_free(p)
 
 
+def test_rows_host_inputs_full_outputs(ctxs):
+    """SV_INPUTS_HOST with create_depth_map's outputs on the root (the peers' int16 bands
+    expanded there): every context uploads its own band rows; bit-exact against the oracle."""
+    H, W, D, win = 83, 330, 48, 11
+    L, R, _ = stereo_pair(H, W, D, seed=123)
+    root = ctxs[0]
+    n = H * W
+    outs = [root.dev_alloc(4 * n), root.dev_alloc(4 * n), root.dev_alloc(n)]
+    try:
+        for nd in (8, 3):
+            depth_map_rows_multi(ctxs[:nd], None, L, R, H, W, W, 0, D, win, 0.3, 2.0, outs[0], outs[1], outs[2],
+                                 scatter="host")
+            root.synchronize()
+            e_disp, e_depth, e_norm = _oracle(L, R, D, win)
+            np.testing.assert_array_equal(root.to_host(outs[1], (H, W), np.float32), e_disp)
+            np.testing.assert_array_equal(root.to_host(outs[0], (H, W), np.float32), e_depth)
+            np.testing.assert_array_equal(root.to_host(outs[2], (H, W), np.uint8), e_norm)
+    finally:
+        for p in outs:
+            root.dev_free(p)
+
+
+def test_batch_stages_apart_equal_the_fused_call(ctxs):
+    """sv_depth_map_batch_dev with SV_STAGE_MATCH on one context and SV_STAGE_MEDIAN on another
+    (the bench's split schedule: the two launches of consecutive batches on two streams) gives
+    the same outputs as SV_STAGE_ALL, for SAD and SSD; a separate stage needs d_disp16."""
+    from stereovision_amd.engine import STAGE_MATCH, STAGE_MEDIAN, SVError, map_out, POST_DEPTH
+    ea, eb = ctxs[0], ctxs[1]
+    for cost, D, win in (("sad", 64, 9), ("ssd", 48, 7)):
+        nf, H, W = 3, 44, 300
+        L = np.stack([stereo_pair(H, W, D, seed=40 + s)[0] for s in range(nf)])
+        R = np.stack([stereo_pair(H, W, D, seed=40 + s)[1] for s in range(nf)])
+        n = H * W
+        dL, dR = _upload(ea, L), _upload(ea, R)
+        d16 = ea.dev_alloc(2 * n * nf)
+        a = [ea.dev_alloc(4 * n * nf), ea.dev_alloc(4 * n * nf), ea.dev_alloc(n * nf)]
+        b = [ea.dev_alloc(4 * n * nf), ea.dev_alloc(4 * n * nf), ea.dev_alloc(n * nf), ea.dev_alloc(2 * n * nf)]
+        try:
+            ea.depth_map_batch_dev(dL, dR, nf, H, W, W, n, 0, D, win, 0.3, 2.0, a[0], a[1], a[2], cost=cost)
+            ea.depth_map_batch_ex(dL, dR, nf, H, W, W, n, 0, D, win, cost, STAGE_MATCH, d16, None)
+            ea.event_record(0, ea.stream)
+            ea.stream_wait_event(0, eb.stream)
+            out = map_out(POST_DEPTH, b[1], b[0], b[2], med16=b[3], min_depth=0.3, max_depth=2.0,
+                          min_disp_global=0)
+            eb.depth_map_batch_ex(0, 0, nf, H, W, W, n, 0, D, win, cost, STAGE_MEDIAN, d16, out, stream=eb.stream)
+            eb.synchronize()
+            ea.synchronize()
+            for x, y, dt in ((a[0], b[0], np.float32), (a[1], b[1], np.float32), (a[2], b[2], np.uint8)):
+                np.testing.assert_array_equal(ea.to_host(x, (nf, H, W), dt), ea.to_host(y, (nf, H, W), dt))
+            m16 = ea.to_host(b[3], (nf, H, W), np.int16)
+            np.testing.assert_array_equal(m16.astype(np.float32) / np.float32(16),
+                                          ea.to_host(a[1], (nf, H, W), np.float32))
+            for z in range(nf):
+                np.testing.assert_array_equal(ea.to_host(a[1] + 4 * n * z, (H, W), np.float32),
+                                              _oracle(L[z], R[z], D, win, cost)[0])
+            with pytest.raises(SVError):
+                ea.depth_map_batch_ex(dL, dR, nf, H, W, W, n, 0, D, win, cost, STAGE_MATCH, 0, None)
+        finally:
+            for p in [dL, dR, d16] + a + b:
+                ea.dev_free(p)
+
+
+def test_median_rows_refuses_d8_for_sgbm_maps(engine):
+    """u8 indices are whole-pixel disparities; an SGBM (sub-pixel) map is refused."""
+    from stereovision_amd.engine import SVError
+    H, W = 16, 64
+    d16, d8 = engine.dev_alloc(2 * H * W), engine.dev_alloc(H * W)
+    try:
+        engine.to_device(d16, np.zeros((H, W), np.int16))
+        engine.median_map_dev(d16, H, W, 0, H, d8, "d8", min_disp=0, num_disp=16, cost="sad")
+        with pytest.raises(SVError):
+            engine.median_map_dev(d16, H, W, 0, H, d8, "d8", min_disp=0, num_disp=16, cost="sgbm")
+    finally:
+        engine.dev_free(d16)
+        engine.dev_free(d8)
+
+
 @pytest.mark.parametrize("ndev,H,cost,win", [(8, 131, "sad", 9), (3, 29, "sad", 15),
                                                (8, 17, "hog", 5), (2, 64, "ssd", 7), (1, 40, "sad", 9)])
 def test_depth_map_rows_multi_reassembles_bit_exactly(ctxs, ndev, H, cost, win):
@@ -439,7 +522,7 @@ def test_c5_row_tiled_over_8_contexts_gathered_on_device_0(ctxs):
 
 
 def _rows_scatter(es, comms, L, R, D, win, cost="sad"):
-    """sv_depth_map_rows_scatter: the frame on es[0]'s device only; bands + halos scattered."""
+    """sv_multi_gpu_dev with SV_INPUTS_SCATTER: the frame on es[0]'s device only; bands + halos scattered."""
     from stereovision_amd.engine import depth_map_rows_scatter
     H, W = L.shape
     root = es[0]
@@ -488,7 +571,7 @@ def test_c5_row_tiled_band_inputs_over_8_contexts(ctxs):
 
 
 def test_rccl_group_scatter_band_inputs(ctxs):
-    """The scatter + gather of sv_depth_map_rows_scatter as RCCL groups over this box's
+    """The scatter + gather of SV_INPUTS_SCATTER as RCCL groups over this box's
     distinct devices."""
     nd = max(1, device_count())
     devs = list(range(min(nd, 8)))
@@ -575,10 +658,15 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("mode,root_outputs,fmt", [("frames", "m16", "auto"), ("frames", "m16", "i16"),
-                                                   ("frames", "full", "auto"), ("rowtile", "m16", "auto"),
-                                                   ("rowtile", "m16", "i16"), ("rowtile", "full", "auto")])
-def test_bench_under_torch_distributed_run_two_ranks(mode, root_outputs, fmt):
+@pytest.mark.parametrize("mode,root_outputs,fmt,bands", [("frames", "m16", "auto", "scatter"),
+                                                         ("frames", "m16", "i16", "scatter"),
+                                                         ("frames", "full", "auto", "scatter"),
+                                                         ("rowtile", "m16", "auto", "scatter"),
+                                                         ("rowtile", "m16", "i16", "scatter"),
+                                                         ("rowtile", "full", "auto", "scatter"),
+                                                         ("rowtile", "m16", "auto", "host"),
+                                                         ("rowtile", "full", "auto", "host")])
+def test_bench_under_torch_distributed_run_two_ranks(mode, root_outputs, fmt, bands):
     """The driver's N>1 launch: torch.distributed.run starts 2 bench.py workers (torch-free).
     On a 1-GPU box both ranks share the GPU, so the group falls back to the file store (RCCL
     refuses two ranks on one device); on a multi-GPU box it is RCCL.  The gather is on by
@@ -590,7 +678,7 @@ def test_bench_under_torch_distributed_run_two_ranks(mode, root_outputs, fmt):
            "--steps", "3", "--warmup", "1", "--height", "96", "--width", "400", "--num-disp", "64",
            "--frames", "2", "--batch", "2", "--mode", mode, "--no-live-pmc", "--no-aux",
            "--no-host-path", "--no-cpu-baseline", "--hang-timeout", "90", "--root-outputs", root_outputs,
-           "--gather-format", fmt]
+           "--gather-format", fmt, "--band-inputs", bands]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     import json
@@ -624,13 +712,17 @@ def test_bench_under_torch_distributed_run_two_ranks(mode, root_outputs, fmt):
         assert d["root_expand_us_per_step"] is None
 
 
-@pytest.mark.parametrize("ngpu,mode,root_outputs,fmt", [(2, "frames", "m16", "auto"), (3, "frames", "full", "auto"),
-                                                        (3, "frames", "m16", "i16"), (4, "rowtile", "m16", "auto"),
-                                                        (3, "rowtile", "m16", "i16"), (2, "rowtile", "full", "auto")])
-def test_bench_one_process_rehearsal(ngpu, mode, root_outputs, fmt):
+@pytest.mark.parametrize("ngpu,mode,root_outputs,fmt,bands", [(2, "frames", "m16", "auto", "scatter"),
+                                                              (3, "frames", "full", "auto", "scatter"),
+                                                              (3, "frames", "m16", "i16", "scatter"),
+                                                              (4, "rowtile", "m16", "auto", "scatter"),
+                                                              (3, "rowtile", "m16", "i16", "scatter"),
+                                                              (2, "rowtile", "full", "auto", "scatter"),
+                                                              (8, "rowtile", "m16", "auto", "host"),
+                                                              (3, "rowtile", "full", "auto", "host")])
+def test_bench_one_process_rehearsal(ngpu, mode, root_outputs, fmt, bands):
     """`bench.py --gpus N` without a launcher (ONE process drives N GPUs: the gather lanes, two
-    context sets, sv_multi_gpu_map_dev / sv_multi_gpu_depth_map_dev / sv_depth_map_rows_map /
-    sv_depth_map_rows_scatter) on N logical GPUs of this box (--rehearse: contexts of the
+    context sets, sv_multi_gpu_dev in all its shard / input / output forms) on N logical GPUs of this box (--rehearse: contexts of the
     visible devices, gathers as device copies): runs end to end and every gathered map of the
     last step is bit-exact against the C oracle; the line reports the gather traffic — u8
     indices (1 B/px) by default, int16 x16 (2 B/px) with --gather-format i16 or full outputs."""
@@ -638,7 +730,7 @@ def test_bench_one_process_rehearsal(ngpu, mode, root_outputs, fmt):
     cmd = [sys.executable, "bench.py", "--gpus", str(ngpu), "--rehearse", "--steps", "3",
            "--warmup", "1", "--height", str(H), "--width", str(W), "--num-disp", "64",
            "--frames", "4", "--batch", str(B), "--mode", mode, "--root-outputs", root_outputs,
-           "--gather-format", fmt,
+           "--gather-format", fmt, "--band-inputs", bands,
            "--no-live-pmc", "--no-aux", "--no-host-path", "--no-cpu-baseline", "--hang-timeout", "90"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]

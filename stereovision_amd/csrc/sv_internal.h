@@ -83,6 +83,10 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
 // whether a launch takes that form, and the elements of one key plane it needs
 bool ring_split(int cost, int win, int num_disp);
 bool ring_ssd(int cost, int win, int num_disp);   // SSD windows 5..9, D <= 256: the ring kind
+// SSD on the matrix cores (sv_ssd_mfma.hip): odd windows <= 15, D a multiple of 32 up to 160
+bool ssd_mfma(int cost, int win, int num_disp);
+bool ssd_mfma_fits(const MatchParams& a, int cost);   // + operand alignment, r == win / 2
+int launch_ssd_mfma(const MatchParams& a, hipStream_t s);
 long long ring_split_elems(int nf, long long fs_out, int row1, int opitch);
 int launch_fill_i16(int16_t* out, int opitch, int H, int W, int16_t v, hipStream_t s);
 

@@ -1477,6 +1477,7 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
     // the size_t-addressed four-row kind instead
     const bool ring_fits = 2LL * ((long long)(a.row1 + 3) * a.opitch + a.W + 64) < 0x7FFFFFFFLL;
     if (ring_kind(cost, a.win, a.D) && ring_fits) return launch_ring<false>(a, s);
+    if (ssd_mfma_fits(a, cost)) return launch_ssd_mfma(a, s);
     if (ring_ssd(cost, a.win, a.D) && ring_fits) return launch_ring<false, true>(a, s);
     if (ring_split(cost, a.win, a.D) && a.keys) {
         // (key planes: 4-byte elements, so half the 2^31-byte range of the int16 maps)

@@ -42,6 +42,22 @@ __global__ void k_rate(const uint8_t* in, uint32_t* out, long long* cyc, int str
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// throughput: 1024 blocks x 256 threads, lane l of the block reads 16 bytes at
+// (base + l * stride) & 2047 for 256 iterations (base advances 64 B); kernel time by events
+__global__ void k_tput(const uint8_t* in, uint32_t* out, int stride, int shift) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[4096];
+    for (int i = threadIdx.x; i < 4096; i += blockDim.x) lds[i] = in[i];
+    __syncthreads();
+    uint32_t acc = 0;
+#pragma unroll 8
+    for (int it = 0; it < 256; ++it) {
+        const int off = ((threadIdx.x & 63) * stride + it * 64 + shift) & 2047;
+        const U16 v = *reinterpret_cast<const U16*>(lds + off);
+        acc += v.a ^ v.b ^ v.c ^ v.d;
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
 int main() {
     uint8_t h[4096];
     for (int i = 0; i < 4096; ++i) h[i] = (uint8_t)(i * 37 + (i >> 8) * 11 + 5);
@@ -70,6 +86,28 @@ int main() {
         double m = 0;
         for (int i = 0; i < 256; ++i) m += (double)c[i];
         printf("stride %2d B: %.2f cycles per ds_read_b128 (one wave per CU)\n", s, m / 256 / 256);
+    }
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    uint32_t* d_big;
+    hipMalloc(&d_big, 1024 * 256 * 4);
+    const int cases[][2] = {{16, 0}, {16, 4}, {16, 1}, {4, 0}, {1, 0}, {0, 0}, {32, 0}};
+    for (auto& cs : cases) {
+        float best = 1e9f;
+        for (int rep = 0; rep < 5; ++rep) {
+            hipEventRecord(e0, 0);
+            hipLaunchKernelGGL(k_tput, dim3(1024), dim3(256), 0, 0, d_in, d_big, cs[0], cs[1]);
+            hipEventRecord(e1, 0);
+            hipEventSynchronize(e1);
+            float ms = 0;
+            hipEventElapsedTime(&ms, e0, e1);
+            if (ms < best) best = ms;
+        }
+        // 1024 blocks x 4 waves x 256 ds_read_b128 over 256 CUs at ~2.4 GHz
+        const double per_cu = 1024.0 * 4 * 256 / 256;
+        printf("throughput stride %2d shift %d: %.3f ms, %.2f cycles per ds_read_b128 per CU\n", cs[0], cs[1], best,
+               best * 1e-3 * 2.4e9 / per_cu);
     }
     hipDeviceSynchronize();
     return bad ? 1 : 0;

@@ -12,6 +12,7 @@ the synchronous call.
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 from concurrent.futures import Future
@@ -22,16 +23,32 @@ from . import colormap
 from .engine import Engine, get_engine
 
 
+def max_in_flight() -> int:
+    """Contexts (streams) one process can keep truly concurrent on a device: the HIP runtime
+    maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default, and on the GPU boxes);
+    a fifth stream shares a queue with another, so its transfers and kernels wait behind that
+    stream's work — measured: 1080p create_depth_map with 6 in flight ran at 1.9k frames/s
+    against 2.5k with 4 (profiles/r05zh/configs.txt, the sweep in profiles/r06*)."""
+    try:
+        return max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
+    except ValueError:
+        return 4
+
+
 class DepthMapPipeline:
     """submit(left, right) -> Future of create_depth_map's (depth_final, disparity,
     depth_colormap) on the MI355X engine, up to `depth` frames in flight."""
 
     def __init__(self, num_disp: int, window_size: int, min_disp: int = 0, min_depth: float = 0.3,
                  max_depth: float = 2.0, cost: str = "sad", depth: int = 3, device: int | None = None,
-                 cmap: str = "turbo"):
+                 cmap: str = "turbo", cap: bool = True):
+        """depth: frames in flight, capped at :func:`max_in_flight` (the hardware queues one
+        process's streams map onto; more contexts than queues only serialise behind each
+        other).  cap=False keeps the requested depth (for measuring the cap itself)."""
         self.num_disp, self.win, self.min_disp = int(num_disp), int(window_size), int(min_disp)
         self.min_depth, self.max_depth, self.cost = float(min_depth), float(max_depth), cost
-        self.depth = max(1, int(depth))
+        self.requested_depth = max(1, int(depth))
+        self.depth = min(self.requested_depth, max_in_flight()) if cap else self.requested_depth
         first = get_engine(device)
         self._engines = [first] + [Engine(first.device) for _ in range(self.depth - 1)]
         self._own = self._engines[1:]

@@ -11,7 +11,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from stereovision_amd import colormap, depth_map as DM  # noqa: E402
-from stereovision_amd.engine import get_engine  # noqa: E402
+from stereovision_amd.engine import get_engine, host_profile  # noqa: E402
 from stereovision_amd.pipeline import DepthMapPipeline  # noqa: E402
 from stereovision_amd.synthetic import stereo_pair, to_bgr  # noqa: E402
 
@@ -50,23 +50,33 @@ def main():
     a = np.random.default_rng(1).integers(0, 256, 6 * H * W, dtype=np.uint8)
     b = np.empty_like(a)
     out["host memcpy 12.4MB warm"] = rate(lambda i: np.copyto(b, a), n=30)
-    for depth in (1, 2, 3, 4, 6):
-        pipe = DepthMapPipeline(D, win, depth=depth)
-        try:
-            for i in range(4):
-                pipe.submit(*frames[i % 4]).result()
-            futs, n = [], 120
-            t0 = time.perf_counter()
-            for i in range(n):
-                futs.append(pipe.submit(*frames[i % 4]))
-                if len(futs) > depth:
-                    futs.pop(0).result()
-            for f in futs:
-                f.result()
-            dt = time.perf_counter() - t0
-            out[f"pipeline depth {depth}"] = (round(n / dt, 1), round(dt * 1e3 / n, 3))
-        finally:
-            pipe.close()
+    # the in-flight sweep: uncapped depths (cap=False) with the host-side stage times per call
+    # (sv_host_profile: prepare, stage+issue, wait for the first piece, expand, wait for the
+    # rest, total), and the capped pipeline a caller gets for the same request
+    for depth in (1, 2, 3, 4, 5, 6, 8):
+        for cap in ((False, True) if depth > 4 else (False,)):
+            pipe = DepthMapPipeline(D, win, depth=depth, cap=cap)
+            try:
+                for i in range(2 * depth):
+                    pipe.submit(*frames[i % 4]).result()
+                host_profile(enable=True, reset=True)
+                futs, n = [], 160
+                t0 = time.perf_counter()
+                for i in range(n):
+                    futs.append(pipe.submit(*frames[i % 4]))
+                    if len(futs) > pipe.depth:
+                        futs.pop(0).result()
+                for f in futs:
+                    f.result()
+                dt = time.perf_counter() - t0
+                st = host_profile(enable=False, reset=True)
+                key = f"pipeline depth {depth}" + (f" capped to {pipe.depth}" if cap else "")
+                out[key] = {"frames_per_s": round(n / dt, 1), "ms_per_frame": round(dt * 1e3 / n, 3),
+                            "per_call_ms": {k: (round(v, 3) if v is not None else None)
+                                            for k, v in st.items() if k != "calls"}}
+            finally:
+                pipe.close()
+    out["GPU_MAX_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES")
     out["cpu_count"] = os.cpu_count()
     out["affinity"] = len(os.sched_getaffinity(0))
     print(json.dumps(out))

@@ -64,30 +64,6 @@ __device__ __forceinline__ uint32_t min3u(uint32_t a, uint32_t b, uint32_t c) {
     return d;
 }
 
-// Reduce-scatter of 8 keys over the 16 lanes of a row: on return lanes 2j and 2j+1 hold the
-// min over the row of key j = (l >> 1) & 7 in v[0] (bank-masked DPP for lane bits 3 and 2, a
-// select for bit 1, then one step with lane l ^ 1: 16 ops for 8 keys; sv_match.hip's form).
-__device__ __forceinline__ void reduce_scatter8(uint32_t (&v)[8], int l) {
-#define SV_BM_PAIR(A, B, CTRL, M0, M1)                                                          \
-    "v_min_u32_dpp %" #A ", %" #A ", %" #A " " CTRL " row_mask:0xf bank_mask:" M0 "\n\t"      \
-    "v_min_u32_dpp %" #A ", %" #B ", %" #B " " CTRL " row_mask:0xf bank_mask:" M1 "\n\t"
-    asm volatile("s_nop 1\n\t"
-                 SV_BM_PAIR(0, 4, "row_mirror", "0x3", "0xc") SV_BM_PAIR(1, 5, "row_mirror", "0x3", "0xc")
-                 SV_BM_PAIR(2, 6, "row_mirror", "0x3", "0xc") SV_BM_PAIR(3, 7, "row_mirror", "0x3", "0xc")
-                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])
-                 : "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
-    asm volatile("s_nop 1\n\t"
-                 SV_BM_PAIR(0, 2, "row_half_mirror", "0x5", "0xa") SV_BM_PAIR(1, 3, "row_half_mirror", "0x5", "0xa")
-                 : "+v"(v[0]), "+v"(v[1])
-                 : "v"(v[2]), "v"(v[3]));
-#undef SV_BM_PAIR
-    const bool hi = (l & 2) != 0;
-    const uint32_t send = hi ? v[0] : v[1];
-    const uint32_t keep = hi ? v[1] : v[0];
-    v[0] = min(keep, (uint32_t)__builtin_amdgcn_update_dpp(0u, (int)send, 0x1B, 0xF, 0xF, false));  // l ^ 3
-    v[0] = min(v[0], (uint32_t)__builtin_amdgcn_update_dpp(0u, (int)v[0], 0xB1, 0xF, 0xF, false));  // l ^ 1
-}
-
 // A staged image row lives in LDS as 4 copies shifted by 0..3 bytes (copy s, dword w = bytes
 // 4w + s .. 4w + s + 3 of the row), so the 16 bytes at ANY byte offset p are 4 dword-aligned
 // ds_read_b32 of copy p & 3: a 16-byte LDS load that is not 16-byte aligned costs ~68 LDS cycles
@@ -117,27 +93,31 @@ struct SsdCfg {
     static constexpr int XW = 32 * XT * kWaves;        // output columns per block
     static constexpr int GT = kWaves * XT + NT - 1;    // x'-tiles per block
     static constexpr int XPW = 32 * GT;                // x' columns per block (ix' in [0, XPW))
+    static constexpr int XPP = XPW + 32;               // hsq / U row length (+ a pad column block)
     static constexpr int LB = XW + 16;                 // L' bytes a row's operands read
     static constexpr int RB = XPW + 16;                // R' bytes
-    using CL = Copies<LB>;
-    using CR = Copies<RB>;
-    static constexpr int SLOT = CL::SIZE + CR::SIZE;   // one staged row: L' copies | R' (or ~R') copies
     // physical dwords of a row the operands read: starts up to XW - 1 (XPW - 1) plus the 4-byte
     // alignment offset, 4 dwords each
     static constexpr int NLD = LB / 4 + 1;
     static constexpr int NRD = RB / 4 + 1;
-    static_assert(NLD <= CL::DW && NRD <= CR::DW, "copies hold every dword the operands read");
-    // 3 entering + 3 leaving slots (a fast wave stages step s + 2 while a slow one reads step s),
-    // the hsq ring (win + 2 rows of XPW ints) and U[2][XPW]
+    // both streams' copies use one stride (immediate LDS offsets in the copy builder); the
+    // dwords past NLD / NRD are never read (the builder's idle threads write one of them)
+    using CP = Copies<(LB > RB ? LB : RB) + 4>;
+    static constexpr int DWC = CP::DW;
+    static_assert(NRD + 1 <= DWC && NLD + 1 <= DWC, "copies hold every dword the operands read + a pad");
+    static constexpr int SIDE = CP::SIZE;              // one stream's 4 copies
+    static constexpr int SLOT = 2 * SIDE;              // one staged row: L' copies | R' (or ~R') copies
     // raw ring (LDS-DMA landing rows): one dword per thread, NLD L dwords then NRD R dwords
     static constexpr int NIT = NLD + NRD;
     static_assert(NIT <= kThreads, "one raw dword per thread");
+    static constexpr int NB = (2 * NIT + kThreads - 1) / kThreads;   // copy-builder items per thread
+    static constexpr int NJ = (XPW + kThreads - 1) / kThreads;       // hsq columns per thread
     static constexpr int RAWB = 4 * kThreads;
     static constexpr int PRE = 5;                      // DMA issue distance (steps)
-    static constexpr int lds(int win) { return 6 * SLOT + (win + 2) * 4 * XPW + 2 * 4 * XPW + (win + PRE) * RAWB; }
+    // 3 entering + 3 leaving slots, the hsq ring (win + 2 rows), U[2], the raw ring (win + PRE)
+    static constexpr int lds(int win) { return 6 * SLOT + (win + 2) * 4 * XPP + 2 * 4 * XPP + (win + PRE) * RAWB; }
     static_assert(XT * NT * 16 <= 160, "accumulators must stay in arch VGPRs");
-    static_assert(XPW <= 3 * kThreads, "three x' columns per thread at most");
-    static_assert(6 * SLOT + 19 * 4 * XPW + (15 + PRE) * RAWB <= 160 * 1024, "LDS per block (win 15)");
+    static_assert(lds(15) <= 160 * 1024, "LDS per block (win 15)");
 };
 
 // The raw rows arrive by LDS-DMA (global_load_lds_dword: wave-uniform LDS base + 4 x lane), one
@@ -146,32 +126,40 @@ struct SsdCfg {
 // (the oracle's replicate border): for blocks whose streams cross an image edge the copy builder
 // re-selects the bytes with one v_perm (selector below); interior blocks skip it.
 __device__ __forceinline__ int clamp_dword(int c0, int W) { return min(max(c0, 0), (W - 1) & ~3); }
-__device__ __forceinline__ uint32_t edge_fix(uint32_t v, int c0, int W) {
+// v_perm selector taking the dword loaded at clamp_dword(c0) to the replicate-clamped bytes of
+// columns c0 .. c0 + 3 (0x03020100, the identity, inside the image)
+__device__ __forceinline__ uint32_t edge_sel(int c0, int W) {
     const int ca = clamp_dword(c0, W);
     uint32_t sel = 0;
 #pragma unroll
     for (int b = 0; b < 4; ++b) sel |= (uint32_t)(min(max(c0 + b, 0), W - 1) - ca) << (8 * b);
-    return __builtin_amdgcn_perm(v, v, sel);
+    return sel;
 }
 
-// SSD matrix-core kernel, MFMA A = L' (rows: 32 x of an x-tile), B = R' (columns: 32 x' of an
-// x'-tile), so a lane holds ONE x' column (its key term U(x') is one register) and 16 x rows.
-// waves per SIMD the register allocation targets: 3 up to 4 accumulator tiles (64 VGPRs), else 2
 template <int XT, int NT> struct SsdOcc {
     static constexpr int W = XT * NT <= 4 ? 3 : 2;
 };
 
-template <int XT, int NT, int MB>
-__global__ __launch_bounds__(kThreads, (SsdOcc<XT, NT>::W)) void k_ssd_mfma(MatchParams a, int hb, int bias, int dbg) {
+// SSD matrix-core kernel.  One block = 4 waves = a band of hb output rows x 128 XT columns; row
+// step s of the band (s = 0 .. rows + win - 2) enters image row y0 - r + s and leaves row
+// y0 - r + s - win.  Software-pipelined: iteration s runs, between two barriers,
+//   B(s)   the MFMAs of step s (operand slot s % 3),
+//   A(s+1) hsq / SR2 / U of step s + 1 (slot (s + 1) % 3's ~R') and the copies of step s + 2
+//          (slot (s + 2) % 3, from the raw ring),
+//   E(s)   the keys and the output row of step s (U buffer s & 1),
+// all independent, and branch-free so the compiler can interleave them (LDS latency under
+// MFMA and VALU work).  BM: edge masking by the accumulator offset (see SsdShape).
+template <int XT, int NT, int MB, bool BM>
+__global__ __launch_bounds__(kThreads, (SsdOcc<XT, NT>::W)) void k_ssd_mfma(MatchParams a, int hb, int bias,
+                                                                          uint32_t off) {
     using C = SsdCfg<XT, NT, MB>;
-    constexpr int M = C::M;
-    constexpr int DWL = C::CL::DW, DWR = C::CR::DW;
+    constexpr int M = C::M, DWC = C::DWC, XPP = C::XPP, PRE = C::PRE;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, j = lane & 31;
     const int z = blockIdx.z;
     const uint8_t* Limg = a.L + z * a.fs_in;
     const uint8_t* Rimg = a.R + z * a.fs_in;
-    int16_t* out = a.out + z * a.fs_out;
     const int W = a.W, H = a.H, r = a.r, win = a.win, D = a.D;
     const int xw = a.X0 + blockIdx.x * C::XW;               // first output column of the block
     const int xpb = xw - (a.minD + D - 1);                  // x' of ix' = 0
@@ -179,68 +167,69 @@ __global__ __launch_bounds__(kThreads, (SsdOcc<XT, NT>::W)) void k_ssd_mfma(Matc
     const int y1 = min(a.row1, y0 + hb);
     if (y0 >= y1) return;
     const int hr = win + 2;                                 // hsq ring rows
+    const int rawr = win + PRE;                             // raw ring rows
     // physical row streams start 4-byte aligned: logical byte b of the L' stream (column
     // xw - r + b) is physical byte b + oL
     const int aL = (xw - r) & ~3, oL = (xw - r) - aL;
     const int aR = (xpb - r) & ~3, oR = (xpb - r) - aR;
-    auto slot = [&](int side, int k) { return smem + (side * 3 + k) * C::SLOT; };   // side 0 enter, 1 leave
-    int32_t* hsq = reinterpret_cast<int32_t*>(smem + 6 * C::SLOT);          // [hr][XPW]
-    uint32_t* Ub = reinterpret_cast<uint32_t*>(smem + 6 * C::SLOT + hr * 4 * C::XPW);   // [2][XPW]
+    uint32_t* const sm32 = reinterpret_cast<uint32_t*>(smem);
+    int32_t* const hsq = reinterpret_cast<int32_t*>(smem + 6 * C::SLOT);                  // [hr][XPP]
+    uint32_t* const Ub = reinterpret_cast<uint32_t*>(smem + 6 * C::SLOT + hr * 4 * XPP);  // [2][XPP]
+    uint32_t* const raw = Ub + 2 * XPP;                                                    // [rawr][kThreads]
 
-    // ---- staging.  Raw rows: the entering row of step k (L' stream dwords, then R') lands in raw
-    // ring row k % rawr by LDS-DMA issued PRE steps ahead (always one per step and thread, so
-    // the counted wait below is exact: rows past the band reload the clamped last row into a
-    // ring row no build reads again).  Copies: phase A of step s builds step s + 1's entering
-    // slot (raw row s + 1: L' and ~R') and leaving slot (raw row s + 1 - win: L' and R').
-    constexpr int PRE = C::PRE;
-    const int rawr = win + PRE;
-    uint32_t* raw = reinterpret_cast<uint32_t*>(Ub + 2 * C::XPW);   // [rawr][kThreads]
+    // ---- raw rows: one LDS-DMA per thread and step (the thread's dword of the L' | R' streams,
+    // clamped into the image row; rows past the band reload the clamped last row into a ring
+    // row no copy reads again), so the counted waits below are exact
     const bool isLq = tid < C::NLD;
-    const int c0q = isLq ? aL + 4 * tid : aR + 4 * (tid - C::NLD);   // this thread's raw dword
+    const int c0q = isLq ? aL + 4 * tid : aR + 4 * (tid - C::NLD);
     const uint8_t* gq = (isLq ? Limg : Rimg) + clamp_dword(c0q, W);
-    const bool edge = aL < 0 || aR < 0 || aL + 4 * C::NLD > W || aR + 4 * C::NRD > W;
-    auto issue_raw = [&](int k, int rk) {   // rk = k % rawr
+    auto issue_raw = [&](int k, int rk) {   // the entering row of step k into ring row rk
         const int y = min(max(y0 - r + k, 0), H - 1);
         typedef __attribute__((address_space(1))) void gvoid;
         typedef __attribute__((address_space(3))) void lvoid;
         __builtin_amdgcn_global_load_lds((gvoid*)(gq + (size_t)y * a.pitch), (lvoid*)(raw + rk * kThreads + wave * 64),
                                          4, 0, 0);
     };
-    // copies of step k into slot ks (= k % 3): side 0 = raw row k (ring row r0 = k % rawr: L',
-    // ~R'), side 1 = raw row k - win (ring row r1: L', R').  All ring indices are block-uniform
-    // and advance incrementally (a runtime modulo is a VALU reciprocal chain plus readfirstlane)
-    auto build = [&](int k, int ks, int r0, int r1) {
-        const int sides = k >= win ? 2 : 1;
-        const uint32_t* p0 = raw + r0 * kThreads;
-        const uint32_t* p1 = raw + r1 * kThreads;
+
+    // ---- the copy builder: item q < NIT of a step builds dword w of the entering slot's L' or
+    // ~R' copies from raw row k, item NIT + q the leaving slot's L' or R' from raw row k - win;
+    // each thread's items are fixed, so their addresses, xor masks and edge selectors are
+    // computed once (the edge byte select is the identity inside the image)
+    int b_rq[C::NB], b_rqh[C::NB], b_dst[C::NB];
+    uint32_t b_x[C::NB], b_slo[C::NB], b_shi[C::NB];
+    bool b_side[C::NB];
 #pragma unroll
-        for (int u = 0; u < (2 * C::NIT + kThreads - 1) / kThreads; ++u) {
-            const int q = tid + u * kThreads;
-            if (q >= sides * C::NIT) break;
-            const int side = q < C::NIT ? 0 : 1;
-            const int rq = side ? q - C::NIT : q;
-            const uint32_t* p = side ? p1 : p0;
-            const bool isL = rq < C::NLD;
-            const int w = isL ? rq : rq - C::NLD;
-            const bool more = isL ? (w + 1 < C::NLD) : (w + 1 < C::NRD);
-            uint32_t lo = p[rq];
-            uint32_t hi = more ? p[rq + 1] : lo;
-            if (edge) {   // block-uniform
-                const int c0 = (isL ? aL : aR) + 4 * w;
-                lo = edge_fix(lo, c0, W);
-                hi = edge_fix(hi, c0 + 4, W);
-            }
-            // L' = L ^ 0x80 both sides; R side: ~R' = R ^ 0x7f entering, R' = R ^ 0x80 leaving
-            const uint32_t x = (isL || side) ? 0x80808080u : 0x7F7F7F7Fu;
-            lo ^= x;
-            hi ^= x;
-            uint32_t* base = reinterpret_cast<uint32_t*>(slot(side, ks) + (isL ? 0 : C::CL::SIZE));
-            const int dw = isL ? DWL : DWR;
+    for (int u = 0; u < C::NB; ++u) {
+        const int q = tid + u * kThreads;
+        const bool real = q < 2 * C::NIT;
+        const int side = real && q >= C::NIT ? 1 : (real ? 0 : 1);
+        const int rq = real ? (side ? q - C::NIT : q) : 0;
+        const bool isL = !real || rq < C::NLD;
+        const int w = real ? (isL ? rq : rq - C::NLD) : C::NLD;   // idle threads: a pad dword
+        const bool more = isL ? (w + 1 < C::NLD) : (w + 1 < C::NRD);
+        const int c0 = (isL ? aL : aR) + 4 * w;
+        b_rq[u] = rq;
+        b_rqh[u] = real && more ? rq + 1 : rq;
+        b_side[u] = side;
+        b_dst[u] = side * 3 * (C::SLOT / 4) + (isL ? 0 : C::SIDE / 4) + w;
+        // L' = L ^ 0x80 both sides; R side: ~R' = R ^ 0x7f entering, R' = R ^ 0x80 leaving
+        b_x[u] = (isL || side) ? 0x80808080u : 0x7F7F7F7Fu;
+        b_slo[u] = edge_sel(c0, W);
+        b_shi[u] = real && more ? edge_sel(c0 + 4, W) : b_slo[u];
+    }
+    auto build = [&](int ks, int r0, int r1) {   // slot ks from ring rows r0 (entering), r1 (leaving)
 #pragma unroll
-            for (int sh = 0; sh < 4; ++sh) base[sh * dw + w] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        for (int u = 0; u < C::NB; ++u) {
+            const uint32_t* p = raw + (b_side[u] ? r1 : r0) * kThreads;
+            const uint32_t lo = __builtin_amdgcn_perm(p[b_rq[u]], p[b_rq[u]], b_slo[u]) ^ b_x[u];
+            const uint32_t hi = __builtin_amdgcn_perm(p[b_rqh[u]], p[b_rqh[u]], b_shi[u]) ^ b_x[u];
+            uint32_t* d = sm32 + ks * (C::SLOT / 4) + b_dst[u];
+#pragma unroll
+            for (int sh = 0; sh < 4; ++sh) d[sh * DWC] = __builtin_amdgcn_alignbyte(hi, lo, sh);
         }
     };
-    // the taps i >= win are zero on the L side (A operand) and in the hsq sums
+
+    // the taps i >= win are zero on the L side (the MFMA's B operand) and in the hsq sums
     v4i wmask;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -248,146 +237,191 @@ __global__ __launch_bounds__(kThreads, (SsdOcc<XT, NT>::W)) void k_ssd_mfma(Matc
         wmask[q] = nb >= 4 ? -1 : (int)((1u << (8 * nb)) - 1u);
     }
 
-    int sr2[3] = {0, 0, 0};
+    // ---- A(k): hsq of step k's entering row (its ~R' copies), SR2 and U(k).  Thread-owned
+    // columns (hsq needs no barrier); columns past XPW compute into the pad column block
+    int sr2[C::NJ];
+#pragma unroll
+    for (int jj = 0; jj < C::NJ; ++jj) sr2[jj] = 0;
+    auto phaseA = [&](int ks, int he, int hl, int ub, bool leave) {
+        const uint32_t* er = sm32 + ks * (C::SLOT / 4) + C::SIDE / 4;   // ~R'
+        int32_t* hs_e = hsq + he * XPP;
+        const int32_t* hs_l = hsq + hl * XPP;
+        uint32_t* U = Ub + ub * XPP;
+        const int lm = leave ? -1 : 0;
+#pragma unroll
+        for (int jj = 0; jj < C::NJ; ++jj) {
+            const int ix = min(tid + jj * kThreads, C::XPW + (tid & 31));
+            const v4i v = ld16c(er, DWC, ix + oR);
+            int hs = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int m = ~v[q] & wmask[q];   // R' = ~(~R')
+                hs = __builtin_amdgcn_sdot4(m, m, hs, false);
+            }
+            const int old = hs_l[ix];
+            hs_e[ix] = hs;
+            sr2[jj] += hs - (old & lm);
+            // unsigned keys: + off (a multiple of M >= the key range's half-width)
+            U[ix] = (uint32_t)((sr2[jj] - bias) * M - ix) + off;
+        }
+    };
+
+    // ---- accumulators; lane-constant selection of the edge tiles: cell (x' row i, x column j)
+    // of the first x'-tile of an x-tile is a valid disparity iff i >= j, of the last iff i < j
+    // (D % 32 == 0).  BM: the invalid cells start at 2^(30 - MB), i.e. their keys sit 2^31 above
+    // the true ones (the sliding sums only add and remove rows, so the offset stays): the valid
+    // keys lie in [0, 2R], the invalid ones in [2^31, 2^31 + 2R] — above every valid one
+    bool sel0[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sel0[q] = ((q & 3) + 8 * (q >> 2) + 4 * h) >= j;
     v16i acc[XT][NT];
 #pragma unroll
     for (int k = 0; k < XT; ++k)
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) acc[k][t][q] = 0;
-    const int h = lane >> 5, j = lane & 31;
-    // lane-constant selection of the edge tiles: cell (x row i, x' column j) of x'-tile 0 is a
-    // valid disparity iff j >= i, of x'-tile NT-1 iff j < i (D % 32 == 0)
-    bool sel0[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) sel0[q] = j >= ((q & 3) + 8 * (q >> 2) + 4 * h);
+            for (int q = 0; q < 16; ++q) {
+                int v = 0;
+                if (BM && t == 0) v = sel0[q] ? 0 : (1 << (30 - MB));
+                if (BM && t == NT - 1) v = sel0[q] ? (1 << (30 - MB)) : 0;
+                acc[k][t][q] = v;
+            }
 
+    // ---- B(s): A = R' rows (32 x' of an x'-tile), B = L' columns (32 x of an x-tile): a lane
+    // holds ONE x column and 16 x' rows, so the minimum over x' stays inside the lane.  K =
+    // [16 taps of the entering row (lanes 0..31) | 16 of the leaving row (lanes 32..63)];
+    // entering ~R' (= -R' - 1), leaving R': the accumulator holds -X - Cor(x)
+    const int hside = h * 3 * (C::SLOT / 4);               // the lane's half: entering / leaving slot
+    const int hmask = h ? 0 : -1;
+    auto phaseB = [&](int ks, bool leave) {
+        const uint32_t* sp = sm32 + ks * (C::SLOT / 4) + hside;
+        const int lm = hmask | (leave ? -1 : 0);          // warm-up: the leaving half adds nothing
+        const v4i wm = wmask & lm;
+        v4i lop[XT];
+#pragma unroll
+        for (int k = 0; k < XT; ++k) lop[k] = ld16c(sp, DWC, 32 * (wave * XT + k) + j + oL) & wm;
+#pragma unroll
+        for (int gi = 0; gi < XT + NT - 1; ++gi) {
+            const v4i rop = ld16c(sp + C::SIDE / 4, DWC, 32 * (wave * XT + gi) + j + oR);
+#pragma unroll
+            for (int k = 0; k < XT; ++k) {
+                const int t = gi - k;
+                if (t >= 0 && t < NT) acc[k][t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(rop, lop[k], acc[k][t], 0, 0, 0);
+            }
+        }
+    };
+
+    // ---- E(s): key = U(x') + 2M * acc; the minimum over the lane's x' rows and x'-tiles, x'-tile
+    // by x'-tile (its U rows serve every x-tile it pairs with); without BM a lane-constant
+    // select voids the edge tiles' invalid cells.  The two lane halves hold the two x' row
+    // halves of one x: v_permlane32_swap exchanges the upper half of one register with the lower
+    // half of the other, so with two x-tiles lanes 0..31 end with x-tile 0 and lanes 32..63 with
+    // x-tile 1 — 64 consecutive output columns, one buffer store (lanes with nothing to write
+    // store past the descriptor's range: dropped, no exec branch, one store per step exactly)
+    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(a.out + z * a.fs_out, 0, 0x7FFFFFFF, 0x00020000);
+    const int kk = XT == 2 ? h : 0;
+    const int cst = 32 * (wave * XT + kk) + j;             // the stored column's block index
+    const bool st_ok = (XT == 2 || h == 0) && xw + cst < a.X1;
+    auto phaseE = [&](int ub, int y) {
+        const uint32_t* U = Ub + ub * XPP + 4 * h;
+        uint32_t b0[XT], b1[XT];
+#pragma unroll
+        for (int k = 0; k < XT; ++k) b0[k] = b1[k] = 0xFFFFFFFFu;
+#pragma unroll
+        for (int gi = 0; gi < XT + NT - 1; ++gi) {
+            // U of the 16 x' rows the lane holds: rows 8g + 4h + 0..3, one 16-byte LDS
+            // broadcast per g (every lane of a half reads the same address)
+            uint32_t u[16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const v4i v = *reinterpret_cast<const v4i*>(U + 32 * (wave * XT + gi) + 8 * g);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) u[4 * g + e] = (uint32_t)v[e];
+            }
+#pragma unroll
+            for (int k = 0; k < XT; ++k) {
+                const int t = gi - k;
+                if (t < 0 || t >= NT) continue;
+                uint32_t kv[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    kv[q] = ((uint32_t)acc[k][t][q] << (MB + 1)) + u[q];
+                    if (!BM && t == 0) kv[q] = sel0[q] ? kv[q] : 0xFFFFFFFFu;
+                    if (!BM && t == NT - 1) kv[q] = sel0[q] ? 0xFFFFFFFFu : kv[q];
+                }
+#pragma unroll
+                for (int q = 0; q < 16; q += 4) {
+                    b0[k] = min3u(b0[k], kv[q], kv[q + 1]);
+                    b1[k] = min3u(b1[k], kv[q + 2], kv[q + 3]);
+                }
+            }
+        }
+        uint32_t res;
+        if constexpr (XT == 2) {
+            const auto p = __builtin_amdgcn_permlane32_swap(min(b0[0], b1[0]), min(b0[1], b1[1]), false, false);
+            res = min((uint32_t)p[0], (uint32_t)p[1]);
+        } else {
+            const uint32_t b = min(b0[0], b1[0]);
+            const auto p = __builtin_amdgcn_permlane32_swap(b, b, false, false);
+            res = min((uint32_t)p[0], (uint32_t)p[1]);
+        }
+        // d - minD = (c - ix') + D - 1 and the key's low MB bits hold -ix' (off % M == 0)
+        const int drel = (int)((res + (uint32_t)(cst + D - 1)) & (uint32_t)(M - 1));
+        const int o = st_ok ? 2 * (y * a.opitch + xw + cst) : (int)0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)((a.minD + drel) * 16), orsrc, o, 0, 0);
+    };
+
+    // ---- prologue: raw rows 0 .. PRE - 1; copies of steps 0 and 1; A(0)
     const int nsteps = (y1 - y0) + win - 1;
-    // the DMA of raw row k is issued at step k - PRE (the prologue issues rows 0 .. PRE - 1) and
-    // retired by the counted wait of step k - 2, whose barrier precedes build(k) in step k - 1:
-    // PRE - 2 younger DMAs per thread may stay in flight (the epilogue's stores, also counted,
-    // only make the wait stricter)
-    static_assert(PRE == 5, "vmcnt immediate below");
+    auto inc = [](int v, int n) { return v + 1 == n ? 0 : v + 1; };
+    static_assert(PRE == 5, "vmcnt immediates below");
 #pragma unroll
     for (int k = 0; k < PRE; ++k) issue_raw(k, k);
     asm volatile("s_waitcnt vmcnt(3)" ::: "memory");   // rows 0 and 1
     lds_barrier();
-    build(0, 0, 0, 0);
+    build(0, 0, 0);                                     // (no leaving row yet: its half is masked)
     lds_barrier();
-    auto inc = [](int v, int n) { return v + 1 == n ? 0 : v + 1; };
-    // s % 3, s % hr, (s + 2) % hr (= the leaving hsq row, hr = win + 2), (s + PRE) % rawr,
-    // (s + 1) % rawr, (s + 1 + PRE) % rawr (= raw row s + 1 - win)
-    int si = 0, he = 0, hl = 2 % hr, rp = PRE, rb = 1 % rawr, rbl = (1 + PRE) % rawr;
-    for (int s = 0; s < nsteps;
-         ++s, si = inc(si, 3), he = inc(he, hr), hl = inc(hl, hr), rp = inc(rp, rawr), rb = inc(rb, rawr),
-         rbl = inc(rbl, rawr)) {
-        const bool leave = s >= win;
+    phaseA(0, 0, 2 % hr, 0, false);
+    build(1, 1 % rawr, (1 + PRE) % rawr);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // row 2
+    lds_barrier();
+
+    // ring indices, advanced incrementally (a runtime modulo is a VALU reciprocal chain):
+    // si = s % 3, ha = (s + 1) % hr, hl = (s + 3) % hr (the row leaving at step s + 1, hr = win
+    // + 2), rp = (s + PRE) % rawr, rb = (s + 2) % rawr, rbl = (s + 2 - win) % rawr
+    int si = 0, ha = 1 % hr, hl = 3 % hr, rp = PRE % rawr, rb = 2 % rawr, rbl = (2 + PRE) % rawr;
+    // raw row s + 3 (issued at iteration s - 2) is retired at the end of iteration s; the ops
+    // younger than it: the DMAs of iterations s - 1 and s and, once outputs are stored (one
+    // store per iteration from step win - 1 on), the stores of iterations s - 2 .. s
+    auto iteration = [&](int s, auto epi) {
+        constexpr bool EPI = decltype(epi)::value;
+        const int s1 = inc(si, 3), s2 = inc(s1, 3);
         issue_raw(s + PRE, rp);
-        // ---- phase A: hsq of the entering row, SR2, U; stage the next step's rows ------------
-        {
-            const uint32_t* er = reinterpret_cast<const uint32_t*>(slot(0, si) + C::CL::SIZE);   // ~R'
-            int32_t* hs_e = hsq + he * C::XPW;
-            const int32_t* hs_l = hsq + hl * C::XPW;
-            uint32_t* U = Ub + (s & 1) * C::XPW;
-#pragma unroll
-            for (int jj = 0; jj < 3; ++jj) {
-                const int ix = tid + jj * kThreads;
-                if (ix < C::XPW) {
-                    const v4i v = ld16c(er, DWR, ix + oR);
-                    int hs = 0;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int m = ~v[q] & wmask[q];   // R' = ~(~R')
-                        hs = __builtin_amdgcn_sdot4(m, m, hs, false);
-                    }
-                    hs_e[ix] = hs;
-                    sr2[jj] += hs - (leave ? hs_l[ix] : 0);
-                    // unsigned keys: + 2^31 makes the signed order the unsigned one
-                    U[ix] = (uint32_t)((sr2[jj] - bias) * M - ix) + 0x80000000u;
-                }
-            }
-            if (s + 1 < nsteps) build(s + 1, inc(si, 3), rb, rbl);
+        phaseB(si, s >= win);
+        phaseA(s1, ha, hl, (s + 1) & 1, s + 1 >= win);
+        build(s2, rb, rbl);
+        if constexpr (EPI) {
+            phaseE(s & 1, y0 + s - (win - 1));
+            const int e = s - (win - 1);                 // stored steps before this one
+            if (e >= 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+            else if (e == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         }
-        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");   // raw row s + 2 (issued at step s - 3)
         lds_barrier();
-        // ---- phase B: one MFMA per (x-tile, x'-tile) pair --------------------------------------
-        const uint8_t* se = slot(0, si);
-        const uint8_t* sl = slot(1, si);
-        v4i aop[XT];
-#pragma unroll
-        for (int k = 0; k < XT; ++k) {
-            const int c = 32 * (wave * XT + k) + j;   // A row = x column xw + c
-            if (h == 0) aop[k] = ld16c(reinterpret_cast<const uint32_t*>(se), DWL, c + oL) & wmask;
-            else if (leave) aop[k] = ld16c(reinterpret_cast<const uint32_t*>(sl), DWL, c + oL) & wmask;
-            else aop[k] = v4i{0, 0, 0, 0};   // warm-up: the leaving half contributes nothing
-        }
-#pragma unroll
-        for (int gi = 0; gi < XT + NT - 1; ++gi) {
-            const int ix = 32 * (wave * XT + gi) + j;   // B column = x' of ix
-            // entering half ~R' (= -R' - 1), leaving half R': the accumulator holds -X - Cor(x)
-            const v4i bop = ld16c(reinterpret_cast<const uint32_t*>((h == 0 ? se : sl) + C::CL::SIZE), DWR, ix + oR);
-#pragma unroll
-            for (int k = 0; k < XT; ++k) {
-                const int t = gi - k;
-                if (t >= 0 && t < NT && !(dbg & 1)) acc[k][t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aop[k], bop, acc[k][t], 0, 0, 0);
-                if (t >= 0 && t < NT && (dbg & 1)) acc[k][t][0] ^= aop[k][0] ^ bop[1];
-            }
-        }
-        if (s < win - 1) continue;   // the window of the first output row is not complete yet
-        if (dbg & 2) {               // A/B timing: no epilogue
-            if (h == 0 && (acc[0][0][0] == 0x7fffffff)) out[0] = 1;
-            continue;
-        }
-        const int y = y0 + s - (win - 1);
-        const uint32_t* U = Ub + (s & 1) * C::XPW;
-        uint32_t T[XT + NT - 1];
-#pragma unroll
-        for (int gi = 0; gi < XT + NT - 1; ++gi) T[gi] = U[32 * (wave * XT + gi) + j];
-        // ---- keys: key = U(x') + 2M * acc, the running minimum over the x'-tiles per x row ----
-#pragma unroll
-        for (int k = 0; k < XT; ++k) {
-            uint32_t best[16], ka[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {   // the edge pair: complementary triangles
-                const uint32_t e0 = ((uint32_t)acc[k][0][q] << (MB + 1)) + T[k];
-                const uint32_t e1 = ((uint32_t)acc[k][NT - 1][q] << (MB + 1)) + T[k + NT - 1];
-                best[q] = sel0[q] ? e0 : e1;
-            }
-#pragma unroll
-            for (int t = 1; t < NT - 1; t += 2) {
-                if (t + 1 < NT - 1) {
-#pragma unroll
-                    for (int q = 0; q < 16; ++q)
-                        best[q] = min3u(best[q], ((uint32_t)acc[k][t][q] << (MB + 1)) + T[k + t],
-                                        ((uint32_t)acc[k][t + 1][q] << (MB + 1)) + T[k + t + 1]);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) best[q] = min(best[q], ((uint32_t)acc[k][t][q] << (MB + 1)) + T[k + t]);
-                }
-            }
-            // min over the 32 x' columns (lanes) of each half, per x row (register): the
-            // 16-lane rows first (permlane16_swap pairs registers), then a reduce-scatter
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const auto p = __builtin_amdgcn_permlane16_swap(best[2 * q], best[2 * q + 1], false, false);
-                ka[q] = min((uint32_t)p[0], (uint32_t)p[1]);
-            }
-            uint32_t v8[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) v8[q] = ka[q];
-            reduce_scatter8(v8, lane & 15);
-            // lanes 2m, 2m+1 of 16-lane row rho hold x row reg = 2m + rho
-            const int reg = 2 * ((lane >> 1) & 7) + ((lane >> 4) & 1);
-            const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            const int c = 32 * (wave * XT + k) + i;
-            const int x = xw + c;
-            if ((lane & 1) == 0 && x < a.X1) {
-                const int drel = (int)((v8[0] + (uint32_t)(c + D - 1)) & (uint32_t)(M - 1));
-                out[(size_t)y * a.opitch + x] = (int16_t)((a.minD + drel) * 16);
-            }
-        }
-    }
+        si = s1;
+        ha = inc(ha, hr);
+        hl = inc(hl, hr);
+        rp = inc(rp, rawr);
+        rb = inc(rb, rawr);
+        rbl = inc(rbl, rawr);
+    };
+    int s = 0;
+    for (; s < win - 1; ++s) iteration(s, std::false_type{});
+    for (; s < nsteps; ++s) iteration(s, std::true_type{});
+    // the DMAs still in flight land in this block's LDS: drain them before the block ends
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // invalid columns [0, X0) and [X1, W) of rows [row0, row1) (the matched band of valid_columns)
@@ -401,12 +435,16 @@ __global__ void k_fill_sides(int16_t* out, int opitch, long long fs_out, int row
 
 struct SsdShape {
     int xt, nt, mb, hb, bias;
+    bool big;       // edge cells masked by the accumulator offset (R < 2^30)
+    uint32_t off;   // key offset (a multiple of M): R rounded up (big) or 2^31
 };
 
 // Whether the MFMA kind runs (win, D) and its tile / band shape.  Key range: val - bias in
 // [-hw, hw] (val = SR2 - 2X, bias = its centre), the leaving-row term bounded by the band height
-// hb: |2M * Cor| <= 2M * (hb + win) * win * 128 (one term per entering row); M * hw + that + the
-// x' index must stay below 2^31 (the keys are compared exactly; the shift wraps nothing).
+// hb: |2M * Cor| <= 2M * (hb + win) * win * 128 (one term per entering row); the half-width
+// R = M * hw + that + the x' index.  The keys are exact modulo 2^32 (the shift may wrap, the
+// sum lands back in [off - R, off + R]): R < 2^31 with off = 2^31, and R < 2^30 for the offset
+// masking (off = R; 1080p D=128: windows <= 13; D=160: <= 9).
 bool ssd_shape(int win, int D, int rows, SsdShape* sh) {
     // D > 160 (7+ x'-tiles): the accumulators no longer fit beside the operands (spills; the
     // 4K D=256 w9 frame ran 3.2x slower than the ring kernel) — the ring / one-row kinds keep it
@@ -428,26 +466,25 @@ bool ssd_shape(int win, int D, int rows, SsdShape* sh) {
     if (hb < 1) hb = 1;
     const long long cor = (long long)(hb + win) * win * 128;
     const long long xpw = 32LL * (4 * xt + nt - 1);
-    if (M * hw + 2 * M * cor + xpw + 64 >= (1LL << 31)) return false;
-    if (2 * M * (sl2 + cor) >= (1LL << 31)) return false;   // 2M * acc itself
-    *sh = SsdShape{xt, nt, mb, hb, (int)bias};
+    const long long R = M * hw + 2 * M * cor + xpw + 64;
+    if (R >= (1LL << 31)) return false;
+    // the offset is a multiple of M: the disparity index is read from the key's low bits
+    const long long off = (R + M - 1) / M * M;
+    const bool big = off < (1LL << 30);
+    *sh = SsdShape{xt, nt, mb, hb, (int)bias, big, big ? (uint32_t)off : 0x80000000u};
     return true;
 }
 
-template <int XT, int NT, int MB>
+template <int XT, int NT, int MB, bool BM>
 int launch_t(const MatchParams& a, const SsdShape& sh, hipStream_t s) {
     using C = SsdCfg<XT, NT, MB>;
     const int nf = a.nf > 1 ? a.nf : 1;
     const int rows = a.row1 - a.row0;
     dim3 grid((a.X1 - a.X0 + C::XW - 1) / C::XW, (rows + sh.hb - 1) / sh.hb, nf);
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ssd_mfma<XT, NT, MB>),
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ssd_mfma<XT, NT, MB, BM>),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, C::lds(15));
     if (attr != hipSuccess) return (int)attr;
-    static const int dbg = [] {
-        const char* e = std::getenv("SV_SSD_DBG");   // A/B timing only: 1 no MFMA, 2 no epilogue
-        return e ? std::atoi(e) : 0;
-    }();
-    hipLaunchKernelGGL((k_ssd_mfma<XT, NT, MB>), grid, dim3(kThreads), C::lds(a.win), s, a, sh.hb, sh.bias, dbg);
+    hipLaunchKernelGGL((k_ssd_mfma<XT, NT, MB, BM>), grid, dim3(kThreads), C::lds(a.win), s, a, sh.hb, sh.bias, sh.off);
     return (int)hipGetLastError();
 }
 
@@ -463,7 +500,9 @@ bool ssd_mfma_fits(const MatchParams& a, int cost) {
     // stride must be multiples of 4 (torch / hipMalloc buffers of even widths are)
     const uintptr_t al = reinterpret_cast<uintptr_t>(a.L) | reinterpret_cast<uintptr_t>(a.R) | (uintptr_t)a.pitch |
                          (uintptr_t)(a.nf > 1 ? a.fs_in : 0);
-    return ssd_mfma(cost, a.win, a.D) && a.r == a.win / 2 && (al & 3) == 0;
+    // the output stores are 32-bit byte offsets from one buffer descriptor per frame
+    const bool ofits = 2LL * ((long long)a.row1 * a.opitch + a.W) < 0x7FFFFFFFLL;
+    return ssd_mfma(cost, a.win, a.D) && a.r == a.win / 2 && (al & 3) == 0 && ofits;
 }
 
 int launch_ssd_mfma(const MatchParams& a, hipStream_t s) {
@@ -487,18 +526,22 @@ int launch_ssd_mfma(const MatchParams& a, hipStream_t s) {
     }();
     SsdShape s2 = sh;
     if (xt_env == 1 || xt_env == 2) s2.xt = sh.nt <= 5 ? xt_env : 1;
-    switch (sh.nt * 4 + s2.xt) {
-        case 2 * 4 + 1: return launch_t<1, 2, 7>(b, s2, s);
-        case 2 * 4 + 2: return launch_t<2, 2, 7>(b, s2, s);
-        case 3 * 4 + 1: return launch_t<1, 3, 7>(b, s2, s);
-        case 3 * 4 + 2: return launch_t<2, 3, 7>(b, s2, s);
-        case 4 * 4 + 1: return launch_t<1, 4, 7>(b, s2, s);
-        case 4 * 4 + 2: return launch_t<2, 4, 7>(b, s2, s);
-        case 5 * 4 + 1: return launch_t<1, 5, 7>(b, s2, s);
-        case 5 * 4 + 2: return launch_t<2, 5, 7>(b, s2, s);
-        case 6 * 4 + 1: return launch_t<1, 6, 8>(b, s2, s);
-    }
-    return (int)hipErrorInvalidValue;
+    const auto go = [&](auto bm) {
+        constexpr bool BM = decltype(bm)::value;
+        switch (sh.nt * 4 + s2.xt) {
+            case 2 * 4 + 1: return launch_t<1, 2, 7, BM>(b, s2, s);
+            case 2 * 4 + 2: return launch_t<2, 2, 7, BM>(b, s2, s);
+            case 3 * 4 + 1: return launch_t<1, 3, 7, BM>(b, s2, s);
+            case 3 * 4 + 2: return launch_t<2, 3, 7, BM>(b, s2, s);
+            case 4 * 4 + 1: return launch_t<1, 4, 7, BM>(b, s2, s);
+            case 4 * 4 + 2: return launch_t<2, 4, 7, BM>(b, s2, s);
+            case 5 * 4 + 1: return launch_t<1, 5, 7, BM>(b, s2, s);
+            case 5 * 4 + 2: return launch_t<2, 5, 7, BM>(b, s2, s);
+            case 6 * 4 + 1: return launch_t<1, 6, 8, BM>(b, s2, s);
+        }
+        return (int)hipErrorInvalidValue;
+    };
+    return s2.big ? go(std::true_type{}) : go(std::false_type{});
 }
 
 }  // namespace sv

@@ -455,7 +455,9 @@ bool ssd_shape(int win, int D, int rows, SsdShape* sh) {
     }();
     if (!on) return false;
     const int nt = D / 32 + 1;
-    const int xt = nt <= 5 ? 2 : 1;
+    // two x-tiles per wave from 4 x'-tiles up (D >= 96; w9 1080p: equal, w15 +15 %), one below
+    // (VGA D=64: +8 %) and at D = 160 (the accumulators of 2 x 6 tiles do not fit)
+    const int xt = nt >= 4 && nt <= 5 ? 2 : 1;
     const int mb = D <= 128 ? 7 : 8;
     const long long M = 1LL << mb;
     const long long n = (long long)win * win;

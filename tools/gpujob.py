@@ -14,6 +14,7 @@ abort, a time limit or a failing test ends the call: nothing more touches the GP
     trace[=ARGS]               rocprofv3 --kernel-trace --stats over bench.py ARGS
     pmc=C1,C2,..[@ARGS]        one rocprofv3 --pmc pass over bench.py ARGS (counters summed
                                per kernel, mean per dispatch printed)
+                               (trace / pmc ARGS may start with NAME=VALUE environment tokens)
     ab=ENV1|ENV2|..[@ARGS]     alternating bench runs under env variants ("-" = none)
     valu[=WPS,..]              tools/microbench/valu_rate at each waves-per-SIMD count
     cmd=SHELL                  any command (bash -c)
@@ -91,6 +92,16 @@ def pmc_summary(outdir):
     return "\n".join(f"  {k[0]:<60} {k[1]:<22} mean {sum(v) / len(v):.4g}  n {len(v)}" for k, v in rows)
 
 
+def split_env(env, args):
+    """Leading NAME=VALUE tokens of ARGS -> (env with them set, the remaining args)."""
+    toks = shlex.split(args)
+    e2 = dict(env)
+    while toks and "=" in toks[0] and not toks[0].startswith("-"):
+        k, _, v = toks.pop(0).partition("=")
+        e2[k] = v
+    return e2, toks
+
+
 def main():
     if len(sys.argv) < 3:
         print(__doc__)
@@ -118,17 +129,19 @@ def main():
                 extra = bench_summary(log)
         elif kind == "trace":
             d = os.path.join(out, f"{i:02d}_trace")
+            e2, bargs = split_env(env, arg)
             cmd = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "trace",
-                   "--", sys.executable, os.path.join(ROOT, "bench.py")] + BENCH_QUIET + ["--no-aux"] + shlex.split(arg)
-            rc, dt = run(cmd, log, limit, env, cwd="/tmp")
+                   "--", sys.executable, os.path.join(ROOT, "bench.py")] + BENCH_QUIET + ["--no-aux"] + bargs
+            rc, dt = run(cmd, log, limit, e2, cwd="/tmp")
             for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
                 extra = "\n".join(ln[:160] for ln in open(f).read().splitlines()[:12])
         elif kind == "pmc":
             counters, _, bargs = arg.partition("@")
             d = os.path.join(out, f"{i:02d}_pmc")
+            e2, bl = split_env(env, bargs)
             cmd = (["rocprofv3", "--pmc"] + counters.split(",") + ["--output-format", "csv", "-d", d, "-o", "pmc",
-                    "--", sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child"] + shlex.split(bargs))
-            rc, dt = run(cmd, log, limit, env, cwd="/tmp")
+                    "--", sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child"] + bl)
+            rc, dt = run(cmd, log, limit, e2, cwd="/tmp")
             if rc == 0:
                 extra = pmc_summary(d)
         elif kind == "ab":

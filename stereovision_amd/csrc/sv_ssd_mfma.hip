@@ -82,11 +82,6 @@ struct Copies {
 // prefetch and the previous row's output stores would then be waited on at every row step.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__device__ __forceinline__ v4i ld16c(const uint32_t* copies, int dw, int p) {
-    const uint32_t* q = copies + (p & 3) * dw + (p >> 2);
-    return v4i{(int)q[0], (int)q[1], (int)q[2], (int)q[3]};
-}
-
 template <int XT, int NT, int MB>
 struct SsdCfg {
     static constexpr int M = 1 << MB;
@@ -112,7 +107,8 @@ struct SsdCfg {
     static_assert(NIT <= kThreads, "one raw dword per thread");
     static constexpr int NB = (2 * NIT + kThreads - 1) / kThreads;   // copy-builder items per thread
     static constexpr int NJ = (XPW + kThreads - 1) / kThreads;       // hsq columns per thread
-    static constexpr int RAWB = 4 * kThreads;
+    static constexpr int RAWD = (NIT + 63) / 64 * 64;   // raw ring row (dwords): the DMA waves' lanes
+    static constexpr int RAWB = 4 * RAWD;
     static constexpr int PRE = 5;                      // DMA issue distance (steps)
     // 3 entering + 3 leaving slots, the hsq ring (win + 2 rows), U[2], the raw ring (win + PRE)
     static constexpr int lds(int win) { return 6 * SLOT + (win + 2) * 4 * XPP + 2 * 4 * XPP + (win + PRE) * RAWB; }
@@ -175,19 +171,23 @@ __global__ __launch_bounds__(kThreads, (SsdOcc<XT, NT>::W)) void k_ssd_mfma(Matc
     uint32_t* const sm32 = reinterpret_cast<uint32_t*>(smem);
     int32_t* const hsq = reinterpret_cast<int32_t*>(smem + 6 * C::SLOT);                  // [hr][XPP]
     uint32_t* const Ub = reinterpret_cast<uint32_t*>(smem + 6 * C::SLOT + hr * 4 * XPP);  // [2][XPP]
-    uint32_t* const raw = Ub + 2 * XPP;                                                    // [rawr][kThreads]
+    uint32_t* const raw = Ub + 2 * XPP;                                                    // [rawr][RAWD]
 
-    // ---- raw rows: one LDS-DMA per thread and step (the thread's dword of the L' | R' streams,
-    // clamped into the image row; rows past the band reload the clamped last row into a ring
-    // row no copy reads again), so the counted waits below are exact
+    // ---- raw rows: one LDS-DMA per step from every wave that holds one of the NIT stream dwords
+    // (the thread's dword of the L' | R' streams, clamped into the image row; rows past the band
+    // reload the clamped last row into a ring row no copy reads again), so each wave's counted
+    // waits below are exact; a wave without stream dwords issues none (its waits then only
+    // cover its own stores)
     const bool isLq = tid < C::NLD;
     const int c0q = isLq ? aL + 4 * tid : aR + 4 * (tid - C::NLD);
     const uint8_t* gq = (isLq ? Limg : Rimg) + clamp_dword(c0q, W);
+    const bool dma_wave = 64 * wave < C::NIT;
     auto issue_raw = [&](int k, int rk) {   // the entering row of step k into ring row rk
+        if (!dma_wave) return;               // wave-uniform
         const int y = min(max(y0 - r + k, 0), H - 1);
         typedef __attribute__((address_space(1))) void gvoid;
         typedef __attribute__((address_space(3))) void lvoid;
-        __builtin_amdgcn_global_load_lds((gvoid*)(gq + (size_t)y * a.pitch), (lvoid*)(raw + rk * kThreads + wave * 64),
+        __builtin_amdgcn_global_load_lds((gvoid*)(gq + (size_t)y * a.pitch), (lvoid*)(raw + rk * C::RAWD + wave * 64),
                                          4, 0, 0);
     };
 
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(kThreads, (SsdOcc<XT, NT>::W)) void k_ssd_mfma(Matc
     auto build = [&](int ks, int r0, int r1) {   // slot ks from ring rows r0 (entering), r1 (leaving)
 #pragma unroll
         for (int u = 0; u < C::NB; ++u) {
-            const uint32_t* p = raw + (b_side[u] ? r1 : r0) * kThreads;
+            const uint32_t* p = raw + (b_side[u] ? r1 : r0) * C::RAWD;
             const uint32_t lo = __builtin_amdgcn_perm(p[b_rq[u]], p[b_rq[u]], b_slo[u]) ^ b_x[u];
             const uint32_t hi = __builtin_amdgcn_perm(p[b_rqh[u]], p[b_rqh[u]], b_shi[u]) ^ b_x[u];
             uint32_t* d = sm32 + ks * (C::SLOT / 4) + b_dst[u];
@@ -239,19 +239,26 @@ __global__ __launch_bounds__(kThreads, (SsdOcc<XT, NT>::W)) void k_ssd_mfma(Matc
 
     // ---- A(k): hsq of step k's entering row (its ~R' copies), SR2 and U(k).  Thread-owned
     // columns (hsq needs no barrier); columns past XPW compute into the pad column block
+    // LDS dword offset of the 16 operand bytes at stream byte p: copy p & 3, dword p >> 2; p
+    // advancing by 32 (one tile) moves it by 8 dwords, so one per-lane base serves every tile
+    // of a wave through the instructions' immediate offsets
+    auto lane_off = [](int p) { return (p & 3) * DWC + (p >> 2); };
+    const int offA = C::SIDE / 4 + lane_off(tid + oR);
     int sr2[C::NJ];
 #pragma unroll
     for (int jj = 0; jj < C::NJ; ++jj) sr2[jj] = 0;
     auto phaseA = [&](int ks, int he, int hl, int ub, bool leave) {
-        const uint32_t* er = sm32 + ks * (C::SLOT / 4) + C::SIDE / 4;   // ~R'
+        const uint32_t* er = sm32 + ks * (C::SLOT / 4) + offA;   // ~R' of column tid
         int32_t* hs_e = hsq + he * XPP;
         const int32_t* hs_l = hsq + hl * XPP;
         uint32_t* U = Ub + ub * XPP;
         const int lm = leave ? -1 : 0;
 #pragma unroll
         for (int jj = 0; jj < C::NJ; ++jj) {
+            // column tid + 256 jj: its copy dwords sit 64 jj further (immediate offsets)
             const int ix = min(tid + jj * kThreads, C::XPW + (tid & 31));
-            const v4i v = ld16c(er, DWC, ix + oR);
+            const uint32_t* e = er + 64 * jj;
+            const v4i v = v4i{(int)e[0], (int)e[1], (int)e[2], (int)e[3]};
             int hs = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -293,16 +300,20 @@ __global__ __launch_bounds__(kThreads, (SsdOcc<XT, NT>::W)) void k_ssd_mfma(Matc
     // entering ~R' (= -R' - 1), leaving R': the accumulator holds -X - Cor(x)
     const int hside = h * 3 * (C::SLOT / 4);               // the lane's half: entering / leaving slot
     const int hmask = h ? 0 : -1;
+    const int offL = hside + lane_off(32 * wave * XT + j + oL);
+    const int offR = hside + C::SIDE / 4 + lane_off(32 * wave * XT + j + oR);
     auto phaseB = [&](int ks, bool leave) {
-        const uint32_t* sp = sm32 + ks * (C::SLOT / 4) + hside;
+        const uint32_t* lp = sm32 + ks * (C::SLOT / 4) + offL;
+        const uint32_t* rp = sm32 + ks * (C::SLOT / 4) + offR;
         const int lm = hmask | (leave ? -1 : 0);          // warm-up: the leaving half adds nothing
         const v4i wm = wmask & lm;
         v4i lop[XT];
 #pragma unroll
-        for (int k = 0; k < XT; ++k) lop[k] = ld16c(sp, DWC, 32 * (wave * XT + k) + j + oL) & wm;
+        for (int k = 0; k < XT; ++k) lop[k] = v4i{(int)lp[8 * k], (int)lp[8 * k + 1], (int)lp[8 * k + 2], (int)lp[8 * k + 3]} & wm;
 #pragma unroll
         for (int gi = 0; gi < XT + NT - 1; ++gi) {
-            const v4i rop = ld16c(sp + C::SIDE / 4, DWC, 32 * (wave * XT + gi) + j + oR);
+            const uint32_t* q = rp + 8 * gi;
+            const v4i rop = v4i{(int)q[0], (int)q[1], (int)q[2], (int)q[3]};
 #pragma unroll
             for (int k = 0; k < XT; ++k) {
                 const int t = gi - k;
@@ -455,9 +466,11 @@ bool ssd_shape(int win, int D, int rows, SsdShape* sh) {
     }();
     if (!on) return false;
     const int nt = D / 32 + 1;
-    // two x-tiles per wave from 4 x'-tiles up (D >= 96; w9 1080p: equal, w15 +15 %), one below
-    // (VGA D=64: +8 %) and at D = 160 (the accumulators of 2 x 6 tiles do not fit)
-    const int xt = nt >= 4 && nt <= 5 ? 2 : 1;
+    // x-tiles per wave: one (<= 128 VGPRs: 3 blocks per CU) unless the edge masking needs the
+    // per-cell select (no offset room: w15 at D=128), where two amortise the operand loads
+    // better — 1080p D=128, one stream, 26 frames: w9 767 vs 847 us, w15 458 vs 424 us; VGA
+    // D=64 w9 136 vs 161 us (profiles/r06_ssd)
+    const int xt = nt >= 4 && nt <= 5 ? 2 : 1;   // refined below once the key range is known
     const int mb = D <= 128 ? 7 : 8;
     const long long M = 1LL << mb;
     const long long n = (long long)win * win;
@@ -473,7 +486,7 @@ bool ssd_shape(int win, int D, int rows, SsdShape* sh) {
     // the offset is a multiple of M: the disparity index is read from the key's low bits
     const long long off = (R + M - 1) / M * M;
     const bool big = off < (1LL << 30);
-    *sh = SsdShape{xt, nt, mb, hb, (int)bias, big, big ? (uint32_t)off : 0x80000000u};
+    *sh = SsdShape{big ? 1 : xt, nt, mb, hb, (int)bias, big, big ? (uint32_t)off : 0x80000000u};
     return true;
 }
 
@@ -522,28 +535,22 @@ int launch_ssd_mfma(const MatchParams& a, hipStream_t s) {
     MatchParams b = a;
     b.fs_out = nf > 1 ? a.fs_out : 0;
     b.fs_in = nf > 1 ? a.fs_in : 0;
-    static const int xt_env = [] {   // A/B only: SV_SSD_XT=1|2 overrides the x-tiles per wave
-        const char* e = std::getenv("SV_SSD_XT");
-        return e ? std::atoi(e) : 0;
-    }();
-    SsdShape s2 = sh;
-    if (xt_env == 1 || xt_env == 2) s2.xt = sh.nt <= 5 ? xt_env : 1;
     const auto go = [&](auto bm) {
         constexpr bool BM = decltype(bm)::value;
-        switch (sh.nt * 4 + s2.xt) {
-            case 2 * 4 + 1: return launch_t<1, 2, 7, BM>(b, s2, s);
-            case 2 * 4 + 2: return launch_t<2, 2, 7, BM>(b, s2, s);
-            case 3 * 4 + 1: return launch_t<1, 3, 7, BM>(b, s2, s);
-            case 3 * 4 + 2: return launch_t<2, 3, 7, BM>(b, s2, s);
-            case 4 * 4 + 1: return launch_t<1, 4, 7, BM>(b, s2, s);
-            case 4 * 4 + 2: return launch_t<2, 4, 7, BM>(b, s2, s);
-            case 5 * 4 + 1: return launch_t<1, 5, 7, BM>(b, s2, s);
-            case 5 * 4 + 2: return launch_t<2, 5, 7, BM>(b, s2, s);
-            case 6 * 4 + 1: return launch_t<1, 6, 8, BM>(b, s2, s);
+        switch (sh.nt * 4 + sh.xt) {
+            case 2 * 4 + 1: return launch_t<1, 2, 7, BM>(b, sh, s);
+            case 2 * 4 + 2: return launch_t<2, 2, 7, BM>(b, sh, s);
+            case 3 * 4 + 1: return launch_t<1, 3, 7, BM>(b, sh, s);
+            case 3 * 4 + 2: return launch_t<2, 3, 7, BM>(b, sh, s);
+            case 4 * 4 + 1: return launch_t<1, 4, 7, BM>(b, sh, s);
+            case 4 * 4 + 2: return launch_t<2, 4, 7, BM>(b, sh, s);
+            case 5 * 4 + 1: return launch_t<1, 5, 7, BM>(b, sh, s);
+            case 5 * 4 + 2: return launch_t<2, 5, 7, BM>(b, sh, s);
+            case 6 * 4 + 1: return launch_t<1, 6, 8, BM>(b, sh, s);
         }
         return (int)hipErrorInvalidValue;
     };
-    return s2.big ? go(std::true_type{}) : go(std::false_type{});
+    return sh.big ? go(std::true_type{}) : go(std::false_type{});
 }
 
 }  // namespace sv

@@ -411,20 +411,52 @@ PMC_PASSES = [("sq", ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_
               ("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE"])]
 
 
-def live_pmc(args, kernel_tag="k_match", timeout=150):
+def live_pmc(args, kernel_tags=("k_match",), timeout=150):
+    """rocprofv3 over short child runs of this script with the same workload: one kernel-trace
+    pass (average duration of the match kernel and the median, to set beside the HIP-event
+    launch times of the timed region) and the PMC passes.  The first of `kernel_tags` found in
+    the trace names the match kernel (SSD: k_ssd_mfma where it runs, else k_match)."""
     rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rocprof):
         return {"error": "rocprofv3 not found"}
     tmp = tempfile.mkdtemp(prefix="sv_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "6", "--warmup", "2",
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--warmup", "2",
              "--height", str(args.height), "--width", str(args.width), "--num-disp", str(args.num_disp),
              "--win", str(args.win), "--cost", args.cost, "--batch", str(args.batch),
-             "--frames", str(args.frames)]
-    agg = {}
+             "--frames", str(args.frames), "--streams", str(args.streams)]
+    agg, trace = {}, {}
+    kernel_tag = kernel_tags[0]
     try:
+        cmd = [rocprof, "--kernel-trace", "--stats", "--output-format", "csv", "-d",
+               os.path.join(tmp, "trace"), "-o", "trace", "--", *child, "--steps", "30"]
+        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=tmp,
+                             start_new_session=True, env=dict(os.environ, TMPDIR=tmp))
+        try:
+            _, err = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            return {"error": "rocprofv3 kernel-trace pass timed out"}
+        if p.returncode != 0:
+            return {"error": f"rocprofv3 kernel-trace pass rc={p.returncode}: {err.decode(errors='replace')[-300:]}"}
+        stats = []
+        for f in glob.glob(os.path.join(tmp, "trace", "**", "*kernel_stats.csv"), recursive=True):
+            stats += list(csv.DictReader(open(f)))
+        for tag in kernel_tags:
+            rows = [r for r in stats if tag in r["Name"]]
+            if rows:
+                kernel_tag = tag
+                r = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+                trace["kernel"] = r["Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+                trace["avg_us"] = round(float(r["AverageNs"]) / 1e3, 2)
+                trace["calls"] = int(r["Calls"])
+                break
+        med = [r for r in stats if "k_median" in r["Name"]]
+        if med:
+            trace["median_avg_us"] = round(float(med[0]["AverageNs"]) / 1e3, 2)
         for name, counters in PMC_PASSES:
             cmd = [rocprof, "--pmc", *counters, "--output-format", "csv", "-d",
-                   os.path.join(tmp, name), "-o", name, "--", *child]
+                   os.path.join(tmp, name), "-o", name, "--", *child, "--steps", "6"]
             p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=tmp,
                                  start_new_session=True, env=dict(os.environ, TMPDIR=tmp))
             try:
@@ -444,6 +476,7 @@ def live_pmc(args, kernel_tag="k_match", timeout=150):
         shutil.rmtree(tmp, ignore_errors=True)
     res = {k: sum(v) / len(v) for k, v in agg.items()}
     res["dispatches"] = max((len(v) for v in agg.values()), default=0)
+    res["trace"] = trace
     return res
 
 
@@ -1211,8 +1244,10 @@ def main():
     if k_avg_s:
         if rank == 0 and not args.no_live_pmc and not launched and len(engines) == 1 and not rowtile:
             t_p = time.perf_counter()
-            pmc = live_pmc(args, "sgbm" if args.cost == "sgbm" else "k_match")
+            pmc = live_pmc(args, ("sgbm",) if args.cost == "sgbm" else
+                           ("k_ssd_mfma", "k_match") if args.cost == "ssd" else ("k_match",))
             pmc["seconds"] = round(time.perf_counter() - t_p, 1)
+        ktrace = pmc.pop("trace", None) or {}
         achieved = k_bytes / k_avg_s / 1e9
         insts = pmc.get("SQ_INSTS_VALU")
         fetch = pmc.get("FETCH_SIZE")
@@ -1278,6 +1313,17 @@ def main():
                     **{k: (round(v, 1) if isinstance(v, float) else v) for k, v in pmc.items()}},
             "median_post_avg_us": round(med_ms / med_n * 1e3, 2) if med_n else None,
         }
+        if ktrace.get("avg_us"):
+            # the same figures from the rocprofv3 kernel trace of a 30-step child run of this
+            # command: per-kernel GPU durations, independent of HIP events
+            ta = ktrace["avg_us"] * 1e-6
+            roofline["trace"] = {
+                "source": "rocprofv3 --kernel-trace --stats over a 30-step child run of this command",
+                "kernel": ktrace["kernel"], "calls": ktrace["calls"], "avg_launch_us": ktrace["avg_us"],
+                "achieved": round(k_bytes / ta / 1e9, 2), "frac": round(k_bytes / ta / 1e9 / HBM_PEAK_GBS, 5),
+                "median_avg_us": ktrace.get("median_avg_us"),
+                "events_vs_trace": round(k_avg_s / ta, 4)}
+            roofline["kernel"] = ktrace["kernel"]
 
     # per step: bytes received by the root (N-1 peers' maps; rowtile: N-1 bands of the three
     # outputs) and, rowtile with band inputs, bytes sent from the root (both images' rows)

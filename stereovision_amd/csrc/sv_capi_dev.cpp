@@ -572,10 +572,12 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
     for (int i = 0; i < 2; ++i) {
         uint8_t* stage = c->hin.as<uint8_t>() + (size_t)i * row * H;
         uint8_t* dst = channels == 1 ? c->gray[i].as<uint8_t>() : c->img[i].as<uint8_t>();
-        c->prof_begin(SV_K_H2D, c->stream);   // (profile on: device events around each upload)
-        rc = stage_rows(c, src[i], 0, H, row, stride, stage, dst, 6);
-        c->prof_end(c->stream);
-        if (rc) return rc;
+        {   // (profile on: device events around each upload; closed on every exit path)
+            ProfScope ph(c, SV_K_H2D, c->stream);
+            rc = stage_rows(c, src[i], 0, H, row, stride, stage, dst, 6);
+            if (rc) return rc;
+            ph.done();
+        }
         if (channels == 3)
             SV_LAUNCH(c, SV_K_GRAY, c->stream,
                       sv::launch_gray(c->img[i].as<uint8_t>(), H, W, (int)row, c->gray[i].as<uint8_t>(), c->stream));
@@ -586,28 +588,30 @@ int host_frame_path(sv_ctx* c, const uint8_t* left, const uint8_t* right, int H,
     SV_LAUNCH(c, SV_K_MEDIAN, c->stream,
               sv::launch_median_i16(c->d16.as<int16_t>(), H, W, 0, H, reg ? c->fb.as<float>() : nullptr, mp,
                                     c->stream));
-    c->prof_begin(SV_K_D2H, ds);
-    for (int q = 0; q < npiece; ++q) {
-        const int p0 = (int)((long long)H * q / npiece), p1 = (int)((long long)H * (q + 1) / npiece);
-        bands[q][0] = p0;
-        bands[q][1] = p1;
-        if (p1 <= p0) continue;
-        const size_t i0 = (size_t)p0 * W, m = (size_t)(p1 - p0) * W;
-        if (reg) {
-            SV_HIP(hipMemcpyAsync(o.disp + i0, c->fb.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
-            SV_HIP(hipMemcpyAsync(o.a + i0, c->fa.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
-            if (o.u8) SV_HIP(hipMemcpyAsync(o.u8 + i0, c->u8.as<uint8_t>() + i0, m, hipMemcpyDeviceToHost, ds));
-            if (scaled) SV_HIP(hipMemcpyAsync(o.b + i0, c->fc.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
-            if (o.bgr)
-                SV_HIP(hipMemcpyAsync(o.bgr + 3 * i0, c->bgr.as<uint8_t>() + 3 * i0, 3 * m, hipMemcpyDeviceToHost, ds));
-        } else {
-            SV_HIP(hipMemcpyAsync(c->hout.as<int16_t>() + i0, c->m16.as<int16_t>() + i0, m * 2, hipMemcpyDeviceToHost,
-                                  ds));
-            if (!c->dev_done[q]) SV_HIP(hipEventCreateWithFlags(&c->dev_done[q], hipEventDisableTiming));
-            SV_HIP(hipEventRecord(c->dev_done[q], ds));
+    {
+        ProfScope pd(c, SV_K_D2H, ds);   // an SV_HIP failure below returns through prof_abort
+        for (int q = 0; q < npiece; ++q) {
+            const int p0 = (int)((long long)H * q / npiece), p1 = (int)((long long)H * (q + 1) / npiece);
+            bands[q][0] = p0;
+            bands[q][1] = p1;
+            if (p1 <= p0) continue;
+            const size_t i0 = (size_t)p0 * W, m = (size_t)(p1 - p0) * W;
+            if (reg) {
+                SV_HIP(hipMemcpyAsync(o.disp + i0, c->fb.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
+                SV_HIP(hipMemcpyAsync(o.a + i0, c->fa.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
+                if (o.u8) SV_HIP(hipMemcpyAsync(o.u8 + i0, c->u8.as<uint8_t>() + i0, m, hipMemcpyDeviceToHost, ds));
+                if (scaled) SV_HIP(hipMemcpyAsync(o.b + i0, c->fc.as<float>() + i0, m * 4, hipMemcpyDeviceToHost, ds));
+                if (o.bgr)
+                    SV_HIP(hipMemcpyAsync(o.bgr + 3 * i0, c->bgr.as<uint8_t>() + 3 * i0, 3 * m, hipMemcpyDeviceToHost, ds));
+            } else {
+                SV_HIP(hipMemcpyAsync(c->hout.as<int16_t>() + i0, c->m16.as<int16_t>() + i0, m * 2, hipMemcpyDeviceToHost,
+                                      ds));
+                if (!c->dev_done[q]) SV_HIP(hipEventCreateWithFlags(&c->dev_done[q], hipEventDisableTiming));
+                SV_HIP(hipEventRecord(c->dev_done[q], ds));
+            }
         }
+        pd.done();
     }
-    c->prof_end(ds);
     if (prof) { const double t = now_ms(); tm[1] = t - tp; tp = t; }
     if (!reg) {
         for (int q = 0; q < npiece; ++q) {

@@ -657,6 +657,11 @@ __global__ __launch_bounds__(64) void k_hog_hist_cr(const uint8_t* __restrict__ 
     for (int t = 2 * r; t < nsteps; ++t) {
         prefetch(t);
         step(t);
+        // the neighbour lanes' vertical sums of this step, just updated by their wavefront-scope
+        // atomics, are read below: an acquire-release fence at wavefront scope orders the two
+        // for the compiler (no instruction on gfx950: a wave's LDS ops complete in order); the
+        // next step's atomics come after the barriers below
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         // horizontal window: a running sum over columns -r .. K-1+r, the outer ones the
         // neighbour lanes' vertical sums (read from LDS; LDS ops of a wave complete in order);
         // each plane's K sums go straight to the row's staging area

@@ -428,7 +428,7 @@ def live_pmc(args, kernel_tags=("k_match",), timeout=150):
     kernel_tag = kernel_tags[0]
     try:
         cmd = [rocprof, "--kernel-trace", "--stats", "--output-format", "csv", "-d",
-               os.path.join(tmp, "trace"), "-o", "trace", "--", *child, "--steps", "30"]
+               os.path.join(tmp, "trace"), "-o", "trace", "--", *child, "--steps", "60", "--warmup-seconds", "1.0"]
         p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=tmp,
                              start_new_session=True, env=dict(os.environ, TMPDIR=tmp))
         try:
@@ -447,7 +447,7 @@ def live_pmc(args, kernel_tags=("k_match",), timeout=150):
             if rows:
                 kernel_tag = tag
                 r = max(rows, key=lambda r: float(r["TotalDurationNs"]))
-                trace["kernel"] = r["Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+                trace["kernel"] = r["Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
                 trace["avg_us"] = round(float(r["AverageNs"]) / 1e3, 2)
                 trace["calls"] = int(r["Calls"])
                 break
@@ -721,7 +721,10 @@ def parse_args(argv=None):
     if args.pmc_child:
         args.no_cpu_baseline = args.no_aux = args.no_live_pmc = args.no_host_path = True
         args.no_profile = args.no_verify = True
-        args.warmup_seconds = 0.0
+        # the PMC passes count per dispatch (no warm-up needed); the kernel-trace pass times
+        # kernels and passes its own --warmup-seconds (after this flag) to reach steady clocks
+        if "--warmup-seconds" not in sys.argv:
+            args.warmup_seconds = 0.0
     return args
 
 
@@ -1314,11 +1317,11 @@ def main():
             "median_post_avg_us": round(med_ms / med_n * 1e3, 2) if med_n else None,
         }
         if ktrace.get("avg_us"):
-            # the same figures from the rocprofv3 kernel trace of a 30-step child run of this
+            # the same figures from the rocprofv3 kernel trace of a 60-step child run of this
             # command: per-kernel GPU durations, independent of HIP events
             ta = ktrace["avg_us"] * 1e-6
             roofline["trace"] = {
-                "source": "rocprofv3 --kernel-trace --stats over a 30-step child run of this command",
+                "source": "rocprofv3 --kernel-trace --stats over a 60-step child run of this command (1 s warm-up)",
                 "kernel": ktrace["kernel"], "calls": ktrace["calls"], "avg_launch_us": ktrace["avg_us"],
                 "achieved": round(k_bytes / ta / 1e9, 2), "frac": round(k_bytes / ta / 1e9 / HBM_PEAK_GBS, 5),
                 "median_avg_us": ktrace.get("median_avg_us"),

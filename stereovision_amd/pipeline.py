@@ -24,15 +24,18 @@ from .engine import Engine, get_engine
 
 
 def max_in_flight() -> int:
-    """Contexts (streams) one process can keep truly concurrent on a device: the HIP runtime
-    maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default, and on the GPU boxes);
-    a fifth stream shares a queue with another, so its transfers and kernels wait behind that
-    stream's work — measured: 1080p create_depth_map with 6 in flight ran at 1.9k frames/s
-    against 2.5k with 4 (profiles/r05zh/configs.txt, the sweep in profiles/r06*)."""
+    """Contexts (streams) worth keeping in flight on one device: two per hardware queue the HIP
+    runtime maps one process's streams onto (GPU_MAX_HW_QUEUES, 4 by default and on the GPU
+    boxes) — while one context's host work (page-locked staging, expansion of the medians into
+    the output maps) runs, the other keeps the queue fed.  Measured at 1080p (profiles/
+    r06_pipeline/sweep.txt, 40 warm-up frames and 3 x 300 timed per depth): depth 8 beats 4 by
+    15-19 % in two sweeps; from 16 the per-call staging/issue time grows to 2.5-3 ms and the
+    rate falls (24: 2.6k).  Round 5's "depth 6 loses to 4" was an artifact: that sweep warmed
+    4 frames in all, so contexts 5 and 6 paid their first-use costs inside the timed region."""
     try:
-        return max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
+        return 2 * max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
     except ValueError:
-        return 4
+        return 8
 
 
 class DepthMapPipeline:
@@ -42,9 +45,9 @@ class DepthMapPipeline:
     def __init__(self, num_disp: int, window_size: int, min_disp: int = 0, min_depth: float = 0.3,
                  max_depth: float = 2.0, cost: str = "sad", depth: int = 3, device: int | None = None,
                  cmap: str = "turbo", cap: bool = True):
-        """depth: frames in flight, capped at :func:`max_in_flight` (the hardware queues one
-        process's streams map onto; more contexts than queues only serialise behind each
-        other).  cap=False keeps the requested depth (for measuring the cap itself)."""
+        """depth: frames in flight, capped at :func:`max_in_flight` (two contexts per hardware
+        queue; deeper pipelines only add per-call staging time).  cap=False keeps the requested
+        depth (for measuring the cap itself)."""
         self.num_disp, self.win, self.min_disp = int(num_disp), int(window_size), int(min_disp)
         self.min_depth, self.max_depth, self.cost = float(min_depth), float(max_depth), cost
         self.requested_depth = max(1, int(depth))

@@ -156,10 +156,10 @@ def test_concurrent_callers_never_share_a_set(monkeypatch):
     assert not errors
 
 
-def test_pipeline_depth_is_capped_at_the_hardware_queues(monkeypatch):
-    """DepthMapPipeline keeps at most GPU_MAX_HW_QUEUES (4 by default) frames in
-    flight — a fifth context's stream shares a hardware queue and only serialises behind
-    another (1.9k vs 2.5k frames/s at 1080p); cap=False keeps the request (the measurement)."""
+def test_pipeline_depth_is_capped_at_two_contexts_per_hardware_queue(monkeypatch):
+    """DepthMapPipeline keeps at most 2 x GPU_MAX_HW_QUEUES (8 by default)
+    frames in flight — past that the per-call staging time grows and the rate falls
+    (profiles/r06_pipeline/sweep.txt); cap=False keeps the request (the measurement)."""
     from stereovision_amd import pipeline as P
 
     class _E:
@@ -173,15 +173,16 @@ def test_pipeline_depth_is_capped_at_the_hardware_queues(monkeypatch):
     monkeypatch.setattr(P, "get_engine", lambda d=None: _E())
     monkeypatch.setattr(P, "Engine", _E)
     monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
-    assert P.max_in_flight() == 4
-    for req, exp in ((1, 1), (3, 3), (4, 4), (6, 4), (16, 4)):
+    assert P.max_in_flight() == 8
+    for req, exp in ((1, 1), (3, 3), (4, 4), (8, 8), (12, 8), (24, 8)):
         p = P.DepthMapPipeline(64, 9, depth=req)
         assert (p.requested_depth, p.depth, len(p._engines)) == (req, exp, exp)
         p.close()
-    p = P.DepthMapPipeline(64, 9, depth=6, cap=False)
-    assert p.depth == 6
+    p = P.DepthMapPipeline(64, 9, depth=12, cap=False)
+    assert p.depth == 12
     p.close()
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
-    p = P.DepthMapPipeline(64, 9, depth=6)
-    assert p.depth == 6
+    assert P.max_in_flight() == 16
+    p = P.DepthMapPipeline(64, 9, depth=12)
+    assert p.depth == 12
     p.close()

@@ -53,25 +53,33 @@ def main():
     # the in-flight sweep: uncapped depths (cap=False) with the host-side stage times per call
     # (sv_host_profile: prepare, stage+issue, wait for the first piece, expand, wait for the
     # rest, total), and the capped pipeline a caller gets for the same request
-    for depth in (1, 2, 3, 4, 5, 6, 8):
+    # the in-flight sweep: uncapped depths (cap=False) and the capped pipeline a caller gets for
+    # the same request; per configuration 40 warm-up frames, then 3 timed runs of 300 frames
+    # (frames/s of each and their median) with the host-side stage times per call
+    # (sv_host_profile: prepare, stage+issue, wait for the first piece, expand, wait for the
+    # rest, total) over the three
+    depths = [int(v) for v in os.environ.get("SV_DEPTHS", "1,2,3,4,5,6,8").split(",")]
+    for depth in depths:
         for cap in ((False, True) if depth > 4 else (False,)):
             pipe = DepthMapPipeline(D, win, depth=depth, cap=cap)
             try:
-                for i in range(2 * depth):
-                    pipe.submit(*frames[i % 4]).result()
+                def run(n):
+                    futs = []
+                    t0 = time.perf_counter()
+                    for i in range(n):
+                        futs.append(pipe.submit(*frames[i % 4]))
+                        if len(futs) > pipe.depth:
+                            futs.pop(0).result()
+                    for f in futs:
+                        f.result()
+                    return n / (time.perf_counter() - t0)
+                run(40)
                 host_profile(enable=True, reset=True)
-                futs, n = [], 160
-                t0 = time.perf_counter()
-                for i in range(n):
-                    futs.append(pipe.submit(*frames[i % 4]))
-                    if len(futs) > pipe.depth:
-                        futs.pop(0).result()
-                for f in futs:
-                    f.result()
-                dt = time.perf_counter() - t0
+                reps = [round(run(300), 1) for _ in range(3)]
                 st = host_profile(enable=False, reset=True)
                 key = f"pipeline depth {depth}" + (f" capped to {pipe.depth}" if cap else "")
-                out[key] = {"frames_per_s": round(n / dt, 1), "ms_per_frame": round(dt * 1e3 / n, 3),
+                out[key] = {"frames_per_s": sorted(reps)[1], "runs": reps,
+                            "ms_per_frame": round(1e3 / sorted(reps)[1], 3),
                             "per_call_ms": {k: (round(v, 3) if v is not None else None)
                                             for k, v in st.items() if k != "calls"}}
             finally:

@@ -335,12 +335,14 @@ def host_path(H, W, D, win, seconds=3.0):
     except Exception as e:  # reported, never required
         out["per_call"] = {"error": str(e)}
     try:
-        from stereovision_amd.pipeline import DepthMapPipeline
+        from stereovision_amd.pipeline import DepthMapPipeline, max_in_flight
     except ImportError:
         return out
-    pipe = DepthMapPipeline(D, win, depth=4)
+    pipe = DepthMapPipeline(D, win, depth=max_in_flight())
     try:
-        for i in range(4):
+        # every context warmed several times: its first frames pay one-time costs (page-locked
+        # staging buffers, first touch — profiles/r06_pipeline/sweep.txt)
+        for i in range(5 * pipe.depth):
             pipe.submit(*frames[i % 4]).result()
         futs, n, t0 = [], 0, time.perf_counter()
         while True:

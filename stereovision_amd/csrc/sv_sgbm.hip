@@ -1146,8 +1146,12 @@ int launch_paths_t(const SgbmArgs& a, int nf, hipStream_t s, hipStream_t aux, hi
         SV_HPATH(16, 12, 8, 2) SV_HPATH(16, 16, 6, 2) SV_HPATH(16, 20, 4, 2) SV_HPATH(16, 24, 4, 2)
         SV_HPATH(16, 32, 4, 1)
     }
-    // (deeper prefetch did not pay for the horizontal lines of a single D=320 frame: one wave
-    // per SIMD with 16 steps ahead 1,105 -> 1,355 us, two waves with 9 steps ahead 1,119 us)
+    // (Deeper prefetch did not pay for the horizontal lines of a single D=320 frame: one wave
+    // per SIMD with 16 steps ahead 1,105 -> 1,355 us, two waves with 9 steps ahead 1,119 us;
+    // round 6, an LDS-DMA ring 11 steps deep (global_load_lds_dwordx4, counted vmcnt, no
+    // register ring for the compiler to drain at the loop back-edge): 1,116 -> 1,175 us.  The
+    // horizontal paths are bound by their volume traffic, 4.43 GB per D=320 frame at ~3.8-4.0
+    // TB/s — DESIGN.md §10.8.)
     SV_HPATH(32, 2, 16, 2) SV_HPATH(32, 4, 12, 2) SV_HPATH(32, 6, 10, 2) SV_HPATH(32, 8, 8, 2)
     SV_HPATH(32, 10, 6, 2) SV_HPATH(32, 12, 4, 2) SV_HPATH(32, 16, 3, 2)
     SV_HPATH(16, 1, 24, 1) SV_HPATH(16, 2, 24, 1) SV_HPATH(16, 4, 16, 1) SV_HPATH(16, 8, 16, 1)

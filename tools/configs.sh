@@ -24,5 +24,10 @@ run metric_1080p_d128_w9
 run metric_batch1 --batch 1
 run c5_4k_d256_w15 --height 2160 --width 3840 --num-disp 256 --win 15 --frames 2 --batch 2 --steps 50
 run c5_4k_d256_w15_hog --height 2160 --width 3840 --num-disp 256 --win 15 --cost hog --frames 2 --batch 2 --steps 20
+run ssd_1080p_d128_w9 --cost ssd
+run ssd_1080p_d128_w11 --cost ssd --win 11
+run ssd_1080p_d128_w15 --cost ssd --win 15
+run sgbm_1080p_d320_w7 --cost sgbm --num-disp 320 --win 7 --batch 1 --steps 40
+run sgbm_1080p_d320_w7_3calls --cost sgbm --num-disp 320 --win 7 --batch 1 --streams 3 --steps 40
 timeout -k 10 300 python tools/host_rate.py > gpurun_out/host_rate.log 2>&1; tail -n 1 gpurun_out/host_rate.log
 timeout -k 10 300 python tools/host_rate.py 480 640 64 9 >> gpurun_out/host_rate.log 2>&1; tail -n 1 gpurun_out/host_rate.log

@@ -42,6 +42,7 @@ struct MatchPlan {
     int lpg;     // lanes per group: 16, 32 or 64
     int ndw;     // dwords per column pack: ceil(win/4) (SAD/SSD), 5 for HOG
     int dbits;   // argmin key index bits
+    int mfma_only = 0;   // SSD whose keys only the matrix-core kind holds (its own key form)
 };
 
 struct MatchParams {
@@ -83,7 +84,8 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
 // whether a launch takes that form, and the elements of one key plane it needs
 bool ring_split(int cost, int win, int num_disp);
 bool ring_ssd(int cost, int win, int num_disp);   // SSD windows 5..9, D <= 256: the ring kind
-// SSD on the matrix cores (sv_ssd_mfma.hip): odd windows <= 15, D a multiple of 32 up to 160
+// SSD on the matrix cores (sv_ssd_mfma.hip): odd windows <= 15, D a multiple of 32 up to 256
+// (the key range decides: D > 128 up to win 13)
 bool ssd_mfma(int cost, int win, int num_disp);
 bool ssd_mfma_fits(const MatchParams& a, int cost);   // + operand alignment, r == win / 2
 int launch_ssd_mfma(const MatchParams& a, hipStream_t s);

@@ -1433,10 +1433,18 @@ int plan_match(int num_disp, int win, int cost, MatchPlan* plan) {
     plan->dbits = bits < 1 ? 1 : bits;
     if (hi_keys(kind, win / 2)) plan->dbits = 16;
     const uint64_t cmax = max_cost(win, cost);
-    if ((cmax << plan->dbits) >= (1ull << 32)) return -34;  // ERANGE: key would overflow
-    // padding disparities (idx >= D) carry keys above (cmax + 1) << dbits
-    if (num_disp < plan->dpl * plan->lpg && cost != COST_HOG && (((2 * cmax + 2) << plan->dbits) >= (1ull << 32)))
-        return -34;
+    // the other kinds' keys (cost << dbits | idx) must fit 32 bits; padding disparities (idx >=
+    // D) carry keys above (cmax + 1) << dbits
+    const bool over = (cmax << plan->dbits) >= (1ull << 32) ||
+                      (num_disp < plan->dpl * plan->lpg && cost != COST_HOG &&
+                       ((2 * cmax + 2) << plan->dbits) >= (1ull << 32));
+    plan->mfma_only = 0;
+    if (over) {
+        // SSD the matrix-core kind holds (centred keys, sv_ssd_mfma.hip): only that kind runs
+        // it (launch_match refuses the call where it cannot: unaligned images)
+        if (!ssd_mfma(cost, win, num_disp)) return -34;   // ERANGE: key would overflow
+        plan->mfma_only = 1;
+    }
     return 0;
 }
 
@@ -1478,6 +1486,7 @@ int launch_match(const MatchParams& a, const MatchPlan& p, int cost, hipStream_t
     const bool ring_fits = 2LL * ((long long)(a.row1 + 3) * a.opitch + a.W + 64) < 0x7FFFFFFFLL;
     if (ring_kind(cost, a.win, a.D) && ring_fits) return launch_ring<false>(a, s);
     if (ssd_mfma_fits(a, cost)) return launch_ssd_mfma(a, s);
+    if (p.mfma_only) return (int)hipErrorInvalidValue;   // no other kind holds these keys
     if (ring_ssd(cost, a.win, a.D) && ring_fits) return launch_ring<false, true>(a, s);
     if (ring_split(cost, a.win, a.D) && a.keys) {
         // (key planes: 4-byte elements, so half the 2^31-byte range of the int16 maps)

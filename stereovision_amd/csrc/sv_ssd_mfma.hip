@@ -43,8 +43,8 @@
 //     leaving (L', R') rows, so every 16-byte operand at any byte offset is 4 aligned
 //     ds_read_b32 (an unaligned ds_read_b128 costs ~7x: tools/microbench/lds_unaligned).
 //   * the hsq ring (win + 2 rows) and U (double-buffered) live in LDS beside them.
-//   * D <= 160 (<= 6 x'-tiles: the accumulators fit in the 256 VGPRs beside the operands); the
-//     4-byte alignment of the images is checked by the launcher (ssd_mfma_fits).
+//   * D <= 256 (<= 9 x'-tiles of accumulators) where the key range fits 32 bits (D > 128: win
+//     <= 13); the 4-byte alignment of the images is checked by the launcher (ssd_mfma_fits).
 #include "sv_internal.h"
 
 namespace sv {
@@ -457,9 +457,9 @@ struct SsdShape {
 // sum lands back in [off - R, off + R]): R < 2^31 with off = 2^31, and R < 2^30 for the offset
 // masking (off = R; 1080p D=128: windows <= 13; D=160: <= 9).
 bool ssd_shape(int win, int D, int rows, SsdShape* sh) {
-    // D > 160 (7+ x'-tiles): the accumulators no longer fit beside the operands (spills; the
-    // 4K D=256 w9 frame ran 3.2x slower than the ring kernel) — the ring / one-row kinds keep it
-    if (win < 1 || win > 15 || (win & 1) == 0 || D < 32 || D > 160 || D % 32 != 0) return false;
+    // D up to 256 (9 x'-tiles of accumulators, 194 VGPRs at one x-tile per wave); the key
+    // range below decides the windows (D > 128 takes 8 index bits: up to win 13)
+    if (win < 1 || win > 15 || (win & 1) == 0 || D < 32 || D > 256 || D % 32 != 0) return false;
     static const bool on = [] {
         const char* e = std::getenv("SV_SSD_MFMA");
         return !(e && e[0] == '0');
@@ -547,6 +547,9 @@ int launch_ssd_mfma(const MatchParams& a, hipStream_t s) {
             case 5 * 4 + 1: return launch_t<1, 5, 7, BM>(b, sh, s);
             case 5 * 4 + 2: return launch_t<2, 5, 7, BM>(b, sh, s);
             case 6 * 4 + 1: return launch_t<1, 6, 8, BM>(b, sh, s);
+            case 7 * 4 + 1: return launch_t<1, 7, 8, BM>(b, sh, s);
+            case 8 * 4 + 1: return launch_t<1, 8, 8, BM>(b, sh, s);
+            case 9 * 4 + 1: return launch_t<1, 9, 8, BM>(b, sh, s);
         }
         return (int)hipErrorInvalidValue;
     };

@@ -1,10 +1,11 @@
 """GPU parity of the SSD matrix-core kind (sv_ssd_mfma.hip: v_mfma_i32_32x32x32_i8 on offset
 images, the window's vertical sum carried in persistent accumulators) against the C oracle's
-SSD winner-take-all (first minimum): every odd window 1..15 and D = 32..160 in steps of 32
+SSD winner-take-all (first minimum): every odd window 1..15 and D = 32..256 in steps of 32
 (VERDICT r05 #2), row bands, frame batches, several row bands per block column, negative and
-positive min_disp, saturated contrast and all-tie frames.  Bit-exact.  D = 192..256 take the
-ring / one-row kinds (the wide cases below pin that hand-over) and so does an image whose
-base is not 4-byte aligned (the LDS-DMA staging loads aligned dwords)."""
+positive min_disp, saturated contrast and all-tie frames.  Bit-exact.  An image whose base is
+not 4-byte aligned takes the ring / one-row kinds (the LDS-DMA staging loads aligned dwords);
+where only this kind's centred keys fit 32 bits (D = 160 w13, say) such a call fails loudly
+instead.  (D > 128 with win 15 fits no kind's keys: the planner refuses it.)"""
 import numpy as np
 import pytest
 
@@ -26,7 +27,7 @@ def test_ssd_mfma_windows(engine, D, win):
     np.testing.assert_array_equal(engine.disparity(L, R, 0, D, win, "ssd"), _ref(L, R, 0, D, win))
 
 
-@pytest.mark.parametrize("D,win", [(96, 9), (160, 7), (192, 11), (224, 5), (256, 9), (256, 13)])
+@pytest.mark.parametrize("D,win", [(96, 9), (160, 7), (160, 13), (192, 11), (224, 5), (256, 9), (256, 13)])
 def test_ssd_mfma_wide_disparity_ranges(engine, D, win):
     H, W = 29, D + 420
     L, R, _ = stereo_pair(H, W, D, seed=D + win)
@@ -108,6 +109,26 @@ def test_ssd_mfma_unaligned_images_fall_back(engine):
         e.disparity_dev(dL + 1, dR + 1, H, W, W, 0, D, win, "ssd", 0, H, d16, W)
         e.synchronize()
         np.testing.assert_array_equal(e.to_host(d16, (H, W), np.int16), _ref(L, R, 0, D, win))
+    finally:
+        for p in (dL, dR, d16):
+            e.dev_free(p)
+
+
+def test_ssd_mfma_only_keys_refuse_unaligned_images(engine):
+    """D=160 w13: the other kinds' (cost << dbits | idx) keys overflow, so the planner admits the
+    call for the matrix-core kind only; an unaligned view cannot take it and must error."""
+    from stereovision_amd.engine import SVError
+    H, W, D, win = 21, 500, 160, 13
+    L, R, _ = stereo_pair(H, W, D, seed=13)
+    n = H * W
+    e = engine
+    dL, dR, d16 = e.dev_alloc(n + 4), e.dev_alloc(n + 4), e.dev_alloc(2 * n)
+    try:
+        e.to_device(dL + 1, L)
+        e.to_device(dR + 1, R)
+        with pytest.raises(SVError):
+            e.disparity_dev(dL + 1, dR + 1, H, W, W, 0, D, win, "ssd", 0, H, d16, W)
+            e.synchronize()
     finally:
         for p in (dL, dR, d16):
             e.dev_free(p)

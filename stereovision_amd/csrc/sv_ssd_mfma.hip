@@ -26,22 +26,25 @@
 //     2M — neither the argmin nor its index bits change (ranges checked by the launcher).
 //   * epilogue per cell (lane = x column, 16 registers = x' rows):
 //       key = U(x') + 2M * acc = U(x') - 2M * X - 2M * Cor(x)   (one v_lshl_add_u32)
-//       U(x') = M * (SR2(x') - bias) - ix'   (per row, built once per x' by the block, in LDS)
-//     so key = M * (val - bias) + d + c_x: for one x, the order of the keys is the order of
-//     (cost, d) — the oracle's first minimum — and d - minD = (key + ix + D - 1) & (M - 1).
-//     best = v_min3(best, key, key) over the x'-tiles; the first and the last x'-tile of an
-//     x-tile hold complementary triangles of valid d (D % 32 == 0), so their keys are merged
-//     with one v_cndmask per cell by a lane-constant mask (row >= column) before the min.
+//       U(x') = M * (SR2(x') - bias) - ix' + off   (per row, built once per x' by the block)
+//     so for one x the order of the keys is the order of (cost, d) — the oracle's first
+//     minimum — and d - minD = (key + c + D - 1) mod M (c: the x column's block index).  The
+//     lane's minimum over its registers and x'-tiles is a v_min3 chain; one v_permlane32_swap
+//     joins the two lane halves (the two x' row halves of one x).  The first and the last
+//     x'-tile of an x-tile hold complementary triangles of valid d (D % 32 == 0): masked by an
+//     offset planted in the accumulators where the key range allows (BM), else by one
+//     v_cndmask per edge cell.
 //   * SR2: per staged row the block computes hsq(x') = sum_{i<win} R'(x'-r+i)^2 (4 v_dot4 on the
 //     masked 16 bytes) once; the per-column running vertical sum adds the entering row's and
 //     subtracts the leaving row's.
 //   * staging: every step one LDS-DMA per thread (global_load_lds_dword) lands the raw dwords of
 //     the row entering PRE = 5 steps later in a ring of win + 5 raw rows, retired by a counted
-//     s_waitcnt vmcnt(3) two steps before use — no global load result ever sits in a VGPR, the
-//     row loop has one barrier per step (lgkmcnt + s_barrier only) and no global latency.
-//     From the raw ring each step builds 4 byte-shifted copies of its entering (L', ~R') and
-//     leaving (L', R') rows, so every 16-byte operand at any byte offset is 4 aligned
-//     ds_read_b32 (an unaligned ds_read_b128 costs ~7x: tools/microbench/lds_unaligned).
+//     s_waitcnt vmcnt before the barrier that precedes its use — no global load result ever
+//     sits in a VGPR, the row loop has one barrier per step (lgkmcnt + s_barrier only) and no
+//     exposed global latency.  From the raw ring each step builds 4 byte-shifted copies of its
+//     entering (L', ~R') and leaving (L', R') rows, so every 16-byte operand at any byte offset
+//     is 4 aligned ds_read_b32 (an unaligned ds_read_b128 costs ~7x:
+//     tools/microbench/lds_unaligned).
 //   * the hsq ring (win + 2 rows) and U (double-buffered) live in LDS beside them.
 //   * D <= 256 (<= 9 x'-tiles of accumulators) where the key range fits 32 bits (D > 128: win
 //     <= 13); the 4-byte alignment of the images is checked by the launcher (ssd_mfma_fits).
@@ -119,8 +122,8 @@ struct SsdCfg {
 // The raw rows arrive by LDS-DMA (global_load_lds_dword: wave-uniform LDS base + 4 x lane), one
 // dword per thread: the 4-byte aligned dword of columns c0 .. c0 + 3 (c0 % 4 == 0) clamped into
 // the row, ca = clamp(c0, 0, (W - 1) & ~3).  Columns outside [0, W) replicate the edge pixel
-// (the oracle's replicate border): for blocks whose streams cross an image edge the copy builder
-// re-selects the bytes with one v_perm (selector below); interior blocks skip it.
+// (the oracle's replicate border): the copy builder re-selects the bytes with one v_perm per
+// dword (the selector below, fixed per thread: the identity inside the image).
 __device__ __forceinline__ int clamp_dword(int c0, int W) { return min(max(c0, 0), (W - 1) & ~3); }
 // v_perm selector taking the dword loaded at clamp_dword(c0) to the replicate-clamped bytes of
 // columns c0 .. c0 + 3 (0x03020100, the identity, inside the image)

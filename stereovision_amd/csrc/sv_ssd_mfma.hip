@@ -499,9 +499,11 @@ int launch_t(const MatchParams& a, const SsdShape& sh, hipStream_t s) {
     const int nf = a.nf > 1 ? a.nf : 1;
     const int rows = a.row1 - a.row0;
     dim3 grid((a.X1 - a.X0 + C::XW - 1) / C::XW, (rows + sh.hb - 1) / sh.hb, nf);
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ssd_mfma<XT, NT, MB, BM>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::lds(15));
-    if (attr != hipSuccess) return (int)attr;
+    if (C::lds(a.win) > 65536) {   // opt in to > 64 KiB of dynamic LDS (per device: every launch)
+        const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ssd_mfma<XT, NT, MB, BM>),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, C::lds(a.win));
+        if (attr != hipSuccess) return (int)attr;
+    }
     hipLaunchKernelGGL((k_ssd_mfma<XT, NT, MB, BM>), grid, dim3(kThreads), C::lds(a.win), s, a, sh.hb, sh.bias, sh.off);
     return (int)hipGetLastError();
 }

@@ -438,9 +438,10 @@ def live_pmc(args, kernel_tags=("k_match",), timeout=150):
         except subprocess.TimeoutExpired:
             os.killpg(p.pid, signal.SIGKILL)
             p.wait()
-            return {"error": "rocprofv3 kernel-trace pass timed out"}
+            err = b"timed out"
+        # a failed trace pass is reported in `trace` and the PMC passes still run
         if p.returncode != 0:
-            return {"error": f"rocprofv3 kernel-trace pass rc={p.returncode}: {err.decode(errors='replace')[-300:]}"}
+            trace["error"] = f"rocprofv3 kernel-trace pass rc={p.returncode}: {err.decode(errors='replace')[-300:]}"
         stats = []
         for f in glob.glob(os.path.join(tmp, "trace", "**", "*kernel_stats.csv"), recursive=True):
             stats += list(csv.DictReader(open(f)))

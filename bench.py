@@ -467,10 +467,10 @@ def live_pmc(args, kernel_tags=("k_match",), timeout=150):
             except subprocess.TimeoutExpired:
                 os.killpg(p.pid, signal.SIGKILL)
                 p.wait()
-                return {"error": f"rocprofv3 pass {name} timed out"}
+                return {"error": f"rocprofv3 pass {name} timed out", "trace": trace}
             if p.returncode != 0:
                 return {"error": f"rocprofv3 pass {name} rc={p.returncode}: "
-                                 f"{err.decode(errors='replace')[-300:]}"}
+                                 f"{err.decode(errors='replace')[-300:]}", "trace": trace}
             for f in glob.glob(os.path.join(tmp, name, "**", "*counter_collection.csv"), recursive=True):
                 for r in csv.DictReader(open(f)):
                     if kernel_tag in r["Kernel_Name"]:
@@ -1330,6 +1330,8 @@ def main():
                 "median_avg_us": ktrace.get("median_avg_us"),
                 "events_vs_trace": round(k_avg_s / ta, 4)}
             roofline["kernel"] = ktrace["kernel"]
+        elif ktrace.get("error"):
+            roofline["trace"] = {"error": ktrace["error"]}
 
     # per step: bytes received by the root (N-1 peers' maps; rowtile: N-1 bands of the three
     # outputs) and, rowtile with band inputs, bytes sent from the root (both images' rows)

@@ -413,6 +413,32 @@ PMC_PASSES = [("sq", ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_
               ("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE"])]
 
 
+def kernel_busy(tmp, tag):
+    """Union of the dispatch intervals of the kernels named `tag` in the kernel trace under
+    `tmp`: with launches of two streams in flight together, each launch's own duration counts
+    the time it shares the device with the other, so per-launch bytes / duration undercounts
+    the kernel's throughput; bytes of all launches / the time any of them runs does not."""
+    spans = []
+    for f in glob.glob(os.path.join(tmp, "trace", "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if tag in r.get("Kernel_Name", ""):
+                spans.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    if len(spans) < 4:
+        return {}
+    spans.sort()
+    spans = spans[len(spans) // 4:]   # past the warm-up
+    busy, cur_s, cur_e = 0, spans[0][0], spans[0][1]
+    for a, b in spans[1:]:
+        if a > cur_e:
+            busy += cur_e - cur_s
+            cur_s, cur_e = a, b
+        else:
+            cur_e = max(cur_e, b)
+    busy += cur_e - cur_s
+    return {"busy_launches": len(spans), "busy_us_per_launch": round(busy / len(spans) / 1e3, 2),
+            "busy_overlap": round(sum(b - a for a, b in spans) / busy, 3) if busy else None}
+
+
 def live_pmc(args, kernel_tags=("k_match",), timeout=150):
     """rocprofv3 over short child runs of this script with the same workload: one kernel-trace
     pass (average duration of the match kernel and the median, to set beside the HIP-event
@@ -457,6 +483,8 @@ def live_pmc(args, kernel_tags=("k_match",), timeout=150):
         med = [r for r in stats if "k_median" in r["Name"]]
         if med:
             trace["median_avg_us"] = round(float(med[0]["AverageNs"]) / 1e3, 2)
+        if trace.get("kernel"):
+            trace.update(kernel_busy(tmp, kernel_tag))
         for name, counters in PMC_PASSES:
             cmd = [rocprof, "--pmc", *counters, "--output-format", "csv", "-d",
                    os.path.join(tmp, name), "-o", name, "--", *child, "--steps", "6"]
@@ -1329,6 +1357,15 @@ def main():
                 "achieved": round(k_bytes / ta / 1e9, 2), "frac": round(k_bytes / ta / 1e9 / HBM_PEAK_GBS, 5),
                 "median_avg_us": ktrace.get("median_avg_us"),
                 "events_vs_trace": round(k_avg_s / ta, 4)}
+            if ktrace.get("busy_us_per_launch"):
+                # all launches' bytes over the time any of them runs (union of the dispatch
+                # intervals): the kernel's throughput when the lanes' launches overlap
+                tb = ktrace["busy_us_per_launch"] * 1e-6
+                roofline["trace"].update({
+                    "busy_us_per_launch": ktrace["busy_us_per_launch"], "busy_launches": ktrace["busy_launches"],
+                    "launch_overlap": ktrace["busy_overlap"],
+                    "achieved_busy": round(k_bytes / tb / 1e9, 2),
+                    "frac_busy": round(k_bytes / tb / 1e9 / HBM_PEAK_GBS, 5)})
             roofline["kernel"] = ktrace["kernel"]
         elif ktrace.get("error"):
             roofline["trace"] = {"error": ktrace["error"]}
